@@ -1,0 +1,117 @@
+"""Fixture case definitions shared by make_golden.py (generator) and the tests (consumers).
+
+Inputs are regenerated from seeds on every machine (torch CPU / numpy generators are deterministic),
+so the .npz files hold only expected outputs and compact summaries.
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+import torch
+
+MODEL_CASES = [
+    dict(name="hybrid_128x128_td768", kind="hybrid", hw=(128, 128), B=4, ctor=dict(latent_dim=128, text_dim=768)),
+    dict(name="hybrid_128x128_td384", kind="hybrid", hw=(128, 128), B=4, ctor=dict(latent_dim=128, text_dim=384)),
+    dict(name="hybrid_128x1024_td768", kind="hybrid", hw=(128, 1024), B=2, ctor=dict(latent_dim=128, text_dim=768)),
+    dict(name="cvae_128x128", kind="cvae", hw=(128, 128), B=4, ctor=dict(latent_dim=64, text_dim=768, num_classes=10)),
+    dict(name="cvae_128x1024", kind="cvae", hw=(128, 1024), B=2, ctor=dict(latent_dim=64, text_dim=768, num_classes=10)),
+    dict(name="simple_370", kind="simple", B=32, ctor=dict(input_dim=370, hidden_dims=[128, 64, 32], latent_dim=32)),
+]
+
+# (N, D, blob centres, k, n_init)
+KMEANS_CASES = [
+    (1336, 128, 10, 10, 10),
+    (1336, 128, 10, 2, 10),
+    (1336, 128, 10, 14, 10),
+    (1336, 64, 10, 10, 10),
+    (4096, 128, 8, 10, 10),
+    (4096, 64, 12, 14, 10),
+    (1336, 64, 10, 10, 1),
+]
+
+N_SAMPLES = 16
+
+
+def oracle_ctor(case):
+    ctor = dict(case["ctor"])
+    if case["kind"] in ("hybrid", "cvae"):
+        ctor["input_hw"] = tuple(case["hw"])
+    return ctor
+
+
+def case_by_name(name):
+    return next(c for c in MODEL_CASES if c["name"] == name)
+
+
+def inputs_fn(case):
+    """step -> (inputs tuple, eps) on CPU float32, seeded per (case, step)."""
+    B = case["B"]
+    kind = case["kind"]
+
+    def fn(step):
+        g = torch.Generator().manual_seed(1000 + 17 * step)
+        if kind == "simple":
+            x = torch.randn(B, case["ctor"]["input_dim"], generator=g)
+            eps = torch.randn(B, case["ctor"]["latent_dim"], generator=g)
+            return (x,), eps
+        H, W = case["hw"]
+        td = case["ctor"]["text_dim"]
+        audio = torch.randn(B, 1, H, W, generator=g)
+        text = torch.randn(B, td, generator=g) / td ** 0.5
+        eps = torch.randn(B, case["ctor"]["latent_dim"], generator=g)
+        if kind == "cvae":
+            C = case["ctor"]["num_classes"]
+            cls = torch.randint(0, C, (B,), generator=g)
+            cond = torch.nn.functional.one_hot(cls, C).float()
+            return (audio, text, cond), eps
+        return (audio, text), eps
+
+    return fn
+
+
+def loss_args(kind, outs, ins):
+    if kind == "simple":
+        recon, mu, logvar, _ = outs
+        return recon, ins[0], mu, logvar
+    ra, rt, mu, logvar = outs
+    return ra, ins[0], rt, ins[1], mu, logvar
+
+
+def encode_args(kind, ins):
+    return ins
+
+
+def _sample_idx(name, numel):
+    rng = np.random.default_rng(zlib.crc32(name.encode()))
+    return rng.integers(0, numel, size=min(N_SAMPLES, numel))
+
+
+def _summ(name, t):
+    a = t.detach().reshape(-1).double().numpy()
+    idx = _sample_idx(name, a.size)
+    row = np.zeros(2 + N_SAMPLES)
+    row[0], row[1] = a.sum(), (a * a).sum()
+    row[2:2 + idx.size] = a[idx]
+    return row
+
+
+def grad_summary(model):
+    return np.stack([_summ(n, p.grad) for n, p in model.named_parameters()])
+
+
+def param_summary(model):
+    return np.stack([_summ(n, p) for n, p in model.named_parameters()])
+
+
+def buffer_summary(model):
+    rows = [_summ(n, b) for n, b in model.named_buffers() if b.dtype.is_floating_point]
+    return np.stack(rows) if rows else np.zeros((0, 2 + N_SAMPLES))
+
+
+def blobs(n, d, k, seed):
+    """Latent-like float32 data: k Gaussian blobs (std 1) around N(0, 3^2) centres."""
+    rng = np.random.default_rng(seed)
+    c = rng.normal(0, 3.0, (k, d))
+    lab = rng.integers(0, k, n)
+    return (c[lab] + rng.normal(0, 1.0, (n, d))).astype(np.float32)

@@ -1,0 +1,292 @@
+// extern "C" boundary of libhlmc (declared in include/hlmc.h).
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "engine.hpp"
+#include "features.hpp"
+
+namespace hlmc {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+const char* get_error() { return g_err.c_str(); }
+
+
+
+}  // namespace hlmc
+
+using namespace hlmc;
+
+struct hlmc_mel_plan {
+    MelPlanImpl* impl;
+    float* d_dct = nullptr;  // DCT-II (ortho) matrix [n_mfcc][n_mels], built on first use
+    int dct_n = 0;
+};
+struct hlmc_net {
+    std::unique_ptr<NetBase> impl;
+};
+
+#define S(stream) reinterpret_cast<hipStream_t>(stream)
+
+extern "C" {
+
+int hlmc_version(void) { return 1; }
+const char* hlmc_last_error(void) { return get_error(); }
+
+// ------------------------------------------------------------------------------------ features
+int hlmc_mel_plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax, hlmc_mel_plan** out) {
+    HLMC_CHECK_ARG(out, "out is NULL");
+    MelPlanImpl* impl = nullptr;
+    HLMC_TRY(feat::plan_create(sr, n_fft, hop, n_mels, fmin, fmax, &impl));
+    auto* p = new hlmc_mel_plan();
+    p->impl = impl;
+    *out = p;
+    return HLMC_OK;
+}
+int hlmc_mel_plan_destroy(hlmc_mel_plan* p) {
+    if (!p) return HLMC_OK;
+    feat::plan_destroy(p->impl);
+    if (p->d_dct) (void)hipFree(p->d_dct);
+    delete p;
+    return HLMC_OK;
+}
+int hlmc_mel_filterbank(const hlmc_mel_plan* p, float* out_host) {
+    HLMC_CHECK_ARG(p && out_host, "NULL argument");
+    std::memcpy(out_host, p->impl->dense.data(), p->impl->dense.size() * sizeof(float));
+    return HLMC_OK;
+}
+int64_t hlmc_mel_frames(const hlmc_mel_plan* p, int64_t n) { return p ? feat::frames(p->impl, n) : -1; }
+int64_t hlmc_mel_workspace(const hlmc_mel_plan* p, int64_t B, int64_t n) { return p ? feat::workspace(p->impl, B, n) : -1; }
+int hlmc_melspectrogram(const hlmc_mel_plan* p, void* stream, const float* pcm, int64_t B, int64_t n, float* out,
+                        void* ws) {
+    HLMC_CHECK_ARG(p, "plan is NULL");
+    return feat::melspectrogram(p->impl, S(stream), pcm, B, n, out, ws);
+}
+int hlmc_mel_db(const hlmc_mel_plan* p, void* stream, const float* pcm, int64_t B, int64_t n, int64_t t_keep, float amin,
+                float top_db, float* out, void* ws) {
+    HLMC_CHECK_ARG(p && t_keep > 0, "bad arguments");
+    return feat::mel_db(p->impl, S(stream), pcm, B, n, t_keep, amin, top_db, out, ws);
+}
+int hlmc_power_to_db(void* stream, const float* S_, int64_t B, int64_t per, int ref_max, float ref_value, float amin,
+                     float top_db, float* out, void* ws) {
+    return feat::power_to_db(S(stream), S_, B, per, ref_max, ref_value, amin, top_db, out, ws);
+}
+int hlmc_mfcc(const hlmc_mel_plan* cp, void* stream, const float* pcm, int64_t B, int64_t n, int n_mfcc, float* out, void* ws) {
+    HLMC_CHECK_ARG(cp, "plan is NULL");
+    auto* p = const_cast<hlmc_mel_plan*>(cp);
+    if (!p->d_dct || p->dct_n != n_mfcc) {
+        const int M = p->impl->n_mels;
+        std::vector<float> D((size_t)n_mfcc * M);
+        for (int k = 0; k < n_mfcc; ++k)
+            for (int m = 0; m < M; ++m) {
+                double c = std::cos(M_PI * k * (2.0 * m + 1) / (2.0 * M)) * std::sqrt(2.0 / M);
+                if (k == 0) c /= std::sqrt(2.0);
+                D[(size_t)k * M + m] = (float)c;
+            }
+        if (p->d_dct) (void)hipFree(p->d_dct);
+        HLMC_HIP(hipMalloc(&p->d_dct, D.size() * sizeof(float)));
+        HLMC_HIP(hipMemcpy(p->d_dct, D.data(), D.size() * sizeof(float), hipMemcpyHostToDevice));
+        p->dct_n = n_mfcc;
+    }
+    return feat::mfcc(p->impl, S(stream), pcm, B, n, n_mfcc, p->d_dct, 1e-10f, 80.f, out, ws);
+}
+int hlmc_row_mean_std(void* stream, const float* x, int64_t rows, int64_t cols, float* mean, float* sd) {
+    return feat::row_mean_std(S(stream), x, rows, cols, mean, sd);
+}
+int64_t hlmc_colstats_workspace(int64_t n, int64_t cols) { return feat::colstats_workspace(n, cols); }
+int hlmc_colstats_sum(void* stream, const float* x, int64_t n, int64_t cols, double* sum, void* ws) {
+    return feat::colstats(S(stream), x, n, cols, nullptr, sum, nullptr, ws);
+}
+int hlmc_colstats_centered(void* stream, const float* x, int64_t n, int64_t cols, const double* mean, double* corr,
+                           double* m2, void* ws) {
+    HLMC_CHECK_ARG(mean && m2, "mean and m2 required");
+    return feat::colstats(S(stream), x, n, cols, mean, corr, m2, ws);
+}
+int hlmc_zscore_apply(void* stream, const float* x, int64_t n, int64_t cols, const double* mean, const double* scale,
+                      int out_dtype, void* out) {
+    return feat::zscore(S(stream), x, n, cols, mean, scale, out_dtype, out);
+}
+
+// ------------------------------------------------------------------------------------ engine
+int hlmc_net_create(int kind, const int64_t* cfg, int ncfg, int dtype, hlmc_net** out) {
+    HLMC_CHECK_ARG(out, "out is NULL");
+    std::unique_ptr<NetBase> n;
+    HLMC_TRY(make_net(kind, cfg, ncfg, dtype, &n));
+    auto* h = new hlmc_net();
+    h->impl = std::move(n);
+    *out = h;
+    return HLMC_OK;
+}
+int hlmc_net_destroy(hlmc_net* n) {
+    delete n;
+    return HLMC_OK;
+}
+int hlmc_net_num_params(const hlmc_net* n) { return n ? (int)n->impl->params.size() : -1; }
+int hlmc_net_param_info(const hlmc_net* n, int i, char* name, int cap, int* ndim, int64_t* shape) {
+    HLMC_CHECK_ARG(n && i >= 0 && i < (int)n->impl->params.size(), "bad parameter index");
+    const ParamInfo& p = n->impl->params[i];
+    if (name && cap > 0) {
+        std::strncpy(name, p.name.c_str(), cap - 1);
+        name[cap - 1] = 0;
+    }
+    if (ndim) *ndim = (int)p.shape.size();
+    if (shape)
+        for (size_t k = 0; k < p.shape.size(); ++k) shape[k] = p.shape[k];
+    return HLMC_OK;
+}
+int hlmc_net_num_bn(const hlmc_net* n) { return n ? n->impl->n_bn : -1; }
+int64_t hlmc_net_state_bytes(const hlmc_net* n) { return n ? (int64_t)n->impl->state_bytes() : -1; }
+int64_t hlmc_net_workspace_bytes(const hlmc_net* n, int64_t batch) {
+    return (n && batch > 0) ? (int64_t)n->impl->ws_bytes(batch) : -1;
+}
+int hlmc_net_bind(hlmc_net* h, float* const* params, float* const* grads, float* const* running, int64_t* const* nbt,
+                  void* state) {
+    HLMC_CHECK_ARG(h && params && grads && running && nbt, "NULL argument");
+    NetBase& n = *h->impl;
+    const size_t np = n.params.size();
+    HLMC_CHECK_ARG(state || n.state_bytes() == 0, "state buffer required");
+    n.P.assign(params, params + np);
+    n.G.assign(grads, grads + np);
+    n.RM.clear();
+    n.RV.clear();
+    for (int i = 0; i < n.n_bn; ++i) {
+        n.RM.push_back(running[2 * i]);
+        n.RV.push_back(running[2 * i + 1]);
+    }
+    n.NBT.assign(nbt, nbt + n.n_bn);
+    for (size_t i = 0; i < np; ++i) HLMC_CHECK_ARG(n.P[i] && n.G[i], "NULL parameter / grad pointer");
+    n.state = reinterpret_cast<char*>(state);
+    return n.bind_state(nullptr);
+}
+int hlmc_net_forward(hlmc_net* h, void* stream, int64_t batch, int train, const float* in0, const float* in1,
+                     const float* in2, const float* eps, const uint8_t* dropout, float* recon, float* recon_text,
+                     float* mu, float* logvar, float* z, void* ws) {
+    HLMC_CHECK_ARG(h && ws && batch > 0, "bad arguments");
+    HLMC_CHECK_ARG(!h->impl->P.empty(), "net is not bound");
+    ForwardArgs a{batch, train, in0, in1, in2, eps, dropout, recon, recon_text, mu, logvar, z, ws, false};
+    return h->impl->forward(S(stream), a);
+}
+int hlmc_net_encode(hlmc_net* h, void* stream, int64_t batch, int train, const float* in0, const float* in1,
+                    const float* in2, float* mu, float* logvar, void* ws) {
+    HLMC_CHECK_ARG(h && ws && batch > 0, "bad arguments");
+    HLMC_CHECK_ARG(!h->impl->P.empty(), "net is not bound");
+    ForwardArgs a{batch, train, in0, in1, in2, nullptr, nullptr, nullptr, nullptr, mu, logvar, nullptr, ws, true};
+    return h->impl->forward(S(stream), a);
+}
+int hlmc_net_backward(hlmc_net* h, void* stream, int64_t batch, const float* d_recon, const float* d_recon_text,
+                      const float* d_mu, const float* d_logvar, void* ws) {
+    HLMC_CHECK_ARG(h && ws && d_recon && d_mu && d_logvar, "bad arguments");
+    BackwardArgs a{batch, d_recon, d_recon_text, d_mu, d_logvar, ws};
+    return h->impl->backward(S(stream), a);
+}
+
+// ------------------------------------------------------------------------------------ loss / optim
+int64_t hlmc_loss_workspace(int64_t na, int64_t nt, int64_t nl) { return (int64_t)ops::vae_sums_ws(na, nt, nl); }
+int hlmc_loss_sums(void* stream, const float* ra, const float* a, int64_t na, const float* rt, const float* t, int64_t nt,
+                   const float* mu, const float* lv, int64_t nl, double* sums3, void* ws) {
+    HLMC_CHECK_ARG(sums3 && ws && (na == 0 || (ra && a)) && (nt == 0 || (rt && t)) && (nl == 0 || (mu && lv)), "bad arguments");
+    return ops::vae_sums(S(stream), ra, a, na, rt, t, nt, mu, lv, nl, sums3,
+                         Ws{reinterpret_cast<float*>(ws), ops::vae_sums_ws(na, nt, nl)});
+}
+int hlmc_loss_backward(void* stream, const float* ra, const float* a, int64_t na, float* dra, const float* rt,
+                       const float* t, int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl,
+                       const float* coef, float* dmu, float* dlv) {
+    HLMC_CHECK_ARG(coef && (na == 0 || (ra && a && dra)) && (nt == 0 || (rt && t && drt)) &&
+                       (nl == 0 || (mu && lv && dmu && dlv)), "bad arguments");
+    return ops::vae_loss_bwd(S(stream), ra, a, na, dra, rt, t, nt, drt, mu, lv, nl, coef, dmu, dlv);
+}
+int64_t hlmc_adam_scratch_bytes(int) { return 0; }
+int hlmc_adam_step(void* stream, int n, float* const* p, const float* const* g, float* const* m, float* const* v,
+                   const int64_t* numel, float lr, float b1, float b2, float eps, float wd, int step, void* scratch) {
+    HLMC_CHECK_ARG(n >= 0 && step >= 1 && p && g && m && v && numel, "bad adam arguments");
+    ops::AdamArgs a{lr, b1, b2, eps, wd, step};
+    return ops::adam(S(stream), n, p, g, m, v, numel, a, scratch);
+}
+
+// ------------------------------------------------------------------------------------ kmeans
+int hlmc_km_center(void* stream, const float* X, int64_t n, int d, float* mean, float* var, float* Xc) {
+    return km::center(S(stream), X, n, d, mean, var, Xc);
+}
+int hlmc_km_sqdist_rows(void* stream, const float* X, int64_t n, int d, const int64_t* cand, int ncand, float* out) {
+    return km::sqdist_rows(S(stream), X, n, d, cand, ncand, out);
+}
+int hlmc_km_assign(void* stream, const float* X, int64_t n, int d, const float* C, int k, int32_t* labels,
+                   const int32_t* old, int32_t* n_changed) {
+    return km::assign(S(stream), X, n, d, C, k, labels, old, n_changed);
+}
+int hlmc_km_sums(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sums, float* w) {
+    return km::sums(S(stream), X, n, d, labels, k, sums, w);
+}
+int hlmc_km_inertia(void* stream, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out,
+                    float* tmp) {
+    return km::inertia(S(stream), X, n, d, C, labels, out, tmp);
+}
+int hlmc_km_rowdist(void* stream, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out) {
+    return km::rowdist(S(stream), X, n, d, C, labels, out);
+}
+
+
+// ------------------------------------------------------------------------------------ op-level entries
+// Individual GEMM-family kernels (the building blocks of hlmc_net_*), exposed for testing and reuse.
+#define DT_DISPATCH(dtype, CALL_F32, CALL_BF16) ((dtype) == HLMC_BF16 ? (CALL_BF16) : (CALL_F32))
+int hlmc_op_conv_s2(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
+                    const float* bias, int Co, void* y, void* ws, int64_t ws_bytes) {
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
+    return DT_DISPATCH(dtype,
+        ops::conv_s2<float>(S(stream), (const float*)x, B, Hi, Wi, Ci, (const float*)wp, bias, Co, (float*)y, w),
+        ops::conv_s2<bf16>(S(stream), (const bf16*)x, B, Hi, Wi, Ci, (const bf16*)wp, bias, Co, (bf16*)y, w));
+}
+int hlmc_op_subpixel(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
+                     const float* bias, int Co, void* y, void* ws, int64_t ws_bytes) {
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
+    return DT_DISPATCH(dtype,
+        ops::subpixel<float>(S(stream), (const float*)x, B, Hi, Wi, Ci, (const float*)wp, bias, Co, (float*)y, w),
+        ops::subpixel<bf16>(S(stream), (const bf16*)x, B, Hi, Wi, Ci, (const bf16*)wp, bias, Co, (bf16*)y, w));
+}
+int hlmc_op_wgrad_s2(void* stream, int dtype, const void* Lo, int B, int Hl, int Wl, int M, const void* Xh, int C,
+                     float* dW, void* ws, int64_t ws_bytes) {
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
+    return DT_DISPATCH(dtype,
+        ops::wgrad_s2<float>(S(stream), (const float*)Lo, B, Hl, Wl, M, (const float*)Xh, C, dW, w),
+        ops::wgrad_s2<bf16>(S(stream), (const bf16*)Lo, B, Hl, Wl, M, (const bf16*)Xh, C, dW, w));
+}
+int hlmc_op_linear(void* stream, int dtype, const void* x, int ldx, int M, int K, const void* wt, int ldw,
+                   const float* bias, int N, void* y, int ldy, int act, int accumulate, int out_f32, void* ws,
+                   int64_t ws_bytes) {
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
+    if (dtype == HLMC_BF16 && out_f32)
+        return ops::linear<bf16, float>(S(stream), (const bf16*)x, ldx, M, K, (const bf16*)wt, ldw, bias, N, (float*)y,
+                                        ldy, act, accumulate, w);
+    if (dtype == HLMC_BF16)
+        return ops::linear<bf16, bf16>(S(stream), (const bf16*)x, ldx, M, K, (const bf16*)wt, ldw, bias, N, (bf16*)y,
+                                       ldy, act, accumulate, w);
+    return ops::linear<float, float>(S(stream), (const float*)x, ldx, M, K, (const float*)wt, ldw, bias, N, (float*)y,
+                                     ldy, act, accumulate, w);
+}
+int hlmc_op_linear_wgrad(void* stream, int dtype, const void* dy, int lddy, const void* x, int ldx, int Mb, int N,
+                         int K, float* dW, void* ws, int64_t ws_bytes) {
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
+    return DT_DISPATCH(dtype,
+        ops::linear_wgrad<float>(S(stream), (const float*)dy, lddy, (const float*)x, ldx, Mb, N, K, dW, w),
+        ops::linear_wgrad<bf16>(S(stream), (const bf16*)dy, lddy, (const bf16*)x, ldx, Mb, N, K, dW, w));
+}
+int hlmc_op_conv_c1_s2(void* stream, int dtype, const float* x, int B, int Hi, int Wi, const float* w,
+                       const float* bias, int Co, void* y) {
+    return DT_DISPATCH(dtype, ops::conv_c1_s2<float>(S(stream), x, B, Hi, Wi, w, bias, Co, (float*)y),
+                       ops::conv_c1_s2<bf16>(S(stream), x, B, Hi, Wi, w, bias, Co, (bf16*)y));
+}
+int hlmc_op_convT_c1(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const float* w,
+                     const float* bias, float* y) {
+    return DT_DISPATCH(dtype, ops::convT_c1<float>(S(stream), (const float*)x, B, Hi, Wi, Ci, w, bias, y),
+                       ops::convT_c1<bf16>(S(stream), (const bf16*)x, B, Hi, Wi, Ci, w, bias, y));
+}
+int hlmc_op_wgrad_c1(void* stream, int dtype, const void* Lo, int B, int Hl, int Wl, int M, const float* Xh,
+                     float* dW, void* ws, int64_t ws_bytes) {
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
+    return DT_DISPATCH(dtype, ops::wgrad_c1<float>(S(stream), (const float*)Lo, B, Hl, Wl, M, Xh, dW, w),
+                       ops::wgrad_c1<bf16>(S(stream), (const bf16*)Lo, B, Hl, Wl, M, Xh, dW, w));
+}
+
+}  // extern "C"

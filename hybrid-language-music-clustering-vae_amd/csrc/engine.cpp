@@ -1,0 +1,976 @@
+// Native VAE engine.  Each reference model is a fixed schedule of libhlmc kernels:
+//   HybridVAE      src/Convolutional_VAE.py:75-185  (+ audio-only variant)
+//   ConditionalVAE src/Conditional_VAE.py:109-231
+//   VAE (Simple)   src/Simple_VAE.py:47-105
+// Activations are NHWC in T (float or bf16), every saved tensor lives in the caller's workspace,
+// parameters are the caller's fp32 tensors (torch registration order), gradients are overwritten.
+#include "engine.hpp"
+
+#include <algorithm>
+#include <climits>
+
+namespace hlmc {
+namespace {
+
+constexpr float kBnEps = 1e-5f;
+constexpr float kBnMomentum = 0.1f;
+constexpr int ENC_CH[7] = {1, 32, 64, 128, 256, 512, 512};
+constexpr int DEC_CH[7] = {512, 512, 256, 128, 64, 32, 1};
+
+inline int pad8(int64_t n) { return (int)((n + 7) & ~int64_t(7)); }
+
+template <typename T>
+class NetT : public NetBase {
+  public:
+    // ---------------------------------------------------------------- packing of GEMM weights
+    struct Pack {
+        int d0 = 0, d1 = 0, taps = 0, ld0 = 0, ld1 = 0;
+        size_t off0 = SIZE_MAX, off1 = SIZE_MAX;
+    };
+    std::vector<Pack> packs;
+    size_t jobs_off = 0, state_size = 0;
+    int64_t pack_max = 0;
+    int njobs = 0;
+
+    void register_pack(int widx, int taps) {
+        if ((int)packs.size() < (int)params.size()) packs.resize(params.size());
+        Pack& p = packs[widx];
+        const auto& sh = params[widx].shape;
+        p.d0 = (int)sh[0];
+        p.d1 = (int)sh[1];
+        p.taps = taps;
+    }
+    void finalize_state() {
+        packs.resize(params.size());
+        Arena A;
+        for (auto& p : packs) {
+            if (!p.taps) continue;
+            p.ld0 = p.taps == 1 ? pad8(p.d1) : p.d1;
+            p.ld1 = p.taps == 1 ? pad8(p.d0) : p.d0;
+            p.off0 = A.take((size_t)p.d0 * p.taps * p.ld0 * sizeof(T));
+            p.off1 = A.take((size_t)p.d1 * p.taps * p.ld1 * sizeof(T));
+            pack_max = std::max<int64_t>(pack_max, (int64_t)p.d0 * p.d1 * p.taps);
+            ++njobs;
+        }
+        jobs_off = A.take(sizeof(ops::PackJob) * std::max(1, njobs));
+        state_size = A.used;
+    }
+    size_t state_bytes() const override { return state_size; }
+    int bind_state(hipStream_t s) override {
+        std::vector<ops::PackJob> jobs;
+        for (size_t i = 0; i < packs.size(); ++i) {
+            const Pack& p = packs[i];
+            if (!p.taps) continue;
+            jobs.push_back({P[i], state + p.off0, state + p.off1, p.d0, p.d1, p.taps, p.ld0, p.ld1});
+        }
+        if (!jobs.empty())
+            HLMC_HIP(hipMemcpyAsync(state + jobs_off, jobs.data(), jobs.size() * sizeof(ops::PackJob), hipMemcpyHostToDevice, s));
+        HLMC_HIP(hipStreamSynchronize(s));
+        return HLMC_OK;
+    }
+    int pack_all(hipStream_t s) {
+        return ops::pack<T>(s, reinterpret_cast<const ops::PackJob*>(state + jobs_off), njobs, pack_max);
+    }
+    T* P0(int w) const { return reinterpret_cast<T*>(state + packs[w].off0); }
+    T* P1(int w) const { return reinterpret_cast<T*>(state + packs[w].off1); }
+    int ld0(int w) const { return packs[w].ld0; }
+    int ld1(int w) const { return packs[w].ld1; }
+
+    // ---------------------------------------------------------------- workspace
+    char* ws = nullptr;
+    Ws scratch{nullptr, 0};
+    size_t scratch_off = 0, scratch_bytes = 0;
+    int64_t planned_B = -1;
+    size_t ws_total = 0;
+
+    T* AT(size_t off) const { return reinterpret_cast<T*>(ws + off); }
+    float* AF(size_t off) const { return reinterpret_cast<float*>(ws + off); }
+    uint8_t* AU8(size_t off) const { return reinterpret_cast<uint8_t*>(ws + off); }
+
+    void need(size_t b) { scratch_bytes = std::max(scratch_bytes, b); }
+
+    virtual void plan(Arena& A, int64_t B) = 0;
+    size_t ws_bytes(int64_t B) override {
+        if (B != planned_B) {
+            Arena A;
+            scratch_bytes = 0;
+            plan(A, B);
+            scratch_off = A.take(scratch_bytes + 256);
+            ws_total = A.used;
+            planned_B = B;
+        }
+        return ws_total;
+    }
+    void set_ws(void* w) {
+        ws = reinterpret_cast<char*>(w);
+        scratch = Ws{reinterpret_cast<float*>(ws + scratch_off), scratch_bytes + 256};
+    }
+
+    // ---------------------------------------------------------------- layer helpers
+    // y = act(x W^T + b)
+    template <typename OutT>
+    int lin_fwd(hipStream_t s, const T* x, int ldx, int B, int w, int b, OutT* y, int ldy, int act, int acc = 0) {
+        const int N = (int)params[w].shape[0], K = (int)params[w].shape[1];
+        return ops::linear<T, OutT>(s, x, ldx, B, K, P0(w), ld0(w), b >= 0 ? P[b] : nullptr, N, y, ldy, act, acc, scratch);
+    }
+    void lin_need(int B, int w) {
+        const int N = (int)params[w].shape[0], K = (int)params[w].shape[1];
+        need(ops::linear_ws<T>(B, K, N));
+        need(ops::linear_ws<T>(B, N, K));
+        need(ops::linear_wgrad_ws<T>(B, N, K));
+        need(ops::colsum_ws(B, N));
+    }
+    // grads of a linear layer from dy (pre-activation grad): dW, db, and optionally dx (+=)
+    int lin_bwd(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int B, int w, int b, T* dx, int lddx, int acc = 0) {
+        const int N = (int)params[w].shape[0], K = (int)params[w].shape[1];
+        HLMC_TRY(ops::linear_wgrad<T>(s, dy, lddy, x, ldx, B, N, K, G[w], scratch));
+        if (b >= 0) HLMC_TRY(ops::colsum<T>(s, dy, lddy, B, N, G[b], scratch));
+        if (dx) HLMC_TRY(ops::linear<T, T>(s, dy, lddy, B, N, P1(w), ld1(w), nullptr, K, dx, lddx, 0, acc, scratch));
+        return HLMC_OK;
+    }
+
+    struct BnBufs {
+        size_t mean = 0, inv = 0;
+    };
+    BnBufs bn_plan(Arena& A, int C) { return BnBufs{A.take(C * 4), A.take(C * 4)}; }
+    int bn_fwd(hipStream_t s, bool train, const T* y, int64_t R, int C, int bn, const BnBufs& bb, int g, int beta, int act,
+               const uint8_t* mask, float mscale, T* a, int lda) {
+        float* mean = AF(bb.mean);
+        float* inv = AF(bb.inv);
+        if (train)
+            HLMC_TRY(ops::bn_stats<T>(s, y, R, C, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps, scratch));
+        else
+            HLMC_TRY(ops::bn_eval_stats(s, RM[bn], RV[bn], C, kBnEps, mean, inv));
+        return ops::bn_act<T>(s, y, R, C, mean, inv, P[g], P[beta], act, mask, mscale, a, lda);
+    }
+    int bn_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const BnBufs& bb, int g, int beta,
+               int act, const uint8_t* mask, float mscale, T* dy, int bias) {
+        return ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask,
+                                  mscale, dy, G[g], G[beta], bias >= 0 ? G[bias] : nullptr, scratch);
+    }
+
+    // ---------------------------------------------------------------- conv encoder (6 x conv-BN-LReLU)
+    struct Enc {
+        int w[6], b[6], g[6], beta[6], bn[6];
+        int H = 0, W = 0;
+        size_t y[6], a[6], audio = 0;
+        BnBufs bb[6];
+    };
+    Enc enc;
+    void enc_register(const std::string& prefix) {
+        for (int l = 0; l < 6; ++l) {
+            const int ci = ENC_CH[l], co = ENC_CH[l + 1];
+            enc.w[l] = add_param(prefix + "." + std::to_string(3 * l) + ".weight", {co, ci, 3, 3});
+            enc.b[l] = add_param(prefix + "." + std::to_string(3 * l) + ".bias", {co});
+            enc.g[l] = add_param(prefix + "." + std::to_string(3 * l + 1) + ".weight", {co});
+            enc.beta[l] = add_param(prefix + "." + std::to_string(3 * l + 1) + ".bias", {co});
+            enc.bn[l] = add_bn();
+            if (l > 0) register_pack(enc.w[l], 9);
+        }
+    }
+    void enc_plan(Arena& A, int64_t B) {
+        int h = enc.H, w = enc.W;
+        enc.audio = A.take((size_t)B * h * w * sizeof(float));
+        for (int l = 0; l < 6; ++l) {
+            const int ci = ENC_CH[l], co = ENC_CH[l + 1];
+            if (l > 0) {
+                need(ops::conv_s2_ws<T>((int)B, h, w, ci, co));
+                need(ops::subpixel_ws<T>((int)B, h / 2, w / 2, co, ci));
+                need(ops::wgrad_s2_ws<T>((int)B, h / 2, w / 2, co, ci));
+            } else {
+                need(ops::wgrad_c1_ws((int)B, h / 2, w / 2, co));
+            }
+            h /= 2;
+            w /= 2;
+            const size_t n = (size_t)B * h * w * co;
+            enc.y[l] = A.take(n * sizeof(T));
+            enc.a[l] = A.take(n * sizeof(T));
+            enc.bb[l] = bn_plan(A, co);
+            need(ops::bn_ws(B * h * w, co));
+        }
+    }
+    size_t enc_max_elems(int64_t B) const { return (size_t)B * (enc.H / 2) * (enc.W / 2) * 32; }
+    int enc_fwd(hipStream_t s, bool train, const float* audio_in, int B) {
+        int h = enc.H, w = enc.W;
+        HLMC_CHECK_ARG(audio_in, "audio input required");
+        // keep the input for the first conv's weight gradient
+        float* audio = AF(enc.audio);
+        HLMC_HIP(hipMemcpyAsync(audio, audio_in, (size_t)B * h * w * sizeof(float), hipMemcpyDeviceToDevice, s));
+        for (int l = 0; l < 6; ++l) {
+            const int ci = ENC_CH[l], co = ENC_CH[l + 1];
+            T* y = AT(enc.y[l]);
+            if (l == 0)
+                HLMC_TRY(ops::conv_c1_s2<T>(s, audio, B, h, w, P[enc.w[0]], P[enc.b[0]], co, y));
+            else
+                HLMC_TRY(ops::conv_s2<T>(s, AT(enc.a[l - 1]), B, h, w, ci, P0(enc.w[l]), P[enc.b[l]], co, y, scratch));
+            h /= 2;
+            w /= 2;
+            HLMC_TRY(bn_fwd(s, train, y, (int64_t)B * h * w, co, enc.bn[l], enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f,
+                            AT(enc.a[l]), co));
+        }
+        return HLMC_OK;
+    }
+    // da5: grad of the last activation in gA; uses gA/gB ping-pong
+    int enc_bwd(hipStream_t s, int B, T* gA, T* gB) {
+        const float* audio = AF(enc.audio);
+        int hs[7], ws_[7];
+        hs[0] = enc.H;
+        ws_[0] = enc.W;
+        for (int l = 0; l < 6; ++l) { hs[l + 1] = hs[l] / 2; ws_[l + 1] = ws_[l] / 2; }
+        for (int l = 5; l >= 0; --l) {
+            const int ci = ENC_CH[l], co = ENC_CH[l + 1];
+            const int ho = hs[l + 1], wo = ws_[l + 1];
+            const int64_t R = (int64_t)B * ho * wo;
+            HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, gB, enc.b[l]));
+            if (l == 0) {
+                HLMC_TRY(ops::wgrad_c1<T>(s, gB, B, ho, wo, co, audio, G[enc.w[0]], scratch));
+            } else {
+                HLMC_TRY(ops::wgrad_s2<T>(s, gB, B, ho, wo, co, AT(enc.a[l - 1]), ci, G[enc.w[l]], scratch));
+                HLMC_TRY(ops::subpixel<T>(s, gB, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));
+            }
+        }
+        return HLMC_OK;
+    }
+
+    // ---------------------------------------------------------------- conv decoder (5 x convT-BN-LReLU + convT)
+    struct Dec {
+        int w[6], b[6], g[5], beta[5], bn[5];
+        int h0 = 0, w0 = 0;  // low-res input grid (H/64, W/64)
+        size_t y[5], a[5];
+        BnBufs bb[5];
+    };
+    Dec dec;
+    // first_index: module index of the first ConvTranspose2d (1 for HybridVAE's Unflatten-led Sequential, 0 for CVAE)
+    void dec_register(const std::string& prefix, int first_index) {
+        for (int l = 0; l < 6; ++l) {
+            const int ci = DEC_CH[l], co = DEC_CH[l + 1];
+            const int mi = first_index + 3 * l;
+            dec.w[l] = add_param(prefix + "." + std::to_string(mi) + ".weight", {ci, co, 3, 3});
+            dec.b[l] = add_param(prefix + "." + std::to_string(mi) + ".bias", {co});
+            if (l < 5) {
+                dec.g[l] = add_param(prefix + "." + std::to_string(mi + 1) + ".weight", {co});
+                dec.beta[l] = add_param(prefix + "." + std::to_string(mi + 1) + ".bias", {co});
+                dec.bn[l] = add_bn();
+                register_pack(dec.w[l], 9);
+            }
+        }
+    }
+    void dec_plan(Arena& A, int64_t B) {
+        int h = dec.h0, w = dec.w0;
+        for (int l = 0; l < 6; ++l) {
+            const int ci = DEC_CH[l], co = DEC_CH[l + 1];
+            if (l < 5) {
+                need(ops::subpixel_ws<T>((int)B, h, w, ci, co));
+                need(ops::conv_s2_ws<T>((int)B, 2 * h, 2 * w, co, ci));
+                need(ops::wgrad_s2_ws<T>((int)B, h, w, ci, co));
+                const size_t n = (size_t)B * 4 * h * w * co;
+                dec.y[l] = A.take(n * sizeof(T));
+                dec.a[l] = A.take(n * sizeof(T));
+                dec.bb[l] = bn_plan(A, co);
+                need(ops::bn_ws(B * 4 * h * w, co));
+            } else {
+                need(ops::wgrad_c1_ws((int)B, h, w, ci));
+                need(ops::colsum_ws((int)(B * 4 * h * w), 1));
+            }
+            h *= 2;
+            w *= 2;
+        }
+    }
+    size_t dec_max_elems(int64_t B) const { return (size_t)B * dec.h0 * 32 * dec.w0 * 32 * 32; }
+    // u: NHWC [B, h0, w0, 512]; recon f32 [B, 64 h0, 64 w0]
+    int dec_fwd(hipStream_t s, bool train, const T* u, int B, float* recon) {
+        int h = dec.h0, w = dec.w0;
+        const T* x = u;
+        for (int l = 0; l < 6; ++l) {
+            const int ci = DEC_CH[l], co = DEC_CH[l + 1];
+            if (l < 5) {
+                T* y = AT(dec.y[l]);
+                HLMC_TRY(ops::subpixel<T>(s, x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co, y, scratch));
+                HLMC_TRY(bn_fwd(s, train, y, (int64_t)B * 4 * h * w, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0,
+                                nullptr, 1.f, AT(dec.a[l]), co));
+                x = AT(dec.a[l]);
+            } else {
+                HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon));
+            }
+            h *= 2;
+            w *= 2;
+        }
+        return HLMC_OK;
+    }
+    // returns grad wrt u in *out (one of gA/gB)
+    int dec_bwd(hipStream_t s, const T* u, int B, const float* d_recon, T* gA, T* gB, T** out) {
+        int hs[7], ws_[7];
+        hs[0] = dec.h0;
+        ws_[0] = dec.w0;
+        for (int l = 0; l < 6; ++l) { hs[l + 1] = hs[l] * 2; ws_[l + 1] = ws_[l] * 2; }
+        // last layer (1 output channel): input a4 [B, hs5, ws5, 32]
+        {
+            const int hl = hs[5], wl = ws_[5];
+            HLMC_TRY(ops::wgrad_c1<T>(s, AT(dec.a[4]), B, hl, wl, DEC_CH[5], d_recon, G[dec.w[5]], scratch));
+            HLMC_TRY(ops::colsum<float>(s, d_recon, 1, B * hs[6] * ws_[6], 1, G[dec.b[5]], scratch));
+            HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA));
+        }
+        for (int l = 4; l >= 0; --l) {
+            const int ci = DEC_CH[l], co = DEC_CH[l + 1];
+            const int hl = hs[l], wl = ws_[l];
+            const int64_t R = (int64_t)B * 4 * hl * wl;
+            HLMC_TRY(bn_bwd(s, gA, co, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f, gB, dec.b[l]));
+            const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
+            HLMC_TRY(ops::wgrad_s2<T>(s, xin, B, hl, wl, ci, gB, co, G[dec.w[l]], scratch));
+            HLMC_TRY(ops::conv_s2<T>(s, gB, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
+        }
+        *out = gA;
+        return HLMC_OK;
+    }
+};
+
+// ============================================================================ HybridVAE
+template <typename T>
+class HybridNet : public NetT<T> {
+    using Base = NetT<T>;
+    using typename Base::BnBufs;
+    using Base::AT;
+    using Base::AF;
+    using Base::AU8;
+    using Base::P;
+    using Base::G;
+
+  public:
+    int L = 128, TD = 768, H = 128, W = 128, F = 0;
+    bool text = true;
+    int afc_w, afc_b, te_w[2], te_b[2], te_g[2], te_beta[2], te_bn[2];
+    int fus_w, fus_b, mu_w, mu_b, lv_w, lv_b, di_w, di_b, ds_w, ds_b, adf_w, adf_b;
+    int td_w[2], td_b[2], td_g, td_beta, td_bn;
+    int FU = 1024, SP = 1024;  // fusion / split widths
+    // workspace
+    size_t flat_, fuse_, tin_, te_y[2], te_a0, h_, mu_, lv_, eps_, z_, d1_, s_, ah_, u_, td_y, td_a, rt_;
+    BnBufs te_bb[2], td_bb;
+    size_t gA_, gB_, gflat_, gfuse_, gh_, gz_, gd1_, gs_, gah_, gte_, gte2_, gtd_, gdmu_, gdlv_, gmuT_, glvT_, grt_;
+    int ldF = 0, ldT = 0, ldFU = 0, ldSP = 0;
+
+    HybridNet(int latent, int text_dim, int h, int w) : L(latent), TD(text_dim), H(h), W(w) {
+        text = text_dim > 0;
+        F = 512 * (H / 64) * (W / 64);
+        FU = text ? 1152 : 1024;
+        SP = FU;
+        this->enc.H = H;
+        this->enc.W = W;
+        this->dec.h0 = H / 64;
+        this->dec.w0 = W / 64;
+        this->enc_register("audio_encoder");
+        afc_w = this->add_param("audio_fc.weight", {1024, F});
+        afc_b = this->add_param("audio_fc.bias", {1024});
+        this->register_pack(afc_w, 1);
+        if (text) {
+            const int dims[3] = {TD, 256, 128};
+            for (int i = 0; i < 2; ++i) {
+                te_w[i] = this->add_param("text_encoder." + std::to_string(3 * i) + ".weight", {dims[i + 1], dims[i]});
+                te_b[i] = this->add_param("text_encoder." + std::to_string(3 * i) + ".bias", {dims[i + 1]});
+                te_g[i] = this->add_param("text_encoder." + std::to_string(3 * i + 1) + ".weight", {dims[i + 1]});
+                te_beta[i] = this->add_param("text_encoder." + std::to_string(3 * i + 1) + ".bias", {dims[i + 1]});
+                te_bn[i] = this->add_bn();
+                this->register_pack(te_w[i], 1);
+            }
+        }
+        fus_w = this->add_param("fc_fusion.weight", {512, FU});
+        fus_b = this->add_param("fc_fusion.bias", {512});
+        mu_w = this->add_param("fc_mu.weight", {L, 512});
+        mu_b = this->add_param("fc_mu.bias", {L});
+        lv_w = this->add_param("fc_logvar.weight", {L, 512});
+        lv_b = this->add_param("fc_logvar.bias", {L});
+        di_w = this->add_param("decoder_input.weight", {512, L});
+        di_b = this->add_param("decoder_input.bias", {512});
+        ds_w = this->add_param("decoder_split.weight", {SP, 512});
+        ds_b = this->add_param("decoder_split.bias", {SP});
+        adf_w = this->add_param("audio_decoder_fc.weight", {F, 1024});
+        adf_b = this->add_param("audio_decoder_fc.bias", {F});
+        for (int w : {fus_w, mu_w, lv_w, di_w, ds_w, adf_w}) this->register_pack(w, 1);
+        this->dec_register("audio_decoder", 1);
+        if (text) {
+            td_w[0] = this->add_param("text_decoder.0.weight", {256, 128});
+            td_b[0] = this->add_param("text_decoder.0.bias", {256});
+            td_g = this->add_param("text_decoder.1.weight", {256});
+            td_beta = this->add_param("text_decoder.1.bias", {256});
+            td_bn = this->add_bn();
+            td_w[1] = this->add_param("text_decoder.3.weight", {TD, 256});
+            td_b[1] = this->add_param("text_decoder.3.bias", {TD});
+            this->register_pack(td_w[0], 1);
+            this->register_pack(td_w[1], 1);
+        }
+        this->finalize_state();
+    }
+
+    void plan(Arena& A, int64_t B) override {
+        ldF = pad8(F);
+        ldT = pad8(TD);
+        ldFU = pad8(FU);
+        ldSP = pad8(SP);
+        this->enc_plan(A, B);
+        this->dec_plan(A, B);
+        const size_t t = sizeof(T);
+        flat_ = A.take(B * ldF * t);
+        fuse_ = A.take(B * ldFU * t);
+        h_ = A.take(B * 512 * t);
+        mu_ = A.take(B * L * 4);
+        lv_ = A.take(B * L * 4);
+        eps_ = A.take(B * L * 4);
+        z_ = A.take(B * L * t);
+        d1_ = A.take(B * 512 * t);
+        s_ = A.take(B * ldSP * t);
+        ah_ = A.take(B * ldF * t);
+        u_ = A.take(B * ldF * t);
+        if (text) {
+            tin_ = A.take(B * ldT * t);
+            te_y[0] = A.take(B * 256 * t);
+            te_a0 = A.take(B * 256 * t);
+            te_y[1] = A.take(B * 128 * t);
+            te_bb[0] = this->bn_plan(A, 256);
+            te_bb[1] = this->bn_plan(A, 128);
+            td_y = A.take(B * 256 * t);
+            td_a = A.take(B * 256 * t);
+            td_bb = this->bn_plan(A, 256);
+            rt_ = A.take(B * ldT * t);
+            gte_ = A.take(B * 256 * t);
+            gte2_ = A.take(B * 256 * t);
+            gtd_ = A.take(B * 256 * t);
+            grt_ = A.take(B * ldT * t);
+            this->need(ops::bn_ws(B, 256));
+            for (int i = 0; i < 2; ++i) this->lin_need((int)B, te_w[i]);
+            this->lin_need((int)B, td_w[0]);
+            this->lin_need((int)B, td_w[1]);
+        }
+        const size_t gmax = std::max(this->enc_max_elems(B), this->dec_max_elems(B));
+        gA_ = A.take(gmax * t);
+        gB_ = A.take(gmax * t);
+        gflat_ = A.take(B * ldF * t);
+        gfuse_ = A.take(B * ldFU * t);
+        gh_ = A.take(B * 512 * t);
+        gz_ = A.take(B * L * t);
+        gd1_ = A.take(B * 512 * t);
+        gs_ = A.take(B * ldSP * t);
+        gah_ = A.take(B * ldF * t);
+        gdmu_ = A.take(B * L * 4);
+        gdlv_ = A.take(B * L * 4);
+        gmuT_ = A.take(B * L * t);
+        glvT_ = A.take(B * L * t);
+        for (int w : {afc_w, fus_w, mu_w, lv_w, di_w, ds_w, adf_w}) this->lin_need((int)B, w);
+        this->need(ops::colsum_ws((int)B, L));
+    }
+
+    int encode(hipStream_t s, const ForwardArgs& a, int B) {
+        const bool tr = a.train != 0;
+        HLMC_TRY(this->enc_fwd(s, tr, a.in0, B));
+        const int hh = H / 64, ww = W / 64;
+        HLMC_TRY(ops::nhwc_to_flat<T>(s, AT(this->enc.a[5]), B, hh, ww, 512, AT(flat_), ldF));
+        HLMC_TRY(this->template lin_fwd<T>(s, AT(flat_), ldF, B, afc_w, afc_b, AT(fuse_), ldFU, 0));
+        if (text) {
+            HLMC_CHECK_ARG(a.in1, "text input required");
+            HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in1, TD, AT(tin_), ldT, B, TD));
+            HLMC_TRY(this->template lin_fwd<T>(s, AT(tin_), ldT, B, te_w[0], te_b[0], AT(te_y[0]), 256, 0));
+            HLMC_TRY(this->bn_fwd(s, tr, AT(te_y[0]), B, 256, te_bn[0], te_bb[0], te_g[0], te_beta[0], 0, nullptr, 1.f,
+                                  AT(te_a0), 256));
+            HLMC_TRY(this->template lin_fwd<T>(s, AT(te_a0), 256, B, te_w[1], te_b[1], AT(te_y[1]), 128, 0));
+            HLMC_TRY(this->bn_fwd(s, tr, AT(te_y[1]), B, 128, te_bn[1], te_bb[1], te_g[1], te_beta[1], 0, nullptr, 1.f,
+                                  AT(fuse_) + 1024, ldFU));
+        }
+        HLMC_TRY(this->template lin_fwd<T>(s, AT(fuse_), ldFU, B, fus_w, fus_b, AT(h_), 512, 1));
+        HLMC_TRY(this->template lin_fwd<float>(s, AT(h_), 512, B, mu_w, mu_b, AF(mu_), L, 0));
+        HLMC_TRY(this->template lin_fwd<float>(s, AT(h_), 512, B, lv_w, lv_b, AF(lv_), L, 0));
+        if (a.mu) HLMC_HIP(hipMemcpyAsync(a.mu, AF(mu_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        if (a.logvar) HLMC_HIP(hipMemcpyAsync(a.logvar, AF(lv_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        return HLMC_OK;
+    }
+
+    int forward(hipStream_t s, const ForwardArgs& a) override {
+        const int B = (int)a.B;
+        HLMC_CHECK_ARG(B >= 2 || !a.train, "BatchNorm in train mode needs batch >= 2");
+        this->ws_bytes(B);
+        this->set_ws(a.ws);
+        HLMC_TRY(this->pack_all(s));
+        HLMC_TRY(encode(s, a, B));
+        if (a.encode_only) return HLMC_OK;
+        HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
+        HLMC_HIP(hipMemcpyAsync(AF(eps_), a.eps, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), L));
+        HLMC_TRY(this->template lin_fwd<T>(s, AT(z_), L, B, di_w, di_b, AT(d1_), 512, 1));
+        HLMC_TRY(this->template lin_fwd<T>(s, AT(d1_), 512, B, ds_w, ds_b, AT(s_), ldSP, 1));
+        HLMC_TRY(this->template lin_fwd<T>(s, AT(s_), ldSP, B, adf_w, adf_b, AT(ah_), ldF, 1));
+        HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(ah_), ldF, B, H / 64, W / 64, 512, AT(u_)));
+        HLMC_TRY(this->dec_fwd(s, a.train != 0, AT(u_), B, a.recon));
+        if (text) {
+            HLMC_CHECK_ARG(a.recon_text, "recon_text required");
+            HLMC_TRY(this->template lin_fwd<T>(s, AT(s_) + 1024, ldSP, B, td_w[0], td_b[0], AT(td_y), 256, 0));
+            HLMC_TRY(this->bn_fwd(s, a.train != 0, AT(td_y), B, 256, td_bn, td_bb, td_g, td_beta, 0, nullptr, 1.f,
+                                  AT(td_a), 256));
+            HLMC_TRY(this->template lin_fwd<float>(s, AT(td_a), 256, B, td_w[1], td_b[1], a.recon_text, TD, 0));
+        }
+        return HLMC_OK;
+    }
+
+    int backward(hipStream_t s, const BackwardArgs& a) override {
+        const int B = (int)a.B;
+        HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
+        this->set_ws(a.ws);
+        T* gA = AT(gA_);
+        T* gB = AT(gB_);
+        // ---- text decoder
+        if (text) {
+            HLMC_CHECK_ARG(a.d_recon_text, "d_recon_text required");
+            HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon_text, TD, AT(grt_), ldT, B, TD));
+            HLMC_TRY(this->lin_bwd(s, AT(grt_), ldT, AT(td_a), 256, B, td_w[1], td_b[1], AT(gtd_), 256));
+            HLMC_TRY(this->bn_bwd(s, AT(gtd_), 256, AT(td_y), B, 256, td_bb, td_g, td_beta, 0, nullptr, 1.f,
+                                  AT(gte2_), td_b[0]));
+            HLMC_TRY(ops::linear_wgrad<T>(s, AT(gte2_), 256, AT(s_) + 1024, ldSP, B, 256, 128, G[td_w[0]], this->scratch));
+            HLMC_TRY(ops::linear<T, T>(s, AT(gte2_), 256, B, 256, this->P1(td_w[0]), this->ld1(td_w[0]), nullptr, 128,
+                                       AT(gs_) + 1024, ldSP, 0, 0, this->scratch));
+        }
+        // ---- audio decoder
+        T* gu = nullptr;
+        HLMC_TRY(this->dec_bwd(s, AT(u_), B, a.d_recon, gA, gB, &gu));
+        HLMC_TRY(ops::nhwc_to_flat<T>(s, gu, B, H / 64, W / 64, 512, AT(gah_), ldF));
+        HLMC_TRY(ops::relu_bwd<T>(s, AT(gah_), ldF, AT(ah_), ldF, B, F));
+        HLMC_TRY(this->lin_bwd(s, AT(gah_), ldF, AT(s_), ldSP, B, adf_w, adf_b, AT(gs_), ldSP));
+        HLMC_TRY(ops::relu_bwd<T>(s, AT(gs_), ldSP, AT(s_), ldSP, B, SP));
+        HLMC_TRY(this->lin_bwd(s, AT(gs_), ldSP, AT(d1_), 512, B, ds_w, ds_b, AT(gd1_), 512));
+        HLMC_TRY(ops::relu_bwd<T>(s, AT(gd1_), 512, AT(d1_), 512, B, 512));
+        HLMC_TRY(this->lin_bwd(s, AT(gd1_), 512, AT(z_), L, B, di_w, di_b, AT(gz_), L));
+        // ---- reparameterisation + heads
+        HLMC_HIP(hipMemcpyAsync(AF(gdmu_), a.d_mu, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_HIP(hipMemcpyAsync(AF(gdlv_), a.d_logvar, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), L, AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
+        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
+        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
+        HLMC_TRY(ops::linear_wgrad<T>(s, AT(gmuT_), L, AT(h_), 512, B, L, 512, G[mu_w], this->scratch));
+        HLMC_TRY(ops::colsum<float>(s, AF(gdmu_), L, B, L, G[mu_b], this->scratch));
+        HLMC_TRY(ops::linear_wgrad<T>(s, AT(glvT_), L, AT(h_), 512, B, L, 512, G[lv_w], this->scratch));
+        HLMC_TRY(ops::colsum<float>(s, AF(gdlv_), L, B, L, G[lv_b], this->scratch));
+        HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, 512, AT(gh_), 512, 0, 0, this->scratch));
+        HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, 512, AT(gh_), 512, 0, 1, this->scratch));
+        HLMC_TRY(ops::relu_bwd<T>(s, AT(gh_), 512, AT(h_), 512, B, 512));
+        HLMC_TRY(this->lin_bwd(s, AT(gh_), 512, AT(fuse_), ldFU, B, fus_w, fus_b, AT(gfuse_), ldFU));
+        // ---- text encoder
+        if (text) {
+            HLMC_TRY(this->bn_bwd(s, AT(gfuse_) + 1024, ldFU, AT(te_y[1]), B, 128, te_bb[1], te_g[1], te_beta[1], 0,
+                                  nullptr, 1.f, AT(gte2_), te_b[1]));
+            HLMC_TRY(this->lin_bwd(s, AT(gte2_), 128, AT(te_a0), 256, B, te_w[1], -1, AT(gte_), 256));
+            HLMC_TRY(this->bn_bwd(s, AT(gte_), 256, AT(te_y[0]), B, 256, te_bb[0], te_g[0], te_beta[0], 0, nullptr, 1.f,
+                                  AT(gte2_), te_b[0]));
+            HLMC_TRY(this->lin_bwd(s, AT(gte2_), 256, AT(tin_), ldT, B, te_w[0], -1, nullptr, 0));
+        }
+        // ---- audio encoder
+        HLMC_TRY(this->lin_bwd(s, AT(gfuse_), ldFU, AT(flat_), ldF, B, afc_w, afc_b, AT(gflat_), ldF));
+        HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(gflat_), ldF, B, H / 64, W / 64, 512, gA));
+        HLMC_TRY(this->enc_bwd(s, B, gA, gB));
+        return HLMC_OK;
+    }
+};
+
+// ============================================================================ ConditionalVAE
+template <typename T>
+class CvaeNet : public NetT<T> {
+    using Base = NetT<T>;
+    using typename Base::BnBufs;
+    using Base::AT;
+    using Base::AF;
+    using Base::AU8;
+    using Base::P;
+    using Base::G;
+
+  public:
+    int L = 64, TD = 768, C = 10, H = 128, W = 128, F = 0;
+    int te_w, te_b, te_g, te_beta, te_bn, mu_w, mu_b, lv_w, lv_b, dfc_w, dfc_b;
+    int td_w[2], td_b[2], td_g, td_beta, td_bn;
+    int ldF = 0, ldT = 0, ldX = 0, ldZ = 0, ldS = 0;
+    size_t tin_, te_y, X_, mu_, lv_, eps_, Z_, S_, u_, td_y, td_a;
+    BnBufs te_bb, td_bb;
+    size_t gA_, gB_, grt_, gtd_, gt2_, gS_, gZ_, gX_, gdmu_, gdlv_, gmuT_, glvT_;
+
+    CvaeNet(int latent, int text_dim, int ncls, int h, int w) : L(latent), TD(text_dim), C(ncls), H(h), W(w) {
+        F = 512 * (H / 64) * (W / 64);
+        this->enc.H = H;
+        this->enc.W = W;
+        this->dec.h0 = H / 64;
+        this->dec.w0 = W / 64;
+        this->enc_register("audio_encoder");
+        te_w = this->add_param("text_encoder.0.weight", {256, TD});
+        te_b = this->add_param("text_encoder.0.bias", {256});
+        te_g = this->add_param("text_encoder.1.weight", {256});
+        te_beta = this->add_param("text_encoder.1.bias", {256});
+        te_bn = this->add_bn();
+        const int fusion = F + 256 + C;
+        mu_w = this->add_param("fc_mu.weight", {L, fusion});
+        mu_b = this->add_param("fc_mu.bias", {L});
+        lv_w = this->add_param("fc_logvar.weight", {L, fusion});
+        lv_b = this->add_param("fc_logvar.bias", {L});
+        dfc_w = this->add_param("decoder_fc.weight", {F + 256, L + C});
+        dfc_b = this->add_param("decoder_fc.bias", {F + 256});
+        td_w[0] = this->add_param("text_decoder.0.weight", {512, 256});
+        td_b[0] = this->add_param("text_decoder.0.bias", {512});
+        td_g = this->add_param("text_decoder.1.weight", {512});
+        td_beta = this->add_param("text_decoder.1.bias", {512});
+        td_bn = this->add_bn();
+        td_w[1] = this->add_param("text_decoder.3.weight", {TD, 512});
+        td_b[1] = this->add_param("text_decoder.3.bias", {TD});
+        for (int w_ : {te_w, mu_w, lv_w, dfc_w, td_w[0], td_w[1]}) this->register_pack(w_, 1);
+        this->dec_register("audio_decoder", 0);
+        this->finalize_state();
+    }
+
+    void plan(Arena& A, int64_t B) override {
+        const size_t t = sizeof(T);
+        ldF = pad8(F);
+        ldT = pad8(TD);
+        ldX = pad8(F + 256 + C);
+        ldZ = pad8(L + C);
+        ldS = pad8(F + 256);
+        this->enc_plan(A, B);
+        this->dec_plan(A, B);
+        tin_ = A.take(B * ldT * t);
+        te_y = A.take(B * 256 * t);
+        te_bb = this->bn_plan(A, 256);
+        X_ = A.take(B * ldX * t);
+        mu_ = A.take(B * L * 4);
+        lv_ = A.take(B * L * 4);
+        eps_ = A.take(B * L * 4);
+        Z_ = A.take(B * ldZ * t);
+        S_ = A.take(B * ldS * t);
+        u_ = A.take(B * ldF * t);
+        td_y = A.take(B * 512 * t);
+        td_a = A.take(B * 512 * t);
+        td_bb = this->bn_plan(A, 512);
+        const size_t gmax = std::max(this->enc_max_elems(B), this->dec_max_elems(B));
+        gA_ = A.take(gmax * t);
+        gB_ = A.take(gmax * t);
+        grt_ = A.take(B * ldT * t);
+        gtd_ = A.take(B * 512 * t);
+        gt2_ = A.take(B * 512 * t);
+        gS_ = A.take(B * ldS * t);
+        gZ_ = A.take(B * ldZ * t);
+        gX_ = A.take(B * ldX * t);
+        gdmu_ = A.take(B * L * 4);
+        gdlv_ = A.take(B * L * 4);
+        gmuT_ = A.take(B * L * t);
+        glvT_ = A.take(B * L * t);
+        for (int w_ : {te_w, mu_w, lv_w, dfc_w, td_w[0], td_w[1]}) this->lin_need((int)B, w_);
+        this->need(ops::bn_ws(B, 512));
+        this->need(ops::colsum_ws((int)B, ldS));
+    }
+
+    int encode(hipStream_t s, const ForwardArgs& a, int B) {
+        const bool tr = a.train != 0;
+        HLMC_CHECK_ARG(a.in1 && a.in2, "text and condition inputs required");
+        HLMC_TRY(this->enc_fwd(s, tr, a.in0, B));
+        HLMC_TRY(ops::nhwc_to_flat<T>(s, AT(this->enc.a[5]), B, H / 64, W / 64, 512, AT(X_), ldX));
+        HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in1, TD, AT(tin_), ldT, B, TD));
+        HLMC_TRY(this->template lin_fwd<T>(s, AT(tin_), ldT, B, te_w, te_b, AT(te_y), 256, 0));
+        HLMC_TRY(this->bn_fwd(s, tr, AT(te_y), B, 256, te_bn, te_bb, te_g, te_beta, 0, nullptr, 1.f, AT(X_) + F, ldX));
+        HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in2, C, AT(X_) + F + 256, ldX, B, C));
+        HLMC_TRY(this->template lin_fwd<float>(s, AT(X_), ldX, B, mu_w, mu_b, AF(mu_), L, 0));
+        HLMC_TRY(this->template lin_fwd<float>(s, AT(X_), ldX, B, lv_w, lv_b, AF(lv_), L, 0));
+        if (a.mu) HLMC_HIP(hipMemcpyAsync(a.mu, AF(mu_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        if (a.logvar) HLMC_HIP(hipMemcpyAsync(a.logvar, AF(lv_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        return HLMC_OK;
+    }
+
+    int forward(hipStream_t s, const ForwardArgs& a) override {
+        const int B = (int)a.B;
+        HLMC_CHECK_ARG(B >= 2 || !a.train, "BatchNorm in train mode needs batch >= 2");
+        this->ws_bytes(B);
+        this->set_ws(a.ws);
+        HLMC_TRY(this->pack_all(s));
+        HLMC_TRY(encode(s, a, B));
+        if (a.encode_only) return HLMC_OK;
+        HLMC_CHECK_ARG(a.eps && a.recon && a.recon_text, "eps / recon / recon_text required");
+        HLMC_HIP(hipMemcpyAsync(AF(eps_), a.eps, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(Z_), ldZ));
+        HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in2, C, AT(Z_) + L, ldZ, B, C));
+        HLMC_TRY(this->template lin_fwd<T>(s, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(S_), ldS, 0));
+        HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(S_), ldS, B, H / 64, W / 64, 512, AT(u_)));
+        HLMC_TRY(this->dec_fwd(s, a.train != 0, AT(u_), B, a.recon));
+        HLMC_TRY(this->template lin_fwd<T>(s, AT(S_) + F, ldS, B, td_w[0], td_b[0], AT(td_y), 512, 0));
+        HLMC_TRY(this->bn_fwd(s, a.train != 0, AT(td_y), B, 512, td_bn, td_bb, td_g, td_beta, 0, nullptr, 1.f, AT(td_a), 512));
+        HLMC_TRY(this->template lin_fwd<float>(s, AT(td_a), 512, B, td_w[1], td_b[1], a.recon_text, TD, 0));
+        return HLMC_OK;
+    }
+
+    int backward(hipStream_t s, const BackwardArgs& a) override {
+        const int B = (int)a.B;
+        HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
+        HLMC_CHECK_ARG(a.d_recon_text, "d_recon_text required");
+        this->set_ws(a.ws);
+        T* gA = AT(gA_);
+        T* gB = AT(gB_);
+        // text decoder
+        HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon_text, TD, AT(grt_), ldT, B, TD));
+        HLMC_TRY(this->lin_bwd(s, AT(grt_), ldT, AT(td_a), 512, B, td_w[1], td_b[1], AT(gtd_), 512));
+        HLMC_TRY(this->bn_bwd(s, AT(gtd_), 512, AT(td_y), B, 512, td_bb, td_g, td_beta, 0, nullptr, 1.f, AT(gt2_), td_b[0]));
+        HLMC_TRY(this->lin_bwd(s, AT(gt2_), 512, AT(S_) + F, ldS, B, td_w[0], -1, AT(gS_) + F, ldS));
+        // audio decoder
+        T* gu = nullptr;
+        HLMC_TRY(this->dec_bwd(s, AT(u_), B, a.d_recon, gA, gB, &gu));
+        HLMC_TRY(ops::nhwc_to_flat<T>(s, gu, B, H / 64, W / 64, 512, AT(gS_), ldS));
+        // decoder_fc (no activation)
+        HLMC_TRY(this->lin_bwd(s, AT(gS_), ldS, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(gZ_), ldZ));
+        // reparameterisation
+        HLMC_HIP(hipMemcpyAsync(AF(gdmu_), a.d_mu, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_HIP(hipMemcpyAsync(AF(gdlv_), a.d_logvar, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gZ_), ldZ, AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
+        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
+        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
+        const int K = F + 256 + C;
+        HLMC_TRY(ops::linear_wgrad<T>(s, AT(gmuT_), L, AT(X_), ldX, B, L, K, G[mu_w], this->scratch));
+        HLMC_TRY(ops::colsum<float>(s, AF(gdmu_), L, B, L, G[mu_b], this->scratch));
+        HLMC_TRY(ops::linear_wgrad<T>(s, AT(glvT_), L, AT(X_), ldX, B, L, K, G[lv_w], this->scratch));
+        HLMC_TRY(ops::colsum<float>(s, AF(gdlv_), L, B, L, G[lv_b], this->scratch));
+        HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, K, AT(gX_), ldX, 0, 0, this->scratch));
+        HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, K, AT(gX_), ldX, 0, 1, this->scratch));
+        // text encoder
+        HLMC_TRY(this->bn_bwd(s, AT(gX_) + F, ldX, AT(te_y), B, 256, te_bb, te_g, te_beta, 0, nullptr, 1.f, AT(gt2_), te_b));
+        HLMC_TRY(this->lin_bwd(s, AT(gt2_), 256, AT(tin_), ldT, B, te_w, -1, nullptr, 0));
+        // audio encoder
+        HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(gX_), ldX, B, H / 64, W / 64, 512, gA));
+        HLMC_TRY(this->enc_bwd(s, B, gA, gB));
+        return HLMC_OK;
+    }
+};
+
+// ============================================================================ Simple VAE (MLP)
+template <typename T>
+class SimpleNet : public NetT<T> {
+    using Base = NetT<T>;
+    using typename Base::BnBufs;
+    using Base::AT;
+    using Base::AF;
+    using Base::AU8;
+    using Base::P;
+    using Base::G;
+
+  public:
+    int D = 370, L = 32;
+    std::vector<int> hid;
+    struct Blk {
+        int w, b, g, beta, bn, din, dout;
+        size_t y, a;
+        BnBufs bb;
+        int64_t mask_off;
+    };
+    std::vector<Blk> encb, decb;
+    int mu_w, mu_b, lv_w, lv_b, out_w, out_b;
+    int ldD = 0;
+    size_t x_, mu_, lv_, eps_, z_, gx1_, gx2_, gdmu_, gdlv_, gmuT_, glvT_, gz_, grec_, mask_;
+    int64_t mask_total = 0;
+
+    SimpleNet(int input_dim, int latent, std::vector<int> hidden) : D(input_dim), L(latent), hid(std::move(hidden)) {
+        int prev = D, mi = 0;
+        for (int h : hid) {
+            Blk b{};
+            b.din = prev;
+            b.dout = h;
+            b.w = this->add_param("encoder." + std::to_string(mi) + ".weight", {h, prev});
+            b.b = this->add_param("encoder." + std::to_string(mi) + ".bias", {h});
+            b.g = this->add_param("encoder." + std::to_string(mi + 1) + ".weight", {h});
+            b.beta = this->add_param("encoder." + std::to_string(mi + 1) + ".bias", {h});
+            b.bn = this->add_bn();
+            this->register_pack(b.w, 1);
+            encb.push_back(b);
+            prev = h;
+            mi += 4;
+        }
+        mu_w = this->add_param("fc_mu.weight", {L, prev});
+        mu_b = this->add_param("fc_mu.bias", {L});
+        lv_w = this->add_param("fc_logvar.weight", {L, prev});
+        lv_b = this->add_param("fc_logvar.bias", {L});
+        this->register_pack(mu_w, 1);
+        this->register_pack(lv_w, 1);
+        prev = L;
+        mi = 0;
+        for (int i = (int)hid.size() - 1; i >= 0; --i) {
+            const int h = hid[i];
+            Blk b{};
+            b.din = prev;
+            b.dout = h;
+            b.w = this->add_param("decoder." + std::to_string(mi) + ".weight", {h, prev});
+            b.b = this->add_param("decoder." + std::to_string(mi) + ".bias", {h});
+            b.g = this->add_param("decoder." + std::to_string(mi + 1) + ".weight", {h});
+            b.beta = this->add_param("decoder." + std::to_string(mi + 1) + ".bias", {h});
+            b.bn = this->add_bn();
+            this->register_pack(b.w, 1);
+            decb.push_back(b);
+            prev = h;
+            mi += 4;
+        }
+        out_w = this->add_param("decoder." + std::to_string(mi) + ".weight", {D, prev});
+        out_b = this->add_param("decoder." + std::to_string(mi) + ".bias", {D});
+        this->register_pack(out_w, 1);
+        this->finalize_state();
+    }
+
+    void plan(Arena& A, int64_t B) override {
+        const size_t t = sizeof(T);
+        ldD = pad8(D);
+        x_ = A.take(B * ldD * t);
+        int64_t moff = 0;
+        int widest = ldD;
+        for (auto* v : {&encb, &decb})
+            for (auto& b : *v) {
+                b.y = A.take(B * b.dout * t);
+                b.a = A.take(B * b.dout * t);
+                b.bb = this->bn_plan(A, b.dout);
+                b.mask_off = moff;
+                moff += B * b.dout;
+                widest = std::max(widest, pad8(b.dout));
+                this->lin_need((int)B, b.w);
+                this->need(ops::bn_ws(B, b.dout));
+            }
+        mask_total = moff;
+        mask_ = A.take((size_t)moff);
+        mu_ = A.take(B * L * 4);
+        lv_ = A.take(B * L * 4);
+        eps_ = A.take(B * L * 4);
+        z_ = A.take(B * pad8(L) * t);
+        gx1_ = A.take(B * widest * t);
+        gx2_ = A.take(B * widest * t);
+        gdmu_ = A.take(B * L * 4);
+        gdlv_ = A.take(B * L * 4);
+        gmuT_ = A.take(B * L * t);
+        glvT_ = A.take(B * L * t);
+        gz_ = A.take(B * pad8(L) * t);
+        grec_ = A.take(B * ldD * t);
+        for (int w_ : {mu_w, lv_w, out_w}) this->lin_need((int)B, w_);
+    }
+
+    const uint8_t* mask_of(const Blk& b) const { return dropout ? dropout + b.mask_off : nullptr; }
+    const uint8_t* dropout = nullptr;
+    static constexpr float kKeepScale = 1.f / 0.8f;  // Dropout(0.2)
+
+    int encode(hipStream_t s, const ForwardArgs& a, int B) {
+        const bool tr = a.train != 0;
+        dropout = nullptr;
+        if (tr && a.dropout) {
+            HLMC_HIP(hipMemcpyAsync(AU8(mask_), a.dropout, (size_t)mask_total, hipMemcpyDeviceToDevice, s));
+            dropout = AU8(mask_);
+        }
+        HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in0, D, AT(x_), ldD, B, D));
+        const T* x = AT(x_);
+        int ldx = ldD;
+        for (auto& b : encb) {
+            HLMC_TRY(this->template lin_fwd<T>(s, x, ldx, B, b.w, b.b, AT(b.y), b.dout, 0));
+            HLMC_TRY(this->bn_fwd(s, tr, AT(b.y), B, b.dout, b.bn, b.bb, b.g, b.beta, 1, mask_of(b), kKeepScale,
+                                  AT(b.a), b.dout));
+            x = AT(b.a);
+            ldx = b.dout;
+        }
+        HLMC_TRY(this->template lin_fwd<float>(s, x, ldx, B, mu_w, mu_b, AF(mu_), L, 0));
+        HLMC_TRY(this->template lin_fwd<float>(s, x, ldx, B, lv_w, lv_b, AF(lv_), L, 0));
+        if (a.mu) HLMC_HIP(hipMemcpyAsync(a.mu, AF(mu_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        if (a.logvar) HLMC_HIP(hipMemcpyAsync(a.logvar, AF(lv_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        return HLMC_OK;
+    }
+
+    int forward(hipStream_t s, const ForwardArgs& a) override {
+        const int B = (int)a.B;
+        HLMC_CHECK_ARG(B >= 2 || !a.train, "BatchNorm in train mode needs batch >= 2");
+        this->ws_bytes(B);
+        this->set_ws(a.ws);
+        HLMC_TRY(this->pack_all(s));
+        HLMC_TRY(encode(s, a, B));
+        if (a.encode_only) return HLMC_OK;
+        HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
+        HLMC_HIP(hipMemcpyAsync(AF(eps_), a.eps, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), pad8(L)));
+        if (a.z) HLMC_TRY(ops::reparam_fwd<float>(s, AF(mu_), AF(lv_), AF(eps_), B, L, a.z, L));
+        const T* x = AT(z_);
+        int ldx = pad8(L);
+        for (auto& b : decb) {
+            HLMC_TRY(this->template lin_fwd<T>(s, x, ldx, B, b.w, b.b, AT(b.y), b.dout, 0));
+            HLMC_TRY(this->bn_fwd(s, a.train != 0, AT(b.y), B, b.dout, b.bn, b.bb, b.g, b.beta, 1, mask_of(b), kKeepScale,
+                                  AT(b.a), b.dout));
+            x = AT(b.a);
+            ldx = b.dout;
+        }
+        HLMC_TRY(this->template lin_fwd<float>(s, x, ldx, B, out_w, out_b, a.recon, D, 0));
+        return HLMC_OK;
+    }
+
+    int backward(hipStream_t s, const BackwardArgs& a) override {
+        const int B = (int)a.B;
+        HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
+        this->set_ws(a.ws);
+        T* g1 = AT(gx1_);
+        T* g2 = AT(gx2_);
+        HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon, D, AT(grec_), ldD, B, D));
+        const Blk& last = decb.back();
+        HLMC_TRY(this->lin_bwd(s, AT(grec_), ldD, AT(last.a), last.dout, B, out_w, out_b, g1, last.dout));
+        for (int i = (int)decb.size() - 1; i >= 0; --i) {
+            const Blk& b = decb[i];
+            HLMC_TRY(this->bn_bwd(s, g1, b.dout, AT(b.y), B, b.dout, b.bb, b.g, b.beta, 1, mask_of(b), kKeepScale, g2, b.b));
+            const T* xin = i == 0 ? AT(z_) : AT(decb[i - 1].a);
+            const int ldx = i == 0 ? pad8(L) : decb[i - 1].dout;
+            T* gin = i == 0 ? AT(gz_) : g1;
+            const int ldg = i == 0 ? pad8(L) : b.din;
+            HLMC_TRY(this->lin_bwd(s, g2, b.dout, xin, ldx, B, b.w, -1, gin, ldg));
+        }
+        HLMC_HIP(hipMemcpyAsync(AF(gdmu_), a.d_mu, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_HIP(hipMemcpyAsync(AF(gdlv_), a.d_logvar, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), pad8(L), AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
+        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
+        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
+        const Blk& top = encb.back();
+        HLMC_TRY(ops::linear_wgrad<T>(s, AT(gmuT_), L, AT(top.a), top.dout, B, L, top.dout, G[mu_w], this->scratch));
+        HLMC_TRY(ops::colsum<float>(s, AF(gdmu_), L, B, L, G[mu_b], this->scratch));
+        HLMC_TRY(ops::linear_wgrad<T>(s, AT(glvT_), L, AT(top.a), top.dout, B, L, top.dout, G[lv_w], this->scratch));
+        HLMC_TRY(ops::colsum<float>(s, AF(gdlv_), L, B, L, G[lv_b], this->scratch));
+        HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, top.dout, g1, top.dout, 0, 0, this->scratch));
+        HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, top.dout, g1, top.dout, 0, 1, this->scratch));
+        for (int i = (int)encb.size() - 1; i >= 0; --i) {
+            const Blk& b = encb[i];
+            HLMC_TRY(this->bn_bwd(s, g1, b.dout, AT(b.y), B, b.dout, b.bb, b.g, b.beta, 1, mask_of(b), kKeepScale, g2, b.b));
+            const T* xin = i == 0 ? AT(x_) : AT(encb[i - 1].a);
+            const int ldx = i == 0 ? ldD : encb[i - 1].dout;
+            HLMC_TRY(this->lin_bwd(s, g2, b.dout, xin, ldx, B, b.w, -1, i == 0 ? nullptr : g1, b.din));
+        }
+        return HLMC_OK;
+    }
+};
+
+template <template <typename> class NetTpl, typename... A>
+std::unique_ptr<NetBase> make_typed(int dtype, A... args) {
+    if (dtype == HLMC_BF16) return std::unique_ptr<NetBase>(new NetTpl<bf16>(args...));
+    return std::unique_ptr<NetBase>(new NetTpl<float>(args...));
+}
+
+}  // namespace
+
+int make_net(int kind, const int64_t* cfg, int ncfg, int dtype, std::unique_ptr<NetBase>* out) {
+    HLMC_CHECK_ARG(dtype == HLMC_F32 || dtype == HLMC_BF16, "dtype must be HLMC_F32 or HLMC_BF16");
+    HLMC_CHECK_ARG(cfg != nullptr, "cfg is NULL");
+    std::unique_ptr<NetBase> n;
+    if (kind == HLMC_NET_HYBRID) {
+        HLMC_CHECK_ARG(ncfg == 4, "hybrid cfg = {latent, text_dim, H, W}");
+        HLMC_CHECK_ARG(cfg[2] % 64 == 0 && cfg[3] % 64 == 0 && cfg[2] >= 64 && cfg[3] >= 64, "H, W must be multiples of 64");
+        HLMC_CHECK_ARG(cfg[0] > 0 && cfg[1] >= 0, "latent > 0, text_dim >= 0");
+        n = make_typed<HybridNet>(dtype, (int)cfg[0], (int)cfg[1], (int)cfg[2], (int)cfg[3]);
+    } else if (kind == HLMC_NET_CVAE) {
+        HLMC_CHECK_ARG(ncfg == 5, "cvae cfg = {latent, text_dim, num_classes, H, W}");
+        HLMC_CHECK_ARG(cfg[3] % 64 == 0 && cfg[4] % 64 == 0 && cfg[3] >= 64 && cfg[4] >= 64, "H, W must be multiples of 64");
+        HLMC_CHECK_ARG(cfg[0] > 0 && cfg[1] > 0 && cfg[2] > 0, "latent, text_dim, num_classes > 0");
+        n = make_typed<CvaeNet>(dtype, (int)cfg[0], (int)cfg[1], (int)cfg[2], (int)cfg[3], (int)cfg[4]);
+    } else if (kind == HLMC_NET_SIMPLE) {
+        HLMC_CHECK_ARG(ncfg >= 3 && cfg[2] >= 1 && ncfg == 3 + cfg[2], "simple cfg = {input_dim, latent, n, h_1..h_n}");
+        std::vector<int> hid;
+        for (int i = 0; i < cfg[2]; ++i) {
+            const int v = dtype == HLMC_BF16 ? 8 : 4;
+            HLMC_CHECK_ARG(cfg[3 + i] % v == 0, "hidden widths must be multiples of the vector width (8 bf16 / 4 f32)");
+            hid.push_back((int)cfg[3 + i]);
+        }
+        n = make_typed<SimpleNet>(dtype, (int)cfg[0], (int)cfg[1], hid);
+    } else {
+        HLMC_CHECK_ARG(false, "unknown net kind");
+    }
+    n->kind = kind;
+    n->dtype = dtype;
+    *out = std::move(n);
+    return HLMC_OK;
+}
+
+}  // namespace hlmc

@@ -1,0 +1,85 @@
+// Native VAE engine: the three reference model families as fixed kernel schedules.
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ops.hpp"
+
+namespace hlmc {
+
+struct ParamInfo {
+    std::string name;
+    std::vector<int64_t> shape;
+    int64_t numel() const {
+        int64_t n = 1;
+        for (auto d : shape) n *= d;
+        return n;
+    }
+};
+
+// Bump allocator over a caller-provided device buffer (offsets only; 256-byte aligned).
+struct Arena {
+    size_t used = 0;
+    size_t take(size_t bytes) {
+        size_t o = used;
+        used += (bytes + 255) & ~size_t(255);
+        return o;
+    }
+};
+
+struct ForwardArgs {
+    int64_t B;
+    int train;
+    const float* in0;
+    const float* in1;
+    const float* in2;
+    const float* eps;
+    const uint8_t* dropout;
+    float* recon;
+    float* recon_text;
+    float* mu;
+    float* logvar;
+    float* z;
+    void* ws;
+    bool encode_only;
+};
+
+struct BackwardArgs {
+    int64_t B;
+    const float* d_recon;
+    const float* d_recon_text;
+    const float* d_mu;
+    const float* d_logvar;
+    void* ws;
+};
+
+class NetBase {
+  public:
+    virtual ~NetBase() = default;
+    int kind = 0, dtype = 0;
+    std::vector<ParamInfo> params;
+    int n_bn = 0;
+
+    // bound storage
+    std::vector<float*> P, G, RM, RV;
+    std::vector<int64_t*> NBT;
+    char* state = nullptr;
+
+    int add_param(const std::string& name, std::vector<int64_t> shape) {
+        params.push_back({name, std::move(shape)});
+        return (int)params.size() - 1;
+    }
+    int add_bn() { return n_bn++; }
+
+    virtual size_t state_bytes() const = 0;
+    virtual size_t ws_bytes(int64_t B) = 0;
+    virtual int bind_state(hipStream_t s) = 0;  // upload pack jobs into state
+    virtual int forward(hipStream_t s, const ForwardArgs& a) = 0;
+    virtual int backward(hipStream_t s, const BackwardArgs& a) = 0;
+};
+
+// factory: kind 0 hybrid, 1 cvae, 2 simple; cfg per hlmc.h
+int make_net(int kind, const int64_t* cfg, int ncfg, int dtype, std::unique_ptr<NetBase>* out);
+
+}  // namespace hlmc

@@ -1,0 +1,55 @@
+// Internal declarations of the feature (mel / MFCC / scaler) and K-Means kernels.
+#pragma once
+#include <vector>
+
+#include "ops.hpp"
+
+namespace hlmc {
+
+struct MelPlanImpl {
+    int sr, n_fft, hop, n_mels;
+    double fmin, fmax;
+    int nbins;                       // 1 + n_fft/2
+    std::vector<float> dense;        // [n_mels][nbins] (host copy, librosa.filters.mel)
+    // device tables
+    float* d_window = nullptr;       // [n_fft]
+    float2* d_tw = nullptr;          // [n_fft/2]   e^{-2 pi i k / (n_fft/2)}
+    float2* d_rtw = nullptr;         // [n_fft/2+1] e^{-2 pi i f / n_fft}
+    int* d_band = nullptr;           // [n_mels][2] first bin, count
+    int* d_woff = nullptr;           // [n_mels] offset into d_w
+    float* d_w = nullptr;            // packed weights
+    int max_band = 0;
+    int nnz = 0;
+};
+
+namespace feat {
+int plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax, MelPlanImpl** out);
+void plan_destroy(MelPlanImpl* p);
+int64_t frames(const MelPlanImpl* p, int64_t n);
+int64_t workspace(const MelPlanImpl* p, int64_t B, int64_t n);
+int melspectrogram(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, float* out, void* ws);
+int mel_db(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, int64_t t_keep, float amin,
+           float top_db, float* out, void* ws);
+int mfcc(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, int n_mfcc, const float* dct,
+         float amin, float top_db, float* out, void* ws);
+int power_to_db(hipStream_t s, const float* S, int64_t B, int64_t per, int ref_max, float ref_value, float amin,
+                float top_db, float* out, void* ws);
+int row_mean_std(hipStream_t s, const float* x, int64_t rows, int64_t cols, float* mean, float* sd);
+int64_t colstats_workspace(int64_t n, int64_t cols);
+int colstats(hipStream_t s, const float* x, int64_t n, int64_t cols, const double* mean, double* o0, double* o1, void* ws);
+int zscore(hipStream_t s, const float* x, int64_t n, int64_t cols, const double* mean, const double* scale, int dtype,
+           void* out);
+}  // namespace feat
+
+namespace km {
+int center(hipStream_t s, const float* X, int64_t n, int d, float* mean, float* var, float* Xc);
+int sqdist_rows(hipStream_t s, const float* X, int64_t n, int d, const int64_t* cand, int ncand, float* out);
+int assign(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, int32_t* labels, const int32_t* old,
+           int32_t* n_changed);
+int sums(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w);
+int inertia(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out,
+            float* tmp);
+int rowdist(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out);
+}  // namespace km
+
+}  // namespace hlmc

@@ -1,0 +1,452 @@
+// MFMA GEMM main loops for the VAE hot path (gfx950).
+//
+//   gemm_nt : C[m][n] = sum_k A(m,k) * B(n,k)   A gathered by a loader policy (conv stride-2 window,
+//             transposed-conv sub-pixel phase, dense row-major), B = packed weight [N][K] (K contiguous).
+//   gemm_tn : C[m][n] = sum_k L(k,m) * H(k,n)   both operands k-major (weight gradients); fragments are
+//             read with ds_read_b64_tr_b16 (bf16) so no transposed staging is needed.
+//
+// T = bf16 -> v_mfma_f32_16x16x32_bf16 (f32 accumulate), BK = 32
+// T = float -> v_mfma_f32_16x16x4_f32 (exact f32 fma chain), BK = 16
+// Every k-row of a tile is 64 bytes (4 x 16-byte chunks); LDS rows are padded to 80 bytes.
+// 256 threads = 4 waves; each wave owns a WM x WN sub-tile of 16x16 MFMA tiles.
+#pragma once
+#include "common.hpp"
+
+namespace hlmc {
+
+// ============================================================================ A / B loaders (NT)
+// A loader contract:  set_phase(p); int K() const; uint4 load(int m, int k) (16 bytes, zero-filled OOB)
+
+template <typename T>
+struct DenseLoader {  // X[m * ld + k], m < M, k < K
+    const T* p;
+    int ld, M, Kd;
+    bool vec;  // ld % VEC == 0 and K % VEC == 0 and p 16B aligned
+    __device__ void set_phase(int) {}
+    __device__ int K() const { return Kd; }
+    __device__ uint4 load(int m, int k) const {
+        constexpr int V = Vec16<T>::N;
+        if (m >= M) return make_uint4(0, 0, 0, 0);
+        const T* r = p + (int64_t)m * ld;
+        if (vec && k + V <= Kd) return *reinterpret_cast<const uint4*>(r + k);
+        union { uint4 u; T e[V]; } x;
+#pragma unroll
+        for (int i = 0; i < V; ++i) x.e[i] = (k + i < Kd) ? r[k + i] : from_f32<T>(0.f);
+        return x.u;
+    }
+};
+
+// Stride-2, pad-1, 3x3 window gather over an NHWC map: A(m = (b,oh,ow), k = (kh,kw,ci))
+//   = X[b, 2oh-1+kh, 2ow-1+kw, ci].  Requires C % (4*VEC) == 0 (a BK chunk never straddles taps).
+template <typename T>
+struct ConvS2Loader {
+    const T* x;
+    int Hi, Wi, C, Ho, Wo, M;
+    __device__ void set_phase(int) {}
+    __device__ int K() const { return 9 * C; }
+    __device__ uint4 load(int m, int k) const {
+        if (m >= M) return make_uint4(0, 0, 0, 0);
+        int ow = m % Wo, t = m / Wo;
+        int oh = t % Ho, b = t / Ho;
+        int tap = k / C, ci = k - tap * C;
+        int kh = tap / 3, kw = tap - kh * 3;
+        int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
+        if ((unsigned)ih >= (unsigned)Hi || (unsigned)iw >= (unsigned)Wi) return make_uint4(0, 0, 0, 0);
+        return *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * Wi + iw) * C + ci);
+    }
+};
+
+// Sub-pixel phase of a stride-2 transposed 3x3 conv (pad 1, output_padding 1) / of the stride-2
+// conv's data gradient.  Output pixel (2r+py, 2c+px) gathers low-res X[b, r+dr, c+dc, ci] over taps:
+//   parity 0 -> {kh=1, dr=0};  parity 1 -> {kh=0, dr=+1}, {kh=2, dr=0}.
+__device__ __forceinline__ int sp_ntaps(int par) { return par ? 2 : 1; }
+__device__ __forceinline__ int sp_kidx(int par, int t) { return par ? (t ? 2 : 0) : 1; }
+__device__ __forceinline__ int sp_delta(int par, int t) { return (par && t == 0) ? 1 : 0; }
+
+template <typename T>
+struct SubpixelLoader {
+    const T* x;  // low-res NHWC [B, Hi, Wi, C]
+    int Hi, Wi, C, M;  // M = B*Hi*Wi
+    int py, px, ntx, Kd;
+    __device__ void set_phase(int p) {
+        py = p >> 1; px = p & 1;
+        ntx = sp_ntaps(px);
+        Kd = sp_ntaps(py) * ntx * C;
+    }
+    __device__ int K() const { return Kd; }
+    __device__ uint4 load(int m, int k) const {
+        if (m >= M) return make_uint4(0, 0, 0, 0);
+        int c = m % Wi, t = m / Wi;
+        int r = t % Hi, b = t / Hi;
+        int tt = k / C, ci = k - tt * C;
+        int ty = tt / ntx, tx = tt - ty * ntx;
+        int ih = r + sp_delta(py, ty), iw = c + sp_delta(px, tx);
+        if (ih >= Hi || iw >= Wi) return make_uint4(0, 0, 0, 0);
+        return *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * Wi + iw) * C + ci);
+    }
+};
+
+// B operand for a sub-pixel phase: packed P[n][kh][kw][C]; k = (ty,tx,ci) -> tap (kh,kw) of the phase.
+template <typename T>
+struct SubpixelWeight {
+    const T* w;
+    int C, N;
+    int py, px, ntx, Kd;
+    __device__ void set_phase(int p) {
+        py = p >> 1; px = p & 1;
+        ntx = sp_ntaps(px);
+        Kd = sp_ntaps(py) * ntx * C;
+    }
+    __device__ int K() const { return Kd; }
+    __device__ uint4 load(int n, int k) const {
+        if (n >= N) return make_uint4(0, 0, 0, 0);
+        int tt = k / C, ci = k - tt * C;
+        int ty = tt / ntx, tx = tt - ty * ntx;
+        int kh = sp_kidx(py, ty), kw = sp_kidx(px, tx);
+        return *reinterpret_cast<const uint4*>(w + ((int64_t)n * 9 + kh * 3 + kw) * C + ci);
+    }
+};
+
+// ============================================================================ epilogues
+// Row-major store with bias, activation, optional accumulate:  out[m*ld + n] (+)= act(v + bias[n])
+// act: 0 none, 1 relu
+template <typename OutT>
+struct StoreRM {
+    OutT* out;
+    const float* bias;
+    int ld, act, accumulate;
+    __device__ void set_phase(int) {}
+    __device__ void store(int m, int n, float v) const {
+        if (bias) v += bias[n];
+        if (act == 1) v = v > 0.f ? v : 0.f;
+        OutT* o = out + (int64_t)m * ld + n;
+        if (accumulate) v += to_f32<OutT>(*o);
+        *o = from_f32<OutT>(v);
+    }
+};
+
+// Sub-pixel phase store into a high-res NHWC map [B, 2Hi, 2Wi, N]; m = (b, r, c) over the low grid.
+template <typename OutT>
+struct StoreSubpixel {
+    OutT* out;
+    const float* bias;
+    int Hi, Wi, N;
+    int py, px;
+    __device__ void set_phase(int p) { py = p >> 1; px = p & 1; }
+    __device__ void store(int m, int n, float v) const {
+        int c = m % Wi, t = m / Wi;
+        int r = t % Hi, b = t / Hi;
+        if (bias) v += bias[n];
+        int64_t pix = ((int64_t)b * 2 * Hi + 2 * r + py) * (2 * Wi) + 2 * c + px;
+        out[pix * N + n] = from_f32<OutT>(v);
+    }
+};
+
+// Split-K partial slab: ws[((phase * S + split) * M + m) * N + n]
+struct StorePartial {
+    float* ws;
+    int M, N, S;
+    int phase, split;
+    __device__ void set_phase(int p) { phase = p; }
+    __device__ void store(int m, int n, float v) const {
+        ws[(((int64_t)phase * S + split) * M + m) * N + n] = v;
+    }
+};
+
+// ============================================================================ NT main loop
+template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len) {
+    constexpr int V = Vec16<T>::N;
+    constexpr int BK = 4 * V;
+    constexpr int BKP = BK + V;  // 80-byte rows
+    constexpr int WAVES_N = BN / WN;
+    static_assert((BM / WM) * WAVES_N == 4, "4 waves per block");
+    constexpr int TM = WM / 16, TN = WN / 16;
+    constexpr int ACH = BM * 4, BCH = BN * 4;           // 16-byte chunks per tile
+    constexpr int AR = (ACH + 255) / 256, BR = (BCH + 255) / 256;
+    __shared__ __attribute__((aligned(16))) T As[2][BM * BKP];
+    __shared__ __attribute__((aligned(16))) T Bs[2][BN * BKP];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
+    const int tiles_n = (N + BN - 1) / BN;
+    const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
+    const int phase = blockIdx.y;
+    al.set_phase(phase); bl.set_phase(phase); ep.set_phase(phase);
+    const int K = al.K();
+    const int kb = blockIdx.z * ksplit_len;
+    const int ke = min(K, kb + ksplit_len);
+
+    f32x4_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    uint4 ra[AR], rb[BR];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+            int c = tid + i * 256;
+            if (c < ACH) ra[i] = al.load(m0 + (c >> 2), k0 + (c & 3) * V);
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+            int c = tid + i * 256;
+            if (c < BCH) rb[i] = bl.load(n0 + (c >> 2), k0 + (c & 3) * V);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+            int c = tid + i * 256;
+            if (c < ACH) *reinterpret_cast<uint4*>(&As[buf][(c >> 2) * BKP + (c & 3) * V]) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+            int c = tid + i * 256;
+            if (c < BCH) *reinterpret_cast<uint4*>(&Bs[buf][(c >> 2) * BKP + (c & 3) * V]) = rb[i];
+        }
+    };
+
+    if (kb < ke) {
+        gload(kb);
+        lstore(0);
+        __syncthreads();
+        int it = 0;
+        for (int k0 = kb; k0 < ke; k0 += BK, ++it) {
+            const int cur = it & 1;
+            const bool more = k0 + BK < ke;
+            if (more) gload(k0 + BK);
+            const T* A = As[cur];
+            const T* B = Bs[cur];
+            if constexpr (sizeof(T) == 2) {
+                bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    af[i] = *reinterpret_cast<const bf16x8_t*>(&A[(wm0 + i * 16 + (lane & 15)) * BKP + (lane >> 4) * 8]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    bfr[j] = *reinterpret_cast<const bf16x8_t*>(&B[(wn0 + j * 16 + (lane & 15)) * BKP + (lane >> 4) * 8]);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    float af[TM], bfr[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) af[i] = A[(wm0 + i * 16 + (lane & 15)) * BKP + s * 4 + (lane >> 4)];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) bfr[j] = B[(wn0 + j * 16 + (lane & 15)) * BKP + s * 4 + (lane >> 4)];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                }
+            }
+            if (more) lstore(cur ^ 1);
+            __syncthreads();
+        }
+    }
+    // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
+                int n = n0 + wn0 + j * 16 + (lane & 15);
+                if (m < M && n < N) ep.store(m, n, acc[i][j][r]);
+            }
+}
+
+// Split-K wrapper epilogue: the z-index of the grid selects the partial slab.
+struct StorePartialZ : StorePartial {
+    __device__ void set_phase(int p) { phase = p; split = blockIdx.z; }
+};
+
+// Reduce split-K partials (fixed order => deterministic) then apply the final epilogue.
+template <class EP>
+__global__ void splitk_reduce_kernel(const float* ws, EP ep, int M, int N, int S, int phases) {
+    int64_t total = (int64_t)phases * M * N;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int n = (int)(i % N);
+        int64_t t = i / N;
+        int m = (int)(t % M);
+        int ph = (int)(t / M);
+        const float* p = ws + ((int64_t)ph * S * M + m) * N + n;
+        float s = 0.f;
+        for (int k = 0; k < S; ++k) s += p[(int64_t)k * M * N];
+        EP e = ep;
+        e.set_phase(ph);
+        e.store(m, n, s);
+    }
+}
+
+// ============================================================================ TN (weight-gradient) loaders
+// L loader: L(k, m) = p[k*ld + m]; loads 16 bytes = V consecutive m.
+template <typename T>
+struct KRowDense {
+    const T* p;
+    int ld, Kd, Md;  // rows (k) and columns (m/n)
+    __device__ uint4 load(int k, int m) const {
+        constexpr int V = Vec16<T>::N;
+        if (k >= Kd) return make_uint4(0, 0, 0, 0);
+        const T* r = p + (int64_t)k * ld;
+        if (m + V <= Md) return *reinterpret_cast<const uint4*>(r + m);
+        union { uint4 u; T e[V]; } x;
+#pragma unroll
+        for (int i = 0; i < V; ++i) x.e[i] = (m + i < Md) ? r[m + i] : from_f32<T>(0.f);
+        return x.u;
+    }
+};
+
+// H loader for stride-2 conv / transposed conv weight gradient: k = (b, r, c) over the LOW-res grid,
+// n = (kh, kw, ci): H(k, n) = Xh[b, 2r-1+kh, 2c-1+kw, ci] over the HIGH-res NHWC map [B, 2Hl, 2Wl, C].
+template <typename T>
+struct KRowConvS2 {
+    const T* x;
+    int Hl, Wl, C, Kd;  // Kd = B*Hl*Wl
+    __device__ uint4 load(int k, int n) const {
+        if (k >= Kd || n >= 9 * C) return make_uint4(0, 0, 0, 0);
+        int c = k % Wl, t = k / Wl;
+        int r = t % Hl, b = t / Hl;
+        int tap = n / C, ci = n - tap * C;
+        int kh = tap / 3, kw = tap - kh * 3;
+        int ih = 2 * r - 1 + kh, iw = 2 * c - 1 + kw;
+        int Hh = 2 * Hl, Wh = 2 * Wl;
+        if ((unsigned)ih >= (unsigned)Hh || (unsigned)iw >= (unsigned)Wh) return make_uint4(0, 0, 0, 0);
+        return *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hh + ih) * Wh + iw) * C + ci);
+    }
+};
+
+// ============================================================================ TN main loop
+// Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_kernel).
+template <typename T, int BM, int BN, int WM, int WN, class LL, class HL>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len) {
+    constexpr int V = Vec16<T>::N;
+    constexpr int BK = 4 * V;              // k rows per tile (32 bf16 / 16 f32)
+    constexpr int LDA = BM + V;             // padded LDS row (elements)
+    constexpr int LDB = BN + V;
+    constexpr int WAVES_N = BN / WN;
+    static_assert((BM / WM) * WAVES_N == 4, "4 waves per block");
+    constexpr int TM = WM / 16, TN = WN / 16;
+    constexpr int ACH = BK * BM / V, BCH = BK * BN / V;
+    constexpr int AR = (ACH + 255) / 256, BR = (BCH + 255) / 256;
+    __shared__ __attribute__((aligned(16))) T Ls[2][BK * LDA];
+    __shared__ __attribute__((aligned(16))) T Hs[2][BK * LDB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
+    const int tiles_n = (N + BN - 1) / BN;
+    const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
+    const int kb = blockIdx.z * ksplit_len;
+    const int ke = min(K, kb + ksplit_len);
+
+    f32x4_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    uint4 ra[AR], rb[BR];
+    constexpr int ACPR = BM / V, BCPR = BN / V;  // chunks per k-row
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+            int c = tid + i * 256;
+            if (c < ACH) ra[i] = ll.load(k0 + c / ACPR, m0 + (c % ACPR) * V);
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+            int c = tid + i * 256;
+            if (c < BCH) rb[i] = hl.load(k0 + c / BCPR, n0 + (c % BCPR) * V);
+        }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+            int c = tid + i * 256;
+            if (c < ACH) *reinterpret_cast<uint4*>(&Ls[buf][(c / ACPR) * LDA + (c % ACPR) * V]) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+            int c = tid + i * 256;
+            if (c < BCH) *reinterpret_cast<uint4*>(&Hs[buf][(c / BCPR) * LDB + (c % BCPR) * V]) = rb[i];
+        }
+    };
+
+    if (kb < ke) {
+        gload(kb);
+        lstore(0);
+        __syncthreads();
+        int it = 0;
+        const int g = lane >> 4, li = lane & 15;
+        for (int k0 = kb; k0 < ke; k0 += BK, ++it) {
+            const int cur = it & 1;
+            const bool more = k0 + BK < ke;
+            if (more) gload(k0 + BK);
+            const T* A = Ls[cur];
+            const T* B = Hs[cur];
+            if constexpr (sizeof(T) == 2) {
+                // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses row q, cols 4p..4p+3;
+                // lane i receives column i of the 4 rows.
+                const int q = li >> 2, p = li & 3;
+                bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const T* base = &A[(8 * g + q) * LDA + wm0 + i * 16 + 4 * p];
+                    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base));
+                    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + 4 * LDA));
+                    af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const T* base = &B[(8 * g + q) * LDB + wn0 + j * 16 + 4 * p];
+                    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base));
+                    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + 4 * LDB));
+                    bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    float af[TM], bfr[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) af[i] = A[(s * 4 + g) * LDA + wm0 + i * 16 + li];
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) bfr[j] = B[(s * 4 + g) * LDB + wn0 + j * 16 + li];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                }
+            }
+            if (more) lstore(cur ^ 1);
+            __syncthreads();
+        }
+    }
+    float* slab = ws + (int64_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
+                int n = n0 + wn0 + j * 16 + (lane & 15);
+                if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
+            }
+}
+
+}  // namespace hlmc

@@ -1,0 +1,259 @@
+// Launchers for the MFMA GEMM families (tile choice + deterministic split-K planning).
+#include "gemm.hpp"
+#include "ops.hpp"
+
+#include <algorithm>
+
+namespace hlmc {
+namespace {
+
+constexpr int kTargetBlocks = 512;  // 256 CUs x 2
+
+// Split-K plan shared by the launcher and the workspace query (must agree).
+struct Plan {
+    int S, ksl;
+};
+inline Plan plan_nt(int tiles, int Kmax, int BK) {
+    int S = 1;
+    if (tiles < kTargetBlocks / 2) {
+        S = cdiv(kTargetBlocks, tiles);
+        S = std::min(S, std::max(1, Kmax / (4 * BK)));
+    }
+    int ksl = cdiv(cdiv(Kmax, S), BK) * BK;
+    S = cdiv(Kmax, ksl);
+    return {S, ksl};
+}
+inline Plan plan_tn(int tiles, int K, int BK) {
+    int S = cdiv(kTargetBlocks, tiles);
+    S = std::max(1, std::min(S, K / (8 * BK)));
+    int ksl = cdiv(cdiv(K, S), BK) * BK;
+    S = cdiv(K, ksl);
+    return {S, ksl};
+}
+
+template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
+int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws) {
+    constexpr int BK = 4 * Vec16<T>::N;
+    const int tmn = cdiv(M, BM) * cdiv(N, BN);
+    Plan pl = plan_nt(tmn * phases, Kmax, BK);
+    dim3 grid(tmn, phases, pl.S);
+    if (pl.S == 1) {
+        gemm_nt_kernel<T, BM, BN, WM, WN, AL, BL, EP><<<grid, 256, 0, s>>>(al, bl, ep, M, N, pl.ksl);
+        HLMC_LAUNCHED();
+        return HLMC_OK;
+    }
+    size_t need = (size_t)phases * pl.S * M * N * sizeof(float);
+    HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "split-K workspace too small");
+    StorePartialZ part;
+    part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
+    gemm_nt_kernel<T, BM, BN, WM, WN, AL, BL, StorePartialZ><<<grid, 256, 0, s>>>(al, bl, part, M, N, pl.ksl);
+    HLMC_LAUNCHED();
+    int64_t total = (int64_t)phases * M * N;
+    int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+    splitk_reduce_kernel<EP><<<blocks, 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+template <int BM, int BN>
+size_t nt_ws(int M, int N, int Kmax, int phases, int BK) {
+    const int tmn = cdiv(M, BM) * cdiv(N, BN);
+    Plan pl = plan_nt(tmn * phases, Kmax, BK);
+    return pl.S == 1 ? 0 : (size_t)phases * pl.S * M * N * sizeof(float);
+}
+
+// Dispatch on N for the NT family: 128x128 / 128x64 / 128x32 tiles.
+template <typename T, class AL, class BL, class EP>
+int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws) {
+    if (N >= 128) return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws);
+    if (N > 32) return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws);
+    return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws);
+}
+template <typename T>
+size_t dispatch_nt_ws(int M, int N, int Kmax, int phases) {
+    constexpr int BK = 4 * Vec16<T>::N;
+    if (N >= 128) return nt_ws<128, 128>(M, N, Kmax, phases, BK);
+    if (N > 32) return nt_ws<128, 64>(M, N, Kmax, phases, BK);
+    return nt_ws<128, 32>(M, N, Kmax, phases, BK);
+}
+
+// Linear layers have small M (= batch): 64x64 tiles so more blocks exist before split-K.
+template <typename T, class AL, class BL, class EP>
+int dispatch_linear(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int K, Ws ws) {
+    if (M >= 1024 && N >= 128) return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, K, 1, ws);
+    return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, K, 1, ws);
+}
+template <typename T>
+size_t dispatch_linear_ws(int M, int N, int K) {
+    constexpr int BK = 4 * Vec16<T>::N;
+    if (M >= 1024 && N >= 128) return nt_ws<128, 128>(M, N, K, 1, BK);
+    return nt_ws<64, 64>(M, N, K, 1, BK);
+}
+
+// Final epilogue of a conv weight gradient: C[m][n = tap*C + ci] -> dW[m][ci][tap] (torch layout).
+struct StoreWgradConv {
+    float* dW;
+    int C;
+    __device__ void set_phase(int) {}
+    __device__ void store(int m, int n, float v) const {
+        int tap = n / C, ci = n - tap * C;
+        dW[((int64_t)m * C + ci) * 9 + tap] = v;
+    }
+};
+
+template <typename T, int BM, int BN, int WM, int WN, class LL, class HL, class EP>
+int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws) {
+    constexpr int BK = 4 * Vec16<T>::N;
+    const int tiles = cdiv(M, BM) * cdiv(N, BN);
+    Plan pl = plan_tn(tiles, K, BK);
+    size_t need = (size_t)pl.S * M * N * sizeof(float);
+    HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "wgrad workspace too small");
+    dim3 grid(tiles, 1, pl.S);
+    gemm_tn_kernel<T, BM, BN, WM, WN, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl);
+    HLMC_LAUNCHED();
+    int64_t total = (int64_t)M * N;
+    int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+    splitk_reduce_kernel<EP><<<blocks, 256, 0, s>>>(ws.p, ep, M, N, pl.S, 1);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <int BM, int BN>
+size_t tn_ws(int M, int N, int K, int BK) {
+    Plan pl = plan_tn(cdiv(M, BM) * cdiv(N, BN), K, BK);
+    return (size_t)pl.S * M * N * sizeof(float);
+}
+
+template <typename T, class LL, class HL, class EP>
+int dispatch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws) {
+    if (M >= 128) return launch_tn<T, 128, 128, 64, 64>(s, ll, hl, ep, M, N, K, ws);
+    if (M > 32) return launch_tn<T, 64, 128, 32, 64>(s, ll, hl, ep, M, N, K, ws);
+    return launch_tn<T, 32, 128, 32, 32>(s, ll, hl, ep, M, N, K, ws);
+}
+template <typename T>
+size_t dispatch_tn_ws(int M, int N, int K) {
+    constexpr int BK = 4 * Vec16<T>::N;
+    if (M >= 128) return tn_ws<128, 128>(M, N, K, BK);
+    if (M > 32) return tn_ws<64, 128>(M, N, K, BK);
+    return tn_ws<32, 128>(M, N, K, BK);
+}
+
+template <typename T>
+struct KRowDenseV {  // KRowDense with a scalar path when rows are not 16-byte aligned
+    const T* p;
+    int ld, Kd, Md;
+    bool vec;
+    __device__ uint4 load(int k, int m) const {
+        constexpr int V = Vec16<T>::N;
+        if (k >= Kd) return make_uint4(0, 0, 0, 0);
+        const T* r = p + (int64_t)k * ld;
+        if (vec && m + V <= Md) return *reinterpret_cast<const uint4*>(r + m);
+        union { uint4 u; T e[V]; } x;
+#pragma unroll
+        for (int i = 0; i < V; ++i) x.e[i] = (m + i < Md) ? r[m + i] : from_f32<T>(0.f);
+        return x.u;
+    }
+};
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+namespace ops {
+
+template <typename T>
+int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws) {
+    constexpr int V = Vec16<T>::N;
+    HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % (4 * V) == 0, "conv_s2: need even H/W and Ci % BK == 0");
+    HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "conv_s2: 16-byte alignment");
+    const int Ho = Hi / 2, Wo = Wi / 2, M = B * Ho * Wo, K = 9 * Ci;
+    ConvS2Loader<T> al{x, Hi, Wi, Ci, Ho, Wo, M};
+    DenseLoader<T> bl{wp, K, Co, K, true};
+    StoreRM<T> ep{y, bias, Co, 0, 0};
+    return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws);
+}
+template <typename T>
+size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {
+    return dispatch_nt_ws<T>(B * (Hi / 2) * (Wi / 2), Co, 9 * Ci, 1);
+}
+
+template <typename T>
+int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws) {
+    constexpr int V = Vec16<T>::N;
+    HLMC_CHECK_ARG(Ci % (4 * V) == 0, "subpixel: Ci % BK == 0");
+    HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "subpixel: 16-byte alignment");
+    const int M = B * Hi * Wi;
+    SubpixelLoader<T> al{x, Hi, Wi, Ci, M, 0, 0, 0, 0};
+    SubpixelWeight<T> bl{wp, Ci, Co, 0, 0, 0, 0};
+    StoreSubpixel<T> ep{y, bias, Hi, Wi, Co, 0, 0};
+    return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws);
+}
+template <typename T>
+size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co) {
+    return dispatch_nt_ws<T>(B * Hi * Wi, Co, 4 * Ci, 4);
+}
+
+template <typename T>
+int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* Xh, int C, float* dW, Ws ws) {
+    constexpr int V = Vec16<T>::N;
+    HLMC_CHECK_ARG(M % V == 0 && C % V == 0, "wgrad_s2: channel counts must be multiples of the vector width");
+    const int K = B * Hl * Wl, N = 9 * C;
+    KRowDense<T> ll{L, M, K, M};
+    KRowConvS2<T> hl{Xh, Hl, Wl, C, K};
+    StoreWgradConv ep{dW, C};
+    return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
+}
+template <typename T>
+size_t wgrad_s2_ws(int B, int Hl, int Wl, int M, int C) {
+    return dispatch_tn_ws<T>(M, 9 * C, B * Hl * Wl);
+}
+
+template <typename T, typename OutT>
+int linear(hipStream_t s, const T* x, int ldx, int M, int K, const T* w, int ldw, const float* bias, int N, OutT* y,
+           int ldy, int act, int accumulate, Ws ws) {
+    constexpr int V = Vec16<T>::N;
+    bool vx = (ldx % V == 0) && aligned16(x);
+    bool vw = (ldw % V == 0) && aligned16(w);
+    DenseLoader<T> al{x, ldx, M, K, vx};
+    DenseLoader<T> bl{w, ldw, N, K, vw};
+    StoreRM<OutT> ep{y, bias, ldy, act, accumulate};
+    return dispatch_linear<T>(s, al, bl, ep, M, N, K, ws);
+}
+template <typename T>
+size_t linear_ws(int M, int K, int N) {
+    return dispatch_linear_ws<T>(M, N, K);
+}
+
+template <typename T>
+int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int Mb, int N, int K, float* dW, Ws ws) {
+    constexpr int V = Vec16<T>::N;
+    KRowDenseV<T> ll{dy, lddy, Mb, N, (lddy % V == 0) && aligned16(dy)};
+    KRowDenseV<T> hl{x, ldx, Mb, K, (ldx % V == 0) && aligned16(x)};
+    StoreRM<float> ep{dW, nullptr, K, 0, 0};
+    return dispatch_tn<T>(s, ll, hl, ep, N, K, Mb, ws);
+}
+template <typename T>
+size_t linear_wgrad_ws(int Mb, int N, int K) {
+    return dispatch_tn_ws<T>(N, K, Mb);
+}
+
+#define INST(T)                                                                                                     \
+    template int conv_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws);        \
+    template size_t conv_s2_ws<T>(int, int, int, int, int);                                                        \
+    template int subpixel<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws);       \
+    template size_t subpixel_ws<T>(int, int, int, int, int);                                                       \
+    template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws);                \
+    template size_t wgrad_s2_ws<T>(int, int, int, int, int);                                                       \
+    template int linear<T, T>(hipStream_t, const T*, int, int, int, const T*, int, const float*, int, T*, int, int, \
+                              int, Ws);                                                                            \
+    template size_t linear_ws<T>(int, int, int);                                                                   \
+    template int linear_wgrad<T>(hipStream_t, const T*, int, const T*, int, int, int, int, float*, Ws);            \
+    template size_t linear_wgrad_ws<T>(int, int, int);
+
+INST(float)
+INST(bf16)
+#undef INST
+template int linear<bf16, float>(hipStream_t, const bf16*, int, int, int, const bf16*, int, const float*, int, float*,
+                                 int, int, int, Ws);
+
+}  // namespace ops
+}  // namespace hlmc

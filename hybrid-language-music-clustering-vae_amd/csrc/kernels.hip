@@ -1,0 +1,826 @@
+// Memory-bound kernels of the VAE hot path: BatchNorm (train/eval) + activation fwd/bwd, the
+// single-channel edge convolutions, layout changes, reparameterisation, loss, Adam, weight packing.
+// Reductions are deterministic: fixed-size block partials in float64, summed in block order.
+#include "ops.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+namespace hlmc {
+namespace {
+
+constexpr int kThreads = 256;
+
+inline int grid_for(int64_t n, int per_block = kThreads, int cap = 8192) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(cap, (n + per_block - 1) / per_block));
+}
+
+// Row-chunking shared by every [R][C] column reduction: nblk blocks, each a contiguous row range.
+inline int col_blocks(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (R + 63) / 64)); }
+
+__device__ __forceinline__ float act_fwd(float z, int act) {
+    if (act == 0) return z > 0.f ? z : 0.01f * z;
+    if (act == 1) return z > 0.f ? z : 0.f;
+    return z;
+}
+__device__ __forceinline__ float act_grad(float z, int act) {
+    if (act == 0) return z > 0.f ? 1.f : 0.01f;
+    if (act == 1) return z > 0.f ? 1.f : 0.f;
+    return 1.f;
+}
+
+// ---------------------------------------------------------------- BN statistics
+// Partial column sums: part[blk][0..C) = sum y, part[blk][C..2C) = sum y^2 (double).
+template <typename T>
+__global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ y, int64_t R, int C, int64_t rows_per_blk,
+                                                          double* __restrict__ part) {
+    constexpr int V = Vec16<T>::N;
+    __shared__ double s1[2048], s2[2048];
+    const int tpr = C / V;                 // threads per row
+    const int rpp = kThreads / tpr;        // rows per pass
+    const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
+    const int64_t r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
+    double a[V], b[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) a[v] = b[v] = 0.0;
+    if (rr < rpp) {
+        for (int64_t r = r0 + rr; r < r1; r += rpp) {
+            float x[V];
+            load16_f32(y + r * C + cg * V, x);
+#pragma unroll
+            for (int v = 0; v < V; ++v) { a[v] += x[v]; b[v] += (double)x[v] * x[v]; }
+        }
+        // rpp * C <= 2048 is guaranteed by the launcher (C/V <= 256 and rpp*tpr == 256)
+#pragma unroll
+        for (int v = 0; v < V; ++v) { s1[rr * C + cg * V + v] = a[v]; s2[rr * C + cg * V + v] = b[v]; }
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += kThreads) {
+        double x = 0.0, q = 0.0;
+        for (int k = 0; k < rpp; ++k) { x += s1[k * C + c]; q += s2[k * C + c]; }
+        part[(int64_t)blockIdx.x * 2 * C + c] = x;
+        part[(int64_t)blockIdx.x * 2 * C + C + c] = q;
+    }
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ part, int nblk, int C, int64_t R, float* mean,
+                                   float* invstd, float* rmean, float* rvar, int64_t* nbt, float momentum, float eps) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c == 0 && nbt) nbt[0] += 1;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < nblk; ++k) { s += part[(int64_t)k * 2 * C + c]; q += part[(int64_t)k * 2 * C + C + c]; }
+    double m = s / (double)R;
+    double var = q / (double)R - m * m;
+    if (var < 0.0) var = 0.0;
+    mean[c] = (float)m;
+    invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (rmean) {
+        double unb = R > 1 ? var * (double)R / (double)(R - 1) : var;
+        rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * m);
+        rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+    }
+}
+
+__global__ void bn_eval_kernel(const float* rmean, const float* rvar, int C, float eps, float* mean, float* invstd) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    mean[c] = rmean[c];
+    invstd[c] = 1.f / sqrtf(rvar[c] + eps);
+}
+
+// a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale]
+template <typename T>
+__global__ void bn_act_kernel(const T* __restrict__ y, int64_t R, int C, const float* __restrict__ mean,
+                              const float* __restrict__ invstd, const float* __restrict__ gamma,
+                              const float* __restrict__ beta, int act, const uint8_t* __restrict__ mask, float mscale,
+                              T* __restrict__ a, int lda) {
+    constexpr int V = Vec16<T>::N;
+    const int tpr = C / V;
+    const int64_t nvec = R * tpr;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t r = i / tpr;
+        int c0 = (int)(i - r * tpr) * V;
+        float x[V], o[V];
+        load16_f32(y + r * C + c0, x);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            int c = c0 + v;
+            float z = (x[v] - mean[c]) * invstd[c] * gamma[c] + beta[c];
+            float t = act_fwd(z, act);
+            if (mask) t = mask[r * C + c] ? t * mscale : 0.f;
+            o[v] = t;
+        }
+        store16_f32(a + r * lda + c0, o);
+    }
+}
+
+// backward partial sums: part[blk][0..C) = sum dz, [C..2C) = sum dz*xhat
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
+                                                             int64_t R, int C, const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, int act,
+                                                             const uint8_t* __restrict__ mask, float mscale,
+                                                             int64_t rows_per_blk, double* __restrict__ part) {
+    constexpr int V = Vec16<T>::N;
+    __shared__ double s1[2048], s2[2048];
+    const int tpr = C / V, rpp = kThreads / tpr;
+    const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
+    const int64_t r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
+    double a[V], b[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) a[v] = b[v] = 0.0;
+    if (rr < rpp) {
+        for (int64_t r = r0 + rr; r < r1; r += rpp) {
+            float x[V], g[V];
+            load16_f32(y + r * C + cg * V, x);
+            load16_f32(da + r * lda + cg * V, g);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                int c = cg * V + v;
+                float xh = (x[v] - mean[c]) * invstd[c];
+                float z = xh * gamma[c] + beta[c];
+                float dz = g[v] * act_grad(z, act);
+                if (mask) dz = mask[r * C + c] ? dz * mscale : 0.f;
+                a[v] += dz;
+                b[v] += (double)dz * xh;
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) { s1[rr * C + cg * V + v] = a[v]; s2[rr * C + cg * V + v] = b[v]; }
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += kThreads) {
+        double x = 0.0, q = 0.0;
+        for (int k = 0; k < rpp; ++k) { x += s1[k * C + c]; q += s2[k * C + c]; }
+        part[(int64_t)blockIdx.x * 2 * C + c] = x;
+        part[(int64_t)blockIdx.x * 2 * C + C + c] = q;
+    }
+}
+
+// reduce backward partials: sums2[0..C) = sum dz (-> dbeta), [C..2C) = sum dz*xhat (-> dgamma)
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int nblk, int C, float* dgamma, float* dbeta,
+                                       float* sums_f) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < nblk; ++k) { s += part[(int64_t)k * 2 * C + c]; q += part[(int64_t)k * 2 * C + C + c]; }
+    dbeta[c] = (float)s;
+    dgamma[c] = (float)q;
+    sums_f[c] = (float)s;
+    sums_f[C + c] = (float)q;
+}
+
+// dy = gamma*invstd*(dz - sum_dz/R - xhat*sum_dzxh/R); also column partial sums of dy (bias grad)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
+                                                           int64_t R, int C, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, int act,
+                                                           const uint8_t* __restrict__ mask, float mscale,
+                                                           const float* __restrict__ sums, T* __restrict__ dy,
+                                                           int64_t rows_per_blk, double* __restrict__ part) {
+    constexpr int V = Vec16<T>::N;
+    __shared__ double s1[2048];
+    const int tpr = C / V, rpp = kThreads / tpr;
+    const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
+    const int64_t r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
+    const float invR = 1.f / (float)R;
+    double a[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) a[v] = 0.0;
+    if (rr < rpp) {
+        for (int64_t r = r0 + rr; r < r1; r += rpp) {
+            float x[V], g[V], o[V];
+            load16_f32(y + r * C + cg * V, x);
+            load16_f32(da + r * lda + cg * V, g);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                int c = cg * V + v;
+                float is = invstd[c];
+                float xh = (x[v] - mean[c]) * is;
+                float z = xh * gamma[c] + beta[c];
+                float dz = g[v] * act_grad(z, act);
+                if (mask) dz = mask[r * C + c] ? dz * mscale : 0.f;
+                float d = gamma[c] * is * (dz - sums[c] * invR - xh * sums[C + c] * invR);
+                o[v] = d;
+            }
+            store16_f32(dy + r * C + cg * V, o);
+            // the bias grad is the sum of the dy actually stored (rounded to T)
+#pragma unroll
+            for (int v = 0; v < V; ++v) a[v] += to_f32<T>(from_f32<T>(o[v]));
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) s1[rr * C + cg * V + v] = a[v];
+    }
+    __syncthreads();
+    for (int c = tid; c < C; c += kThreads) {
+        double x = 0.0;
+        for (int k = 0; k < rpp; ++k) x += s1[k * C + c];
+        part[(int64_t)blockIdx.x * C + c] = x;
+    }
+}
+
+__global__ void colsum_finalize_kernel(const double* __restrict__ part, int nblk, int C, float* out) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s = 0.0;
+    for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * C + c];
+    out[c] = (float)s;
+}
+
+// generic column sum for arbitrary ld/cols (bias grads): block = (row chunk, 64-column slab);
+// 4 waves split the chunk's rows, lanes own columns; fixed-order combine in LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict__ x, int ld, int rows, int cols,
+                                                             int rows_per_blk, double* __restrict__ part) {
+    __shared__ double red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.y * 64 + lane;
+    const int r0 = blockIdx.x * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+    double s = 0.0;
+    if (c < cols)
+        for (int r = r0 + w; r < r1; r += 4) s += to_f32<T>(x[(int64_t)r * ld + c]);
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && c < cols) part[(int64_t)blockIdx.x * cols + c] = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+}
+
+// ---------------------------------------------------------------- edge convs (one channel side)
+// y[b,oh,ow,co] = bias[co] + sum_{kh,kw} x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + kh*3+kw]
+template <typename T, int CO>
+__global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         T* __restrict__ y) {
+    __shared__ float ws[CO * 9];
+    __shared__ float bs[CO];
+    for (int i = threadIdx.x; i < CO * 9; i += blockDim.x) ws[i] = w[i];
+    for (int i = threadIdx.x; i < CO; i += blockDim.x) bs[i] = bias ? bias[i] : 0.f;
+    __syncthreads();
+    const int Ho = Hi / 2, Wo = Wi / 2;
+    const int64_t npix = (int64_t)B * Ho * Wo;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+        int ow = (int)(p % Wo);
+        int64_t t = p / Wo;
+        int oh = (int)(t % Ho);
+        int b = (int)(t / Ho);
+        float in[9];
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
+                in[kh * 3 + kw] = ((unsigned)ih < (unsigned)Hi && (unsigned)iw < (unsigned)Wi)
+                                      ? x[((int64_t)b * Hi + ih) * Wi + iw] : 0.f;
+            }
+        constexpr int V = Vec16<T>::N;
+#pragma unroll
+        for (int c0 = 0; c0 < CO; c0 += V) {
+            float o[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                float s = bs[c0 + v];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) s = fmaf(in[k], ws[(c0 + v) * 9 + k], s);
+                o[v] = s;
+            }
+            store16_f32(y + p * CO + c0, o);
+        }
+    }
+}
+
+// y[b, oh, ow] = bias + sum_ci sum_taps x[b, ih, iw, ci] * w[ci*9 + kh*3 + kw]  (transposed, 1 output channel)
+template <typename T, int CI>
+__global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
+                                                       const float* __restrict__ w, const float* __restrict__ bias,
+                                                       float* __restrict__ y) {
+    __shared__ float ws[CI * 9];
+    for (int i = threadIdx.x; i < CI * 9; i += blockDim.x) ws[i] = w[i];
+    __syncthreads();
+    const float b0 = bias ? bias[0] : 0.f;
+    const int Ho = 2 * Hi, Wo = 2 * Wi;
+    const int64_t npix = (int64_t)B * Ho * Wo;
+    constexpr int V = Vec16<T>::N;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+        int ow = (int)(p % Wo);
+        int64_t t = p / Wo;
+        int oh = (int)(t % Ho);
+        int b = (int)(t / Ho);
+        int py = oh & 1, px = ow & 1, r = oh >> 1, c = ow >> 1;
+        float s = b0;
+        for (int ty = 0; ty < (py ? 2 : 1); ++ty) {
+            int kh = py ? (ty ? 2 : 0) : 1;
+            int ih = r + ((py && ty == 0) ? 1 : 0);
+            if (ih >= Hi) continue;
+            for (int tx = 0; tx < (px ? 2 : 1); ++tx) {
+                int kw = px ? (tx ? 2 : 0) : 1;
+                int iw = c + ((px && tx == 0) ? 1 : 0);
+                if (iw >= Wi) continue;
+                const T* src = x + (((int64_t)b * Hi + ih) * Wi + iw) * CI;
+                const int tap = kh * 3 + kw;
+#pragma unroll
+                for (int c0 = 0; c0 < CI; c0 += V) {
+                    float v[V];
+                    load16_f32(src + c0, v);
+#pragma unroll
+                    for (int q = 0; q < V; ++q) s = fmaf(v[q], ws[(c0 + q) * 9 + tap], s);
+                }
+            }
+        }
+        y[p] = s;
+    }
+}
+
+// dW[m*9+tap] partials: block = chunk of low-res rows (b,r,c); Xh single-channel high-res [B, 2Hl, 2Wl]
+template <typename T, int M>
+__global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, int B, int Hl, int Wl,
+                                                       const float* __restrict__ Xh, int rows_per_blk,
+                                                       float* __restrict__ part) {
+    constexpr int RC = 128;  // rows staged per pass
+    __shared__ float Ls[RC][M + 1];
+    __shared__ float Hs[RC][9];
+    const int64_t K = (int64_t)B * Hl * Wl;
+    const int64_t k0 = (int64_t)blockIdx.x * rows_per_blk, k1 = min(K, k0 + rows_per_blk);
+    const int Hh = 2 * Hl, Wh = 2 * Wl;
+    float acc[2] = {0.f, 0.f};
+    for (int64_t kb = k0; kb < k1; kb += RC) {
+        for (int i = threadIdx.x; i < RC * M; i += blockDim.x) {
+            int rr = i / M, m = i % M;
+            int64_t k = kb + rr;
+            Ls[rr][m] = (k < k1) ? to_f32<T>(L[k * M + m]) : 0.f;
+        }
+        for (int i = threadIdx.x; i < RC * 9; i += blockDim.x) {
+            int rr = i / 9, tap = i % 9;
+            int64_t k = kb + rr;
+            float v = 0.f;
+            if (k < k1) {
+                int c = (int)(k % Wl);
+                int64_t t = k / Wl;
+                int r = (int)(t % Hl);
+                int b = (int)(t / Hl);
+                int ih = 2 * r - 1 + tap / 3, iw = 2 * c - 1 + tap % 3;
+                if ((unsigned)ih < (unsigned)Hh && (unsigned)iw < (unsigned)Wh) v = Xh[((int64_t)b * Hh + ih) * Wh + iw];
+            }
+            Hs[rr][tap] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            int o = threadIdx.x + j * 256;
+            if (o < M * 9) {
+                int m = o / 9, tap = o % 9;
+                float s = 0.f;
+                for (int rr = 0; rr < RC; ++rr) s = fmaf(Ls[rr][m], Hs[rr][tap], s);
+                acc[j] += s;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        int o = threadIdx.x + j * 256;
+        if (o < M * 9) part[(int64_t)blockIdx.x * M * 9 + o] = acc[j];
+    }
+}
+
+__global__ void sum_partials_f32_kernel(const float* __restrict__ part, int nblk, int n, float* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s = 0.0;
+    for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * n + i];
+    out[i] = (float)s;
+}
+
+// ---------------------------------------------------------------- layout / elementwise
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = from_f32<TO>(to_f32<TI>(x[i]));
+}
+template <typename TI, typename TO>
+__global__ void cast2d_kernel(const TI* __restrict__ x, int ldx, TO* __restrict__ y, int ldy, int rows, int cols) {
+    int64_t n = (int64_t)rows * cols;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int r = (int)(i / cols), c = (int)(i % cols);
+        y[(int64_t)r * ldy + c] = from_f32<TO>(to_f32<TI>(x[(int64_t)r * ldx + c]));
+    }
+}
+template <typename T>
+__global__ void nhwc_to_flat_kernel(const T* __restrict__ x, int B, int h, int w, int C, T* __restrict__ y, int ldy) {
+    const int F = C * h * w;
+    int64_t n = (int64_t)B * F;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int b = (int)(i / F), f = (int)(i % F);
+        int c = f / (h * w), hw = f % (h * w);
+        y[(int64_t)b * ldy + f] = x[((int64_t)b * h * w + hw) * C + c];
+    }
+}
+template <typename T>
+__global__ void flat_to_nhwc_kernel(const T* __restrict__ x, int ldx, int B, int h, int w, int C, T* __restrict__ y) {
+    const int F = C * h * w;
+    int64_t n = (int64_t)B * F;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int b = (int)(i / F), rem = (int)(i % F);
+        int hw = rem / C, c = rem % C;  // i enumerates the NHWC output
+        y[i] = x[(int64_t)b * ldx + (int64_t)c * h * w + hw];
+    }
+}
+template <typename T>
+__global__ void relu_bwd_kernel(T* __restrict__ dy, int lddy, const T* __restrict__ y, int ldy, int rows, int cols) {
+    int64_t n = (int64_t)rows * cols;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int r = (int)(i / cols), c = (int)(i % cols);
+        if (!(to_f32<T>(y[(int64_t)r * ldy + c]) > 0.f)) dy[(int64_t)r * lddy + c] = from_f32<T>(0.f);
+    }
+}
+template <typename T>
+__global__ void reparam_fwd_kernel(const float* __restrict__ mu, const float* __restrict__ lv,
+                                   const float* __restrict__ eps, int n_rows, int L, T* __restrict__ z, int ldz) {
+    int64_t n = (int64_t)n_rows * L;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int r = (int)(i / L), c = (int)(i % L);
+        float sd = expf(0.5f * lv[i]);
+        z[(int64_t)r * ldz + c] = from_f32<T>(mu[i] + eps[i] * sd);
+    }
+}
+template <typename T>
+__global__ void reparam_bwd_kernel(const T* __restrict__ dz, int lddz, const float* __restrict__ lv,
+                                   const float* __restrict__ eps, int n_rows, int L, float* __restrict__ dmu,
+                                   float* __restrict__ dlv) {
+    int64_t n = (int64_t)n_rows * L;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int r = (int)(i / L), c = (int)(i % L);
+        float g = to_f32<T>(dz[(int64_t)r * lddz + c]);
+        float sd = expf(0.5f * lv[i]);
+        dmu[i] += g;
+        dlv[i] += g * eps[i] * sd * 0.5f;
+    }
+}
+
+// ---------------------------------------------------------------- loss
+__global__ __launch_bounds__(256) void vae_sums_kernel(const float* __restrict__ ra, const float* __restrict__ a,
+                                                       int64_t na, const float* __restrict__ rt,
+                                                       const float* __restrict__ t, int64_t nt,
+                                                       const float* __restrict__ mu, const float* __restrict__ lv,
+                                                       int64_t nl, double* __restrict__ part) {
+    __shared__ double red[3][4];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = i0; i < na; i += stride) { float d = ra[i] - a[i]; s0 += (double)d * d; }
+    for (int64_t i = i0; i < nt; i += stride) { float d = rt[i] - t[i]; s1 += (double)d * d; }
+    for (int64_t i = i0; i < nl; i += stride) s2 += (double)(1.f + lv[i] - mu[i] * mu[i] - expf(lv[i]));
+    s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = s0; red[1][w] = s1; red[2][w] = s2; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        double s = 0.0;
+        for (int k = 0; k < 4; ++k) s += red[threadIdx.x][k];
+        part[blockIdx.x * 3 + threadIdx.x] = s;
+    }
+}
+__global__ void vae_sums_finalize_kernel(const double* __restrict__ part, int nblk, double* out) {
+    int j = threadIdx.x;
+    if (j >= 3) return;
+    double s = 0.0;
+    for (int k = 0; k < nblk; ++k) s += part[k * 3 + j];
+    out[j] = s;
+}
+__global__ void vae_bwd_kernel(const float* __restrict__ ra, const float* __restrict__ a, int64_t na,
+                               float* __restrict__ dra, const float* __restrict__ rt, const float* __restrict__ t,
+                               int64_t nt, float* __restrict__ drt, const float* __restrict__ mu,
+                               const float* __restrict__ lv, int64_t nl, const float* __restrict__ coef,
+                               float* __restrict__ dmu, float* __restrict__ dlv) {
+    const float ca = coef[0], ct = coef[1], ck = coef[2];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = i0; i < na; i += stride) dra[i] = ca * (ra[i] - a[i]);
+    for (int64_t i = i0; i < nt; i += stride) drt[i] = ct * (rt[i] - t[i]);
+    for (int64_t i = i0; i < nl; i += stride) {
+        dmu[i] = ck * mu[i];
+        dlv[i] = -0.5f * ck * (1.f - expf(lv[i]));
+    }
+}
+
+// ---------------------------------------------------------------- Adam (torch.optim.Adam single-tensor math)
+constexpr int kAdamMax = 48;
+struct AdamBatch {
+    float* p[kAdamMax];
+    const float* g[kAdamMax];
+    float* m[kAdamMax];
+    float* v[kAdamMax];
+    int64_t n[kAdamMax];
+    int blk0[kAdamMax + 1];
+    int count;
+};
+__global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, float lr, float b1, float b2, float eps, float wd,
+                                                   float step_size, float bc2_sqrt) {
+    int t = 0;
+    while (t + 1 < bt.count && (int)blockIdx.x >= bt.blk0[t + 1]) ++t;
+    const int64_t base = (int64_t)(blockIdx.x - bt.blk0[t]) * 1024;
+    float* p = bt.p[t];
+    const float* g = bt.g[t];
+    float* m = bt.m[t];
+    float* v = bt.v[t];
+    const int64_t n = bt.n[t];
+    for (int64_t i = base + threadIdx.x; i < min(n, base + 1024); i += blockDim.x) {
+        float gi = g[i];
+        if (wd != 0.f) gi = gi + wd * p[i];
+        float mi = m[i];
+        mi = mi + (gi - mi) * (1.f - b1);
+        float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] = p[i] - step_size * (mi / denom);
+    }
+}
+
+// ---------------------------------------------------------------- weight packing
+template <typename T>
+__global__ void pack_kernel(const ops::PackJob* __restrict__ jobs, int njobs) {
+    const ops::PackJob jb = jobs[blockIdx.y];
+    const int64_t n = (int64_t)jb.d0 * jb.d1 * jb.taps;
+    T* p0 = (T*)jb.p0;
+    T* p1 = (T*)jb.p1;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i0 = e / ((int64_t)jb.d1 * jb.taps);
+        int64_t rem = e - i0 * jb.d1 * jb.taps;
+        int64_t i1 = rem / jb.taps;
+        int tap = (int)(rem - i1 * jb.taps);
+        T v = from_f32<T>(jb.w[e]);
+        if (p0) p0[(i0 * jb.taps + tap) * jb.ld0 + i1] = v;
+        if (p1) p1[(i1 * jb.taps + tap) * jb.ld1 + i0] = v;
+    }
+}
+
+}  // namespace
+
+// ============================================================================ launchers
+namespace ops {
+
+size_t bn_ws(int64_t R, int C) { return (size_t)col_blocks(R) * 2 * C * sizeof(double) + 2 * C * sizeof(float); }
+
+template <typename T>
+static int check_bn_shape(int C) {
+    constexpr int V = Vec16<T>::N;
+    HLMC_CHECK_ARG(C % V == 0 && C / V <= 256 && 256 % (C / V) == 0, "BatchNorm channel count unsupported");
+    return HLMC_OK;
+}
+
+template <typename T>
+int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean, float* run_var,
+             int64_t* nbt, float momentum, float eps, Ws ws) {
+    HLMC_TRY(check_bn_shape<T>(C));
+    const int nblk = col_blocks(R);
+    HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
+    const int64_t rpb = (R + nblk - 1) / nblk;
+    double* part = reinterpret_cast<double*>(ws.p);
+    col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, rpb, part);
+    HLMC_LAUNCHED();
+    bn_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, nblk, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, int C, float eps, float* mean, float* invstd) {
+    bn_eval_kernel<<<cdiv(C, 256), 256, 0, s>>>(run_mean, run_var, C, eps, mean, invstd);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+template <typename T>
+int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const float* invstd, const float* gamma,
+           const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda) {
+    HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act: output row stride must be a multiple of 16 bytes");
+    int64_t nvec = R * (C / Vec16<T>::N);
+    bn_act_kernel<T><<<grid_for(nvec), kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+template <typename T>
+int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
+               const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
+               float* dbeta, float* dbias, Ws ws) {
+    HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act_bwd: grad row stride must be a multiple of 16 bytes");
+    const int nblk = col_blocks(R);
+    HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
+    const int64_t rpb = (R + nblk - 1) / nblk;
+    double* part = reinterpret_cast<double*>(ws.p);
+    float* sums = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
+    bn_bwd_moments_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb, part);
+    HLMC_LAUNCHED();
+    bn_bwd_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, nblk, C, dgamma, dbeta, sums);
+    HLMC_LAUNCHED();
+    bn_bwd_apply_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
+                                                     dy, rpb, part);
+    HLMC_LAUNCHED();
+    if (dbias) {
+        colsum_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, nblk, C, dbias);
+        HLMC_LAUNCHED();
+    }
+    return HLMC_OK;
+}
+
+template <typename T>
+int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y) {
+    HLMC_CHECK_ARG(Co == 32 && Hi % 2 == 0 && Wi % 2 == 0, "conv_c1_s2: only Co == 32, even H/W");
+    int64_t npix = (int64_t)B * (Hi / 2) * (Wi / 2);
+    conv_c1_s2_kernel<T, 32><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+template <typename T>
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y) {
+    HLMC_CHECK_ARG(Ci == 32, "convT_c1: only Ci == 32");
+    int64_t npix = (int64_t)B * 4 * Hi * Wi;
+    convT_c1_kernel<T, 32><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+static int wgrad_c1_blocks(int64_t K) { return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (K + 1023) / 1024)); }
+size_t wgrad_c1_ws(int B, int Hl, int Wl, int M) {
+    return (size_t)wgrad_c1_blocks((int64_t)B * Hl * Wl) * M * 9 * sizeof(float);
+}
+
+template <typename T>
+int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws) {
+    HLMC_CHECK_ARG(M == 32, "wgrad_c1: only M == 32");
+    int64_t K = (int64_t)B * Hl * Wl;
+    int nblk = wgrad_c1_blocks(K);
+    HLMC_CHECK_ARG(ws.bytes >= wgrad_c1_ws(B, Hl, Wl, M), "wgrad_c1 workspace");
+    int rpb = (int)((K + nblk - 1) / nblk);
+    wgrad_c1_kernel<T, 32><<<nblk, kThreads, 0, s>>>(L, B, Hl, Wl, Xh, rpb, ws.p);
+    HLMC_LAUNCHED();
+    sum_partials_f32_kernel<<<cdiv(M * 9, 256), 256, 0, s>>>(ws.p, nblk, M * 9, dW);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+template <typename T>
+int cast_from_f32(hipStream_t s, const float* x, T* y, int64_t n) {
+    cast_kernel<float, T><<<grid_for(n), kThreads, 0, s>>>(x, y, n);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int cast_to_f32(hipStream_t s, const T* x, float* y, int64_t n) {
+    cast_kernel<T, float><<<grid_for(n), kThreads, 0, s>>>(x, y, n);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int copy2d(hipStream_t s, const T* x, int ldx, T* y, int ldy, int rows, int cols) {
+    cast2d_kernel<T, T><<<grid_for((int64_t)rows * cols), kThreads, 0, s>>>(x, ldx, y, ldy, rows, cols);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int cast2d_from_f32(hipStream_t s, const float* x, int ldx, T* y, int ldy, int rows, int cols) {
+    cast2d_kernel<float, T><<<grid_for((int64_t)rows * cols), kThreads, 0, s>>>(x, ldx, y, ldy, rows, cols);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int nhwc_to_flat(hipStream_t s, const T* x, int B, int h, int w, int C, T* y, int ldy) {
+    nhwc_to_flat_kernel<T><<<grid_for((int64_t)B * C * h * w), kThreads, 0, s>>>(x, B, h, w, C, y, ldy);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int flat_to_nhwc(hipStream_t s, const T* x, int ldx, int B, int h, int w, int C, T* y) {
+    flat_to_nhwc_kernel<T><<<grid_for((int64_t)B * C * h * w), kThreads, 0, s>>>(x, ldx, B, h, w, C, y);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int relu_bwd(hipStream_t s, T* dy, int lddy, const T* y, int ldy, int rows, int cols) {
+    relu_bwd_kernel<T><<<grid_for((int64_t)rows * cols), kThreads, 0, s>>>(dy, lddy, y, ldy, rows, cols);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+static int colsum_blocks(int rows) { return std::max(1, std::min(1024, rows / 256)); }
+size_t colsum_ws(int rows, int cols) { return (size_t)colsum_blocks(rows) * cols * sizeof(double); }
+template <typename T>
+int colsum(hipStream_t s, const T* dy, int ld, int rows, int cols, float* db, Ws ws) {
+    int nblk = colsum_blocks(rows);
+    HLMC_CHECK_ARG(ws.bytes >= colsum_ws(rows, cols), "colsum workspace");
+    int rpb = (rows + nblk - 1) / nblk;
+    double* part = reinterpret_cast<double*>(ws.p);
+    dim3 grid(nblk, cdiv(cols, 64));
+    colsum_partial_kernel<T><<<grid, 256, 0, s>>>(dy, ld, rows, cols, rpb, part);
+    HLMC_LAUNCHED();
+    colsum_finalize_kernel<<<cdiv(cols, 256), 256, 0, s>>>(part, nblk, cols, db);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz) {
+    reparam_fwd_kernel<T><<<grid_for((int64_t)n_rows * L), kThreads, 0, s>>>(mu, lv, eps, n_rows, L, z, ldz);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int reparam_bwd(hipStream_t s, const T* dz, int lddz, const float* lv, const float* eps, int n_rows, int L, float* dmu,
+                float* dlv) {
+    reparam_bwd_kernel<T><<<grid_for((int64_t)n_rows * L), kThreads, 0, s>>>(dz, lddz, lv, eps, n_rows, L, dmu, dlv);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+static int vae_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n + 2047) / 2048)); }
+size_t vae_sums_ws(int64_t na, int64_t nt, int64_t nl) {
+    return (size_t)vae_blocks(std::max(na, std::max(nt, nl))) * 3 * sizeof(double);
+}
+int vae_sums(hipStream_t s, const float* ra, const float* a, int64_t na, const float* rt, const float* t, int64_t nt,
+             const float* mu, const float* lv, int64_t nl, double* out3, Ws ws) {
+    int nblk = vae_blocks(std::max(na, std::max(nt, nl)));
+    HLMC_CHECK_ARG(ws.bytes >= vae_sums_ws(na, nt, nl), "loss workspace");
+    double* part = reinterpret_cast<double*>(ws.p);
+    vae_sums_kernel<<<nblk, kThreads, 0, s>>>(ra, a, na, rt, t, nt, mu, lv, nl, part);
+    HLMC_LAUNCHED();
+    vae_sums_finalize_kernel<<<1, 64, 0, s>>>(part, nblk, out3);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+int vae_loss_bwd(hipStream_t s, const float* ra, const float* a, int64_t na, float* dra, const float* rt, const float* t,
+                 int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl, const float* coef, float* dmu,
+                 float* dlv) {
+    int64_t n = std::max(na, std::max(nt, nl));
+    vae_bwd_kernel<<<grid_for(n, kThreads, 4096), kThreads, 0, s>>>(ra, a, na, dra, rt, t, nt, drt, mu, lv, nl, coef,
+                                                                     dmu, dlv);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, float* const* m, float* const* v,
+         const int64_t* numel, AdamArgs a, void*) {
+    const double bc1 = 1.0 - std::pow((double)a.beta1, (double)a.step);
+    const double bc2 = 1.0 - std::pow((double)a.beta2, (double)a.step);
+    const float step_size = (float)(a.lr / bc1);
+    const float bc2_sqrt = (float)std::sqrt(bc2);
+    for (int t0 = 0; t0 < ntensors; t0 += kAdamMax) {
+        AdamBatch bt{};
+        bt.count = std::min(kAdamMax, ntensors - t0);
+        int blocks = 0;
+        for (int i = 0; i < bt.count; ++i) {
+            bt.p[i] = p[t0 + i]; bt.g[i] = g[t0 + i]; bt.m[i] = m[t0 + i]; bt.v[i] = v[t0 + i];
+            bt.n[i] = numel[t0 + i];
+            bt.blk0[i] = blocks;
+            blocks += (int)((numel[t0 + i] + 1023) / 1024);
+        }
+        bt.blk0[bt.count] = blocks;
+        if (blocks == 0) continue;
+        adam_kernel<<<blocks, 256, 0, s>>>(bt, a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, step_size, bc2_sqrt);
+        HLMC_LAUNCHED();
+    }
+    return HLMC_OK;
+}
+
+template <typename T>
+int pack(hipStream_t s, const PackJob* jobs_dev, int njobs, int64_t max_elems) {
+    if (njobs == 0) return HLMC_OK;
+    dim3 grid((unsigned)std::min<int64_t>(1024, (max_elems + 255) / 256), njobs);
+    pack_kernel<T><<<grid, 256, 0, s>>>(jobs_dev, njobs);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+#define INST(T)                                                                                                      \
+    template int bn_stats<T>(hipStream_t, const T*, int64_t, int, float*, float*, float*, float*, int64_t*, float,     \
+                             float, Ws);                                                                              \
+    template int bn_act<T>(hipStream_t, const T*, int64_t, int, const float*, const float*, const float*, const float*, \
+                           int, const uint8_t*, float, T*, int);                                                      \
+    template int bn_act_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,          \
+                               const float*, const float*, int, const uint8_t*, float, T*, float*, float*, float*, Ws);\
+    template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*);        \
+    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);          \
+    template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws);                    \
+    template int cast_from_f32<T>(hipStream_t, const float*, T*, int64_t);                                           \
+    template int cast_to_f32<T>(hipStream_t, const T*, float*, int64_t);                                             \
+    template int copy2d<T>(hipStream_t, const T*, int, T*, int, int, int);                                           \
+    template int cast2d_from_f32<T>(hipStream_t, const float*, int, T*, int, int, int);                              \
+    template int nhwc_to_flat<T>(hipStream_t, const T*, int, int, int, int, T*, int);                                \
+    template int flat_to_nhwc<T>(hipStream_t, const T*, int, int, int, int, int, T*);                                \
+    template int relu_bwd<T>(hipStream_t, T*, int, const T*, int, int, int);                                         \
+    template int colsum<T>(hipStream_t, const T*, int, int, int, float*, Ws);                                        \
+    template int reparam_fwd<T>(hipStream_t, const float*, const float*, const float*, int, int, T*, int);           \
+    template int reparam_bwd<T>(hipStream_t, const T*, int, const float*, const float*, int, int, float*, float*);   \
+    template int pack<T>(hipStream_t, const PackJob*, int, int64_t);
+
+INST(float)
+INST(bf16)
+#undef INST
+
+}  // namespace ops
+}  // namespace hlmc

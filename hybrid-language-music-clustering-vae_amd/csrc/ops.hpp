@@ -1,0 +1,126 @@
+// Internal op layer: shape-checked launchers for every kernel of the hot path.
+// All tensors are caller-owned device pointers; activations are NHWC (channel fastest).
+#pragma once
+#include "common.hpp"
+
+namespace hlmc {
+
+struct Ws {  // split-K / reduction scratch handed down by the caller
+    float* p;
+    size_t bytes;
+};
+
+namespace ops {
+
+// ---------------------------------------------------------------- GEMM-shaped (gemm_ops.hip)
+// y[B, Hi/2, Wi/2, Co] = conv3x3_s2_p1(x[B,Hi,Wi,Ci]) + bias ; wp packed [Co][3][3][Ci]
+template <typename T>
+int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws);
+template <typename T>
+size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
+
+// y[B, 2Hi, 2Wi, Co] = convT3x3_s2_p1_op1(x[B,Hi,Wi,Ci]) + bias ; wp packed [Co][3][3][Ci]
+// (also the data gradient of a stride-2 conv with the conv weight re-packed [Ci_conv][3][3][Co_conv])
+template <typename T>
+int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws);
+template <typename T>
+size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co);
+
+// dW[M][C][3][3] = sum_{b,r,c} L[b,r,c,m] * Xh[b, 2r-1+kh, 2c-1+kw, ci]   (L low-res [B,Hl,Wl,M], Xh [B,2Hl,2Wl,C])
+template <typename T>
+int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* Xh, int C, float* dW, Ws ws);
+template <typename T>
+size_t wgrad_s2_ws(int B, int Hl, int Wl, int M, int C);
+
+// y[m*ldy + n] (+)= act(sum_k x[m*ldx+k] * w[n*ldw+k] + bias[n]),  act 0 none / 1 relu
+template <typename T, typename OutT>
+int linear(hipStream_t s, const T* x, int ldx, int M, int K, const T* w, int ldw, const float* bias, int N, OutT* y,
+           int ldy, int act, int accumulate, Ws ws);
+template <typename T>
+size_t linear_ws(int M, int K, int N);
+
+// dW[n][k] = sum_b dy[b*lddy+n] * x[b*ldx+k]
+template <typename T>
+int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int Mb, int N, int K, float* dW, Ws ws);
+template <typename T>
+size_t linear_wgrad_ws(int Mb, int N, int K);
+
+// ---------------------------------------------------------------- edge convs with one channel (kernels.hip)
+// y[B,Hi/2,Wi/2,32] = sum_taps x[B,Hi,Wi] * w[co*9+tap] (+ bias)  (conv1 fwd, convT6 dgrad)
+template <typename T>
+int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y);
+// y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel)
+template <typename T>
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y);
+// dW[m*9+tap] = sum L[b,r,c,m] * Xh[b, 2r-1+kh, 2c-1+kw]   (Xh single channel f32)
+template <typename T>
+int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws);
+size_t wgrad_c1_ws(int B, int Hl, int Wl, int M);
+
+// ---------------------------------------------------------------- batch norm / activation (kernels.hip)
+// Train-mode statistics over R rows of an [R][C] map; writes mean / invstd and updates running stats.
+template <typename T>
+int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean, float* run_var,
+             int64_t* nbt, float momentum, float eps, Ws ws);
+size_t bn_ws(int64_t R, int C);
+// Eval-mode statistics from running buffers.
+int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, int C, float eps, float* mean, float* invstd);
+// a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale];  act: 0 lrelu(0.01), 1 relu, 2 none
+template <typename T>
+int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const float* invstd, const float* gamma,
+           const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda);
+// backward through act+BN: dy from da (ld lda); dgamma, dbeta, dbias(sum of dy; nullable)
+template <typename T>
+int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
+               const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
+               float* dbeta, float* dbias, Ws ws);
+
+// ---------------------------------------------------------------- misc elementwise (kernels.hip)
+template <typename T> int cast_from_f32(hipStream_t s, const float* x, T* y, int64_t n);
+template <typename T> int cast_to_f32(hipStream_t s, const T* x, float* y, int64_t n);
+// rows x cols submatrix copy with leading dims (T -> T)
+template <typename T> int copy2d(hipStream_t s, const T* x, int ldx, T* y, int ldy, int rows, int cols);
+template <typename T> int cast2d_from_f32(hipStream_t s, const float* x, int ldx, T* y, int ldy, int rows, int cols);
+// NHWC [B,h,w,C] <-> flat NCHW [B, C*h*w] (ld = row stride of the flat side)
+template <typename T> int nhwc_to_flat(hipStream_t s, const T* x, int B, int h, int w, int C, T* y, int ldy);
+template <typename T> int flat_to_nhwc(hipStream_t s, const T* x, int ldx, int B, int h, int w, int C, T* y);
+// dy[i] *= (y[i] > 0) for an [rows][cols] slice (relu backward on the stored post-relu output)
+template <typename T> int relu_bwd(hipStream_t s, T* dy, int lddy, const T* y, int ldy, int rows, int cols);
+// db[n] = sum_r dy[r*ld + n]
+template <typename T> int colsum(hipStream_t s, const T* dy, int ld, int rows, int cols, float* db, Ws ws);
+size_t colsum_ws(int rows, int cols);
+// z = mu + eps * exp(0.5 logvar)  (z written as T with row stride ldz)
+template <typename T> int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz);
+// dmu += dz ; dlv += dz * eps * 0.5 exp(0.5 lv)
+template <typename T> int reparam_bwd(hipStream_t s, const T* dz, int lddz, const float* lv, const float* eps, int n_rows, int L, float* dmu, float* dlv);
+
+// ---------------------------------------------------------------- loss (kernels.hip)
+// partial sums: out[0] = sum (ra-a)^2, out[1] = sum (rt-t)^2, out[2] = sum(1 + lv - mu^2 - e^lv)  (double)
+int vae_sums(hipStream_t s, const float* ra, const float* a, int64_t na, const float* rt, const float* t, int64_t nt,
+             const float* mu, const float* lv, int64_t nl, double* out3, Ws ws);
+size_t vae_sums_ws(int64_t na, int64_t nt, int64_t nl);
+// gradients: dra = ca*(ra-a), drt = ct*(rt-t), dmu = ck*mu, dlv = ck*(-0.5)*(1 - e^lv)... (see kernels.hip)
+int vae_loss_bwd(hipStream_t s, const float* ra, const float* a, int64_t na, float* dra, const float* rt, const float* t,
+                 int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl, const float* coef, float* dmu,
+                 float* dlv);
+
+// ---------------------------------------------------------------- optimizer / packing (kernels.hip)
+struct AdamArgs {
+    float lr, beta1, beta2, eps, weight_decay;
+    int step;
+};
+int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, float* const* m, float* const* v,
+         const int64_t* numel, AdamArgs a, void* dev_scratch);
+// conv weight [d0][d1][3][3] f32 -> P0 [d0][3][3][d1], P1 [d1][3][3][d0] (T); linear [d0][d1] -> P0 copy, P1 transpose
+struct PackJob {
+    const float* w;
+    void* p0;  // [d0][taps][ld0 >= d1]
+    void* p1;  // [d1][taps][ld1 >= d0]
+    int d0, d1, taps;  // taps 9 (conv) or 1 (linear)
+    int ld0, ld1;
+};
+template <typename T>
+int pack(hipStream_t s, const PackJob* jobs_dev, int njobs, int64_t max_elems);
+
+}  // namespace ops
+}  // namespace hlmc

@@ -1,0 +1,126 @@
+"""Fused VAE train step + data-parallel gradient sync.
+
+One step = the body of the reference's batch loop (src/Convolutional_VAE.py:224-240,
+src/Conditional_VAE.py:321-331): forward -> loss -> backward -> optimizer.step, issued as a fixed
+sequence of libhlmc calls on the current stream with no host synchronisation (the reference's
+per-batch ``loss.item()`` is replaced by device-side loss sums that the caller may read lazily).
+
+Data parallel: one process per GPU; the flat fp32 gradient buffer is all-reduced with SUM over
+``torch.distributed`` (backend "nccl" = RCCL over xGMI on MI355X), i.e. gradients of the loss summed
+over the global batch — the reference's sum-reduced losses make SUM the matching reduction.
+BatchNorm statistics stay per rank (DDP semantics).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from .models import ConditionalVAE, HybridVAE, VAE
+
+
+class Trainer:
+    def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, beta=None, text_weight=None,
+                 process_group=None, distributed=False, grad_dtype=torch.float32):
+        self.model = model
+        self.kind = "simple" if isinstance(model, VAE) else ("cvae" if isinstance(model, ConditionalVAE) else "hybrid")
+        self.net = model._native_net()
+        dev = next(model.parameters()).device
+        self.device = dev
+        self.params = list(model.parameters())
+        self.gflat = model._gflat
+        self.grads = model._grad_views
+        n = self.gflat.numel()
+        self.m = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(n, dtype=torch.float32, device=dev)
+        mv, vv, off = [], [], 0
+        for p in self.params:
+            mv.append(self.m[off:off + p.numel()])
+            vv.append(self.v[off:off + p.numel()])
+            off += p.numel()
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.step_count = 0
+        if beta is None:
+            beta = {"hybrid": 1.0, "cvae": 4.0, "simple": 0.8}[self.kind]
+        if text_weight is None:
+            text_weight = {"hybrid": 350.0, "cvae": 200.0, "simple": 0.0}[self.kind]
+        self.beta, self.text_weight = float(beta), float(text_weight)
+        self.distributed = distributed or process_group is not None
+        self.process_group = process_group
+        self.grad_dtype = grad_dtype
+        self._adam_args = (L.vp_array([p.data_ptr() for p in self.params]),
+                           L.vp_array([g.data_ptr() for g in self.grads]),
+                           L.vp_array([t.data_ptr() for t in mv]), L.vp_array([t.data_ptr() for t in vv]),
+                           L.i64_array([p.numel() for p in self.params]))
+        self._cache = {}
+
+    def _buffers(self, B):
+        if B not in self._cache:
+            dev = self.device
+            m = self.model
+            out = m._alloc_outputs(B, dev)
+            d = {k: torch.empty_like(v) for k, v in out.items()}
+            ws = self.net.new_workspace(B, dev)
+            na = out["recon"].numel()
+            nt = out["recon_text"].numel() if "recon_text" in out else 0
+            nl = out["mu"].numel()
+            lws = torch.empty(max(16, int(L.lib().hlmc_loss_workspace(na, nt, nl))), dtype=torch.uint8, device=dev)
+            sums = torch.zeros(3, dtype=torch.float64, device=dev)
+            if self.kind == "simple":
+                coef = torch.tensor([2.0 / na, 0.0, self.beta / nl], device=dev)
+            else:
+                coef = torch.tensor([2.0, 2.0 * self.text_weight, self.beta], device=dev)
+            self._cache[B] = dict(out=out, d=d, ws=ws, lws=lws, sums=sums, coef=coef, n=(na, nt, nl))
+        return self._cache[B]
+
+    def step(self, in0, in1=None, in2=None, eps=None, dropout=None):
+        """One optimisation step on a batch; returns device float64 sums (sum sq audio err, sum sq text err,
+        sum(1+lv-mu^2-e^lv)) from which the reference's loss tuple follows."""
+        lib = L.lib()
+        s = L.stream()
+        B = in0.shape[0]
+        c = self._buffers(B)
+        out, d = c["out"], c["d"]
+        if eps is None:
+            eps = torch.randn(B, self.model.latent_dim, device=self.device)
+        if self.kind == "simple" and dropout is None:
+            dropout = self.model.make_dropout_mask(B, self.device)
+        L.check(lib.hlmc_net_forward(self.net.h, s, B, 1, L.ptr(in0), L.ptr(in1), L.ptr(in2), L.ptr(eps),
+                                     L.ptr(dropout), L.ptr(out["recon"]), L.ptr(out.get("recon_text")),
+                                     L.ptr(out["mu"]), L.ptr(out["logvar"]), L.ptr(out.get("z")), c["ws"].data_ptr()),
+                "hlmc_net_forward")
+        na, nt, nl = c["n"]
+        rt, t = out.get("recon_text"), (in1 if nt else None)
+        L.check(lib.hlmc_loss_sums(s, L.ptr(out["recon"]), L.ptr(in0), na, L.ptr(rt), L.ptr(t), nt, L.ptr(out["mu"]),
+                                   L.ptr(out["logvar"]), nl, c["sums"].data_ptr(), c["lws"].data_ptr()), "hlmc_loss_sums")
+        L.check(lib.hlmc_loss_backward(s, L.ptr(out["recon"]), L.ptr(in0), na, L.ptr(d["recon"]), L.ptr(rt), L.ptr(t),
+                                       nt, L.ptr(d.get("recon_text")), L.ptr(out["mu"]), L.ptr(out["logvar"]), nl,
+                                       c["coef"].data_ptr(), L.ptr(d["mu"]), L.ptr(d["logvar"])), "hlmc_loss_backward")
+        L.check(lib.hlmc_net_backward(self.net.h, s, B, L.ptr(d["recon"]), L.ptr(d.get("recon_text")), L.ptr(d["mu"]),
+                                      L.ptr(d["logvar"]), c["ws"].data_ptr()), "hlmc_net_backward")
+        if self.distributed:
+            self.allreduce_grads()
+        self.step_count += 1
+        b1, b2 = self.betas
+        L.check(lib.hlmc_adam_step(s, len(self.params), *self._adam_args, float(self.lr), float(b1), float(b2),
+                                   float(self.eps), float(self.wd), self.step_count, None), "hlmc_adam_step")
+        return c["sums"]
+
+    def allreduce_grads(self):
+        """SUM all-reduce of the flat gradient buffer (RCCL under backend 'nccl')."""
+        import torch.distributed as dist
+        if self.grad_dtype == torch.float32:
+            dist.all_reduce(self.gflat, op=dist.ReduceOp.SUM, group=self.process_group)
+        else:
+            g = self.gflat.to(self.grad_dtype)
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.process_group)
+            self.gflat.copy_(g)
+
+    def loss_tuple(self, sums, batch=None):
+        """Host floats (total, l_audio, l_text, kld) from device sums (synchronises)."""
+        s = sums.cpu().tolist()
+        if self.kind == "simple":
+            na, _, nl = self._cache[batch or next(iter(self._cache))]["n"]
+            la, kl = s[0] / na, -0.5 * s[2] / nl
+            return la + self.beta * kl, la, 0.0, kl
+        kld = -0.5 * s[2]
+        return s[0] + self.text_weight * s[1] + self.beta * kld, s[0], s[1], kld

@@ -1,0 +1,196 @@
+/* libhlmc — MI355X (gfx950) hot path of Shahriar1638/Hybrid-Language-Music-Clustering-VAE.
+ *
+ * C ABI: plain device pointers (caller-owned, contiguous, 16-byte aligned), sizes, scalars.
+ * Every call is stream-ordered and asynchronous on `stream` (a hipStream_t; NULL = default stream),
+ * performs no device allocation and no host<->device synchronisation unless stated.
+ * Return 0 (HLMC_OK) on success or a negative hlmc_status; hlmc_last_error() gives a thread-local
+ * message.  The library never aborts the process.
+ *
+ * The reference is pure Python; it has no FFI.  Each entry point below names the reference call it
+ * replaces (file:line in the reference repo) — the Python package in
+ * hybrid-language-music-clustering-vae_amd/ binds them with ctypes.
+ */
+#ifndef HLMC_H_
+#define HLMC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum hlmc_status {
+    HLMC_OK = 0,
+    HLMC_EINVAL = -1, /* bad shape / pointer / argument */
+    HLMC_EHIP = -2,   /* HIP runtime error */
+    HLMC_EUNSUP = -3, /* configuration not supported */
+};
+
+enum hlmc_dtype { HLMC_F32 = 0, HLMC_BF16 = 1 };
+
+int hlmc_version(void);
+const char* hlmc_last_error(void);
+
+/* ============================================================== features
+ * Replaces librosa.feature.melspectrogram + librosa.power_to_db at
+ *   src/1_preprocessing_advanced.py:97-114 and src/1_preprocessing.py:48-58,
+ * librosa.feature.mfcc at src/1_preprocessing.py:61-70, the mean/std pooling at
+ * src/1_preprocessing.py:115-121 and sklearn StandardScaler at src/1_preprocessing_advanced.py:376-382.
+ * STFT: center=True (zero pad n_fft/2), periodic Hann, hop; power |X|^2; Slaney mel (norm='slaney'). */
+typedef struct hlmc_mel_plan hlmc_mel_plan;
+
+int hlmc_mel_plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax, hlmc_mel_plan** out);
+int hlmc_mel_plan_destroy(hlmc_mel_plan* plan);
+/* host copy of the dense [n_mels][1 + n_fft/2] float32 filterbank (librosa.filters.mel) */
+int hlmc_mel_filterbank(const hlmc_mel_plan* plan, float* out_host);
+int64_t hlmc_mel_frames(const hlmc_mel_plan* plan, int64_t n_samples);
+/* bytes of scratch for hlmc_mel_db / hlmc_mfcc */
+int64_t hlmc_mel_workspace(const hlmc_mel_plan* plan, int64_t batch, int64_t n_samples);
+/* power mel spectrogram: pcm [batch][n_samples] f32 -> out [batch][n_mels][T] f32 (ws: >= 8*batch bytes) */
+int hlmc_melspectrogram(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch,
+                        int64_t n_samples, float* out, void* ws);
+/* extract_mel_spectrogram: mel -> power_to_db(ref=max over ALL frames of the clip, amin, top_db)
+ * -> keep the first t_keep frames (pad with the clip minimum if t_keep > T). out [batch][n_mels][t_keep] */
+int hlmc_mel_db(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
+                int64_t t_keep, float amin, float top_db, float* out, void* ws);
+/* librosa.power_to_db on a [batch][per_clip] array: ref_max!=0 -> ref = per-clip max, else ref_value
+ * (ws: >= 8*batch bytes) */
+int hlmc_power_to_db(void* stream, const float* S, int64_t batch, int64_t per_clip, int ref_max, float ref_value,
+                     float amin, float top_db, float* out, void* ws);
+/* librosa.feature.mfcc(n_mfcc): power_to_db(ref=1.0, top_db=80) then DCT-II ortho over mels.
+ * out [batch][n_mfcc][T] */
+int hlmc_mfcc(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
+              int n_mfcc, float* out, void* ws);
+/* mean and std (ddof=0) of each row of x [rows][cols] (the mean/std pooling of the feature vectors) */
+int hlmc_row_mean_std(void* stream, const float* x, int64_t rows, int64_t cols, float* mean, float* std);
+/* StandardScaler fit, two passes with float64 accumulators (sklearn _incremental_mean_and_var):
+ *   pass 1: sum[c] = sum_i x[i][c];  pass 2: corr[c] = sum_i (x - mean), m2[c] = sum_i (x - mean)^2
+ * (all-reduce the outputs of each pass across ranks for a distributed fit). */
+int64_t hlmc_colstats_workspace(int64_t n, int64_t cols);
+int hlmc_colstats_sum(void* stream, const float* x, int64_t n, int64_t cols, double* sum, void* ws);
+int hlmc_colstats_centered(void* stream, const float* x, int64_t n, int64_t cols, const double* mean, double* corr,
+                           double* m2, void* ws);
+/* StandardScaler.transform: y = f32(f32(x - mean) / scale) evaluated in float64; out dtype f32 or bf16 */
+int hlmc_zscore_apply(void* stream, const float* x, int64_t n, int64_t cols, const double* mean, const double* scale,
+                      int out_dtype, void* out);
+
+/* ============================================================== VAE engine
+ * Replaces the nn.Module forward/backward of
+ *   HybridVAE        src/Convolutional_VAE.py:75-185   (kind 0; cfg = {latent, text_dim (0 = audio-only), H, W})
+ *   ConditionalVAE   src/Conditional_VAE.py:109-231    (kind 1; cfg = {latent, text_dim, num_classes, H, W})
+ *   VAE (Simple)     src/Simple_VAE.py:47-105          (kind 2; cfg = {input_dim, latent, n_hidden, h_1..h_n})
+ * and the torch train step of src/Convolutional_VAE.py:224-240.  Parameters are bound in the
+ * reference's registration order (hlmc_net_param_info) as fp32 "master" tensors; dtype selects the
+ * activation / MFMA operand type (HLMC_F32 exact fp32 MFMA, HLMC_BF16 bf16 MFMA with fp32 accumulate). */
+typedef struct hlmc_net hlmc_net;
+enum hlmc_net_kind { HLMC_NET_HYBRID = 0, HLMC_NET_CVAE = 1, HLMC_NET_SIMPLE = 2 };
+
+int hlmc_net_create(int kind, const int64_t* cfg, int ncfg, int dtype, hlmc_net** out);
+int hlmc_net_destroy(hlmc_net* net);
+int hlmc_net_num_params(const hlmc_net* net);
+/* name (NUL-terminated, truncated to cap), ndim and shape (<= 4 dims) of parameter i */
+int hlmc_net_param_info(const hlmc_net* net, int i, char* name, int cap, int* ndim, int64_t* shape);
+/* float buffers: every BatchNorm's running_mean, running_var (in registration order);
+ * num_batches_tracked (int64) is passed separately, one per BatchNorm */
+int hlmc_net_num_bn(const hlmc_net* net);
+int64_t hlmc_net_state_bytes(const hlmc_net* net);
+int64_t hlmc_net_workspace_bytes(const hlmc_net* net, int64_t batch);
+/* params / grads: arrays of num_params device pointers (fp32); running: 2*num_bn device pointers
+ * (mean, var per BN); nbt: num_bn device int64 pointers; state: hlmc_net_state_bytes of device memory */
+int hlmc_net_bind(hlmc_net* net, float* const* params, float* const* grads, float* const* running,
+                  int64_t* const* nbt, void* state);
+/* Forward.  train!=0: BatchNorm batch statistics (running stats updated), dropout mask applied (Simple);
+ * eps [batch][latent] is the reparameterisation noise (host/torch generated, like torch.randn_like).
+ * hybrid/cvae: in0 = audio [B][1][H][W], in1 = text [B][text_dim], in2 = condition [B][C] (cvae);
+ * simple: in0 = x [B][input_dim], dropout = uint8 keep-mask per hidden unit (NULL = no dropout).
+ * outputs: recon [B][...], recon_text [B][text_dim] (hybrid with text, cvae), mu, logvar [B][latent],
+ * z [B][latent] (simple; nullable elsewhere).  Saves activations in ws for hlmc_net_backward. */
+int hlmc_net_forward(hlmc_net* net, void* stream, int64_t batch, int train, const float* in0, const float* in1,
+                     const float* in2, const float* eps, const uint8_t* dropout, float* recon, float* recon_text,
+                     float* mu, float* logvar, float* z, void* ws);
+/* encoder only (latent extraction, src/Convolutional_VAE.py:286-303): mu, logvar */
+int hlmc_net_encode(hlmc_net* net, void* stream, int64_t batch, int train, const float* in0, const float* in1,
+                    const float* in2, float* mu, float* logvar, void* ws);
+/* Backward of the last hlmc_net_forward (same ws): writes (overwrites) all parameter gradients.
+ * d_recon_text may be NULL when the model has no text branch. */
+int hlmc_net_backward(hlmc_net* net, void* stream, int64_t batch, const float* d_recon, const float* d_recon_text,
+                      const float* d_mu, const float* d_logvar, void* ws);
+
+/* ============================================================== losses
+ * loss_function (src/Convolutional_VAE.py:187-194), cvae_loss_function (src/Conditional_VAE.py:233-246),
+ * vae_loss (src/Simple_VAE.py:108-114).  sums3 (device, double[3]) receives
+ *   { sum (ra-a)^2, sum (rt-t)^2, sum (1 + lv - mu^2 - exp lv) }; the caller forms the reference's tuple. */
+int hlmc_loss_sums(void* stream, const float* ra, const float* a, int64_t na, const float* rt, const float* t,
+                   int64_t nt, const float* mu, const float* lv, int64_t nl, double* sums3, void* ws);
+int64_t hlmc_loss_workspace(int64_t na, int64_t nt, int64_t nl);
+/* coef (DEVICE float[3]) = {ca, ct, ck}:  d ra = ca (ra - a), d rt = ct (rt - t), d mu = ck mu,
+ * d lv = -0.5 ck (1 - exp lv).  For the summed hybrid loss with upstream grads (gT, gA, gX, gK) of
+ * (total, l_audio, l_text, kld): ca = 2 (gT + gA), ct = 2 (w_text gT + gX), ck = beta gT + gK. */
+int hlmc_loss_backward(void* stream, const float* ra, const float* a, int64_t na, float* dra, const float* rt,
+                       const float* t, int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl,
+                       const float* coef, float* dmu, float* dlv);
+
+/* ============================================================== optimizer
+ * torch.optim.Adam(lr, betas, eps, weight_decay) step (src/Convolutional_VAE.py:208,235) over
+ * n tensors in one launch.  ptr arrays are HOST arrays of device pointers. */
+int hlmc_adam_step(void* stream, int n, float* const* params, const float* const* grads, float* const* exp_avg,
+                   float* const* exp_avg_sq, const int64_t* numel, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int step, void* scratch);
+int64_t hlmc_adam_scratch_bytes(int n);
+
+/* ============================================================== K-Means (sklearn semantics)
+ * Device kernels under the Python KMeans host (src/Convolutional_VAE.py:317-319,
+ * src/Conditional_VAE.py:293-295, :528; src/Simple_VAE.py:244-261).  X row-major float32 [n][d]. */
+/* X_mean = sequential float32 column sums / n (numpy mean(axis=0) order); Xc = X - X_mean;
+ * var (nullable) = np.var(X, axis=0) in the same order (sklearn's tolerance input) */
+int hlmc_km_center(void* stream, const float* X, int64_t n, int d, float* mean, float* var, float* Xc);
+/* out[t][i] = float32(max(0, ||x_c||^2 - 2 x_c.x_i + ||x_i||^2)) evaluated in float64, c = cand[t]
+ * (cand is a HOST array of ncand <= 16 row indices) — sklearn _euclidean_distances_upcast */
+int hlmc_km_sqdist_rows(void* stream, const float* X, int64_t n, int d, const int64_t* cand, int ncand, float* out);
+/* E-step: labels[i] = argmin_j (||c_j||^2 + (-2) x_i.c_j) (float32, first minimum);
+ * n_changed (device int32) += count(labels != labels_old) when labels_old != NULL */
+int hlmc_km_assign(void* stream, const float* X, int64_t n, int d, const float* centers, int k, int32_t* labels,
+                   const int32_t* labels_old, int32_t* n_changed);
+/* M-step sums in index order (float32, as sklearn's single-thread loop): sums [k][d], weight [k] */
+int hlmc_km_sums(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sums,
+                 float* weight);
+/* per-row ||x_i - c_{l_i}||^2 in sklearn's _euclidean_dense_dense float32 order -> out [n] */
+int hlmc_km_rowdist(void* stream, const float* X, int64_t n, int d, const float* centers, const int32_t* labels,
+                    float* out);
+/* sum of the row distances accumulated sequentially in float32 (sklearn _inertia_dense) -> out[0]; tmp [n] */
+int hlmc_km_inertia(void* stream, const float* X, int64_t n, int d, const float* centers, const int32_t* labels,
+                    float* out, float* tmp);
+
+
+/* ============================================================== op-level entry points
+ * The kernels hlmc_net_* is built from, on NHWC activations (dtype HLMC_F32 / HLMC_BF16 for x, y, packed
+ * weights; bias / dW always f32).  ws = split-K scratch (>= 256 MiB is always enough at B <= 256).
+ *   conv_s2   y[B,Hi/2,Wi/2,Co] = Conv2d(k3,s2,p1)(x[B,Hi,Wi,Ci]) + bias;  wp [Co][3][3][Ci]
+ *   subpixel  y[B,2Hi,2Wi,Co]  = ConvTranspose2d(k3,s2,p1,op1)(x[B,Hi,Wi,Ci]) + bias; wp [Co][3][3][Ci]
+ *             (w_torch[Ci][Co][kh][kw] -> wp[co][kh][kw][ci]; also the data gradient of conv_s2)
+ *   wgrad_s2  dW[M][C][3][3] = sum_{b,r,c} L[b,r,c,m] Xh[b,2r-1+kh,2c-1+kw,ci]   (L [B,Hl,Wl,M], Xh [B,2Hl,2Wl,C])
+ *   linear    y[m*ldy+n] (+)= act(sum_k x[m*ldx+k] w[n*ldw+k] + bias[n]), act 0 none / 1 relu
+ *   linear_wgrad dW[n][k] = sum_b dy[b*lddy+n] x[b*ldx+k]
+ *   conv_c1_s2 / convT_c1 / wgrad_c1: the single-channel first / last layers (f32 input image). */
+int hlmc_op_conv_s2(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
+                    const float* bias, int Co, void* y, void* ws, int64_t ws_bytes);
+int hlmc_op_subpixel(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
+                     const float* bias, int Co, void* y, void* ws, int64_t ws_bytes);
+int hlmc_op_wgrad_s2(void* stream, int dtype, const void* L, int B, int Hl, int Wl, int M, const void* Xh, int C,
+                     float* dW, void* ws, int64_t ws_bytes);
+int hlmc_op_linear(void* stream, int dtype, const void* x, int ldx, int M, int K, const void* w, int ldw,
+                   const float* bias, int N, void* y, int ldy, int act, int accumulate, int out_f32, void* ws,
+                   int64_t ws_bytes);
+int hlmc_op_linear_wgrad(void* stream, int dtype, const void* dy, int lddy, const void* x, int ldx, int Mb, int N,
+                         int K, float* dW, void* ws, int64_t ws_bytes);
+int hlmc_op_conv_c1_s2(void* stream, int dtype, const float* x, int B, int Hi, int Wi, const float* w,
+                       const float* bias, int Co, void* y);
+int hlmc_op_convT_c1(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const float* w,
+                     const float* bias, float* y);
+int hlmc_op_wgrad_c1(void* stream, int dtype, const void* L, int B, int Hl, int Wl, int M, const float* Xh,
+                     float* dW, void* ws, int64_t ws_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HLMC_H_ */

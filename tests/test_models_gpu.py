@@ -1,0 +1,203 @@
+"""Model-level parity: hlmc_amd.{HybridVAE, ConditionalVAE, VAE} (HIP engine, fp32 mode) vs the torch-CPU
+oracle (oracle/models_oracle.py, itself pinned bit-exact to the AST-loaded reference classes by
+tests/golden/make_golden.py) on the golden fixture cases, from identical weights / inputs / eps.
+
+Tolerances (fp32, per step from shared state — SURVEY §0.6):
+  * mu, logvar, reconstructions, ELBO terms: relative error <= 1e-4 (north_star), typically ~1e-6.
+  * parameter gradients: relative L2 <= 1e-3 per tensor; conv biases that feed train-mode BatchNorm
+    have a mathematically-zero gradient (pure rounding noise) and are checked absolutely against the
+    scale of their layer's weight gradient.
+  * BatchNorm running statistics after the step: relative <= 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+import hlmc_amd
+from oracle import models_oracle as OM
+from tests.golden import fixtures as FX
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def _bias_feeds_bn(model, name):
+    """conv / linear biases directly followed by a BatchNorm (zero true gradient)."""
+    mods = dict(model.named_modules())
+    parent, idx, leaf = name.rsplit(".", 2) if name.count(".") >= 2 else (None, None, None)
+    if leaf != "bias" or parent is None:
+        return False
+    seq = mods.get(parent)
+    if not isinstance(seq, torch.nn.Sequential):
+        return False
+    i = int(idx)
+    return i + 1 < len(seq) and isinstance(seq[i + 1], torch.nn.modules.batchnorm._BatchNorm) and not isinstance(
+        seq[i], torch.nn.modules.batchnorm._BatchNorm)
+
+
+def build(case, dtype="fp32"):
+    ctor = FX.oracle_ctor(case)
+    torch.manual_seed(42)
+    ora = {"hybrid": OM.HybridVAE, "cvae": OM.ConditionalVAE, "simple": OM.VAE}[case["kind"]](**ctor)
+    torch.manual_seed(42)
+    cls = {"hybrid": hlmc_amd.HybridVAE, "cvae": hlmc_amd.ConditionalVAE, "simple": hlmc_amd.VAE}[case["kind"]]
+    ours = cls(**ctor, compute_dtype=dtype)
+    so, sm = ora.state_dict(), ours.state_dict()
+    assert list(so) == list(sm)
+    for k in so:
+        assert torch.equal(so[k], sm[k]), f"init differs at {k}"
+    return ora, ours.cuda()
+
+
+def run_oracle_step(case, ora, ins, eps, masks=None):
+    ora.train()
+    if case["kind"] == "simple":
+        hooks = []
+        it = iter(masks)
+
+        def hook(mod, inp, out):
+            m = next(it)
+            return inp[0] * m.to(inp[0].dtype) / 0.8
+
+        for mod in ora.modules():
+            if isinstance(mod, torch.nn.Dropout):
+                hooks.append(mod.register_forward_hook(hook))
+        out = ora(*ins, eps=eps)
+        for h in hooks:
+            h.remove()
+        loss = OM.vae_loss(out[0], ins[0], out[1], out[2], beta=0.8)
+    else:
+        out = ora(*ins, eps=eps)
+        if case["kind"] == "hybrid":
+            loss = OM.loss_function(out[0], ins[0], out[1], ins[1], out[2], out[3])
+        else:
+            loss = OM.cvae_loss_function(out[0], ins[0], out[1], ins[1], out[2], out[3], beta=4.0)
+    loss[0].backward()
+    return out, loss
+
+
+def run_ours_step(case, ours, ins, eps, mask=None):
+    ours.train()
+    cins = [t.cuda() for t in ins]
+    if case["kind"] == "simple":
+        out = ours(cins[0], eps=eps.cuda(), dropout_mask=mask)
+        loss = hlmc_amd.vae_loss(out[0], cins[0], out[1], out[2], beta=0.8)
+    else:
+        out = ours(*cins, eps=eps.cuda())
+        if case["kind"] == "hybrid":
+            loss = hlmc_amd.loss_function(out[0], cins[0], out[1], cins[1], out[2], out[3])
+        else:
+            loss = hlmc_amd.cvae_loss_function(out[0], cins[0], out[1], cins[1], out[2], out[3], beta=4.0)
+    loss[0].backward()
+    return out, loss
+
+
+def simple_masks(case, B, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    widths = case["ctor"]["hidden_dims"] + case["ctor"]["hidden_dims"][::-1]
+    masks = [(torch.rand(B, w, generator=g) >= 0.2) for w in widths]
+    flat = torch.cat([m.reshape(-1) for m in masks]).to(torch.uint8).cuda()
+    return masks, flat
+
+
+def compare_step(case, ora, ours, tol_out=1e-4, tol_grad=1e-3):
+    ins, eps = FX.inputs_fn(case)(0)
+    masks, flat = (simple_masks(case, case["B"]) if case["kind"] == "simple" else (None, None))
+    o_out, o_loss = run_oracle_step(case, ora, ins, eps, masks)
+    m_out, m_loss = run_ours_step(case, ours, ins, eps, flat)
+    for i, (a, b) in enumerate(zip(m_out, o_out)):
+        if a is None or b is None or (case["kind"] == "simple" and i == 3):
+            continue
+        assert rel(a.detach(), b.detach()) < tol_out, f"output {i}: {rel(a.detach(), b.detach())}"
+    for i, (a, b) in enumerate(zip(m_loss, o_loss)):
+        if float(b) != 0.0:
+            assert abs(float(a) - float(b)) <= tol_out * abs(float(b)) + 1e-6, f"loss {i}: {float(a)} vs {float(b)}"
+    onames = dict(ora.named_parameters())
+    mparams = dict(ours.named_parameters())
+    for name, po in onames.items():
+        gm, go = mparams[name].grad, po.grad
+        assert gm is not None, name
+        if _bias_feeds_bn(ora, name):
+            wname = name[:-4] + "weight"
+            scale = float(onames[wname].grad.abs().max())
+            assert float((gm.cpu() - go).abs().max()) <= 1e-4 * scale + 1e-6, name
+        else:
+            assert rel(gm, go) < tol_grad, f"grad {name}: {rel(gm, go)}"
+    for (n, bo), (_, bm) in zip(ora.named_buffers(), ours.named_buffers()):
+        if bo.dtype.is_floating_point:
+            assert rel(bm, bo) < tol_out, f"buffer {n}: {rel(bm, bo)}"
+        else:
+            assert torch.equal(bm.cpu(), bo), n
+    return o_loss, m_loss
+
+
+@pytest.mark.parametrize("name", ["hybrid_128x128_td768", "hybrid_128x128_td384", "cvae_128x128", "simple_370",
+                                  "hybrid_128x1024_td768", "cvae_128x1024"])
+def test_model_step_matches_oracle(cuda, name):
+    case = FX.case_by_name(name)
+    ora, ours = build(case)
+    o_loss, m_loss = compare_step(case, ora, ours)
+    # the fixture pins the oracle itself (bit-exact to the reference at generation time)
+    fx = np.load(f"tests/golden/model_{name}.npz")
+    if case["kind"] != "simple":
+        np.testing.assert_allclose([float(t) for t in m_loss], fx["loss_step0"], rtol=1e-4, atol=1e-6)
+
+
+def test_hybrid_audio_only_and_adam(cuda):
+    """Audio-only ConvVAE (BASELINE config[1]) — one fwd/bwd + Adam step vs the oracle + torch Adam."""
+    ctor = dict(latent_dim=128, text_dim=768, input_hw=(128, 128), audio_only=True)
+    torch.manual_seed(42)
+    ora = OM.HybridVAE(**ctor)
+    torch.manual_seed(42)
+    ours = hlmc_amd.HybridVAE(**ctor).cuda()
+    opt_o = torch.optim.Adam(ora.parameters(), lr=1e-4)
+    opt_m = hlmc_amd.Adam(ours.parameters(), lr=1e-4)
+    g = torch.Generator().manual_seed(3)
+    audio = torch.randn(4, 1, 128, 128, generator=g)
+    eps = torch.randn(4, 128, generator=g)
+    o = ora(audio, None, eps=eps)
+    lo = OM.loss_function(o[0], audio, None, None, o[2], o[3])
+    lo[0].backward()
+    m = ours(audio.cuda(), None, eps=eps.cuda())
+    lm = hlmc_amd.loss_function(m[0], audio.cuda(), None, None, m[2], m[3])
+    lm[0].backward()
+    assert rel(m[2].detach(), o[2].detach()) < 1e-4
+    assert abs(float(lm[0]) - float(lo[0])) < 1e-4 * abs(float(lo[0]))
+    opt_o.step()
+    opt_m.step()
+    on = dict(ora.named_parameters())
+    for n, p in ours.named_parameters():
+        d = (p.detach().cpu() - on[n].detach()).abs().max().item()
+        # first Adam step moves each weight by ~lr * sign(g); sign flips of near-zero grads cost <= 2 lr
+        assert d <= (2.1e-4 if _bias_feeds_bn(ora, n) else 2e-5), (n, d)
+
+
+def test_eval_encode_matches_oracle(cuda):
+    case = FX.case_by_name("hybrid_128x128_td768")
+    ora, ours = build(case)
+    ins, _ = FX.inputs_fn(case)(0)
+    ora.eval()
+    ours.eval()
+    with torch.no_grad():
+        mo, lo = ora.encode(*ins)
+        mm, lm = ours.encode(*[t.cuda() for t in ins])
+    assert rel(mm, mo) < 1e-5 and rel(lm, lo) < 1e-5
+
+
+def test_bf16_mode_tracks_fp32(cuda):
+    """Throughput mode: same model in bf16 activations stays close to the fp32 oracle (loose bound)."""
+    case = FX.case_by_name("hybrid_128x128_td768")
+    ora, ours = build(case, "bf16")
+    ins, eps = FX.inputs_fn(case)(0)
+    o_out, o_loss = run_oracle_step(case, ora, ins, eps)
+    m_out, m_loss = run_ours_step(case, ours, ins, eps)
+    assert rel(m_out[2].detach(), o_out[2].detach()) < 3e-2
+    assert abs(float(m_loss[0]) - float(o_loss[0])) < 2e-2 * abs(float(o_loss[0]))
+    gm = torch.cat([p.grad.reshape(-1).cpu() for p in ours.parameters()])
+    go = torch.cat([p.grad.reshape(-1) for p in ora.parameters()])
+    assert rel(gm, go) < 5e-2

@@ -1,0 +1,181 @@
+"""Op-level parity of the HIP GEMM families vs torch CPU float64 references (NHWC <-> NCHW).
+
+fp32 path (exact-fp32 MFMA): relative L2 error <= 1e-5.  bf16 path: operands rounded to bf16 on
+both sides, fp32 accumulation; relative L2 error <= 1e-2 (bf16 output rounding ~4e-3)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import hlmc_amd
+from hlmc_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+DT = {"fp32": (L.HLMC_F32, torch.float32, 1e-5), "bf16": (L.HLMC_BF16, torch.bfloat16, 1e-2)}
+WS_BYTES = 512 << 20
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+def q(t, dt):  # round to the device dtype and back (reference sees the same operands)
+    return t.to(dt).to(torch.float64)
+
+
+@pytest.fixture(scope="module")
+def ws(cuda):
+    return torch.empty(WS_BYTES, dtype=torch.uint8, device=cuda)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,Hi,Wi,Ci,Co", [(2, 16, 16, 32, 64), (2, 8, 8, 64, 128), (3, 4, 4, 128, 256),
+                                          (2, 4, 4, 256, 512), (2, 2, 2, 512, 512), (1, 8, 32, 32, 32),
+                                          (5, 4, 8, 64, 64)])
+def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
+    code, tdt, tol = DT[dt]
+    g = torch.Generator().manual_seed(B * 1000 + Ci)
+    x = torch.randn(B, Hi, Wi, Ci, generator=g)
+    w = torch.randn(Co, Ci, 3, 3, generator=g) / (3 * Ci ** 0.5)
+    b = torch.randn(Co, generator=g)
+    ref = F.conv2d(q(x, tdt).permute(0, 3, 1, 2), q(w, tdt), b.double(), stride=2, padding=1).permute(0, 2, 3, 1)
+    xd = x.to(cuda, tdt).contiguous()
+    wp = w.permute(0, 2, 3, 1).contiguous().to(cuda, tdt)
+    y = torch.empty(B, Hi // 2, Wi // 2, Co, dtype=tdt, device=cuda)
+    L.check(L.lib().hlmc_op_conv_s2(L.stream(), code, xd.data_ptr(), B, Hi, Wi, Ci, wp.data_ptr(),
+                                    b.to(cuda).data_ptr(), Co, y.data_ptr(), ws.data_ptr(), WS_BYTES))
+    assert rel(y, ref) < tol
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,Hi,Wi,Ci,Co", [(2, 2, 2, 512, 512), (2, 4, 4, 512, 256), (2, 8, 8, 256, 128),
+                                          (3, 16, 16, 128, 64), (2, 32, 32, 64, 32), (1, 2, 16, 512, 512),
+                                          (2, 4, 4, 32, 64)])
+def test_subpixel_convT(cuda, ws, dt, B, Hi, Wi, Ci, Co):
+    code, tdt, tol = DT[dt]
+    g = torch.Generator().manual_seed(B * 7 + Ci + Co)
+    x = torch.randn(B, Hi, Wi, Ci, generator=g)
+    w = torch.randn(Ci, Co, 3, 3, generator=g) / (3 * Ci ** 0.5)   # ConvTranspose2d weight layout
+    b = torch.randn(Co, generator=g)
+    ref = F.conv_transpose2d(q(x, tdt).permute(0, 3, 1, 2), q(w, tdt), b.double(), stride=2, padding=1,
+                             output_padding=1).permute(0, 2, 3, 1)
+    xd = x.to(cuda, tdt).contiguous()
+    wp = w.permute(1, 2, 3, 0).contiguous().to(cuda, tdt)           # [Co][kh][kw][Ci]
+    y = torch.empty(B, 2 * Hi, 2 * Wi, Co, dtype=tdt, device=cuda)
+    L.check(L.lib().hlmc_op_subpixel(L.stream(), code, xd.data_ptr(), B, Hi, Wi, Ci, wp.data_ptr(),
+                                     b.to(cuda).data_ptr(), Co, y.data_ptr(), ws.data_ptr(), WS_BYTES))
+    assert rel(y, ref) < tol
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("B,Hl,Wl,M,C", [(2, 8, 8, 64, 32), (2, 4, 4, 128, 64), (2, 2, 2, 512, 256),
+                                        (3, 1, 1, 512, 512), (2, 16, 16, 32, 64), (4, 2, 8, 256, 128)])
+def test_wgrad_s2_conv(cuda, ws, dt, B, Hl, Wl, M, C):
+    """Conv2d weight gradient: L = dY (low-res, M=Co), Xh = X (high-res, C=Ci)."""
+    code, tdt, tol = DT[dt]
+    g = torch.Generator().manual_seed(M + C + B)
+    dy = torch.randn(B, Hl, Wl, M, generator=g)
+    x = torch.randn(B, 2 * Hl, 2 * Wl, C, generator=g)
+    ref = torch.nn.grad.conv2d_weight(q(x, tdt).permute(0, 3, 1, 2), (M, C, 3, 3), q(dy, tdt).permute(0, 3, 1, 2),
+                                      stride=2, padding=1)
+    dW = torch.empty(M, C, 3, 3, device=cuda)
+    L.check(L.lib().hlmc_op_wgrad_s2(L.stream(), code, dy.to(cuda, tdt).contiguous().data_ptr(), B, Hl, Wl, M,
+                                     x.to(cuda, tdt).contiguous().data_ptr(), C, dW.data_ptr(), ws.data_ptr(),
+                                     WS_BYTES))
+    assert rel(dW, ref) < (1e-5 if dt == "fp32" else 5e-3)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_wgrad_s2_convT(cuda, ws, dt):
+    """ConvTranspose2d weight gradient: L = X (low-res input, M=Ci), Xh = dY (high-res, C=Co)."""
+    code, tdt, tol = DT[dt]
+    B, Hl, Wl, Ci, Co = 2, 4, 4, 128, 64
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, Hl, Wl, Ci, generator=g)
+    dy = torch.randn(B, 2 * Hl, 2 * Wl, Co, generator=g)
+    w = torch.zeros(Ci, Co, 3, 3, dtype=torch.float64, requires_grad=True)
+    out = F.conv_transpose2d(q(x, tdt).permute(0, 3, 1, 2), w, stride=2, padding=1, output_padding=1)
+    out.backward(q(dy, tdt).permute(0, 3, 1, 2))
+    dW = torch.empty(Ci, Co, 3, 3, device=cuda)
+    L.check(L.lib().hlmc_op_wgrad_s2(L.stream(), code, x.to(cuda, tdt).contiguous().data_ptr(), B, Hl, Wl, Ci,
+                                     dy.to(cuda, tdt).contiguous().data_ptr(), Co, dW.data_ptr(), ws.data_ptr(),
+                                     WS_BYTES))
+    assert rel(dW, w.grad) < (1e-5 if dt == "fp32" else 5e-3)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,K,N,ldx,act,acc", [(4, 768, 256, 768, 0, 0), (256, 2048, 1024, 2048, 0, 0),
+                                              (5, 370, 128, 376, 1, 0), (256, 2314, 64, 2320, 0, 1),
+                                              (33, 128, 1152, 136, 1, 0), (256, 74, 2304, 80, 0, 0)])
+def test_linear(cuda, ws, dt, M, K, N, ldx, act, acc):
+    code, tdt, tol = DT[dt]
+    g = torch.Generator().manual_seed(M + K + N)
+    x = torch.randn(M, ldx, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    y0 = torch.randn(M, N, generator=g)
+    ref = q(x[:, :K], tdt) @ q(w, tdt).T + b.double()
+    if act:
+        ref = ref.clamp_min(0)
+    if acc:
+        ref = ref + q(y0, tdt)
+    ldw = ((K + 7) // 8) * 8
+    wpad = torch.zeros(N, ldw)
+    wpad[:, :K] = w
+    y = y0.to(cuda, tdt).contiguous()
+    L.check(L.lib().hlmc_op_linear(L.stream(), code, x.to(cuda, tdt).contiguous().data_ptr(), ldx, M, K,
+                                   wpad.to(cuda, tdt).data_ptr(), ldw, b.to(cuda).data_ptr(), N, y.data_ptr(), N, act,
+                                   acc, 0, ws.data_ptr(), WS_BYTES))
+    assert rel(y, ref) < tol
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("Mb,N,K", [(4, 256, 768), (256, 1024, 2048), (32, 128, 370), (256, 64, 2314),
+                                    (7, 2048, 1024)])
+def test_linear_wgrad(cuda, ws, dt, Mb, N, K):
+    code, tdt, tol = DT[dt]
+    g = torch.Generator().manual_seed(Mb + N + K)
+    ldd, ldx = ((N + 7) // 8) * 8, ((K + 7) // 8) * 8
+    dy = torch.randn(Mb, ldd, generator=g)
+    x = torch.randn(Mb, ldx, generator=g)
+    ref = q(dy[:, :N], tdt).T @ q(x[:, :K], tdt)
+    dW = torch.empty(N, K, device=cuda)
+    L.check(L.lib().hlmc_op_linear_wgrad(L.stream(), code, dy.to(cuda, tdt).contiguous().data_ptr(), ldd,
+                                         x.to(cuda, tdt).contiguous().data_ptr(), ldx, Mb, N, K, dW.data_ptr(),
+                                         ws.data_ptr(), WS_BYTES))
+    assert rel(dW, ref) < (1e-5 if dt == "fp32" else 5e-3)
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_edge_convs(cuda, ws, dt):
+    code, tdt, tol = DT[dt]
+    g = torch.Generator().manual_seed(9)
+    B, H, W = 3, 16, 32
+    img = torch.randn(B, H, W, generator=g)
+    w1 = torch.randn(32, 1, 3, 3, generator=g) / 3
+    b1 = torch.randn(32, generator=g)
+    # conv1 forward
+    ref = F.conv2d(img.double()[:, None], w1.double(), b1.double(), stride=2, padding=1).permute(0, 2, 3, 1)
+    y = torch.empty(B, H // 2, W // 2, 32, dtype=tdt, device=cuda)
+    L.check(L.lib().hlmc_op_conv_c1_s2(L.stream(), code, img.to(cuda).data_ptr(), B, H, W, w1.to(cuda).data_ptr(),
+                                       b1.to(cuda).data_ptr(), 32, y.data_ptr()))
+    assert rel(y, ref) < (1e-6 if dt == "fp32" else 1e-2)
+    # last convT (32 -> 1)
+    a = torch.randn(B, H // 2, W // 2, 32, generator=g)
+    wT = torch.randn(32, 1, 3, 3, generator=g) / 10
+    bT = torch.randn(1, generator=g)
+    refT = F.conv_transpose2d(q(a, tdt).permute(0, 3, 1, 2), wT.double(), bT.double(), stride=2, padding=1,
+                              output_padding=1)[:, 0]
+    out = torch.empty(B, H, W, device=cuda)
+    L.check(L.lib().hlmc_op_convT_c1(L.stream(), code, a.to(cuda, tdt).contiguous().data_ptr(), B, H // 2, W // 2,
+                                     32, wT.to(cuda).data_ptr(), bT.to(cuda).data_ptr(), out.data_ptr()))
+    assert rel(out, refT) < 1e-6
+    # weight gradients of both (one-channel high-res side)
+    dy = torch.randn(B, H // 2, W // 2, 32, generator=g)
+    refw = torch.nn.grad.conv2d_weight(img.double()[:, None], (32, 1, 3, 3), q(dy, tdt).permute(0, 3, 1, 2),
+                                       stride=2, padding=1)
+    dW = torch.empty(32, 1, 3, 3, device=cuda)
+    L.check(L.lib().hlmc_op_wgrad_c1(L.stream(), code, dy.to(cuda, tdt).contiguous().data_ptr(), B, H // 2, W // 2,
+                                     32, img.to(cuda).data_ptr(), dW.data_ptr(), ws.data_ptr(), WS_BYTES))
+    assert rel(dW, refw) < 1e-5

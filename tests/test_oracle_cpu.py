@@ -1,0 +1,90 @@
+"""CPU checks of the oracle itself against the reference's pins and the committed golden fixtures."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import kmeans_oracle as KO
+from oracle import mel_oracle as MO
+from oracle import models_oracle as OM
+from tests.golden import fixtures as FX
+
+
+def test_librosa_documented_filterbank_value():
+    # librosa docs: filters.mel(sr=22050, n_fft=2048)[0, 1] ~= 0.016; 2018 non-zeros; band 0 = bins 1..4
+    W = MO.mel_filterbank()
+    assert abs(W[0, 1] - 0.016) < 5e-4
+    assert (W > 0).sum() == 2018
+    nz0 = np.nonzero(W[0])[0]
+    nz127 = np.nonzero(W[127])[0]
+    assert (nz0[0], nz0[-1]) == (1, 4) and (nz127[0], nz127[-1]) == (971, 1023)
+
+
+def test_frames_and_shapes():
+    assert MO.n_frames(65024) == 128 and MO.n_frames(661500) == 1292
+    y = MO.synthetic_pcm(1, 65024, seed=1)[0]
+    assert MO.extract_mel_spectrogram(y).shape == (128, 128)
+    assert MO.extract_mel_spectrogram(y, fixed_time_steps=1024).shape == (128, 1024)
+    assert MO.mfcc(y).shape == (40, 128)
+
+
+def test_mel_fixture_reproduces():
+    fx = np.load("tests/golden/features.npz")
+    y = MO.synthetic_pcm(2, 65024, seed=7)
+    np.testing.assert_array_equal(np.stack([MO.extract_mel_spectrogram(c) for c in y]), fx["mel_db"])
+    np.testing.assert_array_equal(MO.mel_filterbank(), fx["mel_basis"])
+
+
+def test_db_properties():
+    y = MO.synthetic_pcm(1, 65024, seed=3)[0]
+    db = MO.extract_mel_spectrogram(y)
+    assert db.max() == 0.0 and db.min() >= -80.0
+    assert np.all(MO.extract_mel_spectrogram(np.zeros(65024, np.float32)) == 0.0)
+
+
+@pytest.mark.parametrize("case", FX.KMEANS_CASES[:4], ids=lambda c: f"n{c[0]}_d{c[1]}_k{c[3]}")
+def test_kmeans_oracle_matches_sklearn_fixture(case):
+    n, d, centers, k, n_init = case
+    X = FX.blobs(n, d, centers, seed=n + d + k)
+    fx = np.load(f"tests/golden/kmeans_n{n}_d{d}_k{k}_i{n_init}.npz")
+    km = KO.KMeans(k, random_state=42, n_init=n_init).fit(X)
+    np.testing.assert_array_equal(km.labels_, fx["labels"])
+    assert km.n_iter_ == int(fx["n_iter"])
+
+
+def test_scaler_oracle_matches_fixture():
+    fx = np.load("tests/golden/features.npz")
+    rng = np.random.default_rng(11)
+    cols = (rng.standard_normal((64, 300)) * rng.uniform(0.1, 5, 300) + rng.uniform(-3, 3, 300)).astype(np.float32)
+    cols[:, 5] = 2.5
+    m, v, s = KO.standard_scaler_fit(cols)
+    np.testing.assert_array_equal(s, fx["scaler_scale"])
+    np.testing.assert_array_equal(KO.standard_scaler_transform(cols, m, s), fx["scaler_out"])
+
+
+@pytest.mark.parametrize("name", ["hybrid_128x128_td768", "cvae_128x128", "simple_370"])
+def test_model_oracle_reproduces_fixture(name):
+    case = FX.case_by_name(name)
+    fx = np.load(f"tests/golden/model_{name}.npz")
+    torch.manual_seed(42)
+    m = {"hybrid": OM.HybridVAE, "cvae": OM.ConditionalVAE, "simple": OM.VAE}[case["kind"]](**FX.oracle_ctor(case))
+    assert [n for n, _ in m.named_parameters()] == list(fx["param_names"])
+    np.testing.assert_array_equal(FX.param_summary(m), fx["param_checksum_init"])
+    ins, eps = FX.inputs_fn(case)(0)
+    torch.manual_seed(7)
+    m.train()
+    out = m(*ins, eps=eps)
+    if case["kind"] == "simple":
+        loss = OM.vae_loss(out[0], ins[0], out[1], out[2], beta=0.8)
+    elif case["kind"] == "hybrid":
+        loss = OM.loss_function(out[0], ins[0], out[1], ins[1], out[2], out[3])
+    else:
+        loss = OM.cvae_loss_function(out[0], ins[0], out[1], ins[1], out[2], out[3], beta=4.0)
+    np.testing.assert_allclose([float(t) for t in loss], fx["loss_step0"], rtol=1e-6)
+    loss[0].backward()
+    np.testing.assert_allclose(FX.grad_summary(m), fx["grad_summary"], rtol=1e-5, atol=1e-7)
+
+
+def test_native_shapes_match_reference_at_128x1024():
+    torch.manual_seed(42)
+    m = OM.HybridVAE()  # reference default (128 x 1024)
+    assert m.audio_fc.weight.shape == (1024, 16384) and sum(p.numel() for p in m.parameters()) == 43272065

@@ -52,105 +52,123 @@ constexpr int kFFT = 1024;  // complex points (n_fft = 2048 real)
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
 
-// 1024-point complex FFT (forward) of buf in LDS, Stockham radix-4, result in buf.  256 threads.
-__device__ void fft1024(float2* __restrict__ buf, float2* __restrict__ tmp, const float2* __restrict__ tw) {
-    float2* src = buf;
-    float2* dst = tmp;
-    const int j = threadIdx.x;  // butterfly index 0..255
-#pragma unroll
-    for (int Ns = 1; Ns < kFFT; Ns *= 4) {
-        const int k = j % Ns;
-        float2 a[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) a[r] = src[j + r * (kFFT / 4)];
-        // twiddle e^{-2 pi i k r / (4 Ns)} = tw[(k r kFFT / (4 Ns)) mod kFFT]
-        const int step = kFFT / (4 * Ns);
-#pragma unroll
-        for (int r = 1; r < 4; ++r) a[r] = cmul(a[r], tw[(k * r * step) & (kFFT - 1)]);
-        const float2 b0 = make_float2(a[0].x + a[2].x, a[0].y + a[2].y);
-        const float2 b1 = make_float2(a[0].x - a[2].x, a[0].y - a[2].y);
-        const float2 b2 = make_float2(a[1].x + a[3].x, a[1].y + a[3].y);
-        const float2 b3 = make_float2(a[1].y - a[3].y, -(a[1].x - a[3].x));  // -i (a1 - a3)
-        const int d = (j / Ns) * Ns * 4 + k;
-        dst[d] = make_float2(b0.x + b2.x, b0.y + b2.y);
-        dst[d + Ns] = make_float2(b1.x + b3.x, b1.y + b3.y);
-        dst[d + 2 * Ns] = make_float2(b0.x - b2.x, b0.y - b2.y);
-        dst[d + 3 * Ns] = make_float2(b1.x - b3.x, b1.y - b3.y);
-        __syncthreads();
-        float2* t = src;
-        src = dst;
-        dst = t;
-    }
-    // 5 stages (odd): result is in tmp; copy back
-    for (int i = j; i < kFFT; i += 256) buf[i] = src[i];
-    __syncthreads();
-}
-
 // stft -> power -> mel for FPB frames of one clip. out [B][n_mels][T]; clip_max/min (uint bits of f32 >= 0)
+// LDS: frame buffers, the real-FFT twiddles (e^{-2 pi i f/2048}; the 1024-point twiddles are its even
+// entries), the banded filterbank and the frame's power spectrum.  Two threads per mel band.
+constexpr int kMaxW = 4096;  // packed filterbank weights held in LDS
 template <int FPB>
 __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__ pcm, int64_t n_samples, int T,
                                                        int hop, const float* __restrict__ window,
                                                        const float2* __restrict__ tw, const float2* __restrict__ rtw,
                                                        const int* __restrict__ band, const int* __restrict__ woff,
-                                                       const float* __restrict__ wts, int n_mels,
+                                                       const float* __restrict__ wts, int n_mels, int nnz,
                                                        float* __restrict__ out, unsigned* __restrict__ clip_max,
                                                        unsigned* __restrict__ clip_min) {
     __shared__ float2 buf[kFFT];
     __shared__ float2 tmp[kFFT];
-    __shared__ float2 stw[kFFT];
+    __shared__ float2 srtw[kFFT + 1];
+    __shared__ float sw[kMaxW];
+    __shared__ int sband[128][3];
     __shared__ float pw[kFFT + 1];
-    __shared__ float mel[FPB][128];
+    __shared__ float mel[FPB][129];
     const int b = blockIdx.y;
     const int t0 = blockIdx.x * FPB;
     const float* x = pcm + (int64_t)b * n_samples;
-    for (int i = threadIdx.x; i < kFFT; i += 256) stw[i] = tw[i];
+    for (int i = threadIdx.x; i <= kFFT; i += 256) srtw[i] = rtw[i];
+    for (int i = threadIdx.x; i < nnz; i += 256) sw[i] = wts[i];
+    for (int m = threadIdx.x; m < n_mels; m += 256) {
+        sband[m][0] = band[2 * m];
+        sband[m][1] = band[2 * m + 1];
+        sband[m][2] = woff[m];
+    }
     float lmax = 0.f, lmin = INFINITY;
-    for (int f = 0; f < FPB; ++f) {
+    const int nf = min(FPB, T - t0);
+    for (int f = 0; f < nf; ++f) {
         const int t = t0 + f;
-        if (t >= T) break;
         const int64_t start = (int64_t)t * hop - kFFT;  // center=True: pad n_fft/2 = 1024 zeros
         // pack even/odd windowed samples: z[k] = x[2k] w[2k] + i x[2k+1] w[2k+1]
         for (int kk = threadIdx.x; kk < kFFT; kk += 256) {
             const int64_t i0 = start + 2 * kk, i1 = i0 + 1;
+            const float2 wv = *reinterpret_cast<const float2*>(window + 2 * kk);
             const float v0 = (i0 >= 0 && i0 < n_samples) ? x[i0] : 0.f;
             const float v1 = (i1 >= 0 && i1 < n_samples) ? x[i1] : 0.f;
-            buf[kk] = make_float2(v0 * window[2 * kk], v1 * window[2 * kk + 1]);
+            buf[kk] = make_float2(v0 * wv.x, v1 * wv.y);
         }
         __syncthreads();
-        fft1024(buf, tmp, stw);
+        // 1024-point complex FFT, Stockham radix-4 (5 stages), twiddle(k) = srtw[2k]
+        {
+            float2* src = buf;
+            float2* dst = tmp;
+            const int j = threadIdx.x;
+#pragma unroll
+            for (int st = 0; st < 5; ++st) {
+                const int Ns = 1 << (2 * st);
+                const int k = j & (Ns - 1);
+                float2 a[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) a[r] = src[j + r * (kFFT / 4)];
+                const int step = kFFT / (4 * Ns);
+#pragma unroll
+                for (int r = 1; r < 4; ++r) a[r] = cmul(a[r], srtw[2 * ((k * r * step) & (kFFT - 1))]);
+                const float2 b0 = make_float2(a[0].x + a[2].x, a[0].y + a[2].y);
+                const float2 b1 = make_float2(a[0].x - a[2].x, a[0].y - a[2].y);
+                const float2 b2 = make_float2(a[1].x + a[3].x, a[1].y + a[3].y);
+                const float2 b3 = make_float2(a[1].y - a[3].y, -(a[1].x - a[3].x));  // -i (a1 - a3)
+                const int d = ((j >> (2 * st)) << (2 * st + 2)) + k;
+                dst[d] = make_float2(b0.x + b2.x, b0.y + b2.y);
+                dst[d + Ns] = make_float2(b1.x + b3.x, b1.y + b3.y);
+                dst[d + 2 * Ns] = make_float2(b0.x - b2.x, b0.y - b2.y);
+                dst[d + 3 * Ns] = make_float2(b1.x - b3.x, b1.y - b3.y);
+                __syncthreads();
+                float2* tt = src;
+                src = dst;
+                dst = tt;
+            }
+            // after 5 stages the spectrum Z is in tmp
+        }
         // real-FFT split: X[f] = E[f] + e^{-2 pi i f / 2048} O[f],  f = 0..1024
         for (int fb = threadIdx.x; fb <= kFFT; fb += 256) {
-            const float2 zf = buf[fb & (kFFT - 1)];
-            const float2 zc = buf[(kFFT - fb) & (kFFT - 1)];
+            const float2 zf = tmp[fb & (kFFT - 1)];
+            const float2 zc = tmp[(kFFT - fb) & (kFFT - 1)];
             const float2 e = make_float2(0.5f * (zf.x + zc.x), 0.5f * (zf.y - zc.y));
-            // O = (zf - conj(zc)) / (2i) = ((zf.y + zc.y) - i (zf.x - zc.x)) / 2
             const float2 o = make_float2(0.5f * (zf.y + zc.y), -0.5f * (zf.x - zc.x));
-            const float2 X = make_float2(e.x, e.y);
-            const float2 ot = cmul(o, rtw[fb]);
-            const float re = X.x + ot.x, im = X.y + ot.y;
+            const float2 ot = cmul(o, srtw[fb]);
+            const float re = e.x + ot.x, im = e.y + ot.y;
             pw[fb] = re * re + im * im;
         }
         __syncthreads();
-        for (int m = threadIdx.x; m < n_mels; m += 256) {
-            const int f0 = band[2 * m], nb = band[2 * m + 1];
-            const float* w = wts + woff[m];
+        // banded mel: threads (2m, 2m+1) share band m, interleaved bins, combined in a fixed order
+        {
+            const int m = threadIdx.x >> 1, h = threadIdx.x & 1;
             float s = 0.f;
-            for (int q = 0; q < nb; ++q) s = fmaf(pw[f0 + q], w[q], s);
-            mel[f][m] = s;
-            lmax = fmaxf(lmax, s);
-            lmin = fminf(lmin, s);
+            if (m < n_mels) {
+                const int f0 = sband[m][0], nb = sband[m][1], wo = sband[m][2];
+                for (int q = h; q < nb; q += 2) s = fmaf(pw[f0 + q], sw[wo + q], s);
+            }
+            const float o = __shfl_xor(s, 1, 64);
+            const float tot = h == 0 ? s + o : o + s;
+            if (m < n_mels && h == 0) {
+                mel[f][m] = tot;
+                lmax = fmaxf(lmax, tot);
+                lmin = fminf(lmin, tot);
+            }
         }
         __syncthreads();
     }
     // write [n_mels][frames] slabs: out[b][m][t0 + f]
-    const int nf = min(FPB, T - t0);
     for (int i = threadIdx.x; i < n_mels * FPB; i += 256) {
         const int m = i / FPB, f = i % FPB;
         if (f < nf) out[((int64_t)b * n_mels + m) * T + t0 + f] = mel[f][m];
     }
-    // per-clip max / min (non-negative floats order like their bit patterns)
-    if (lmax > 0.f) atomicMax(clip_max + b, __float_as_uint(lmax));
-    if (lmin < INFINITY) atomicMin(clip_min + b, __float_as_uint(lmin));
+    // per-clip max / min (non-negative floats order like their bit patterns); wave-reduce first
+    for (int o = 32; o > 0; o >>= 1) {
+        lmax = fmaxf(lmax, __shfl_xor(lmax, o, 64));
+        lmin = fminf(lmin, __shfl_xor(lmin, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (lmax > 0.f) atomicMax(clip_max + b, __float_as_uint(lmax));
+        if (lmin < INFINITY) atomicMin(clip_min + b, __float_as_uint(lmin));
+    }
 }
 
 __device__ __forceinline__ float db_of(float S, float amin) { return 10.f * log10f(fmaxf(amin, S)); }
@@ -336,10 +354,11 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
     const int T = (int)frames(p, n);
     HLMC_HIP(hipMemsetAsync(cmax, 0, B * sizeof(unsigned), s));
     HLMC_HIP(hipMemsetAsync(cmin, 0x7f, B * sizeof(unsigned), s));  // 0x7f7f7f7f = large positive float
-    constexpr int FPB = 8;
+    HLMC_CHECK_ARG(p->nnz <= kMaxW, "filterbank too large for the LDS-resident mel stage");
+    constexpr int FPB = 16;
     dim3 grid((T + FPB - 1) / FPB, (unsigned)B);
     stft_mel_kernel<FPB><<<grid, 256, 0, s>>>(pcm, n, T, p->hop, p->d_window, p->d_tw, p->d_rtw, p->d_band, p->d_woff,
-                                              p->d_w, p->n_mels, out, cmax, cmin);
+                                              p->d_w, p->n_mels, p->nnz, out, cmax, cmin);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -30,6 +30,24 @@ __device__ __forceinline__ float act_grad(float z, int act) {
     return 1.f;
 }
 
+
+// Deterministic block reduction of per-block partials: part[k * stride + col] for k < nblk.
+// Thread t sums k = t, t+256, ... in order; the 256 thread sums are combined by a fixed tree.
+__device__ __forceinline__ double block_sum_partials(const double* __restrict__ part, int nblk, int64_t stride,
+                                                     int64_t col, double* sh) {
+    double s = 0.0;
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x) s += part[(int64_t)k * stride + col];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+    }
+    double r = sh[0];
+    __syncthreads();
+    return r;
+}
+
 // ---------------------------------------------------------------- BN statistics
 // Partial column sums: part[blk][0..C) = sum y, part[blk][C..2C) = sum y^2 (double).
 template <typename T>
@@ -64,20 +82,23 @@ __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ 
     }
 }
 
-__global__ void bn_finalize_kernel(const double* __restrict__ part, int nblk, int C, int64_t R, float* mean,
-                                   float* invstd, float* rmean, float* rvar, int64_t* nbt, float momentum, float eps) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
+// one block per channel: reduce the block partials of sum / sum of squares, then mean / invstd / running
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ part, int nblk, int C, int64_t R,
+                                                          float* mean, float* invstd, float* rmean, float* rvar,
+                                                          int64_t* nbt, float momentum, float eps) {
+    __shared__ double sh[256];
+    const int c = blockIdx.x;
+    const double s = block_sum_partials(part, nblk, 2 * C, c, sh);
+    const double q = block_sum_partials(part, nblk, 2 * C, C + c, sh);
+    if (threadIdx.x != 0) return;
     if (c == 0 && nbt) nbt[0] += 1;
-    if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int k = 0; k < nblk; ++k) { s += part[(int64_t)k * 2 * C + c]; q += part[(int64_t)k * 2 * C + C + c]; }
-    double m = s / (double)R;
+    const double m = s / (double)R;
     double var = q / (double)R - m * m;
     if (var < 0.0) var = 0.0;
     mean[c] = (float)m;
     invstd[c] = (float)(1.0 / sqrt(var + (double)eps));
     if (rmean) {
-        double unb = R > 1 ? var * (double)R / (double)(R - 1) : var;
+        const double unb = R > 1 ? var * (double)R / (double)(R - 1) : var;
         rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * m);
         rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
     }
@@ -161,13 +182,14 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
     }
 }
 
-// reduce backward partials: sums2[0..C) = sum dz (-> dbeta), [C..2C) = sum dz*xhat (-> dgamma)
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int nblk, int C, float* dgamma, float* dbeta,
-                                       float* sums_f) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0.0, q = 0.0;
-    for (int k = 0; k < nblk; ++k) { s += part[(int64_t)k * 2 * C + c]; q += part[(int64_t)k * 2 * C + C + c]; }
+// reduce backward partials (one block per channel): sum dz (-> dbeta), sum dz*xhat (-> dgamma)
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nblk, int C,
+                                                              float* dgamma, float* dbeta, float* sums_f) {
+    __shared__ double sh[256];
+    const int c = blockIdx.x;
+    const double s = block_sum_partials(part, nblk, 2 * C, c, sh);
+    const double q = block_sum_partials(part, nblk, 2 * C, C + c, sh);
+    if (threadIdx.x != 0) return;
     dbeta[c] = (float)s;
     dgamma[c] = (float)q;
     sums_f[c] = (float)s;
@@ -225,12 +247,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     }
 }
 
-__global__ void colsum_finalize_kernel(const double* __restrict__ part, int nblk, int C, float* out) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * C + c];
-    out[c] = (float)s;
+__global__ __launch_bounds__(256) void colsum_finalize_kernel(const double* __restrict__ part, int nblk, int C,
+                                                              float* out) {
+    __shared__ double sh[256];
+    const int c = blockIdx.x;
+    const double s = block_sum_partials(part, nblk, C, c, sh);
+    if (threadIdx.x == 0) out[c] = (float)s;
 }
 
 // generic column sum for arbitrary ld/cols (bias grads): block = (row chunk, 64-column slab);
@@ -387,12 +409,19 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, 
     }
 }
 
-__global__ void sum_partials_f32_kernel(const float* __restrict__ part, int nblk, int n, float* out) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__global__ __launch_bounds__(256) void sum_partials_f32_kernel(const float* __restrict__ part, int nblk, int n,
+                                                               float* out) {
+    __shared__ double sh[256];
+    const int i = blockIdx.x;
     double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += part[(int64_t)k * n + i];
-    out[i] = (float)s;
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x) s += part[(int64_t)k * n + i];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[i] = (float)sh[0];
 }
 
 // ---------------------------------------------------------------- layout / elementwise
@@ -484,12 +513,11 @@ __global__ __launch_bounds__(256) void vae_sums_kernel(const float* __restrict__
         part[blockIdx.x * 3 + threadIdx.x] = s;
     }
 }
-__global__ void vae_sums_finalize_kernel(const double* __restrict__ part, int nblk, double* out) {
-    int j = threadIdx.x;
-    if (j >= 3) return;
-    double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += part[k * 3 + j];
-    out[j] = s;
+__global__ __launch_bounds__(256) void vae_sums_finalize_kernel(const double* __restrict__ part, int nblk, double* out) {
+    __shared__ double sh[256];
+    const int j = blockIdx.x;
+    const double s = block_sum_partials(part, nblk, 3, j, sh);
+    if (threadIdx.x == 0) out[j] = s;
 }
 __global__ void vae_bwd_kernel(const float* __restrict__ ra, const float* __restrict__ a, int64_t na,
                                float* __restrict__ dra, const float* __restrict__ rt, const float* __restrict__ t,
@@ -583,7 +611,7 @@ int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* in
     double* part = reinterpret_cast<double*>(ws.p);
     col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, rpb, part);
     HLMC_LAUNCHED();
-    bn_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, nblk, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
+    bn_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -618,13 +646,13 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
     float* sums = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
     bn_bwd_moments_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb, part);
     HLMC_LAUNCHED();
-    bn_bwd_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, nblk, C, dgamma, dbeta, sums);
+    bn_bwd_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, dgamma, dbeta, sums);
     HLMC_LAUNCHED();
     bn_bwd_apply_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
                                                      dy, rpb, part);
     HLMC_LAUNCHED();
     if (dbias) {
-        colsum_finalize_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, nblk, C, dbias);
+        colsum_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, dbias);
         HLMC_LAUNCHED();
     }
     return HLMC_OK;
@@ -662,7 +690,7 @@ int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const floa
     int rpb = (int)((K + nblk - 1) / nblk);
     wgrad_c1_kernel<T, 32><<<nblk, kThreads, 0, s>>>(L, B, Hl, Wl, Xh, rpb, ws.p);
     HLMC_LAUNCHED();
-    sum_partials_f32_kernel<<<cdiv(M * 9, 256), 256, 0, s>>>(ws.p, nblk, M * 9, dW);
+    sum_partials_f32_kernel<<<M * 9, 256, 0, s>>>(ws.p, nblk, M * 9, dW);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -712,15 +740,44 @@ int relu_bwd(hipStream_t s, T* dy, int lddy, const T* y, int ldy, int rows, int 
 static int colsum_blocks(int rows) { return std::max(1, std::min(1024, rows / 256)); }
 size_t colsum_ws(int rows, int cols) { return (size_t)colsum_blocks(rows) * cols * sizeof(double); }
 template <typename T>
+__global__ __launch_bounds__(256) void colsum_narrow_kernel(const T* __restrict__ x, int ld, int rows, int cols,
+                                                            int rows_per_blk, double* __restrict__ part) {
+    __shared__ double sh[256];
+    const int r0 = blockIdx.x * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+    for (int c = 0; c < cols; ++c) {
+        double s = 0.0;
+        for (int r = r0 + threadIdx.x; r < r1; r += blockDim.x) s += to_f32<T>(x[(int64_t)r * ld + c]);
+        sh[threadIdx.x] = s;
+        __syncthreads();
+        for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) part[(int64_t)blockIdx.x * cols + c] = sh[0];
+        __syncthreads();
+    }
+}
+
+template <typename T>
 int colsum(hipStream_t s, const T* dy, int ld, int rows, int cols, float* db, Ws ws) {
     int nblk = colsum_blocks(rows);
+    if (cols < 16) {
+        HLMC_CHECK_ARG(ws.bytes >= colsum_ws(rows, cols), "colsum workspace");
+        const int rpb = (rows + nblk - 1) / nblk;
+        double* part = reinterpret_cast<double*>(ws.p);
+        colsum_narrow_kernel<T><<<nblk, 256, 0, s>>>(dy, ld, rows, cols, rpb, part);
+        HLMC_LAUNCHED();
+        colsum_finalize_kernel<<<cols, 256, 0, s>>>(part, nblk, cols, db);
+        HLMC_LAUNCHED();
+        return HLMC_OK;
+    }
     HLMC_CHECK_ARG(ws.bytes >= colsum_ws(rows, cols), "colsum workspace");
     int rpb = (rows + nblk - 1) / nblk;
     double* part = reinterpret_cast<double*>(ws.p);
     dim3 grid(nblk, cdiv(cols, 64));
     colsum_partial_kernel<T><<<grid, 256, 0, s>>>(dy, ld, rows, cols, rpb, part);
     HLMC_LAUNCHED();
-    colsum_finalize_kernel<<<cdiv(cols, 256), 256, 0, s>>>(part, nblk, cols, db);
+    colsum_finalize_kernel<<<cols, 256, 0, s>>>(part, nblk, cols, db);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -749,7 +806,7 @@ int vae_sums(hipStream_t s, const float* ra, const float* a, int64_t na, const f
     double* part = reinterpret_cast<double*>(ws.p);
     vae_sums_kernel<<<nblk, kThreads, 0, s>>>(ra, a, na, rt, t, nt, mu, lv, nl, part);
     HLMC_LAUNCHED();
-    vae_sums_finalize_kernel<<<1, 64, 0, s>>>(part, nblk, out3);
+    vae_sums_finalize_kernel<<<3, 256, 0, s>>>(part, nblk, out3);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -43,8 +43,9 @@ def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
     xd = x.to(cuda, tdt).contiguous()
     wp = w.permute(0, 2, 3, 1).contiguous().to(cuda, tdt)
     y = torch.empty(B, Hi // 2, Wi // 2, Co, dtype=tdt, device=cuda)
-    L.check(L.lib().hlmc_op_conv_s2(L.stream(), code, xd.data_ptr(), B, Hi, Wi, Ci, wp.data_ptr(),
-                                    b.to(cuda).data_ptr(), Co, y.data_ptr(), ws.data_ptr(), WS_BYTES))
+    bd = b.to(cuda)
+    L.check(L.lib().hlmc_op_conv_s2(L.stream(), code, xd.data_ptr(), B, Hi, Wi, Ci, wp.data_ptr(), bd.data_ptr(), Co,
+                                    y.data_ptr(), ws.data_ptr(), WS_BYTES))
     assert rel(y, ref) < tol
 
 
@@ -63,8 +64,9 @@ def test_subpixel_convT(cuda, ws, dt, B, Hi, Wi, Ci, Co):
     xd = x.to(cuda, tdt).contiguous()
     wp = w.permute(1, 2, 3, 0).contiguous().to(cuda, tdt)           # [Co][kh][kw][Ci]
     y = torch.empty(B, 2 * Hi, 2 * Wi, Co, dtype=tdt, device=cuda)
-    L.check(L.lib().hlmc_op_subpixel(L.stream(), code, xd.data_ptr(), B, Hi, Wi, Ci, wp.data_ptr(),
-                                     b.to(cuda).data_ptr(), Co, y.data_ptr(), ws.data_ptr(), WS_BYTES))
+    bd = b.to(cuda)
+    L.check(L.lib().hlmc_op_subpixel(L.stream(), code, xd.data_ptr(), B, Hi, Wi, Ci, wp.data_ptr(), bd.data_ptr(), Co,
+                                     y.data_ptr(), ws.data_ptr(), WS_BYTES))
     assert rel(y, ref) < tol
 
 
@@ -80,9 +82,9 @@ def test_wgrad_s2_conv(cuda, ws, dt, B, Hl, Wl, M, C):
     ref = torch.nn.grad.conv2d_weight(q(x, tdt).permute(0, 3, 1, 2), (M, C, 3, 3), q(dy, tdt).permute(0, 3, 1, 2),
                                       stride=2, padding=1)
     dW = torch.empty(M, C, 3, 3, device=cuda)
-    L.check(L.lib().hlmc_op_wgrad_s2(L.stream(), code, dy.to(cuda, tdt).contiguous().data_ptr(), B, Hl, Wl, M,
-                                     x.to(cuda, tdt).contiguous().data_ptr(), C, dW.data_ptr(), ws.data_ptr(),
-                                     WS_BYTES))
+    dyd, xd = dy.to(cuda, tdt).contiguous(), x.to(cuda, tdt).contiguous()
+    L.check(L.lib().hlmc_op_wgrad_s2(L.stream(), code, dyd.data_ptr(), B, Hl, Wl, M, xd.data_ptr(), C, dW.data_ptr(),
+                                     ws.data_ptr(), WS_BYTES))
     assert rel(dW, ref) < (1e-5 if dt == "fp32" else 5e-3)
 
 
@@ -98,9 +100,9 @@ def test_wgrad_s2_convT(cuda, ws, dt):
     out = F.conv_transpose2d(q(x, tdt).permute(0, 3, 1, 2), w, stride=2, padding=1, output_padding=1)
     out.backward(q(dy, tdt).permute(0, 3, 1, 2))
     dW = torch.empty(Ci, Co, 3, 3, device=cuda)
-    L.check(L.lib().hlmc_op_wgrad_s2(L.stream(), code, x.to(cuda, tdt).contiguous().data_ptr(), B, Hl, Wl, Ci,
-                                     dy.to(cuda, tdt).contiguous().data_ptr(), Co, dW.data_ptr(), ws.data_ptr(),
-                                     WS_BYTES))
+    xd, dyd = x.to(cuda, tdt).contiguous(), dy.to(cuda, tdt).contiguous()
+    L.check(L.lib().hlmc_op_wgrad_s2(L.stream(), code, xd.data_ptr(), B, Hl, Wl, Ci, dyd.data_ptr(), Co,
+                                     dW.data_ptr(), ws.data_ptr(), WS_BYTES))
     assert rel(dW, w.grad) < (1e-5 if dt == "fp32" else 5e-3)
 
 
@@ -124,9 +126,9 @@ def test_linear(cuda, ws, dt, M, K, N, ldx, act, acc):
     wpad = torch.zeros(N, ldw)
     wpad[:, :K] = w
     y = y0.to(cuda, tdt).contiguous()
-    L.check(L.lib().hlmc_op_linear(L.stream(), code, x.to(cuda, tdt).contiguous().data_ptr(), ldx, M, K,
-                                   wpad.to(cuda, tdt).data_ptr(), ldw, b.to(cuda).data_ptr(), N, y.data_ptr(), N, act,
-                                   acc, 0, ws.data_ptr(), WS_BYTES))
+    xd, wd, bd = x.to(cuda, tdt).contiguous(), wpad.to(cuda, tdt), b.to(cuda)
+    L.check(L.lib().hlmc_op_linear(L.stream(), code, xd.data_ptr(), ldx, M, K, wd.data_ptr(), ldw, bd.data_ptr(), N,
+                                   y.data_ptr(), N, act, acc, 0, ws.data_ptr(), WS_BYTES))
     assert rel(y, ref) < tol
 
 
@@ -141,9 +143,9 @@ def test_linear_wgrad(cuda, ws, dt, Mb, N, K):
     x = torch.randn(Mb, ldx, generator=g)
     ref = q(dy[:, :N], tdt).T @ q(x[:, :K], tdt)
     dW = torch.empty(N, K, device=cuda)
-    L.check(L.lib().hlmc_op_linear_wgrad(L.stream(), code, dy.to(cuda, tdt).contiguous().data_ptr(), ldd,
-                                         x.to(cuda, tdt).contiguous().data_ptr(), ldx, Mb, N, K, dW.data_ptr(),
-                                         ws.data_ptr(), WS_BYTES))
+    dyd, xd = dy.to(cuda, tdt).contiguous(), x.to(cuda, tdt).contiguous()
+    L.check(L.lib().hlmc_op_linear_wgrad(L.stream(), code, dyd.data_ptr(), ldd, xd.data_ptr(), ldx, Mb, N, K,
+                                         dW.data_ptr(), ws.data_ptr(), WS_BYTES))
     assert rel(dW, ref) < (1e-5 if dt == "fp32" else 5e-3)
 
 
@@ -158,8 +160,9 @@ def test_edge_convs(cuda, ws, dt):
     # conv1 forward
     ref = F.conv2d(img.double()[:, None], w1.double(), b1.double(), stride=2, padding=1).permute(0, 2, 3, 1)
     y = torch.empty(B, H // 2, W // 2, 32, dtype=tdt, device=cuda)
-    L.check(L.lib().hlmc_op_conv_c1_s2(L.stream(), code, img.to(cuda).data_ptr(), B, H, W, w1.to(cuda).data_ptr(),
-                                       b1.to(cuda).data_ptr(), 32, y.data_ptr()))
+    imgd, w1d, b1d = img.to(cuda), w1.to(cuda), b1.to(cuda)
+    L.check(L.lib().hlmc_op_conv_c1_s2(L.stream(), code, imgd.data_ptr(), B, H, W, w1d.data_ptr(), b1d.data_ptr(), 32,
+                                       y.data_ptr()))
     assert rel(y, ref) < (1e-6 if dt == "fp32" else 1e-2)
     # last convT (32 -> 1)
     a = torch.randn(B, H // 2, W // 2, 32, generator=g)
@@ -168,14 +171,16 @@ def test_edge_convs(cuda, ws, dt):
     refT = F.conv_transpose2d(q(a, tdt).permute(0, 3, 1, 2), wT.double(), bT.double(), stride=2, padding=1,
                               output_padding=1)[:, 0]
     out = torch.empty(B, H, W, device=cuda)
-    L.check(L.lib().hlmc_op_convT_c1(L.stream(), code, a.to(cuda, tdt).contiguous().data_ptr(), B, H // 2, W // 2,
-                                     32, wT.to(cuda).data_ptr(), bT.to(cuda).data_ptr(), out.data_ptr()))
+    ad, wTd, bTd = a.to(cuda, tdt).contiguous(), wT.to(cuda), bT.to(cuda)
+    L.check(L.lib().hlmc_op_convT_c1(L.stream(), code, ad.data_ptr(), B, H // 2, W // 2, 32, wTd.data_ptr(),
+                                     bTd.data_ptr(), out.data_ptr()))
     assert rel(out, refT) < 1e-6
     # weight gradients of both (one-channel high-res side)
     dy = torch.randn(B, H // 2, W // 2, 32, generator=g)
     refw = torch.nn.grad.conv2d_weight(img.double()[:, None], (32, 1, 3, 3), q(dy, tdt).permute(0, 3, 1, 2),
                                        stride=2, padding=1)
     dW = torch.empty(32, 1, 3, 3, device=cuda)
-    L.check(L.lib().hlmc_op_wgrad_c1(L.stream(), code, dy.to(cuda, tdt).contiguous().data_ptr(), B, H // 2, W // 2,
-                                     32, img.to(cuda).data_ptr(), dW.data_ptr(), ws.data_ptr(), WS_BYTES))
+    dyd = dy.to(cuda, tdt).contiguous()
+    L.check(L.lib().hlmc_op_wgrad_c1(L.stream(), code, dyd.data_ptr(), B, H // 2, W // 2, 32, imgd.data_ptr(),
+                                     dW.data_ptr(), ws.data_ptr(), WS_BYTES))
     assert rel(dW, refw) < 1e-5

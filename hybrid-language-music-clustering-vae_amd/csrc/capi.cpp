@@ -158,6 +158,7 @@ int hlmc_net_bind(hlmc_net* h, float* const* params, float* const* grads, float*
     n.NBT.assign(nbt, nbt + n.n_bn);
     for (size_t i = 0; i < np; ++i) HLMC_CHECK_ARG(n.P[i] && n.G[i], "NULL parameter / grad pointer");
     n.state = reinterpret_cast<char*>(state);
+    n.packs_valid = false;
     return n.bind_state(nullptr);
 }
 int hlmc_net_forward(hlmc_net* h, void* stream, int64_t batch, int train, const float* in0, const float* in1,
@@ -182,6 +183,19 @@ int hlmc_net_backward(hlmc_net* h, void* stream, int64_t batch, const float* d_r
     return h->impl->backward(S(stream), a);
 }
 
+int hlmc_net_adam_step(hlmc_net* h, void* stream, float* const* exp_avg, float* const* exp_avg_sq, float lr, float b1,
+                       float b2, float eps, float wd, int step) {
+    HLMC_CHECK_ARG(h && exp_avg && exp_avg_sq && step >= 1, "bad arguments");
+    HLMC_CHECK_ARG(!h->impl->P.empty(), "net is not bound");
+    return h->impl->adam_step(S(stream), exp_avg, exp_avg_sq, ops::AdamArgs{lr, b1, b2, eps, wd, step});
+}
+int hlmc_net_set_trust_packs(hlmc_net* h, int trust) {
+    HLMC_CHECK_ARG(h, "net is NULL");
+    h->impl->trust_packs = trust != 0;
+    if (!trust) h->impl->packs_valid = false;
+    return HLMC_OK;
+}
+
 // ------------------------------------------------------------------------------------ loss / optim
 int64_t hlmc_loss_workspace(int64_t na, int64_t nt, int64_t nl) { return (int64_t)ops::vae_sums_ws(na, nt, nl); }
 int hlmc_loss_sums(void* stream, const float* ra, const float* a, int64_t na, const float* rt, const float* t, int64_t nt,
@@ -202,7 +216,8 @@ int hlmc_adam_step(void* stream, int n, float* const* p, const float* const* g, 
                    const int64_t* numel, float lr, float b1, float b2, float eps, float wd, int step, void* scratch) {
     HLMC_CHECK_ARG(n >= 0 && step >= 1 && p && g && m && v && numel, "bad adam arguments");
     ops::AdamArgs a{lr, b1, b2, eps, wd, step};
-    return ops::adam(S(stream), n, p, g, m, v, numel, a, scratch);
+    (void)scratch;
+    return ops::adam(S(stream), n, p, g, m, v, numel, a);
 }
 
 // ------------------------------------------------------------------------------------ kmeans

@@ -69,7 +69,28 @@ class NetT : public NetBase {
         return HLMC_OK;
     }
     int pack_all(hipStream_t s) {
-        return ops::pack<T>(s, reinterpret_cast<const ops::PackJob*>(state + jobs_off), njobs, pack_max);
+        if (trust_packs && packs_valid) return HLMC_OK;
+        HLMC_TRY(ops::pack<T>(s, reinterpret_cast<const ops::PackJob*>(state + jobs_off), njobs, pack_max));
+        packs_valid = true;
+        return HLMC_OK;
+    }
+    int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a) override {
+        const size_t np = params.size();
+        std::vector<int64_t> numel(np);
+        std::vector<ops::PackJob> pk(np);
+        for (size_t i = 0; i < np; ++i) {
+            numel[i] = params[i].numel();
+            pk[i] = ops::PackJob{nullptr, nullptr, nullptr, 1, 1, 1, 1, 1};
+            if (i < packs.size() && packs[i].taps) {
+                const Pack& p = packs[i];
+                pk[i] = ops::PackJob{nullptr, state + p.off0, state + p.off1, p.d0, p.d1, p.taps, p.ld0, p.ld1};
+            }
+        }
+        std::vector<const float*> g(G.begin(), G.end());
+        HLMC_TRY(ops::adam(s, (int)np, P.data(), g.data(), m, v, numel.data(), a, pk.data(),
+                           sizeof(T) == 2 ? HLMC_BF16 : HLMC_F32));
+        packs_valid = true;
+        return HLMC_OK;
     }
     T* P0(int w) const { return reinterpret_cast<T*>(state + packs[w].off0); }
     T* P1(int w) const { return reinterpret_cast<T*>(state + packs[w].off1); }

@@ -77,6 +77,10 @@ class NetBase {
     virtual int bind_state(hipStream_t s) = 0;  // upload pack jobs into state
     virtual int forward(hipStream_t s, const ForwardArgs& a) = 0;
     virtual int backward(hipStream_t s, const BackwardArgs& a) = 0;
+    // Adam over all bound parameters with the packed GEMM weights refreshed in the same pass
+    virtual int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a) = 0;
+    bool trust_packs = false;  // forward skips re-packing when packs are known current
+    bool packs_valid = false;
 };
 
 // factory: kind 0 hybrid, 1 cvae, 2 simple; cfg per hlmc.h

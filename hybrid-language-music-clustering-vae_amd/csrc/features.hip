@@ -67,13 +67,23 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
     __shared__ float2 buf[kFFT];
     __shared__ float2 tmp[kFFT];
     __shared__ float2 srtw[kFFT + 1];
-    __shared__ float sw[kMaxW];
     __shared__ int sband[128][3];
     __shared__ float pw[kFFT + 1];
     __shared__ float mel[FPB][129];
+    extern __shared__ float sw[];  // nnz packed filterbank weights (dynamic, exact size)
     const int b = blockIdx.y;
     const int t0 = blockIdx.x * FPB;
     const float* x = pcm + (int64_t)b * n_samples;
+    // this thread's 4 samples of a frame: pairs kk = tid, tid + 256, tid + 512, tid + 768
+    auto fetch = [&](int t, float* v) {
+        const int64_t start = (int64_t)t * hop - kFFT;  // center=True: pad n_fft/2 = 1024 zeros
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t i0 = start + 2 * (threadIdx.x + 256 * q), i1 = i0 + 1;
+            v[2 * q] = (i0 >= 0 && i0 < n_samples) ? x[i0] : 0.f;
+            v[2 * q + 1] = (i1 >= 0 && i1 < n_samples) ? x[i1] : 0.f;
+        }
+    };
     for (int i = threadIdx.x; i <= kFFT; i += 256) srtw[i] = rtw[i];
     for (int i = threadIdx.x; i < nnz; i += 256) sw[i] = wts[i];
     for (int m = threadIdx.x; m < n_mels; m += 256) {
@@ -83,18 +93,18 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
     }
     float lmax = 0.f, lmin = INFINITY;
     const int nf = min(FPB, T - t0);
+    float2 wv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wv[q] = *reinterpret_cast<const float2*>(window + 2 * (threadIdx.x + 256 * q));
+    float cur[8];
+    fetch(t0, cur);
     for (int f = 0; f < nf; ++f) {
-        const int t = t0 + f;
-        const int64_t start = (int64_t)t * hop - kFFT;  // center=True: pad n_fft/2 = 1024 zeros
         // pack even/odd windowed samples: z[k] = x[2k] w[2k] + i x[2k+1] w[2k+1]
-        for (int kk = threadIdx.x; kk < kFFT; kk += 256) {
-            const int64_t i0 = start + 2 * kk, i1 = i0 + 1;
-            const float2 wv = *reinterpret_cast<const float2*>(window + 2 * kk);
-            const float v0 = (i0 >= 0 && i0 < n_samples) ? x[i0] : 0.f;
-            const float v1 = (i1 >= 0 && i1 < n_samples) ? x[i1] : 0.f;
-            buf[kk] = make_float2(v0 * wv.x, v1 * wv.y);
-        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            buf[threadIdx.x + 256 * q] = make_float2(cur[2 * q] * wv[q].x, cur[2 * q + 1] * wv[q].y);
         __syncthreads();
+        if (f + 1 < nf) fetch(t0 + f + 1, cur);  // next frame's samples are in flight during this FFT
         // 1024-point complex FFT, Stockham radix-4 (5 stages), twiddle(k) = srtw[2k]
         {
             float2* src = buf;
@@ -109,7 +119,13 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
                 for (int r = 0; r < 4; ++r) a[r] = src[j + r * (kFFT / 4)];
                 const int step = kFFT / (4 * Ns);
 #pragma unroll
-                for (int r = 1; r < 4; ++r) a[r] = cmul(a[r], srtw[2 * ((k * r * step) & (kFFT - 1))]);
+                for (int r = 1; r < 4; ++r) {
+                    // e^{-2 pi i m / 1024} = srtw[2m] for 2m <= 1024, else -srtw[2m - 1024]
+                    const int f2 = 2 * ((k * r * step) & (kFFT - 1));
+                    float2 w = srtw[f2 <= kFFT ? f2 : f2 - kFFT];
+                    if (f2 > kFFT) w = make_float2(-w.x, -w.y);
+                    a[r] = cmul(a[r], w);
+                }
                 const float2 b0 = make_float2(a[0].x + a[2].x, a[0].y + a[2].y);
                 const float2 b1 = make_float2(a[0].x - a[2].x, a[0].y - a[2].y);
                 const float2 b2 = make_float2(a[1].x + a[3].x, a[1].y + a[3].y);
@@ -355,9 +371,9 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
     HLMC_HIP(hipMemsetAsync(cmax, 0, B * sizeof(unsigned), s));
     HLMC_HIP(hipMemsetAsync(cmin, 0x7f, B * sizeof(unsigned), s));  // 0x7f7f7f7f = large positive float
     HLMC_CHECK_ARG(p->nnz <= kMaxW, "filterbank too large for the LDS-resident mel stage");
-    constexpr int FPB = 16;
+    constexpr int FPB = 8;
     dim3 grid((T + FPB - 1) / FPB, (unsigned)B);
-    stft_mel_kernel<FPB><<<grid, 256, 0, s>>>(pcm, n, T, p->hop, p->d_window, p->d_tw, p->d_rtw, p->d_band, p->d_woff,
+    stft_mel_kernel<FPB><<<grid, 256, (size_t)std::max(1, p->nnz) * sizeof(float), s>>>(pcm, n, T, p->hop, p->d_window, p->d_tw, p->d_rtw, p->d_band, p->d_woff,
                                               p->d_w, p->n_mels, p->nnz, out, cmax, cmin);
     HLMC_LAUNCHED();
     return HLMC_OK;

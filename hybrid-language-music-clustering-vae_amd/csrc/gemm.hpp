@@ -280,8 +280,15 @@ __global__ void splitk_reduce_kernel(const float* ws, EP ep, int M, int N, int S
         int m = (int)(t % M);
         int ph = (int)(t / M);
         const float* p = ws + ((int64_t)ph * S * M + m) * N + n;
+        const int64_t st = (int64_t)M * N;
+        // fixed summation order (k ascending) with 4 slab loads in flight
         float s = 0.f;
-        for (int k = 0; k < S; ++k) s += p[(int64_t)k * M * N];
+        int k = 0;
+        for (; k + 4 <= S; k += 4) {
+            const float a0 = p[k * st], a1 = p[(k + 1) * st], a2 = p[(k + 2) * st], a3 = p[(k + 3) * st];
+            s += a0; s += a1; s += a2; s += a3;
+        }
+        for (; k < S; ++k) s += p[k * st];
         EP e = ep;
         e.set_phase(ph);
         e.store(m, n, s);

@@ -24,8 +24,10 @@ inline Plan plan_nt(int tiles, int Kmax, int BK) {
     return {S, ksl};
 }
 inline Plan plan_tn(int tiles, int K, int BK) {
-    int S = cdiv(kTargetBlocks, tiles);
-    S = std::max(1, std::min(S, K / (8 * BK)));
+    // weight gradients: long K (= batch x pixels), tiny M x N; each split keeps >= 32 k-tiles so the
+    // partial slabs (and their reduction) stay small next to the GEMM itself
+    int S = cdiv(kTargetBlocks / 2, tiles);
+    S = std::max(1, std::min(S, K / (32 * BK)));
     int ksl = cdiv(cdiv(K, S), BK) * BK;
     S = cdiv(K, ksl);
     return {S, ksl};

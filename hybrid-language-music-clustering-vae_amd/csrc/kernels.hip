@@ -274,15 +274,11 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
 
 // ---------------------------------------------------------------- edge convs (one channel side)
 // y[b,oh,ow,co] = bias[co] + sum_{kh,kw} x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + kh*3+kw]
+// One thread per output pixel; the 9*CO weights are read at wave-uniform addresses (scalar loads).
 template <typename T, int CO>
 __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
                                                          T* __restrict__ y) {
-    __shared__ float ws[CO * 9];
-    __shared__ float bs[CO];
-    for (int i = threadIdx.x; i < CO * 9; i += blockDim.x) ws[i] = w[i];
-    for (int i = threadIdx.x; i < CO; i += blockDim.x) bs[i] = bias ? bias[i] : 0.f;
-    __syncthreads();
     const int Ho = Hi / 2, Wo = Wi / 2;
     const int64_t npix = (int64_t)B * Ho * Wo;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
@@ -305,9 +301,9 @@ __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict
             float o[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                float s = bs[c0 + v];
+                float s = bias ? bias[c0 + v] : 0.f;
 #pragma unroll
-                for (int k = 0; k < 9; ++k) s = fmaf(in[k], ws[(c0 + v) * 9 + k], s);
+                for (int k = 0; k < 9; ++k) s = fmaf(in[k], w[(c0 + v) * 9 + k], s);
                 o[v] = s;
             }
             store16_f32(y + p * CO + c0, o);
@@ -357,55 +353,83 @@ __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, 
     }
 }
 
-// dW[m*9+tap] partials: block = chunk of low-res rows (b,r,c); Xh single-channel high-res [B, 2Hl, 2Wl]
+// dW[m*9+tap] partials: block = chunk of low-res rows (b,r,c); Xh single-channel high-res [B, 2Hl, 2Wl].
+// Rows are staged in LDS 256 at a time; thread (mg, rg) accumulates a 4(m) x 9(tap) register block over
+// rows rg, rg+32, ... (13 LDS reads per 36 FMAs); the 32 row-groups are combined in a fixed order.
 template <typename T, int M>
 __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, int B, int Hl, int Wl,
                                                        const float* __restrict__ Xh, int rows_per_blk,
                                                        float* __restrict__ part) {
-    constexpr int RC = 128;  // rows staged per pass
-    __shared__ float Ls[RC][M + 1];
-    __shared__ float Hs[RC][9];
+    static_assert(M == 32, "one 8 x 4 channel tiling");
+    constexpr int RC = 256;
+    // one LDS block: [RC][M+1] rows + [RC][9] taps during accumulation, [32][M*9] partials afterwards
+    constexpr int kAcc = RC * (M + 1) + RC * 9, kRed = 32 * M * 9;
+    __shared__ float smem[kAcc > kRed ? kAcc : kRed];
+    float (*Ls)[M + 1] = reinterpret_cast<float (*)[M + 1]>(smem);
+    float (*Hs)[9] = reinterpret_cast<float (*)[9]>(smem + RC * (M + 1));
     const int64_t K = (int64_t)B * Hl * Wl;
     const int64_t k0 = (int64_t)blockIdx.x * rows_per_blk, k1 = min(K, k0 + rows_per_blk);
     const int Hh = 2 * Hl, Wh = 2 * Wl;
-    float acc[2] = {0.f, 0.f};
+    const int mg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+    float acc[4][9];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) acc[i][j] = 0.f;
+    constexpr int V = Vec16<T>::N;
     for (int64_t kb = k0; kb < k1; kb += RC) {
-        for (int i = threadIdx.x; i < RC * M; i += blockDim.x) {
-            int rr = i / M, m = i % M;
-            int64_t k = kb + rr;
-            Ls[rr][m] = (k < k1) ? to_f32<T>(L[k * M + m]) : 0.f;
+        for (int i = threadIdx.x; i < RC * (M / V); i += blockDim.x) {
+            const int rr = i / (M / V), cg = i % (M / V);
+            const int64_t k = kb + rr;
+            float v[V];
+            if (k < k1) {
+                load16_f32(L + k * M + cg * V, v);
+            } else {
+#pragma unroll
+                for (int q = 0; q < V; ++q) v[q] = 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < V; ++q) Ls[rr][cg * V + q] = v[q];
         }
         for (int i = threadIdx.x; i < RC * 9; i += blockDim.x) {
-            int rr = i / 9, tap = i % 9;
-            int64_t k = kb + rr;
+            const int rr = i / 9, tap = i % 9;
+            const int64_t k = kb + rr;
             float v = 0.f;
             if (k < k1) {
-                int c = (int)(k % Wl);
-                int64_t t = k / Wl;
-                int r = (int)(t % Hl);
-                int b = (int)(t / Hl);
-                int ih = 2 * r - 1 + tap / 3, iw = 2 * c - 1 + tap % 3;
+                const int c = (int)(k % Wl);
+                const int64_t t = k / Wl;
+                const int r = (int)(t % Hl);
+                const int b = (int)(t / Hl);
+                const int ih = 2 * r - 1 + tap / 3, iw = 2 * c - 1 + tap % 3;
                 if ((unsigned)ih < (unsigned)Hh && (unsigned)iw < (unsigned)Wh) v = Xh[((int64_t)b * Hh + ih) * Wh + iw];
             }
             Hs[rr][tap] = v;
         }
         __syncthreads();
+        for (int rr = rg; rr < RC; rr += 32) {
+            float l[4], h[9];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            int o = threadIdx.x + j * 256;
-            if (o < M * 9) {
-                int m = o / 9, tap = o % 9;
-                float s = 0.f;
-                for (int rr = 0; rr < RC; ++rr) s = fmaf(Ls[rr][m], Hs[rr][tap], s);
-                acc[j] += s;
-            }
+            for (int i = 0; i < 4; ++i) l[i] = Ls[rr][4 * mg + i];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) h[j] = Hs[rr][j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 9; ++j) acc[i][j] = fmaf(l[i], h[j], acc[i][j]);
         }
         __syncthreads();
     }
+    // combine the 32 row-groups: stage [rg][m*9+tap] in LDS (reuses Ls), then fixed-order sums
+    float* red = smem;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        int o = threadIdx.x + j * 256;
-        if (o < M * 9) part[(int64_t)blockIdx.x * M * 9 + o] = acc[j];
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) red[rg * (M * 9) + (4 * mg + i) * 9 + j] = acc[i][j];
+    __syncthreads();
+    for (int o = threadIdx.x; o < M * 9; o += blockDim.x) {
+        float s = 0.f;
+        for (int g = 0; g < 32; ++g) s += red[g * (M * 9) + o];
+        part[(int64_t)blockIdx.x * M * 9 + o] = s;
     }
 }
 
@@ -536,17 +560,25 @@ __global__ void vae_bwd_kernel(const float* __restrict__ ra, const float* __rest
 }
 
 // ---------------------------------------------------------------- Adam (torch.optim.Adam single-tensor math)
-constexpr int kAdamMax = 48;
+constexpr int kAdamMax = 32;
+struct AdamPack {
+    void* p0;
+    void* p1;
+    int d0, d1, taps, ld0, ld1;
+};
 struct AdamBatch {
     float* p[kAdamMax];
     const float* g[kAdamMax];
     float* m[kAdamMax];
     float* v[kAdamMax];
     int64_t n[kAdamMax];
+    AdamPack pk[kAdamMax];
     int blk0[kAdamMax + 1];
     int count;
 };
-__global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, float lr, float b1, float b2, float eps, float wd,
+// torch.optim.Adam (single-tensor) update; optionally re-packs the updated weight for the GEMMs
+template <typename PT>
+__global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, float b1, float b2, float eps, float wd,
                                                    float step_size, float bc2_sqrt) {
     int t = 0;
     while (t + 1 < bt.count && (int)blockIdx.x >= bt.blk0[t + 1]) ++t;
@@ -556,6 +588,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, float lr, float
     float* m = bt.m[t];
     float* v = bt.v[t];
     const int64_t n = bt.n[t];
+    const AdamPack pk = bt.pk[t];
     for (int64_t i = base + threadIdx.x; i < min(n, base + 1024); i += blockDim.x) {
         float gi = g[i];
         if (wd != 0.f) gi = gi + wd * p[i];
@@ -565,7 +598,17 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, float lr, float
         m[i] = mi;
         v[i] = vi;
         float denom = sqrtf(vi) / bc2_sqrt + eps;
-        p[i] = p[i] - step_size * (mi / denom);
+        const float np = p[i] - step_size * (mi / denom);
+        p[i] = np;
+        if (pk.p0 || pk.p1) {
+            const int64_t i0 = i / ((int64_t)pk.d1 * pk.taps);
+            const int64_t rem = i - i0 * pk.d1 * pk.taps;
+            const int64_t i1 = rem / pk.taps;
+            const int tap = (int)(rem - i1 * pk.taps);
+            const PT q = from_f32<PT>(np);
+            if (pk.p0) reinterpret_cast<PT*>(pk.p0)[(i0 * pk.taps + tap) * pk.ld0 + i1] = q;
+            if (pk.p1) reinterpret_cast<PT*>(pk.p1)[(i1 * pk.taps + tap) * pk.ld1 + i0] = q;
+        }
     }
 }
 
@@ -821,7 +864,7 @@ int vae_loss_bwd(hipStream_t s, const float* ra, const float* a, int64_t na, flo
 }
 
 int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, float* const* m, float* const* v,
-         const int64_t* numel, AdamArgs a, void*) {
+         const int64_t* numel, AdamArgs a, const PackJob* packs, int pack_dtype) {
     const double bc1 = 1.0 - std::pow((double)a.beta1, (double)a.step);
     const double bc2 = 1.0 - std::pow((double)a.beta2, (double)a.step);
     const float step_size = (float)(a.lr / bc1);
@@ -833,12 +876,21 @@ int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, fl
         for (int i = 0; i < bt.count; ++i) {
             bt.p[i] = p[t0 + i]; bt.g[i] = g[t0 + i]; bt.m[i] = m[t0 + i]; bt.v[i] = v[t0 + i];
             bt.n[i] = numel[t0 + i];
+            if (packs && (packs[t0 + i].p0 || packs[t0 + i].p1)) {
+                const PackJob& j = packs[t0 + i];
+                bt.pk[i] = AdamPack{j.p0, j.p1, j.d0, j.d1, j.taps, j.ld0, j.ld1};
+            } else {
+                bt.pk[i] = AdamPack{nullptr, nullptr, 1, 1, 1, 1, 1};
+            }
             bt.blk0[i] = blocks;
             blocks += (int)((numel[t0 + i] + 1023) / 1024);
         }
         bt.blk0[bt.count] = blocks;
         if (blocks == 0) continue;
-        adam_kernel<<<blocks, 256, 0, s>>>(bt, a.lr, a.beta1, a.beta2, a.eps, a.weight_decay, step_size, bc2_sqrt);
+        if (pack_dtype == HLMC_BF16)
+            adam_kernel<bf16><<<blocks, 256, 0, s>>>(bt, a.beta1, a.beta2, a.eps, a.weight_decay, step_size, bc2_sqrt);
+        else
+            adam_kernel<float><<<blocks, 256, 0, s>>>(bt, a.beta1, a.beta2, a.eps, a.weight_decay, step_size, bc2_sqrt);
         HLMC_LAUNCHED();
     }
     return HLMC_OK;

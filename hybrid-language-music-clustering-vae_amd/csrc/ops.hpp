@@ -109,8 +109,11 @@ struct AdamArgs {
     float lr, beta1, beta2, eps, weight_decay;
     int step;
 };
+struct PackJob;
+// packs (nullable): per tensor, PackJob describing packed copies (p0/p1 may be NULL) written from the updated
+// parameter in dtype pack_dtype (HLMC_F32 / HLMC_BF16) — the GEMM weight layouts refreshed in the same pass
 int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, float* const* m, float* const* v,
-         const int64_t* numel, AdamArgs a, void* dev_scratch);
+         const int64_t* numel, AdamArgs a, const PackJob* packs = nullptr, int pack_dtype = HLMC_F32);
 // conv weight [d0][d1][3][3] f32 -> P0 [d0][3][3][d1], P1 [d1][3][3][d0] (T); linear [d0][d1] -> P0 copy, P1 transpose
 struct PackJob {
     const float* w;

@@ -47,10 +47,9 @@ class Trainer:
         self.distributed = distributed or process_group is not None
         self.process_group = process_group
         self.grad_dtype = grad_dtype
-        self._adam_args = (L.vp_array([p.data_ptr() for p in self.params]),
-                           L.vp_array([g.data_ptr() for g in self.grads]),
-                           L.vp_array([t.data_ptr() for t in mv]), L.vp_array([t.data_ptr() for t in vv]),
-                           L.i64_array([p.numel() for p in self.params]))
+        self._mv = (L.vp_array([t.data_ptr() for t in mv]), L.vp_array([t.data_ptr() for t in vv]))
+        # weights change only through hlmc_net_adam_step (which refreshes the packed GEMM layouts)
+        L.check(L.lib().hlmc_net_set_trust_packs(self.net.h, 1))
         self._cache = {}
 
     def _buffers(self, B):
@@ -101,9 +100,13 @@ class Trainer:
             self.allreduce_grads()
         self.step_count += 1
         b1, b2 = self.betas
-        L.check(lib.hlmc_adam_step(s, len(self.params), *self._adam_args, float(self.lr), float(b1), float(b2),
-                                   float(self.eps), float(self.wd), self.step_count, None), "hlmc_adam_step")
+        L.check(lib.hlmc_net_adam_step(self.net.h, s, *self._mv, float(self.lr), float(b1), float(b2), float(self.eps),
+                                       float(self.wd), self.step_count), "hlmc_net_adam_step")
         return c["sums"]
+
+    def release(self):
+        """Hand the model back to the nn.Module path (forward re-packs weights every call again)."""
+        L.check(L.lib().hlmc_net_set_trust_packs(self.net.h, 0))
 
     def allreduce_grads(self):
         """SUM all-reduce of the flat gradient buffer (RCCL under backend 'nccl')."""

@@ -116,6 +116,14 @@ int hlmc_net_encode(hlmc_net* net, void* stream, int64_t batch, int train, const
 int hlmc_net_backward(hlmc_net* net, void* stream, int64_t batch, const float* d_recon, const float* d_recon_text,
                       const float* d_mu, const float* d_logvar, void* ws);
 
+/* torch.optim.Adam step over every bound parameter (exp_avg / exp_avg_sq: num_params device pointers),
+ * refreshing the packed GEMM weight layouts in the same pass. */
+int hlmc_net_adam_step(hlmc_net* net, void* stream, float* const* exp_avg, float* const* exp_avg_sq, float lr,
+                       float beta1, float beta2, float eps, float weight_decay, int step);
+/* trust != 0: forward re-packs weights only when they changed through hlmc_net_adam_step (a caller that
+ * writes parameters any other way must pass 0, the default, so forward always re-packs). */
+int hlmc_net_set_trust_packs(hlmc_net* net, int trust);
+
 /* ============================================================== losses
  * loss_function (src/Convolutional_VAE.py:187-194), cvae_loss_function (src/Conditional_VAE.py:233-246),
  * vae_loss (src/Simple_VAE.py:108-114).  sums3 (device, double[3]) receives

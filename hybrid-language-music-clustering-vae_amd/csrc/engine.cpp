@@ -49,7 +49,7 @@ class NetT : public NetBase {
             p.ld1 = p.taps == 1 ? pad8(p.d0) : p.d0;
             p.off0 = A.take((size_t)p.d0 * p.taps * p.ld0 * sizeof(T));
             p.off1 = A.take((size_t)p.d1 * p.taps * p.ld1 * sizeof(T));
-            pack_max = std::max<int64_t>(pack_max, (int64_t)p.d0 * p.d1 * p.taps);
+            pack_max = std::max<int64_t>(pack_max, std::max(p.d0, p.d1));  // largest dimension (tile grid)
             ++njobs;
         }
         jobs_off = A.take(sizeof(ops::PackJob) * std::max(1, njobs));
@@ -70,27 +70,20 @@ class NetT : public NetBase {
     }
     int pack_all(hipStream_t s) {
         if (trust_packs && packs_valid) return HLMC_OK;
+        // pack_max = largest weight dimension (the tiled pack kernel's grid)
         HLMC_TRY(ops::pack<T>(s, reinterpret_cast<const ops::PackJob*>(state + jobs_off), njobs, pack_max));
         packs_valid = true;
         return HLMC_OK;
     }
     int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a) override {
+        // Adam over all parameters (one multi-tensor launch per 32 tensors), then one tiled re-pack
         const size_t np = params.size();
         std::vector<int64_t> numel(np);
-        std::vector<ops::PackJob> pk(np);
-        for (size_t i = 0; i < np; ++i) {
-            numel[i] = params[i].numel();
-            pk[i] = ops::PackJob{nullptr, nullptr, nullptr, 1, 1, 1, 1, 1};
-            if (i < packs.size() && packs[i].taps) {
-                const Pack& p = packs[i];
-                pk[i] = ops::PackJob{nullptr, state + p.off0, state + p.off1, p.d0, p.d1, p.taps, p.ld0, p.ld1};
-            }
-        }
+        for (size_t i = 0; i < np; ++i) numel[i] = params[i].numel();
         std::vector<const float*> g(G.begin(), G.end());
-        HLMC_TRY(ops::adam(s, (int)np, P.data(), g.data(), m, v, numel.data(), a, pk.data(),
-                           sizeof(T) == 2 ? HLMC_BF16 : HLMC_F32));
-        packs_valid = true;
-        return HLMC_OK;
+        HLMC_TRY(ops::adam(s, (int)np, P.data(), g.data(), m, v, numel.data(), a));
+        packs_valid = false;
+        return pack_all(s);
     }
     T* P0(int w) const { return reinterpret_cast<T*>(state + packs[w].off0); }
     T* P1(int w) const { return reinterpret_cast<T*>(state + packs[w].off1); }

@@ -14,45 +14,72 @@
 
 namespace hlmc {
 
+// ============================================================================ helpers
+// Division by a runtime constant via a precomputed magic number (n < 2^31): q = (umulhi(n, mul) + n) >> sh
+struct FastDiv {
+    uint32_t d, mul, sh;
+    FastDiv() = default;
+    explicit FastDiv(uint32_t div) : d(div) {
+        sh = 0;
+        while ((1u << sh) < div) ++sh;
+        mul = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << sh) - div)) / div + 1);
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, mul) + n) >> sh; }
+};
+
 // ============================================================================ A / B loaders (NT)
-// A loader contract:  set_phase(p); int K() const; uint4 load(int m, int k) (16 bytes, zero-filled OOB)
+// Loader contract: set_phase(p); int K() const; Row prep(int m) (once per tile row, outside the K loop);
+// uint4 load(const Row&, int k) (16 bytes = V consecutive k, zero-filled outside the operand).
 
 template <typename T>
 struct DenseLoader {  // X[m * ld + k], m < M, k < K
     const T* p;
     int ld, M, Kd;
-    bool vec;  // ld % VEC == 0 and K % VEC == 0 and p 16B aligned
+    bool vec;  // ld % VEC == 0 and p 16B aligned
+    struct Row {
+        const T* r;
+    };
     __device__ void set_phase(int) {}
     __device__ int K() const { return Kd; }
-    __device__ uint4 load(int m, int k) const {
+    __device__ Row prep(int m) const { return Row{m < M ? p + (int64_t)m * ld : nullptr}; }
+    __device__ uint4 load(const Row& rw, int k) const {
         constexpr int V = Vec16<T>::N;
-        if (m >= M) return make_uint4(0, 0, 0, 0);
-        const T* r = p + (int64_t)m * ld;
-        if (vec && k + V <= Kd) return *reinterpret_cast<const uint4*>(r + k);
+        if (!rw.r) return make_uint4(0, 0, 0, 0);
+        if (vec && k + V <= Kd) return *reinterpret_cast<const uint4*>(rw.r + k);
         union { uint4 u; T e[V]; } x;
 #pragma unroll
-        for (int i = 0; i < V; ++i) x.e[i] = (k + i < Kd) ? r[k + i] : from_f32<T>(0.f);
+        for (int i = 0; i < V; ++i) x.e[i] = (k + i < Kd) ? rw.r[k + i] : from_f32<T>(0.f);
         return x.u;
     }
 };
 
 // Stride-2, pad-1, 3x3 window gather over an NHWC map: A(m = (b,oh,ow), k = (kh,kw,ci))
 //   = X[b, 2oh-1+kh, 2ow-1+kw, ci].  Requires C % (4*VEC) == 0 (a BK chunk never straddles taps).
+// Only the top row (kh = 0, oh = 0) and left column (kw = 0, ow = 0) of the window can fall outside.
 template <typename T>
 struct ConvS2Loader {
     const T* x;
     int Hi, Wi, C, Ho, Wo, M;
+    int cshift;  // log2(C) when C is a power of two, else -1
+    struct Row {
+        int64_t base;  // element offset of (b, 2oh-1, 2ow-1, 0)
+        int flags;     // bit0 valid, bit1 top row, bit2 left column
+    };
     __device__ void set_phase(int) {}
     __device__ int K() const { return 9 * C; }
-    __device__ uint4 load(int m, int k) const {
-        if (m >= M) return make_uint4(0, 0, 0, 0);
-        int ow = m % Wo, t = m / Wo;
-        int oh = t % Ho, b = t / Ho;
-        int tap = k / C, ci = k - tap * C;
-        int kh = tap / 3, kw = tap - kh * 3;
-        int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
-        if ((unsigned)ih >= (unsigned)Hi || (unsigned)iw >= (unsigned)Wi) return make_uint4(0, 0, 0, 0);
-        return *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * Wi + iw) * C + ci);
+    __device__ Row prep(int m) const {
+        if (m >= M) return Row{0, 0};
+        const int ow = m % Wo, t = m / Wo;
+        const int oh = t % Ho, b = t / Ho;
+        return Row{(((int64_t)b * Hi + 2 * oh - 1) * Wi + 2 * ow - 1) * C, 1 | (oh == 0 ? 2 : 0) | (ow == 0 ? 4 : 0)};
+    }
+    __device__ uint4 load(const Row& rw, int k) const {
+        const int tap = cshift >= 0 ? (k >> cshift) : k / C;
+        const int ci = k - tap * C;
+        const int kh = tap / 3, kw = tap - kh * 3;
+        if (!(rw.flags & 1) || (kh == 0 && (rw.flags & 2)) || (kw == 0 && (rw.flags & 4)))
+            return make_uint4(0, 0, 0, 0);
+        return *reinterpret_cast<const uint4*>(x + rw.base + ((int64_t)kh * Wi + kw) * C + ci);
     }
 };
 
@@ -67,22 +94,31 @@ template <typename T>
 struct SubpixelLoader {
     const T* x;  // low-res NHWC [B, Hi, Wi, C]
     int Hi, Wi, C, M;  // M = B*Hi*Wi
+    int cshift;
     int py, px, ntx, Kd;
+    struct Row {
+        int64_t base;  // offset of (b, r, c, 0)
+        int flags;     // bit0 valid, bit1 last row (r+1 out), bit2 last column
+    };
     __device__ void set_phase(int p) {
         py = p >> 1; px = p & 1;
         ntx = sp_ntaps(px);
         Kd = sp_ntaps(py) * ntx * C;
     }
     __device__ int K() const { return Kd; }
-    __device__ uint4 load(int m, int k) const {
-        if (m >= M) return make_uint4(0, 0, 0, 0);
-        int c = m % Wi, t = m / Wi;
-        int r = t % Hi, b = t / Hi;
-        int tt = k / C, ci = k - tt * C;
-        int ty = tt / ntx, tx = tt - ty * ntx;
-        int ih = r + sp_delta(py, ty), iw = c + sp_delta(px, tx);
-        if (ih >= Hi || iw >= Wi) return make_uint4(0, 0, 0, 0);
-        return *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * Wi + iw) * C + ci);
+    __device__ Row prep(int m) const {
+        if (m >= M) return Row{0, 0};
+        const int c = m % Wi, t = m / Wi;
+        const int r = t % Hi, b = t / Hi;
+        return Row{(((int64_t)b * Hi + r) * Wi + c) * C, 1 | (r == Hi - 1 ? 2 : 0) | (c == Wi - 1 ? 4 : 0)};
+    }
+    __device__ uint4 load(const Row& rw, int k) const {
+        const int tt = cshift >= 0 ? (k >> cshift) : k / C;
+        const int ci = k - tt * C;
+        const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
+        const int dr = sp_delta(py, ty), dc = sp_delta(px, tx);
+        if (!(rw.flags & 1) || (dr && (rw.flags & 2)) || (dc && (rw.flags & 4))) return make_uint4(0, 0, 0, 0);
+        return *reinterpret_cast<const uint4*>(x + rw.base + ((int64_t)dr * Wi + dc) * C + ci);
     }
 };
 
@@ -91,23 +127,30 @@ template <typename T>
 struct SubpixelWeight {
     const T* w;
     int C, N;
+    int cshift;
     int py, px, ntx, Kd;
+    struct Row {
+        const T* r;
+    };
     __device__ void set_phase(int p) {
         py = p >> 1; px = p & 1;
         ntx = sp_ntaps(px);
         Kd = sp_ntaps(py) * ntx * C;
     }
     __device__ int K() const { return Kd; }
-    __device__ uint4 load(int n, int k) const {
-        if (n >= N) return make_uint4(0, 0, 0, 0);
-        int tt = k / C, ci = k - tt * C;
-        int ty = tt / ntx, tx = tt - ty * ntx;
-        int kh = sp_kidx(py, ty), kw = sp_kidx(px, tx);
-        return *reinterpret_cast<const uint4*>(w + ((int64_t)n * 9 + kh * 3 + kw) * C + ci);
+    __device__ Row prep(int n) const { return Row{n < N ? w + (int64_t)n * 9 * C : nullptr}; }
+    __device__ uint4 load(const Row& rw, int k) const {
+        if (!rw.r) return make_uint4(0, 0, 0, 0);
+        const int tt = cshift >= 0 ? (k >> cshift) : k / C;
+        const int ci = k - tt * C;
+        const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
+        const int kh = sp_kidx(py, ty), kw = sp_kidx(px, tx);
+        return *reinterpret_cast<const uint4*>(rw.r + (kh * 3 + kw) * C + ci);
     }
 };
 
 // ============================================================================ epilogues
+// Epilogue contract: set_phase(p); Row row(int m) (once per output row); store(const Row&, int n, float v).
 // Row-major store with bias, activation, optional accumulate:  out[m*ld + n] (+)= act(v + bias[n])
 // act: 0 none, 1 relu
 template <typename OutT>
@@ -115,11 +158,15 @@ struct StoreRM {
     OutT* out;
     const float* bias;
     int ld, act, accumulate;
+    struct Row {
+        OutT* r;
+    };
     __device__ void set_phase(int) {}
-    __device__ void store(int m, int n, float v) const {
+    __device__ Row row(int m) const { return Row{out + (int64_t)m * ld}; }
+    __device__ void store(const Row& rw, int n, float v) const {
         if (bias) v += bias[n];
         if (act == 1) v = v > 0.f ? v : 0.f;
-        OutT* o = out + (int64_t)m * ld + n;
+        OutT* o = rw.r + n;
         if (accumulate) v += to_f32<OutT>(*o);
         *o = from_f32<OutT>(v);
     }
@@ -132,13 +179,19 @@ struct StoreSubpixel {
     const float* bias;
     int Hi, Wi, N;
     int py, px;
+    struct Row {
+        OutT* r;
+    };
     __device__ void set_phase(int p) { py = p >> 1; px = p & 1; }
-    __device__ void store(int m, int n, float v) const {
-        int c = m % Wi, t = m / Wi;
-        int r = t % Hi, b = t / Hi;
+    __device__ Row row(int m) const {
+        const int c = m % Wi, t = m / Wi;
+        const int r = t % Hi, b = t / Hi;
+        const int64_t pix = ((int64_t)b * 2 * Hi + 2 * r + py) * (2 * Wi) + 2 * c + px;
+        return Row{out + pix * N};
+    }
+    __device__ void store(const Row& rw, int n, float v) const {
         if (bias) v += bias[n];
-        int64_t pix = ((int64_t)b * 2 * Hi + 2 * r + py) * (2 * Wi) + 2 * c + px;
-        out[pix * N + n] = from_f32<OutT>(v);
+        rw.r[n] = from_f32<OutT>(v);
     }
 };
 
@@ -147,10 +200,12 @@ struct StorePartial {
     float* ws;
     int M, N, S;
     int phase, split;
+    struct Row {
+        float* r;
+    };
     __device__ void set_phase(int p) { phase = p; }
-    __device__ void store(int m, int n, float v) const {
-        ws[(((int64_t)phase * S + split) * M + m) * N + n] = v;
-    }
+    __device__ Row row(int m) const { return Row{ws + (((int64_t)phase * S + split) * M + m) * N}; }
+    __device__ void store(const Row& rw, int n, float v) const { rw.r[n] = v; }
 };
 
 // ============================================================================ NT main loop
@@ -184,16 +239,22 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     uint4 ra[AR], rb[BR];
+    typename AL::Row arow[AR];
+    typename BL::Row brow[BR];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) arow[i] = al.prep(m0 + ((tid + i * 256) >> 2));
+#pragma unroll
+    for (int i = 0; i < BR; ++i) brow[i] = bl.prep(n0 + ((tid + i * 256) >> 2));
     auto gload = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) ra[i] = al.load(m0 + (c >> 2), k0 + (c & 3) * V);
+            if (c < ACH) ra[i] = al.load(arow[i], k0 + (c & 3) * V);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) rb[i] = bl.load(n0 + (c >> 2), k0 + (c & 3) * V);
+            if (c < BCH) rb[i] = bl.load(brow[i], k0 + (c & 3) * V);
         }
     };
     auto lstore = [&](int buf) {
@@ -256,13 +317,16 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
+            if (m >= M) continue;
+            const typename EP::Row er = ep.row(m);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
-                int n = n0 + wn0 + j * 16 + (lane & 15);
-                if (m < M && n < N) ep.store(m, n, acc[i][j][r]);
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wn0 + j * 16 + (lane & 15);
+                if (n < N) ep.store(er, n, acc[i][j][r]);
             }
+        }
 }
 
 // Split-K wrapper epilogue: the z-index of the grid selects the partial slab.
@@ -291,21 +355,28 @@ __global__ void splitk_reduce_kernel(const float* ws, EP ep, int M, int N, int S
         for (; k < S; ++k) s += p[k * st];
         EP e = ep;
         e.set_phase(ph);
-        e.store(m, n, s);
+        e.store(e.row(m), n, s);
     }
 }
 
 // ============================================================================ TN (weight-gradient) loaders
-// L loader: L(k, m) = p[k*ld + m]; loads 16 bytes = V consecutive m.
+// Contract: Col prep(int col) (once per chunk column, outside the K loop); uint4 load(int k, const Col&)
+// returns V consecutive columns of k-row k.
 template <typename T>
 struct KRowDense {
     const T* p;
     int ld, Kd, Md;  // rows (k) and columns (m/n)
-    __device__ uint4 load(int k, int m) const {
+    bool vec;        // rows 16-byte aligned (ld % V == 0)
+    struct Col {
+        int m;
+    };
+    __device__ Col prep(int m) const { return Col{m}; }
+    __device__ uint4 load(int k, const Col& cl) const {
         constexpr int V = Vec16<T>::N;
+        const int m = cl.m;
         if (k >= Kd) return make_uint4(0, 0, 0, 0);
         const T* r = p + (int64_t)k * ld;
-        if (m + V <= Md) return *reinterpret_cast<const uint4*>(r + m);
+        if (vec && m + V <= Md) return *reinterpret_cast<const uint4*>(r + m);
         union { uint4 u; T e[V]; } x;
 #pragma unroll
         for (int i = 0; i < V; ++i) x.e[i] = (m + i < Md) ? r[m + i] : from_f32<T>(0.f);
@@ -319,16 +390,27 @@ template <typename T>
 struct KRowConvS2 {
     const T* x;
     int Hl, Wl, C, Kd;  // Kd = B*Hl*Wl
-    __device__ uint4 load(int k, int n) const {
-        if (k >= Kd || n >= 9 * C) return make_uint4(0, 0, 0, 0);
-        int c = k % Wl, t = k / Wl;
-        int r = t % Hl, b = t / Hl;
-        int tap = n / C, ci = n - tap * C;
-        int kh = tap / 3, kw = tap - kh * 3;
-        int ih = 2 * r - 1 + kh, iw = 2 * c - 1 + kw;
-        int Hh = 2 * Hl, Wh = 2 * Wl;
-        if ((unsigned)ih >= (unsigned)Hh || (unsigned)iw >= (unsigned)Wh) return make_uint4(0, 0, 0, 0);
-        return *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hh + ih) * Wh + iw) * C + ci);
+    FastDiv dW, dH;     // division by Wl and Hl
+    struct Col {
+        int off;  // (kh*Wh + kw)*C + ci relative to pixel (2r-1, 2c-1)
+        int kh, kw;
+        bool ok;
+    };
+    __device__ Col prep(int n) const {
+        if (n >= 9 * C) return Col{0, 0, 0, false};
+        const int tap = n / C, ci = n - tap * C;
+        const int kh = tap / 3, kw = tap - kh * 3;
+        return Col{(kh * 2 * Wl + kw) * C + ci, kh, kw, true};
+    }
+    __device__ uint4 load(int k, const Col& cl) const {
+        if (k >= Kd || !cl.ok) return make_uint4(0, 0, 0, 0);
+        const uint32_t t = dW.div((uint32_t)k);
+        const int c = k - (int)t * Wl;
+        const uint32_t b = dH.div(t);
+        const int r = (int)t - (int)b * Hl;
+        if ((r == 0 && cl.kh == 0) || (c == 0 && cl.kw == 0)) return make_uint4(0, 0, 0, 0);
+        const int64_t pix = ((int64_t)b * 2 * Hl + 2 * r - 1) * (2 * Wl) + 2 * c - 1;
+        return *reinterpret_cast<const uint4*>(x + pix * C + cl.off);
     }
 };
 
@@ -363,16 +445,22 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
 
     uint4 ra[AR], rb[BR];
     constexpr int ACPR = BM / V, BCPR = BN / V;  // chunks per k-row
+    typename LL::Col acol[AR];
+    typename HL::Col bcol[BR];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) acol[i] = ll.prep(m0 + ((tid + i * 256) % ACPR) * V);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) bcol[i] = hl.prep(n0 + ((tid + i * 256) % BCPR) * V);
     auto gload = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) ra[i] = ll.load(k0 + c / ACPR, m0 + (c % ACPR) * V);
+            if (c < ACH) ra[i] = ll.load(k0 + c / ACPR, acol[i]);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) rb[i] = hl.load(k0 + c / BCPR, n0 + (c % BCPR) * V);
+            if (c < BCH) rb[i] = hl.load(k0 + c / BCPR, bcol[i]);
         }
     };
     auto lstore = [&](int buf) {

@@ -24,10 +24,10 @@ inline Plan plan_nt(int tiles, int Kmax, int BK) {
     return {S, ksl};
 }
 inline Plan plan_tn(int tiles, int K, int BK) {
-    // weight gradients: long K (= batch x pixels), tiny M x N; each split keeps >= 32 k-tiles so the
-    // partial slabs (and their reduction) stay small next to the GEMM itself
-    int S = cdiv(kTargetBlocks / 2, tiles);
-    S = std::max(1, std::min(S, K / (32 * BK)));
+    // weight gradients: long K (= batch x pixels), tiny M x N: split K until the grid fills the chip
+    // (>= 8 k-tiles per split); the slab reduction keeps 4 loads in flight
+    int S = cdiv(kTargetBlocks, tiles);
+    S = std::max(1, std::min(S, K / (8 * BK)));
     int ksl = cdiv(cdiv(K, S), BK) * BK;
     S = cdiv(K, ksl);
     return {S, ksl};
@@ -96,10 +96,14 @@ size_t dispatch_linear_ws(int M, int N, int K) {
 struct StoreWgradConv {
     float* dW;
     int C;
+    struct Row {
+        float* r;
+    };
     __device__ void set_phase(int) {}
-    __device__ void store(int m, int n, float v) const {
+    __device__ Row row(int m) const { return Row{dW + (int64_t)m * C * 9}; }
+    __device__ void store(const Row& rw, int n, float v) const {
         int tap = n / C, ci = n - tap * C;
-        dW[((int64_t)m * C + ci) * 9 + tap] = v;
+        rw.r[ci * 9 + tap] = v;
     }
 };
 
@@ -139,24 +143,8 @@ size_t dispatch_tn_ws(int M, int N, int K) {
     return tn_ws<32, 128>(M, N, K, BK);
 }
 
-template <typename T>
-struct KRowDenseV {  // KRowDense with a scalar path when rows are not 16-byte aligned
-    const T* p;
-    int ld, Kd, Md;
-    bool vec;
-    __device__ uint4 load(int k, int m) const {
-        constexpr int V = Vec16<T>::N;
-        if (k >= Kd) return make_uint4(0, 0, 0, 0);
-        const T* r = p + (int64_t)k * ld;
-        if (vec && m + V <= Md) return *reinterpret_cast<const uint4*>(r + m);
-        union { uint4 u; T e[V]; } x;
-#pragma unroll
-        for (int i = 0; i < V; ++i) x.e[i] = (m + i < Md) ? r[m + i] : from_f32<T>(0.f);
-        return x.u;
-    }
-};
-
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+inline int log2_exact(int c) { return (c > 0 && (c & (c - 1)) == 0) ? __builtin_ctz(c) : -1; }
 
 }  // namespace
 
@@ -168,7 +156,7 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % (4 * V) == 0, "conv_s2: need even H/W and Ci % BK == 0");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "conv_s2: 16-byte alignment");
     const int Ho = Hi / 2, Wo = Wi / 2, M = B * Ho * Wo, K = 9 * Ci;
-    ConvS2Loader<T> al{x, Hi, Wi, Ci, Ho, Wo, M};
+    ConvS2Loader<T> al{x, Hi, Wi, Ci, Ho, Wo, M, log2_exact(Ci)};
     DenseLoader<T> bl{wp, K, Co, K, true};
     StoreRM<T> ep{y, bias, Co, 0, 0};
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws);
@@ -184,8 +172,8 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
     HLMC_CHECK_ARG(Ci % (4 * V) == 0, "subpixel: Ci % BK == 0");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "subpixel: 16-byte alignment");
     const int M = B * Hi * Wi;
-    SubpixelLoader<T> al{x, Hi, Wi, Ci, M, 0, 0, 0, 0};
-    SubpixelWeight<T> bl{wp, Ci, Co, 0, 0, 0, 0};
+    SubpixelLoader<T> al{x, Hi, Wi, Ci, M, log2_exact(Ci), 0, 0, 0, 0};
+    SubpixelWeight<T> bl{wp, Ci, Co, log2_exact(Ci), 0, 0, 0, 0};
     StoreSubpixel<T> ep{y, bias, Hi, Wi, Co, 0, 0};
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws);
 }
@@ -199,8 +187,8 @@ int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* X
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(M % V == 0 && C % V == 0, "wgrad_s2: channel counts must be multiples of the vector width");
     const int K = B * Hl * Wl, N = 9 * C;
-    KRowDense<T> ll{L, M, K, M};
-    KRowConvS2<T> hl{Xh, Hl, Wl, C, K};
+    KRowDense<T> ll{L, M, K, M, aligned16(L)};
+    KRowConvS2<T> hl{Xh, Hl, Wl, C, K, FastDiv((uint32_t)Wl), FastDiv((uint32_t)Hl)};
     StoreWgradConv ep{dW, C};
     return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
 }
@@ -228,8 +216,8 @@ size_t linear_ws(int M, int K, int N) {
 template <typename T>
 int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int Mb, int N, int K, float* dW, Ws ws) {
     constexpr int V = Vec16<T>::N;
-    KRowDenseV<T> ll{dy, lddy, Mb, N, (lddy % V == 0) && aligned16(dy)};
-    KRowDenseV<T> hl{x, ldx, Mb, K, (ldx % V == 0) && aligned16(x)};
+    KRowDense<T> ll{dy, lddy, Mb, N, (lddy % V == 0) && aligned16(dy)};
+    KRowDense<T> hl{x, ldx, Mb, K, (ldx % V == 0) && aligned16(x)};
     StoreRM<float> ep{dW, nullptr, K, 0, 0};
     return dispatch_tn<T>(s, ll, hl, ep, N, K, Mb, ws);
 }

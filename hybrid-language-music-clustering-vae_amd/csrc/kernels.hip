@@ -613,21 +613,36 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, float b1, float
 }
 
 // ---------------------------------------------------------------- weight packing
+// W [d0][d1][taps] f32 -> P0 [d0][taps][ld0] and P1 [d1][taps][ld1] (T).  Block = one (job, 32 x 32 tile of
+// (i0, i1)); the tile's 32 x 32 x taps floats are staged in LDS (coalesced reads of W rows), then each
+// (i0, tap) row segment of P0 and each (i1, tap) row segment of P1 is written as 32 consecutive elements.
 template <typename T>
-__global__ void pack_kernel(const ops::PackJob* __restrict__ jobs, int njobs) {
-    const ops::PackJob jb = jobs[blockIdx.y];
-    const int64_t n = (int64_t)jb.d0 * jb.d1 * jb.taps;
+__global__ __launch_bounds__(256) void pack_kernel(const ops::PackJob* __restrict__ jobs, int njobs) {
+    const ops::PackJob jb = jobs[blockIdx.z];
+    const int t0 = blockIdx.x * 32, t1 = blockIdx.y * 32;   // i0 / i1 tile origin
+    if (t0 >= jb.d0 || t1 >= jb.d1) return;
+    const int taps = jb.taps;
+    const int n0 = min(32, jb.d0 - t0), n1 = min(32, jb.d1 - t1);
+    __shared__ float tile[32 * 32 * 9 + 32];
+    // rows of W: for each i0 in the tile, n1 * taps contiguous floats starting at (t0+a)*d1*taps + t1*taps
+    const int rowlen = n1 * taps;
+    for (int e = threadIdx.x; e < n0 * 32 * taps; e += blockDim.x) {
+        const int a = e / (32 * taps), r = e % (32 * taps);
+        if (r < rowlen) tile[(a * 32) * taps + r] = jb.w[((int64_t)(t0 + a) * jb.d1 + t1) * taps + r];
+    }
+    __syncthreads();
     T* p0 = (T*)jb.p0;
     T* p1 = (T*)jb.p1;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        int64_t i0 = e / ((int64_t)jb.d1 * jb.taps);
-        int64_t rem = e - i0 * jb.d1 * jb.taps;
-        int64_t i1 = rem / jb.taps;
-        int tap = (int)(rem - i1 * jb.taps);
-        T v = from_f32<T>(jb.w[e]);
-        if (p0) p0[(i0 * jb.taps + tap) * jb.ld0 + i1] = v;
-        if (p1) p1[(i1 * jb.taps + tap) * jb.ld1 + i0] = v;
-    }
+    if (p0)  // P0[(i0*taps + tap)*ld0 + i1]: for each (a, tap) write n1 consecutive i1
+        for (int e = threadIdx.x; e < n0 * taps * 32; e += blockDim.x) {
+            const int q = e % 32, at = e / 32, a = at / taps, tap = at % taps;
+            if (q < n1) p0[((int64_t)(t0 + a) * taps + tap) * jb.ld0 + t1 + q] = from_f32<T>(tile[(a * 32 + q) * taps + tap]);
+        }
+    if (p1)  // P1[(i1*taps + tap)*ld1 + i0]: for each (c, tap) write n0 consecutive i0
+        for (int e = threadIdx.x; e < n1 * taps * 32; e += blockDim.x) {
+            const int q = e % 32, ct = e / 32, c = ct / taps, tap = ct % taps;
+            if (q < n0) p1[((int64_t)(t1 + c) * taps + tap) * jb.ld1 + t0 + q] = from_f32<T>(tile[(q * 32 + c) * taps + tap]);
+        }
 }
 
 }  // namespace
@@ -897,9 +912,10 @@ int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, fl
 }
 
 template <typename T>
-int pack(hipStream_t s, const PackJob* jobs_dev, int njobs, int64_t max_elems) {
+int pack(hipStream_t s, const PackJob* jobs_dev, int njobs, int64_t max_dim) {
     if (njobs == 0) return HLMC_OK;
-    dim3 grid((unsigned)std::min<int64_t>(1024, (max_elems + 255) / 256), njobs);
+    const unsigned tiles = (unsigned)((max_dim + 31) / 32);
+    dim3 grid(tiles, tiles, njobs);
     pack_kernel<T><<<grid, 256, 0, s>>>(jobs_dev, njobs);
     HLMC_LAUNCHED();
     return HLMC_OK;

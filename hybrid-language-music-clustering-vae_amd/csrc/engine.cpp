@@ -28,9 +28,10 @@ class NetT : public NetBase {
         size_t off0 = SIZE_MAX, off1 = SIZE_MAX;
     };
     std::vector<Pack> packs;
-    size_t jobs_off = 0, state_size = 0;
-    int64_t pack_max = 0;
-    int njobs = 0;
+    size_t jobs_off = 0, ajobs_off = 0, state_size = 0;
+    int njobs = 0, pack_tiles = 0, adam_tiles = 0;
+    std::vector<ops::AdamJob> ajobs;  // host copy of the uploaded Adam job list (kept alive for the async copy)
+    std::vector<float*> ajobs_m, ajobs_v;
 
     void register_pack(int widx, int taps) {
         if ((int)packs.size() < (int)params.size()) packs.resize(params.size());
@@ -49,41 +50,67 @@ class NetT : public NetBase {
             p.ld1 = p.taps == 1 ? pad8(p.d0) : p.d0;
             p.off0 = A.take((size_t)p.d0 * p.taps * p.ld0 * sizeof(T));
             p.off1 = A.take((size_t)p.d1 * p.taps * p.ld1 * sizeof(T));
-            pack_max = std::max<int64_t>(pack_max, std::max(p.d0, p.d1));  // largest dimension (tile grid)
             ++njobs;
         }
-        jobs_off = A.take(sizeof(ops::PackJob) * std::max(1, njobs));
+        jobs_off = A.take(sizeof(ops::AdamJob) * std::max<size_t>(1, njobs));
+        ajobs_off = A.take(sizeof(ops::AdamJob) * std::max<size_t>(1, params.size()));
         state_size = A.used;
     }
     size_t state_bytes() const override { return state_size; }
-    int bind_state(hipStream_t s) override {
-        std::vector<ops::PackJob> jobs;
-        for (size_t i = 0; i < packs.size(); ++i) {
-            const Pack& p = packs[i];
-            if (!p.taps) continue;
-            jobs.push_back({P[i], state + p.off0, state + p.off1, p.d0, p.d1, p.taps, p.ld0, p.ld1});
+    ops::AdamJob job_for(size_t i, float* m, float* v) const {
+        const Pack& p = packs[i];
+        ops::AdamJob j{P[i], G[i], m, v, nullptr, nullptr, params[i].numel(), 0, 0, 0, 0, 0, 0, 0};
+        if (p.taps) {
+            j.p0 = state + p.off0;
+            j.p1 = state + p.off1;
+            j.d0 = p.d0; j.d1 = p.d1; j.taps = p.taps; j.ld0 = p.ld0; j.ld1 = p.ld1;
         }
-        if (!jobs.empty())
-            HLMC_HIP(hipMemcpyAsync(state + jobs_off, jobs.data(), jobs.size() * sizeof(ops::PackJob), hipMemcpyHostToDevice, s));
+        return j;
+    }
+    std::vector<ops::AdamJob> pjobs;
+    int bind_state(hipStream_t s) override {
+        pjobs.clear();
+        pack_tiles = 0;
+        for (size_t i = 0; i < packs.size(); ++i) {
+            if (!packs[i].taps) continue;
+            ops::AdamJob j = job_for(i, nullptr, nullptr);
+            j.tile0 = pack_tiles;
+            pack_tiles += ops::adam_job_tiles(j);
+            pjobs.push_back(j);
+        }
+        if (!pjobs.empty())
+            HLMC_HIP(hipMemcpyAsync(state + jobs_off, pjobs.data(), pjobs.size() * sizeof(ops::AdamJob), hipMemcpyHostToDevice, s));
+        ajobs_m.clear();  // Adam job list is rebuilt on the next adam_step (parameter pointers changed)
         HLMC_HIP(hipStreamSynchronize(s));
         return HLMC_OK;
     }
     int pack_all(hipStream_t s) {
         if (trust_packs && packs_valid) return HLMC_OK;
-        // pack_max = largest weight dimension (the tiled pack kernel's grid)
-        HLMC_TRY(ops::pack<T>(s, reinterpret_cast<const ops::PackJob*>(state + jobs_off), njobs, pack_max));
+        HLMC_TRY(ops::pack<T>(s, reinterpret_cast<const ops::AdamJob*>(state + jobs_off), njobs, pack_tiles));
         packs_valid = true;
         return HLMC_OK;
     }
     int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a) override {
-        // Adam over all parameters (one multi-tensor launch per 32 tensors), then one tiled re-pack
+        // one launch: torch-Adam update of every parameter + refresh of the packed GEMM weights
         const size_t np = params.size();
-        std::vector<int64_t> numel(np);
-        for (size_t i = 0; i < np; ++i) numel[i] = params[i].numel();
-        std::vector<const float*> g(G.begin(), G.end());
-        HLMC_TRY(ops::adam(s, (int)np, P.data(), g.data(), m, v, numel.data(), a));
-        packs_valid = false;
-        return pack_all(s);
+        if (ajobs_m.size() != np || !std::equal(ajobs_m.begin(), ajobs_m.end(), m) ||
+            !std::equal(ajobs_v.begin(), ajobs_v.end(), v)) {
+            ajobs_m.assign(m, m + np);
+            ajobs_v.assign(v, v + np);
+            ajobs.clear();
+            adam_tiles = 0;
+            for (size_t i = 0; i < np; ++i) {
+                ops::AdamJob j = job_for(i, m[i], v[i]);
+                j.tile0 = adam_tiles;
+                adam_tiles += ops::adam_job_tiles(j);
+                ajobs.push_back(j);
+            }
+            HLMC_HIP(hipMemcpyAsync(state + ajobs_off, ajobs.data(), ajobs.size() * sizeof(ops::AdamJob),
+                                    hipMemcpyHostToDevice, s));
+        }
+        HLMC_TRY(ops::adam_pack<T>(s, reinterpret_cast<const ops::AdamJob*>(state + ajobs_off), (int)np, adam_tiles, a));
+        packs_valid = true;
+        return HLMC_OK;
     }
     T* P0(int w) const { return reinterpret_cast<T*>(state + packs[w].off0); }
     T* P1(int w) const { return reinterpret_cast<T*>(state + packs[w].off1); }

@@ -2,10 +2,9 @@
 // pooling and the StandardScaler fit/apply.  Replaces librosa / sklearn calls of
 // src/1_preprocessing.py:48-70,115-121,305-311 and src/1_preprocessing_advanced.py:97-114,376-391.
 //
-// STFT kernel: one 256-thread workgroup per (clip, group of frames).  A 2048-point real frame is
-// packed into a 1024-point complex sequence (even/odd samples), transformed with a radix-4 Stockham
-// FFT in LDS (5 stages, one butterfly per thread per stage), and split back into the 1025 real-FFT
-// bins.  Window / twiddle tables are built on the host in double precision.  The Slaney filterbank is
+// STFT kernel: one 256-thread workgroup per (clip, 16 frames), one wavefront per frame.  A 2048-point
+// real frame is packed into a 1024-point complex sequence (even/odd samples), transformed with a
+// register-resident radix-16/16/4 Stockham FFT, and split back into the 1025 real-FFT bins.  Window / twiddle tables are built on the host in double precision.  The Slaney filterbank is
 // banded (each filter spans 4..53 bins) and stored as (first bin, count, weights) per mel band.
 #include <algorithm>
 #include <cmath>
@@ -52,136 +51,237 @@ constexpr int kFFT = 1024;  // complex points (n_fft = 2048 real)
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
 
-// stft -> power -> mel for FPB frames of one clip. out [B][n_mels][T]; clip_max/min (uint bits of f32 >= 0)
-// LDS: frame buffers, the real-FFT twiddles (e^{-2 pi i f/2048}; the 1024-point twiddles are its even
-// entries), the banded filterbank and the frame's power spectrum.  Two threads per mel band.
-constexpr int kMaxW = 4096;  // packed filterbank weights held in LDS
-template <int FPB>
+// ---------------------------------------------------------------- STFT -> |X|^2 -> mel, one wavefront per frame
+// A 2048-sample real frame is packed into z[n] = x[2n] w[2n] + i x[2n+1] w[2n+1] (n < 1024) and transformed
+// with a Stockham FFT of radices 16, 16, 4: every lane holds 16 complex points, the radix-16 butterflies run
+// in registers (as 4 x 4), and the stage-to-stage exchanges go through a wave-private LDS buffer (no block
+// barriers: one wave's LDS accesses complete in issue order).  The real-FFT split produces the 1025 power
+// bins, then lane l accumulates the banded Slaney filters l, l+64, ...  Twiddles are e^{-2 pi i m / 2048}
+// from a double-precision host table (LDS-resident); the filterbank is packed per band (first bin, count).
+constexpr int kMaxW = 8192;    // filterbank weight floats held in LDS (chunk-transposed, zero padded)
+constexpr int kWaves = 4;      // frames in flight per workgroup
+constexpr int kFpw = 4;        // frames per wave
+constexpr int kFpb = kWaves * kFpw;
+constexpr int kZ = kFFT + kFFT / 16;  // padded complex buffer (one pad slot per 16: conflict-free stage writes)
+constexpr int kTw2 = 15 * 16, kTw3 = 3 * 256;
+constexpr int kMelLanes = 64;  // band pairs (n_mels <= 128)
+
+__device__ __forceinline__ int zpad(int i) { return i + (i >> 4); }
+// Lanes of one wavefront exchange data through LDS without a workgroup barrier: a wavefront-scope
+// release/acquire pair around wave_barrier orders the exchange's writes before the other lanes' reads.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // -i * a
+
+// y_k = sum_n a_n (-i)^{nk}
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 s02 = cadd(a0, a2), d02 = csub(a0, a2), s13 = cadd(a1, a3), d13 = mul_mi(csub(a1, a3));
+    a0 = cadd(s02, s13);
+    a1 = cadd(d02, d13);
+    a2 = csub(s02, s13);
+    a3 = csub(d02, d13);
+}
+// 16-point DFT in place (output in slot order, see slot16): n = 4 n1 + n2, k = k1 + 4 k2
+__device__ __forceinline__ void dft16(float2 (&a)[16]) {
+    constexpr float c1 = 0.92387953251128674f, s1 = 0.38268343236508977f, h = 0.70710678118654752f;
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) dft4(a[n2], a[4 + n2], a[8 + n2], a[12 + n2]);
+    // twiddles W16^{n2 k1}: slot 4 k1 + n2 holds column n2, row k1
+    a[5] = cmul(a[5], make_float2(c1, -s1));    // n2=1,k1=1: W^1
+    a[9] = cmul(a[9], make_float2(h, -h));      // n2=1,k1=2: W^2
+    a[13] = cmul(a[13], make_float2(s1, -c1));  // n2=1,k1=3: W^3
+    a[6] = cmul(a[6], make_float2(h, -h));      // n2=2,k1=1: W^2
+    a[10] = mul_mi(a[10]);                      // n2=2,k1=2: W^4
+    a[14] = cmul(a[14], make_float2(-h, -h));   // n2=2,k1=3: W^6
+    a[7] = cmul(a[7], make_float2(s1, -c1));    // n2=3,k1=1: W^3
+    a[11] = cmul(a[11], make_float2(-h, -h));   // n2=3,k1=2: W^6
+    a[15] = cmul(a[15], make_float2(-c1, s1));  // n2=3,k1=3: W^9
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) dft4(a[4 * k1], a[4 * k1 + 1], a[4 * k1 + 2], a[4 * k1 + 3]);
+    // slot 4 k1 + k2 now holds X[k1 + 4 k2]; callers read X[r] from a[slot16(r)]
+}
+__device__ __forceinline__ constexpr int slot16(int r) { return 4 * (r & 3) + (r >> 2); }
+
 __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__ pcm, int64_t n_samples, int T,
                                                        int hop, const float* __restrict__ window,
-                                                       const float2* __restrict__ tw, const float2* __restrict__ rtw,
-                                                       const int* __restrict__ band, const int* __restrict__ woff,
-                                                       const float* __restrict__ wts, int n_mels, int nnz,
-                                                       float* __restrict__ out, unsigned* __restrict__ clip_max,
-                                                       unsigned* __restrict__ clip_min) {
-    __shared__ float2 buf[kFFT];
-    __shared__ float2 tmp[kFFT];
-    __shared__ float2 srtw[kFFT + 1];
-    __shared__ int sband[128][3];
-    __shared__ float pw[kFFT + 1];
-    __shared__ float mel[FPB][129];
-    extern __shared__ float sw[];  // nnz packed filterbank weights (dynamic, exact size)
+                                                       const float2* __restrict__ rtw, const float2* __restrict__ tw23,
+                                                       const int* __restrict__ band,
+                                                       const int* __restrict__ woff, const float* __restrict__ wts,
+                                                       int n_mels, int nnz, float* __restrict__ out,
+                                                       unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min) {
+    __shared__ float2 stw[kFFT + 1];
+    __shared__ float2 stw23[kTw2 + kTw3];
+    __shared__ __align__(16) float2 zb[kWaves][kZ];
+    // dynamic: chunk-transposed filterbank W[c][lane][4] (nnz floats) | per-lane band info int4[64] |
+    // mel staging [kFpb][n_mels + 1]
+    extern __shared__ float4 sw4[];
+    int4* sbl = reinterpret_cast<int4*>(sw4 + nnz / 4);
+    float* smel = reinterpret_cast<float*>(sbl + kMelLanes);
     const int b = blockIdx.y;
-    const int t0 = blockIdx.x * FPB;
+    const int t0 = blockIdx.x * kFpb;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const float* x = pcm + (int64_t)b * n_samples;
-    // this thread's 4 samples of a frame: pairs kk = tid, tid + 256, tid + 512, tid + 768
-    auto fetch = [&](int t, float* v) {
-        const int64_t start = (int64_t)t * hop - kFFT;  // center=True: pad n_fft/2 = 1024 zeros
+    for (int i = threadIdx.x; i <= kFFT; i += 256) stw[i] = rtw[i];
+    for (int i = threadIdx.x; i < kTw2 + kTw3; i += 256) stw23[i] = tw23[i];
+    for (int i = threadIdx.x; i < nnz / 4; i += 256) sw4[i] = reinterpret_cast<const float4*>(wts)[i];
+    for (int l = threadIdx.x; l < kMelLanes; l += 256) sbl[l] = reinterpret_cast<const int4*>(band)[l];
+    __syncthreads();
+    float2* z = zb[wave];
+    float* pw = reinterpret_cast<float*>(z);  // power bins overwrite the spectrum after the split
+    float lmax = 0.f, lmin = INFINITY;
+    const int nf = min(kFpb, T - t0);
+    // raw sample pairs (x[2n], x[2n+1]) of frame t: n = lane + 64 r; zero outside the clip (center padding)
+    auto fetch = [&](int t, int ln, float2 (&v)[16]) {
+        const int64_t start = (int64_t)t * hop - kFFT;  // center=True: n_fft/2 = 1024 zeros of padding
+        const bool interior = start >= 0 && start + 2 * kFFT <= n_samples && ((start & 1) == 0) &&
+                              ((reinterpret_cast<uintptr_t>(x) & 7) == 0);
+        if (interior) {
+            const float2* xs = reinterpret_cast<const float2*>(x + start);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t i0 = start + 2 * (threadIdx.x + 256 * q), i1 = i0 + 1;
-            v[2 * q] = (i0 >= 0 && i0 < n_samples) ? x[i0] : 0.f;
-            v[2 * q + 1] = (i1 >= 0 && i1 < n_samples) ? x[i1] : 0.f;
+            for (int r = 0; r < 16; ++r) v[r] = xs[ln + 64 * r];
+        } else {
+            // edge frame: clamped (always in-bounds) loads, zeroed outside the clip; no divergent branches
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t i0 = start + 2 * (ln + 64 * r);
+                const int64_t c0 = min(max(i0, (int64_t)0), n_samples - 1), c1 = min(max(i0 + 1, (int64_t)0), n_samples - 1);
+                const float x0 = x[c0], x1 = x[c1];
+                v[r].x = (i0 >= 0 && i0 < n_samples) ? x0 : 0.f;
+                v[r].y = (i0 + 1 >= 0 && i0 + 1 < n_samples) ? x1 : 0.f;
+            }
         }
     };
-    for (int i = threadIdx.x; i <= kFFT; i += 256) srtw[i] = rtw[i];
-    for (int i = threadIdx.x; i < nnz; i += 256) sw[i] = wts[i];
-    for (int m = threadIdx.x; m < n_mels; m += 256) {
-        sband[m][0] = band[2 * m];
-        sband[m][1] = band[2 * m + 1];
-        sband[m][2] = woff[m];
-    }
-    float lmax = 0.f, lmin = INFINITY;
-    const int nf = min(FPB, T - t0);
-    float2 wv[4];
+    float2 nxt[16];
+    if (wave < nf) fetch(t0 + wave, lane, nxt);
+    for (int fl = wave; fl < nf; fl += kWaves) {
+        // opaque copy of the lane id: keeps the frame-invariant window / twiddle loads inside the loop
+        // (hoisted, they pin ~120 extra VGPRs and drop occupancy to one wave per SIMD)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        float2 a[16];
+        // ---- stage 1 (radix 16, Ns = 1): z[j + 64 r] = windowed sample pairs (prefetched one frame ahead)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) wv[q] = *reinterpret_cast<const float2*>(window + 2 * (threadIdx.x + 256 * q));
-    float cur[8];
-    fetch(t0, cur);
-    for (int f = 0; f < nf; ++f) {
-        // pack even/odd windowed samples: z[k] = x[2k] w[2k] + i x[2k+1] w[2k+1]
+        for (int r = 0; r < 16; ++r) {
+            const float2 w = *reinterpret_cast<const float2*>(window + 2 * (ln + 64 * r));
+            a[r] = make_float2(nxt[r].x * w.x, nxt[r].y * w.y);
+        }
+        if (fl + kWaves < nf) fetch(t0 + fl + kWaves, ln, nxt);
+        dft16(a);
+        // padded exchange addresses as lane base + compile-time offsets: zpad(i) = i + (i >> 4)
+        const int bw1 = ln * 17;                   // zpad(16 ln + r)        = 17 ln + r
+        const int brd = ln + (ln >> 4);            // zpad(ln + 64 q + 256 r) = brd + 68 q + 272 r
+        const int bw2 = (ln >> 4) * 272 + (ln & 15);  // zpad(256 g + k + 16 r) = 272 g + k + 17 r
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z[bw1 + r] = a[slot16(r)];
+        wave_lds_fence();
+        // ---- stage 2 (radix 16, Ns = 16)
+        const int k = ln & 15;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) a[r] = z[brd + 68 * r];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) a[r] = cmul(a[r], stw23[(r - 1) * 16 + k]);
+        dft16(a);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) z[bw2 + 17 * r] = a[slot16(r)];
+        wave_lds_fence();
+        // ---- stage 3 (radix 4, Ns = 256): butterflies j = ln + 64 q, in place
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int j = ln + 64 * q;
+            float2 c0 = z[brd + 68 * q], c1 = z[brd + 68 * q + 272], c2 = z[brd + 68 * q + 544], c3 = z[brd + 68 * q + 816];
+            c1 = cmul(c1, stw23[kTw2 + j]);
+            c2 = cmul(c2, stw23[kTw2 + 256 + j]);
+            c3 = cmul(c3, stw23[kTw2 + 512 + j]);
+            dft4(c0, c1, c2, c3);
+            a[4 * q] = c0; a[4 * q + 1] = c1; a[4 * q + 2] = c2; a[4 * q + 3] = c3;
+        }
+        wave_lds_fence();
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            buf[threadIdx.x + 256 * q] = make_float2(cur[2 * q] * wv[q].x, cur[2 * q + 1] * wv[q].y);
-        __syncthreads();
-        if (f + 1 < nf) fetch(t0 + f + 1, cur);  // next frame's samples are in flight during this FFT
-        // 1024-point complex FFT, Stockham radix-4 (5 stages), twiddle(k) = srtw[2k]
-        {
-            float2* src = buf;
-            float2* dst = tmp;
-            const int j = threadIdx.x;
 #pragma unroll
-            for (int st = 0; st < 5; ++st) {
-                const int Ns = 1 << (2 * st);
-                const int k = j & (Ns - 1);
-                float2 a[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) a[r] = src[j + r * (kFFT / 4)];
-                const int step = kFFT / (4 * Ns);
-#pragma unroll
-                for (int r = 1; r < 4; ++r) {
-                    // e^{-2 pi i m / 1024} = srtw[2m] for 2m <= 1024, else -srtw[2m - 1024]
-                    const int f2 = 2 * ((k * r * step) & (kFFT - 1));
-                    float2 w = srtw[f2 <= kFFT ? f2 : f2 - kFFT];
-                    if (f2 > kFFT) w = make_float2(-w.x, -w.y);
-                    a[r] = cmul(a[r], w);
-                }
-                const float2 b0 = make_float2(a[0].x + a[2].x, a[0].y + a[2].y);
-                const float2 b1 = make_float2(a[0].x - a[2].x, a[0].y - a[2].y);
-                const float2 b2 = make_float2(a[1].x + a[3].x, a[1].y + a[3].y);
-                const float2 b3 = make_float2(a[1].y - a[3].y, -(a[1].x - a[3].x));  // -i (a1 - a3)
-                const int d = ((j >> (2 * st)) << (2 * st + 2)) + k;
-                dst[d] = make_float2(b0.x + b2.x, b0.y + b2.y);
-                dst[d + Ns] = make_float2(b1.x + b3.x, b1.y + b3.y);
-                dst[d + 2 * Ns] = make_float2(b0.x - b2.x, b0.y - b2.y);
-                dst[d + 3 * Ns] = make_float2(b1.x - b3.x, b1.y - b3.y);
-                __syncthreads();
-                float2* tt = src;
-                src = dst;
-                dst = tt;
-            }
-            // after 5 stages the spectrum Z is in tmp
-        }
-        // real-FFT split: X[f] = E[f] + e^{-2 pi i f / 2048} O[f],  f = 0..1024
-        for (int fb = threadIdx.x; fb <= kFFT; fb += 256) {
-            const float2 zf = tmp[fb & (kFFT - 1)];
-            const float2 zc = tmp[(kFFT - fb) & (kFFT - 1)];
+            for (int r = 0; r < 4; ++r) z[brd + 68 * q + 272 * r] = a[4 * q + r];
+        wave_lds_fence();
+        // ---- real-FFT split: X[f] = E[f] + e^{-2 pi i f / 2048} O[f], f = 0..1024
+        float p[17];
+        // conjugate partner 1024 - f of f = ln + 64 q: zpad = 68 (16 - q) + bcj (f = 0 pairs with itself)
+        const int bcj = -ln + ((-ln) >> 4);
+        auto split = [&](float2 zf, float2 zc, float2 w) -> float {
             const float2 e = make_float2(0.5f * (zf.x + zc.x), 0.5f * (zf.y - zc.y));
             const float2 o = make_float2(0.5f * (zf.y + zc.y), -0.5f * (zf.x - zc.x));
-            const float2 ot = cmul(o, srtw[fb]);
+            const float2 ot = cmul(o, w);
             const float re = e.x + ot.x, im = e.y + ot.y;
-            pw[fb] = re * re + im * im;
+            return re * re + im * im;
+        };
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const float2 zf = z[brd + 68 * q];
+            const int ic = (q == 0 && ln == 0) ? 0 : 68 * (16 - q) + bcj;  // index select, one LDS read
+            const float2 zc = z[ic];
+            p[q] = split(zf, zc, stw[ln + 64 * q]);
         }
-        __syncthreads();
-        // banded mel: threads (2m, 2m+1) share band m, interleaved bins, combined in a fixed order
         {
-            const int m = threadIdx.x >> 1, h = threadIdx.x & 1;
-            float s = 0.f;
-            if (m < n_mels) {
-                const int f0 = sband[m][0], nb = sband[m][1], wo = sband[m][2];
-                for (int q = h; q < nb; q += 2) s = fmaf(pw[f0 + q], sw[wo + q], s);
+            const float2 z0 = z[0];
+            p[16] = split(z0, z0, stw[kFFT]);  // Nyquist bin (every lane computes it; lane 0 stores it)
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) pw[ln + 64 * q] = p[q];
+        if (ln == 0) pw[kFFT] = p[16];
+        wave_lds_fence();
+        // ---- banded mel: lane l owns the band pair (l, n_mels-1-l) (narrow + wide filter); each band is a
+        // fixed-order fma chain over 8-bin steps of b128 LDS reads (power bins and chunk-transposed weights)
+        {
+            const float4* pw4 = reinterpret_cast<const float4*>(pw);
+            const int4 bl = sbl[ln];
+            float acc0 = 0.f, acc1 = 0.f;
+            for (int c = 0; c < bl.y; c += 2) {
+                const float4 p0 = pw4[(bl.x >> 2) + c], p1 = pw4[(bl.x >> 2) + c + 1];
+                const float4 w0 = sw4[c * kMelLanes + ln], w1 = sw4[(c + 1) * kMelLanes + ln];
+                acc0 = fmaf(p0.x, w0.x, acc0); acc0 = fmaf(p0.y, w0.y, acc0);
+                acc0 = fmaf(p0.z, w0.z, acc0); acc0 = fmaf(p0.w, w0.w, acc0);
+                acc0 = fmaf(p1.x, w1.x, acc0); acc0 = fmaf(p1.y, w1.y, acc0);
+                acc0 = fmaf(p1.z, w1.z, acc0); acc0 = fmaf(p1.w, w1.w, acc0);
             }
-            const float o = __shfl_xor(s, 1, 64);
-            const float tot = h == 0 ? s + o : o + s;
-            if (m < n_mels && h == 0) {
-                mel[f][m] = tot;
-                lmax = fmaxf(lmax, tot);
-                lmin = fminf(lmin, tot);
+            for (int c = 0; c < bl.w; c += 2) {
+                const int cw = bl.y + c;
+                const float4 p0 = pw4[(bl.z >> 2) + c], p1 = pw4[(bl.z >> 2) + c + 1];
+                const float4 w0 = sw4[cw * kMelLanes + ln], w1 = sw4[(cw + 1) * kMelLanes + ln];
+                acc1 = fmaf(p0.x, w0.x, acc1); acc1 = fmaf(p0.y, w0.y, acc1);
+                acc1 = fmaf(p0.z, w0.z, acc1); acc1 = fmaf(p0.w, w0.w, acc1);
+                acc1 = fmaf(p1.x, w1.x, acc1); acc1 = fmaf(p1.y, w1.y, acc1);
+                acc1 = fmaf(p1.z, w1.z, acc1); acc1 = fmaf(p1.w, w1.w, acc1);
+            }
+            const int m0 = ln, m1 = n_mels - 1 - ln;
+            if (m0 < (n_mels + 1) / 2) {
+                smel[fl * (n_mels + 1) + m0] = acc0;
+                lmax = fmaxf(lmax, acc0);
+                lmin = fminf(lmin, acc0);
+                if (m1 != m0) {
+                    smel[fl * (n_mels + 1) + m1] = acc1;
+                    lmax = fmaxf(lmax, acc1);
+                    lmin = fminf(lmin, acc1);
+                }
             }
         }
-        __syncthreads();
+        wave_lds_fence();
     }
-    // write [n_mels][frames] slabs: out[b][m][t0 + f]
-    for (int i = threadIdx.x; i < n_mels * FPB; i += 256) {
-        const int m = i / FPB, f = i % FPB;
-        if (f < nf) out[((int64_t)b * n_mels + m) * T + t0 + f] = mel[f][m];
+    __syncthreads();
+    // write [n_mels][frames] rows: out[b][m][t0 + f]
+    for (int i = threadIdx.x; i < n_mels * kFpb; i += 256) {
+        const int m = i / kFpb, f = i % kFpb;
+        if (f < nf) out[((int64_t)b * n_mels + m) * T + t0 + f] = smel[f * (n_mels + 1) + m];
     }
     // per-clip max / min (non-negative floats order like their bit patterns); wave-reduce first
     for (int o = 32; o > 0; o >>= 1) {
         lmax = fmaxf(lmax, __shfl_xor(lmax, o, 64));
         lmin = fminf(lmin, __shfl_xor(lmin, o, 64));
     }
-    if ((threadIdx.x & 63) == 0) {
+    if (lane == 0) {
         if (lmax > 0.f) atomicMax(clip_max + b, __float_as_uint(lmax));
         if (lmin < INFINITY) atomicMin(clip_min + b, __float_as_uint(lmin));
     }
@@ -321,24 +421,61 @@ int plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax
     p->dense = slaney_filterbank(sr, n_fft, n_mels, fmin, fmax);
     std::vector<float> win(n_fft);
     for (int j = 0; j < n_fft; ++j) win[j] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * j / n_fft));
-    std::vector<float2> tw(kFFT), rtw(kFFT + 1);
-    for (int k = 0; k < kFFT; ++k) tw[k] = make_float2((float)std::cos(-2.0 * M_PI * k / kFFT), (float)std::sin(-2.0 * M_PI * k / kFFT));
+    // stage twiddles of the radix-16/16/4 FFT: tw2[(r-1)*16 + k] = e^{-2 pi i r k / 256} (r 1..15, k 0..15),
+    // tw3[(r-1)*256 + j] = e^{-2 pi i r j / 1024} (r 1..3, j 0..255)
+    std::vector<float2> tw(kTw2 + kTw3), rtw(kFFT + 1);
+    for (int r = 1; r < 16; ++r)
+        for (int k = 0; k < 16; ++k)
+            tw[(r - 1) * 16 + k] = make_float2((float)std::cos(-2.0 * M_PI * r * k / 256), (float)std::sin(-2.0 * M_PI * r * k / 256));
+    for (int r = 1; r < 4; ++r)
+        for (int j = 0; j < 256; ++j)
+            tw[kTw2 + (r - 1) * 256 + j] = make_float2((float)std::cos(-2.0 * M_PI * r * j / kFFT),
+                                                       (float)std::sin(-2.0 * M_PI * r * j / kFFT));
     for (int f = 0; f <= kFFT; ++f) rtw[f] = make_float2((float)std::cos(-2.0 * M_PI * f / n_fft), (float)std::sin(-2.0 * M_PI * f / n_fft));
-    std::vector<int> band(2 * n_mels), woff(n_mels);
-    std::vector<float> w;
+    // Banded filterbank for the kernel's mel stage.  Lane l of a wavefront owns the band pair
+    // (l, n_mels-1-l) (a narrow and a wide filter).  Each band starts at its first non-zero bin rounded
+    // down to a multiple of 4 and spans an even number of 4-bin chunks (zero weights outside the filter).
+    // Weights are stored chunk-transposed, W[c][lane][4], so one b128 LDS read across lanes is
+    // contiguous; band info per lane is (start0, chunks0, start1, chunks1).
+    const int npairs = (n_mels + 1) / 2;
+    std::vector<int> lo(n_mels), cnt(n_mels);
     for (int m = 0; m < n_mels; ++m) {
-        int lo = -1, hi = -1;
+        int l = -1, h = -1;
         for (int f = 0; f < p->nbins; ++f)
-            if (p->dense[(size_t)m * p->nbins + f] != 0.f) { if (lo < 0) lo = f; hi = f; }
-        if (lo < 0) { lo = 0; hi = -1; }
-        band[2 * m] = lo;
-        band[2 * m + 1] = hi - lo + 1;
-        woff[m] = (int)w.size();
-        for (int f = lo; f <= hi; ++f) w.push_back(p->dense[(size_t)m * p->nbins + f]);
-        p->max_band = std::max(p->max_band, hi - lo + 1);
+            if (p->dense[(size_t)m * p->nbins + f] != 0.f) { if (l < 0) l = f; h = f; }
+        if (l < 0) { lo[m] = 0; cnt[m] = 0; continue; }
+        lo[m] = l & ~3;
+        const int span = h + 1 - lo[m];
+        cnt[m] = ((span + 7) / 8) * 2;  // chunks of 4, even
+        p->max_band = std::max(p->max_band, h - l + 1);
     }
-    p->nnz = (int)w.size();
-    if (w.empty()) w.push_back(0.f);
+    std::vector<int> band(4 * kMelLanes, 0);
+    int C = 0;
+    for (int l = 0; l < npairs; ++l) {
+        const int m0 = l, m1 = n_mels - 1 - l;
+        band[4 * l] = lo[m0];
+        band[4 * l + 1] = cnt[m0];
+        band[4 * l + 2] = m1 != m0 ? lo[m1] : 0;
+        band[4 * l + 3] = m1 != m0 ? cnt[m1] : 0;
+        C = std::max(C, band[4 * l + 1] + band[4 * l + 3]);
+    }
+    std::vector<float> w((size_t)std::max(1, C) * kMelLanes * 4, 0.f);
+    for (int l = 0; l < npairs; ++l) {
+        const int ms[2] = {l, n_mels - 1 - l};
+        int c0 = 0;
+        for (int h = 0; h < (ms[1] != ms[0] ? 2 : 1); ++h) {
+            const int m = ms[h];
+            for (int e = 0; e < 4 * cnt[m]; ++e) {
+                const int f = lo[m] + e;
+                const float v = f < p->nbins ? p->dense[(size_t)m * p->nbins + f] : 0.f;
+                const int c = c0 + e / 4;
+                w[((size_t)c * kMelLanes + l) * 4 + (e & 3)] = v;
+            }
+            c0 += cnt[m];
+        }
+    }
+    p->nnz = C * kMelLanes * 4;  // floats of the chunk-transposed weight table
+    std::vector<int> woff(1, 0);
     int st = HLMC_OK;
     if ((st = upload(win, &p->d_window)) || (st = upload(tw, &p->d_tw)) || (st = upload(rtw, &p->d_rtw)) ||
         (st = upload(band, &p->d_band)) || (st = upload(woff, &p->d_woff)) || (st = upload(w, &p->d_w))) {
@@ -371,10 +508,11 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
     HLMC_HIP(hipMemsetAsync(cmax, 0, B * sizeof(unsigned), s));
     HLMC_HIP(hipMemsetAsync(cmin, 0x7f, B * sizeof(unsigned), s));  // 0x7f7f7f7f = large positive float
     HLMC_CHECK_ARG(p->nnz <= kMaxW, "filterbank too large for the LDS-resident mel stage");
-    constexpr int FPB = 8;
-    dim3 grid((T + FPB - 1) / FPB, (unsigned)B);
-    stft_mel_kernel<FPB><<<grid, 256, (size_t)std::max(1, p->nnz) * sizeof(float), s>>>(pcm, n, T, p->hop, p->d_window, p->d_tw, p->d_rtw, p->d_band, p->d_woff,
-                                              p->d_w, p->n_mels, p->nnz, out, cmax, cmin);
+    HLMC_CHECK_ARG(p->n_mels <= 2 * kMelLanes, "n_mels <= 128");
+    dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
+    const size_t dyn = ((size_t)p->nnz + 4 * kMelLanes + (size_t)kFpb * (p->n_mels + 1)) * 4;
+    stft_mel_kernel<<<grid, 256, dyn, s>>>(
+        pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff, p->d_w, p->n_mels, p->nnz, out, cmax, cmin);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

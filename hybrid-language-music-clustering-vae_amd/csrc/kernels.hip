@@ -50,6 +50,12 @@ __device__ __forceinline__ double block_sum_partials(const double* __restrict__ 
 
 // ---------------------------------------------------------------- BN statistics
 // Partial column sums: part[blk][0..C) = sum y, part[blk][C..2C) = sum y^2 (double).
+// Column-streaming kernels over a row-major [R][C] map: thread = (row lane rr, column group cg of V channels);
+// a block pass covers rpp = 256 / (C/V) consecutive rows (one contiguous 4 KB span); each thread keeps its
+// V channels' parameters in registers and has kU rows in flight.
+constexpr int kU = 4;   // rows in flight, forward streaming kernels
+constexpr int kUb = 2;  // backward (two operands per row)
+
 template <typename T>
 __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ y, int64_t R, int C, int64_t rows_per_blk,
                                                           double* __restrict__ part) {
@@ -62,17 +68,21 @@ __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ 
     double a[V], b[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) a[v] = b[v] = 0.0;
-    if (rr < rpp) {
-        for (int64_t r = r0 + rr; r < r1; r += rpp) {
-            float x[V];
-            load16_f32(y + r * C + cg * V, x);
+    const T* yp = y + cg * V;
+    for (int64_t r = r0 + rr; r < r1; r += kU * rpp) {
+        float x[kU][V];
 #pragma unroll
-            for (int v = 0; v < V; ++v) { a[v] += x[v]; b[v] += (double)x[v] * x[v]; }
-        }
-        // rpp * C <= 2048 is guaranteed by the launcher (C/V <= 256 and rpp*tpr == 256)
+        for (int u = 0; u < kU; ++u)
+            if (r + u * rpp < r1) load16_f32(yp + (r + u * rpp) * C, x[u]);
 #pragma unroll
-        for (int v = 0; v < V; ++v) { s1[rr * C + cg * V + v] = a[v]; s2[rr * C + cg * V + v] = b[v]; }
+        for (int u = 0; u < kU; ++u)
+            if (r + u * rpp < r1)
+#pragma unroll
+                for (int v = 0; v < V; ++v) { a[v] += x[u][v]; b[v] += (double)x[u][v] * x[u][v]; }
     }
+    // rpp * C == 256 * V <= 2048
+#pragma unroll
+    for (int v = 0; v < V; ++v) { s1[rr * C + cg * V + v] = a[v]; s2[rr * C + cg * V + v] = b[v]; }
     __syncthreads();
     for (int c = tid; c < C; c += kThreads) {
         double x = 0.0, q = 0.0;
@@ -111,29 +121,50 @@ __global__ void bn_eval_kernel(const float* rmean, const float* rvar, int C, flo
     invstd[c] = 1.f / sqrtf(rvar[c] + eps);
 }
 
-// a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale]
-template <typename T>
-__global__ void bn_act_kernel(const T* __restrict__ y, int64_t R, int C, const float* __restrict__ mean,
-                              const float* __restrict__ invstd, const float* __restrict__ gamma,
-                              const float* __restrict__ beta, int act, const uint8_t* __restrict__ mask, float mscale,
-                              T* __restrict__ a, int lda) {
-    constexpr int V = Vec16<T>::N;
-    const int tpr = C / V;
-    const int64_t nvec = R * tpr;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t r = i / tpr;
-        int c0 = (int)(i - r * tpr) * V;
-        float x[V], o[V];
-        load16_f32(y + r * C + c0, x);
+struct BnChan {  // one thread's V channels of BatchNorm parameters
+    template <int V>
+    __device__ static void load(const float* __restrict__ src, int c0, float (&dst)[V]) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) {
-            int c = c0 + v;
-            float z = (x[v] - mean[c]) * invstd[c] * gamma[c] + beta[c];
-            float t = act_fwd(z, act);
-            if (mask) t = mask[r * C + c] ? t * mscale : 0.f;
-            o[v] = t;
+        for (int v = 0; v < V; ++v) dst[v] = src[c0 + v];
+    }
+};
+
+// a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale]; grid-stride over row passes
+template <typename T>
+__global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ y, int64_t R, int C,
+                                                     const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     int act, const uint8_t* __restrict__ mask, float mscale,
+                                                     T* __restrict__ a, int lda) {
+    constexpr int V = Vec16<T>::N;
+    const int tpr = C / V, rpp = kThreads / tpr;
+    const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
+    const int c0 = cg * V;
+    float mu[V], is[V], ga[V], be[V];
+    BnChan::load(mean, c0, mu);
+    BnChan::load(invstd, c0, is);
+    BnChan::load(gamma, c0, ga);
+    BnChan::load(beta, c0, be);
+    const int64_t step = (int64_t)gridDim.x * rpp;
+    for (int64_t r = (int64_t)blockIdx.x * rpp + rr; r < R; r += kU * step) {
+        float x[kU][V];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (r + u * step < R) load16_f32(y + (r + u * step) * C + c0, x[u]);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t ru = r + u * step;
+            if (ru >= R) break;
+            float o[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                float z = (x[u][v] - mu[v]) * is[v] * ga[v] + be[v];
+                float t = act_fwd(z, act);
+                if (mask) t = mask[ru * C + c0 + v] ? t * mscale : 0.f;
+                o[v] = t;
+            }
+            store16_f32(a + ru * lda + c0, o);
         }
-        store16_f32(a + r * lda + c0, o);
     }
 }
 
@@ -150,29 +181,41 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
     __shared__ double s1[2048], s2[2048];
     const int tpr = C / V, rpp = kThreads / tpr;
     const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
+    const int c0 = cg * V;
     const int64_t r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
+    float mu[V], is[V], ga[V], be[V];
+    BnChan::load(mean, c0, mu);
+    BnChan::load(invstd, c0, is);
+    BnChan::load(gamma, c0, ga);
+    BnChan::load(beta, c0, be);
     double a[V], b[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) a[v] = b[v] = 0.0;
-    if (rr < rpp) {
-        for (int64_t r = r0 + rr; r < r1; r += rpp) {
-            float x[V], g[V];
-            load16_f32(y + r * C + cg * V, x);
-            load16_f32(da + r * lda + cg * V, g);
+    for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
+        float x[kUb][V], g[kUb][V];
+#pragma unroll
+        for (int u = 0; u < kUb; ++u)
+            if (r + u * rpp < r1) {
+                load16_f32(y + (r + u * rpp) * C + c0, x[u]);
+                load16_f32(da + (r + u * rpp) * lda + c0, g[u]);
+            }
+#pragma unroll
+        for (int u = 0; u < kUb; ++u) {
+            const int64_t ru = r + u * rpp;
+            if (ru >= r1) break;
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                int c = cg * V + v;
-                float xh = (x[v] - mean[c]) * invstd[c];
-                float z = xh * gamma[c] + beta[c];
-                float dz = g[v] * act_grad(z, act);
-                if (mask) dz = mask[r * C + c] ? dz * mscale : 0.f;
+                float xh = (x[u][v] - mu[v]) * is[v];
+                float z = xh * ga[v] + be[v];
+                float dz = g[u][v] * act_grad(z, act);
+                if (mask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
                 a[v] += dz;
                 b[v] += (double)dz * xh;
             }
         }
-#pragma unroll
-        for (int v = 0; v < V; ++v) { s1[rr * C + cg * V + v] = a[v]; s2[rr * C + cg * V + v] = b[v]; }
     }
+#pragma unroll
+    for (int v = 0; v < V; ++v) { s1[rr * C + c0 + v] = a[v]; s2[rr * C + c0 + v] = b[v]; }
     __syncthreads();
     for (int c = tid; c < C; c += kThreads) {
         double x = 0.0, q = 0.0;
@@ -210,35 +253,48 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     __shared__ double s1[2048];
     const int tpr = C / V, rpp = kThreads / tpr;
     const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
+    const int c0 = cg * V;
     const int64_t r0 = blockIdx.x * rows_per_blk, r1 = min(R, r0 + rows_per_blk);
     const float invR = 1.f / (float)R;
+    float mu[V], is[V], ga[V], be[V], s0[V], sx[V];
+    BnChan::load(mean, c0, mu);
+    BnChan::load(invstd, c0, is);
+    BnChan::load(gamma, c0, ga);
+    BnChan::load(beta, c0, be);
+    BnChan::load(sums, c0, s0);
+    BnChan::load(sums + C, c0, sx);
     double a[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) a[v] = 0.0;
-    if (rr < rpp) {
-        for (int64_t r = r0 + rr; r < r1; r += rpp) {
-            float x[V], g[V], o[V];
-            load16_f32(y + r * C + cg * V, x);
-            load16_f32(da + r * lda + cg * V, g);
+    for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
+        float x[kUb][V], g[kUb][V];
+#pragma unroll
+        for (int u = 0; u < kUb; ++u)
+            if (r + u * rpp < r1) {
+                load16_f32(y + (r + u * rpp) * C + c0, x[u]);
+                load16_f32(da + (r + u * rpp) * lda + c0, g[u]);
+            }
+#pragma unroll
+        for (int u = 0; u < kUb; ++u) {
+            const int64_t ru = r + u * rpp;
+            if (ru >= r1) break;
+            float o[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                int c = cg * V + v;
-                float is = invstd[c];
-                float xh = (x[v] - mean[c]) * is;
-                float z = xh * gamma[c] + beta[c];
-                float dz = g[v] * act_grad(z, act);
-                if (mask) dz = mask[r * C + c] ? dz * mscale : 0.f;
-                float d = gamma[c] * is * (dz - sums[c] * invR - xh * sums[C + c] * invR);
-                o[v] = d;
+                float xh = (x[u][v] - mu[v]) * is[v];
+                float z = xh * ga[v] + be[v];
+                float dz = g[u][v] * act_grad(z, act);
+                if (mask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
+                o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
             }
-            store16_f32(dy + r * C + cg * V, o);
+            store16_f32(dy + ru * C + c0, o);
             // the bias grad is the sum of the dy actually stored (rounded to T)
 #pragma unroll
             for (int v = 0; v < V; ++v) a[v] += to_f32<T>(from_f32<T>(o[v]));
         }
-#pragma unroll
-        for (int v = 0; v < V; ++v) s1[rr * C + cg * V + v] = a[v];
     }
+#pragma unroll
+    for (int v = 0; v < V; ++v) s1[rr * C + c0 + v] = a[v];
     __syncthreads();
     for (int c = tid; c < C; c += kThreads) {
         double x = 0.0;
@@ -561,87 +617,136 @@ __global__ void vae_bwd_kernel(const float* __restrict__ ra, const float* __rest
 
 // ---------------------------------------------------------------- Adam (torch.optim.Adam single-tensor math)
 constexpr int kAdamMax = 32;
-struct AdamPack {
-    void* p0;
-    void* p1;
-    int d0, d1, taps, ld0, ld1;
-};
 struct AdamBatch {
     float* p[kAdamMax];
     const float* g[kAdamMax];
     float* m[kAdamMax];
     float* v[kAdamMax];
     int64_t n[kAdamMax];
-    AdamPack pk[kAdamMax];
     int blk0[kAdamMax + 1];
     int count;
 };
-// torch.optim.Adam (single-tensor) update; optionally re-packs the updated weight for the GEMMs
-template <typename PT>
-__global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, float b1, float b2, float eps, float wd,
-                                                   float step_size, float bc2_sqrt) {
+struct AdamCoef {
+    float b1, b2, eps, wd, step_size, bc2_sqrt;
+};
+// one element of torch.optim.Adam (foreach=False, amsgrad=False, maximize=False); returns the new parameter
+__device__ __forceinline__ float adam_elem(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                           float* __restrict__ v, int64_t i, const AdamCoef& c) {
+#pragma clang fp contract(off)  // identical rounding in every kernel that inlines this (no FMA contraction)
+    float gi = g[i];
+    const float pi = p[i];
+    if (c.wd != 0.f) gi = gi + c.wd * pi;
+    float mi = m[i];
+    mi = mi + (gi - mi) * (1.f - c.b1);
+    const float vi = v[i] * c.b2 + (1.f - c.b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / c.bc2_sqrt + c.eps;
+    const float np = pi - c.step_size * (mi / denom);
+    p[i] = np;
+    return np;
+}
+__global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, AdamCoef c) {
     int t = 0;
     while (t + 1 < bt.count && (int)blockIdx.x >= bt.blk0[t + 1]) ++t;
     const int64_t base = (int64_t)(blockIdx.x - bt.blk0[t]) * 1024;
-    float* p = bt.p[t];
-    const float* g = bt.g[t];
-    float* m = bt.m[t];
-    float* v = bt.v[t];
     const int64_t n = bt.n[t];
-    const AdamPack pk = bt.pk[t];
-    for (int64_t i = base + threadIdx.x; i < min(n, base + 1024); i += blockDim.x) {
-        float gi = g[i];
-        if (wd != 0.f) gi = gi + wd * p[i];
-        float mi = m[i];
-        mi = mi + (gi - mi) * (1.f - b1);
-        float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-        m[i] = mi;
-        v[i] = vi;
-        float denom = sqrtf(vi) / bc2_sqrt + eps;
-        const float np = p[i] - step_size * (mi / denom);
-        p[i] = np;
-        if (pk.p0 || pk.p1) {
-            const int64_t i0 = i / ((int64_t)pk.d1 * pk.taps);
-            const int64_t rem = i - i0 * pk.d1 * pk.taps;
-            const int64_t i1 = rem / pk.taps;
-            const int tap = (int)(rem - i1 * pk.taps);
-            const PT q = from_f32<PT>(np);
-            if (pk.p0) reinterpret_cast<PT*>(pk.p0)[(i0 * pk.taps + tap) * pk.ld0 + i1] = q;
-            if (pk.p1) reinterpret_cast<PT*>(pk.p1)[(i1 * pk.taps + tap) * pk.ld1 + i0] = q;
-        }
-    }
+    for (int64_t i = base + threadIdx.x; i < min(n, base + 1024); i += blockDim.x) adam_elem(bt.p[t], bt.g[t], bt.m[t], bt.v[t], i, c);
 }
 
-// ---------------------------------------------------------------- weight packing
-// W [d0][d1][taps] f32 -> P0 [d0][taps][ld0] and P1 [d1][taps][ld1] (T).  Block = one (job, 32 x 32 tile of
-// (i0, i1)); the tile's 32 x 32 x taps floats are staged in LDS (coalesced reads of W rows), then each
-// (i0, tap) row segment of P0 and each (i1, tap) row segment of P1 is written as 32 consecutive elements.
+// ---------------------------------------------------------------- Adam + GEMM weight packing, one launch
+// W [d0][d1][taps] f32 -> P0 [d0][taps][ld0] and P1 [d1][taps][ld1] (T).  A block owns one 32 x 32 (i0, i1)
+// tile of one weight: it streams the tile's p/g/m/v rows (n1*taps contiguous floats per i0) through the
+// Adam update, keeps the new values in LDS (row stride 32*taps+1: conflict-free for both read-outs) and
+// writes each (i0, tap) segment of P0 and each (i1, tap) segment of P1 as 32 consecutive elements.
+// Unpacked tensors (BatchNorm affine, biases) are 4096-element chunks of the same launch.
 template <typename T>
-__global__ __launch_bounds__(256) void pack_kernel(const ops::PackJob* __restrict__ jobs, int njobs) {
-    const ops::PackJob jb = jobs[blockIdx.z];
-    const int t0 = blockIdx.x * 32, t1 = blockIdx.y * 32;   // i0 / i1 tile origin
-    if (t0 >= jb.d0 || t1 >= jb.d1) return;
+__global__ __launch_bounds__(256) void adam_pack_kernel(const ops::AdamJob* __restrict__ jobs, int njobs, AdamCoef c) {
+    const int bid = blockIdx.x;
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].tile0 <= bid) lo = mid; else hi = mid - 1;
+    }
+    const ops::AdamJob jb = jobs[lo];
+    const int tl = bid - jb.tile0;
+    if (jb.taps == 0) {
+        const int64_t base = (int64_t)tl * 4096, end = min(jb.n, base + 4096);
+        for (int64_t i = base + threadIdx.x; i < end; i += 256) adam_elem(jb.p, jb.g, jb.m, jb.v, i, c);
+        return;
+    }
     const int taps = jb.taps;
+    const int tt0 = tl / jb.nt1, tt1 = tl - tt0 * jb.nt1;
+    const int t0 = tt0 * 32, t1 = tt1 * 32;
     const int n0 = min(32, jb.d0 - t0), n1 = min(32, jb.d1 - t1);
-    __shared__ float tile[32 * 32 * 9 + 32];
-    // rows of W: for each i0 in the tile, n1 * taps contiguous floats starting at (t0+a)*d1*taps + t1*taps
+    const int RS = 32 * taps + 1;
+    __shared__ float tile[32 * (32 * 9 + 1)];
     const int rowlen = n1 * taps;
-    for (int e = threadIdx.x; e < n0 * 32 * taps; e += blockDim.x) {
-        const int a = e / (32 * taps), r = e % (32 * taps);
-        if (r < rowlen) tile[(a * 32) * taps + r] = jb.w[((int64_t)(t0 + a) * jb.d1 + t1) * taps + r];
+    {
+        int a = 0, r = threadIdx.x;
+        while (r >= rowlen) { r -= rowlen; ++a; }
+        for (; a < n0;) {
+            const int64_t idx = ((int64_t)(t0 + a) * jb.d1 + t1) * taps + r;
+            tile[a * RS + r] = adam_elem(jb.p, jb.g, jb.m, jb.v, idx, c);
+            r += 256;
+            while (r >= rowlen) { r -= rowlen; ++a; }
+        }
     }
     __syncthreads();
     T* p0 = (T*)jb.p0;
     T* p1 = (T*)jb.p1;
-    if (p0)  // P0[(i0*taps + tap)*ld0 + i1]: for each (a, tap) write n1 consecutive i1
-        for (int e = threadIdx.x; e < n0 * taps * 32; e += blockDim.x) {
-            const int q = e % 32, at = e / 32, a = at / taps, tap = at % taps;
-            if (q < n1) p0[((int64_t)(t0 + a) * taps + tap) * jb.ld0 + t1 + q] = from_f32<T>(tile[(a * 32 + q) * taps + tap]);
+    if (p0)
+        for (int e = threadIdx.x; e < n0 * taps * 32; e += 256) {
+            const int q = e & 31, at = e >> 5, a = at / taps, tap = at - a * taps;
+            if (q < n1) p0[((int64_t)(t0 + a) * taps + tap) * jb.ld0 + t1 + q] = from_f32<T>(tile[a * RS + q * taps + tap]);
         }
-    if (p1)  // P1[(i1*taps + tap)*ld1 + i0]: for each (c, tap) write n0 consecutive i0
-        for (int e = threadIdx.x; e < n1 * taps * 32; e += blockDim.x) {
-            const int q = e % 32, ct = e / 32, c = ct / taps, tap = ct % taps;
-            if (q < n0) p1[((int64_t)(t1 + c) * taps + tap) * jb.ld1 + t0 + q] = from_f32<T>(tile[(q * 32 + c) * taps + tap]);
+    if (p1)
+        for (int e = threadIdx.x; e < n1 * taps * 32; e += 256) {
+            const int q = e & 31, ct = e >> 5, cc = ct / taps, tap = ct - cc * taps;
+            if (q < n0) p1[((int64_t)(t1 + cc) * taps + tap) * jb.ld1 + t0 + q] = from_f32<T>(tile[q * RS + cc * taps + tap]);
+        }
+}
+
+// packing alone (forward of a model whose weights were changed outside the engine)
+template <typename T>
+__global__ __launch_bounds__(256) void pack_kernel(const ops::AdamJob* __restrict__ jobs, int njobs) {
+    const int bid = blockIdx.x;
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].tile0 <= bid) lo = mid; else hi = mid - 1;
+    }
+    const ops::AdamJob jb = jobs[lo];
+    if (jb.taps == 0) return;
+    const int tl = bid - jb.tile0;
+    const int taps = jb.taps;
+    const int tt0 = tl / jb.nt1, tt1 = tl - tt0 * jb.nt1;
+    const int t0 = tt0 * 32, t1 = tt1 * 32;
+    const int n0 = min(32, jb.d0 - t0), n1 = min(32, jb.d1 - t1);
+    const int RS = 32 * taps + 1;
+    __shared__ float tile[32 * (32 * 9 + 1)];
+    const int rowlen = n1 * taps;
+    {
+        int a = 0, r = threadIdx.x;
+        while (r >= rowlen) { r -= rowlen; ++a; }
+        for (; a < n0;) {
+            tile[a * RS + r] = jb.p[((int64_t)(t0 + a) * jb.d1 + t1) * taps + r];
+            r += 256;
+            while (r >= rowlen) { r -= rowlen; ++a; }
+        }
+    }
+    __syncthreads();
+    T* p0 = (T*)jb.p0;
+    T* p1 = (T*)jb.p1;
+    if (p0)
+        for (int e = threadIdx.x; e < n0 * taps * 32; e += 256) {
+            const int q = e & 31, at = e >> 5, a = at / taps, tap = at - a * taps;
+            if (q < n1) p0[((int64_t)(t0 + a) * taps + tap) * jb.ld0 + t1 + q] = from_f32<T>(tile[a * RS + q * taps + tap]);
+        }
+    if (p1)
+        for (int e = threadIdx.x; e < n1 * taps * 32; e += 256) {
+            const int q = e & 31, ct = e >> 5, cc = ct / taps, tap = ct - cc * taps;
+            if (q < n0) p1[((int64_t)(t1 + cc) * taps + tap) * jb.ld1 + t0 + q] = from_f32<T>(tile[q * RS + cc * taps + tap]);
         }
 }
 
@@ -685,8 +790,8 @@ int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const
            const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda) {
     HLMC_TRY(check_bn_shape<T>(C));
     HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act: output row stride must be a multiple of 16 bytes");
-    int64_t nvec = R * (C / Vec16<T>::N);
-    bn_act_kernel<T><<<grid_for(nvec), kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
+    const int rpp = kThreads / (C / Vec16<T>::N);
+    bn_act_kernel<T><<<grid_for(R, rpp * kU), kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -878,12 +983,15 @@ int vae_loss_bwd(hipStream_t s, const float* ra, const float* a, int64_t na, flo
     return HLMC_OK;
 }
 
-int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, float* const* m, float* const* v,
-         const int64_t* numel, AdamArgs a, const PackJob* packs, int pack_dtype) {
+static AdamCoef adam_coef(const AdamArgs& a) {
     const double bc1 = 1.0 - std::pow((double)a.beta1, (double)a.step);
     const double bc2 = 1.0 - std::pow((double)a.beta2, (double)a.step);
-    const float step_size = (float)(a.lr / bc1);
-    const float bc2_sqrt = (float)std::sqrt(bc2);
+    return AdamCoef{a.beta1, a.beta2, a.eps, a.weight_decay, (float)(a.lr / bc1), (float)std::sqrt(bc2)};
+}
+
+int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, float* const* m, float* const* v,
+         const int64_t* numel, AdamArgs a) {
+    const AdamCoef c = adam_coef(a);
     for (int t0 = 0; t0 < ntensors; t0 += kAdamMax) {
         AdamBatch bt{};
         bt.count = std::min(kAdamMax, ntensors - t0);
@@ -891,32 +999,38 @@ int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, fl
         for (int i = 0; i < bt.count; ++i) {
             bt.p[i] = p[t0 + i]; bt.g[i] = g[t0 + i]; bt.m[i] = m[t0 + i]; bt.v[i] = v[t0 + i];
             bt.n[i] = numel[t0 + i];
-            if (packs && (packs[t0 + i].p0 || packs[t0 + i].p1)) {
-                const PackJob& j = packs[t0 + i];
-                bt.pk[i] = AdamPack{j.p0, j.p1, j.d0, j.d1, j.taps, j.ld0, j.ld1};
-            } else {
-                bt.pk[i] = AdamPack{nullptr, nullptr, 1, 1, 1, 1, 1};
-            }
             bt.blk0[i] = blocks;
             blocks += (int)((numel[t0 + i] + 1023) / 1024);
         }
         bt.blk0[bt.count] = blocks;
         if (blocks == 0) continue;
-        if (pack_dtype == HLMC_BF16)
-            adam_kernel<bf16><<<blocks, 256, 0, s>>>(bt, a.beta1, a.beta2, a.eps, a.weight_decay, step_size, bc2_sqrt);
-        else
-            adam_kernel<float><<<blocks, 256, 0, s>>>(bt, a.beta1, a.beta2, a.eps, a.weight_decay, step_size, bc2_sqrt);
+        adam_kernel<<<blocks, 256, 0, s>>>(bt, c);
         HLMC_LAUNCHED();
     }
     return HLMC_OK;
 }
 
+int adam_job_tiles(AdamJob& j) {
+    if (j.taps == 0) {
+        j.nt1 = 0;
+        return (int)((j.n + 4095) / 4096);
+    }
+    j.nt1 = (j.d1 + 31) / 32;
+    return ((j.d0 + 31) / 32) * j.nt1;
+}
+
 template <typename T>
-int pack(hipStream_t s, const PackJob* jobs_dev, int njobs, int64_t max_dim) {
-    if (njobs == 0) return HLMC_OK;
-    const unsigned tiles = (unsigned)((max_dim + 31) / 32);
-    dim3 grid(tiles, tiles, njobs);
-    pack_kernel<T><<<grid, 256, 0, s>>>(jobs_dev, njobs);
+int adam_pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles, AdamArgs a) {
+    if (njobs == 0 || total_tiles == 0) return HLMC_OK;
+    adam_pack_kernel<T><<<total_tiles, 256, 0, s>>>(jobs_dev, njobs, adam_coef(a));
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+template <typename T>
+int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
+    if (njobs == 0 || total_tiles == 0) return HLMC_OK;
+    pack_kernel<T><<<total_tiles, 256, 0, s>>>(jobs_dev, njobs);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -941,7 +1055,8 @@ int pack(hipStream_t s, const PackJob* jobs_dev, int njobs, int64_t max_dim) {
     template int colsum<T>(hipStream_t, const T*, int, int, int, float*, Ws);                                        \
     template int reparam_fwd<T>(hipStream_t, const float*, const float*, const float*, int, int, T*, int);           \
     template int reparam_bwd<T>(hipStream_t, const T*, int, const float*, const float*, int, int, float*, float*);   \
-    template int pack<T>(hipStream_t, const PackJob*, int, int64_t);
+    template int pack<T>(hipStream_t, const AdamJob*, int, int);                                                     \
+    template int adam_pack<T>(hipStream_t, const AdamJob*, int, int, AdamArgs);
 
 INST(float)
 INST(bf16)

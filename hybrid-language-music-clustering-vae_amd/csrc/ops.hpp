@@ -109,21 +109,27 @@ struct AdamArgs {
     float lr, beta1, beta2, eps, weight_decay;
     int step;
 };
-struct PackJob;
-// packs (nullable): per tensor, PackJob describing packed copies (p0/p1 may be NULL) written from the updated
-// parameter in dtype pack_dtype (HLMC_F32 / HLMC_BF16) — the GEMM weight layouts refreshed in the same pass
 int adam(hipStream_t s, int ntensors, float* const* p, const float* const* g, float* const* m, float* const* v,
-         const int64_t* numel, AdamArgs a, const PackJob* packs = nullptr, int pack_dtype = HLMC_F32);
-// conv weight [d0][d1][3][3] f32 -> P0 [d0][3][3][d1], P1 [d1][3][3][d0] (T); linear [d0][d1] -> P0 copy, P1 transpose
-struct PackJob {
-    const float* w;
-    void* p0;  // [d0][taps][ld0 >= d1]
-    void* p1;  // [d1][taps][ld1 >= d0]
-    int d0, d1, taps;  // taps 9 (conv) or 1 (linear)
-    int ld0, ld1;
+         const int64_t* numel, AdamArgs a);
+// One parameter tensor of a fused Adam + GEMM-weight-pack launch.  taps 9 (conv weight [d0][d1][3][3]
+// -> P0 [d0][3][3][ld0 >= d1], P1 [d1][3][3][ld1 >= d0]) or 1 (linear [d0][d1] -> P0 copy, P1 transpose) or
+// 0 (unpacked tensor of n elements).  tile0 = first block of this job in the launch (ascending).
+struct AdamJob {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    void* p0;
+    void* p1;
+    int64_t n;
+    int d0, d1, taps, ld0, ld1;
+    int tile0, nt1;
 };
+int adam_job_tiles(AdamJob& j);  // sets nt1, returns the job's block count
 template <typename T>
-int pack(hipStream_t s, const PackJob* jobs_dev, int njobs, int64_t max_elems);
+int adam_pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles, AdamArgs a);
+template <typename T>
+int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles);  // packing only (g/m/v unused)
 
 }  // namespace ops
 }  // namespace hlmc

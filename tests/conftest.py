@@ -18,3 +18,9 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but no GPU is visible (run -m 'not gpu' on CPU hosts)")
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(autouse=True)
+def _repo_cwd(monkeypatch):
+    """Fixture paths (tests/golden/...) are repo-relative: run every test from the repository root."""
+    monkeypatch.chdir(ROOT)

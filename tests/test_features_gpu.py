@@ -103,3 +103,20 @@ def test_standard_scaler_golden(cuda):
     ours = hlmc_amd.StandardScaler().fit(cols)
     np.testing.assert_allclose(ours.scale_, fx["scaler_scale"], rtol=1e-10)
     np.testing.assert_allclose(ours.transform(cols), fx["scaler_out"], rtol=1e-6, atol=1e-6)
+
+
+def test_mel_deterministic_repeat(cuda):
+    """The STFT-mel path is deterministic: repeated calls are bit-identical and stay within tolerance."""
+    fx = np.load("tests/golden/features.npz")
+    y = MO.synthetic_pcm(2, 65024, seed=7)
+    d0, m0 = hlmc_amd.extract_mel_spectrogram(y), hlmc_amd.mfcc(y, n_mfcc=40)
+    bad = []
+    for i in range(10):
+        d, m = hlmc_amd.extract_mel_spectrogram(y), hlmc_amd.mfcc(y, n_mfcc=40)
+        if not (np.array_equal(d, d0) and np.array_equal(m, m0)):
+            bad.append((i, float(np.abs(d - d0).max()), float(np.abs(m - m0).max())))
+    e_db = float(np.abs(d0 - fx["mel_db"]).max())
+    e_mf = np.abs(m0 - fx["mfcc"]) - (0.05 + 1e-3 * np.abs(fx["mfcc"]))
+    assert not bad, f"non-deterministic repeats: {bad}"
+    assert e_db < 0.05, e_db
+    assert float(e_mf.max()) <= 0, (float(e_mf.max()), np.unravel_index(e_mf.argmax(), e_mf.shape))

@@ -15,6 +15,12 @@
 namespace hlmc {
 
 // ============================================================================ helpers
+// Largest K-step of both GEMM families: 8 16-byte chunks per tile row (64 bf16 / 32 f32).  Kernels
+// take the chunk count KCH (4 or 8) as a template parameter; split-K ranges are multiples of this.
+constexpr int kKCH = 8;
+template <typename T>
+constexpr int gemm_bk() { return kKCH * Vec16<T>::N; }
+
 // Division by a runtime constant via a precomputed magic number (n < 2^31): q = (umulhi(n, mul) + n) >> sh
 struct FastDiv {
     uint32_t d, mul, sh;
@@ -54,7 +60,8 @@ struct DenseLoader {  // X[m * ld + k], m < M, k < K
 };
 
 // Stride-2, pad-1, 3x3 window gather over an NHWC map: A(m = (b,oh,ow), k = (kh,kw,ci))
-//   = X[b, 2oh-1+kh, 2ow-1+kw, ci].  Requires C % (4*VEC) == 0 (a BK chunk never straddles taps).
+//   = X[b, 2oh-1+kh, 2ow-1+kw, ci].  Requires C % VEC == 0 (a 16-byte chunk never straddles taps);
+// chunks past K = 9C read as zeros.
 // Only the top row (kh = 0, oh = 0) and left column (kw = 0, ow = 0) of the window can fall outside.
 template <typename T>
 struct ConvS2Loader {
@@ -77,7 +84,7 @@ struct ConvS2Loader {
         const int tap = cshift >= 0 ? (k >> cshift) : k / C;
         const int ci = k - tap * C;
         const int kh = tap / 3, kw = tap - kh * 3;
-        if (!(rw.flags & 1) || (kh == 0 && (rw.flags & 2)) || (kw == 0 && (rw.flags & 4)))
+        if (!(rw.flags & 1) || tap >= 9 || (kh == 0 && (rw.flags & 2)) || (kw == 0 && (rw.flags & 4)))
             return make_uint4(0, 0, 0, 0);
         return *reinterpret_cast<const uint4*>(x + rw.base + ((int64_t)kh * Wi + kw) * C + ci);
     }
@@ -117,7 +124,7 @@ struct SubpixelLoader {
         const int ci = k - tt * C;
         const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
         const int dr = sp_delta(py, ty), dc = sp_delta(px, tx);
-        if (!(rw.flags & 1) || (dr && (rw.flags & 2)) || (dc && (rw.flags & 4))) return make_uint4(0, 0, 0, 0);
+        if (!(rw.flags & 1) || k >= Kd || (dr && (rw.flags & 2)) || (dc && (rw.flags & 4))) return make_uint4(0, 0, 0, 0);
         return *reinterpret_cast<const uint4*>(x + rw.base + ((int64_t)dr * Wi + dc) * C + ci);
     }
 };
@@ -140,7 +147,7 @@ struct SubpixelWeight {
     __device__ int K() const { return Kd; }
     __device__ Row prep(int n) const { return Row{n < N ? w + (int64_t)n * 9 * C : nullptr}; }
     __device__ uint4 load(const Row& rw, int k) const {
-        if (!rw.r) return make_uint4(0, 0, 0, 0);
+        if (!rw.r || k >= Kd) return make_uint4(0, 0, 0, 0);
         const int tt = cshift >= 0 ? (k >> cshift) : k / C;
         const int ci = k - tt * C;
         const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
@@ -209,15 +216,15 @@ struct StorePartial {
 };
 
 // ============================================================================ NT main loop
-template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
+template <typename T, int BM, int BN, int WM, int WN, int KCH, class AL, class BL, class EP>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len) {
     constexpr int V = Vec16<T>::N;
-    constexpr int BK = 4 * V;
-    constexpr int BKP = BK + V;  // 80-byte rows
+    constexpr int BK = KCH * V;
+    constexpr int BKP = BK + V;  // rows padded by one 16-byte chunk
     constexpr int WAVES_N = BN / WN;
     static_assert((BM / WM) * WAVES_N == 4, "4 waves per block");
     constexpr int TM = WM / 16, TN = WN / 16;
-    constexpr int ACH = BM * 4, BCH = BN * 4;           // 16-byte chunks per tile
+    constexpr int ACH = BM * KCH, BCH = BN * KCH;     // 16-byte chunks per tile
     constexpr int AR = (ACH + 255) / 256, BR = (BCH + 255) / 256;
     __shared__ __attribute__((aligned(16))) T As[2][BM * BKP];
     __shared__ __attribute__((aligned(16))) T Bs[2][BN * BKP];
@@ -242,31 +249,31 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
     typename AL::Row arow[AR];
     typename BL::Row brow[BR];
 #pragma unroll
-    for (int i = 0; i < AR; ++i) arow[i] = al.prep(m0 + ((tid + i * 256) >> 2));
+    for (int i = 0; i < AR; ++i) arow[i] = al.prep(m0 + ((tid + i * 256) / KCH));
 #pragma unroll
-    for (int i = 0; i < BR; ++i) brow[i] = bl.prep(n0 + ((tid + i * 256) >> 2));
+    for (int i = 0; i < BR; ++i) brow[i] = bl.prep(n0 + ((tid + i * 256) / KCH));
     auto gload = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) ra[i] = al.load(arow[i], k0 + (c & 3) * V);
+            if (c < ACH) ra[i] = al.load(arow[i], k0 + (c % KCH) * V);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) rb[i] = bl.load(brow[i], k0 + (c & 3) * V);
+            if (c < BCH) rb[i] = bl.load(brow[i], k0 + (c % KCH) * V);
         }
     };
     auto lstore = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) *reinterpret_cast<uint4*>(&As[buf][(c >> 2) * BKP + (c & 3) * V]) = ra[i];
+            if (c < ACH) *reinterpret_cast<uint4*>(&As[buf][(c / KCH) * BKP + (c % KCH) * V]) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) *reinterpret_cast<uint4*>(&Bs[buf][(c >> 2) * BKP + (c & 3) * V]) = rb[i];
+            if (c < BCH) *reinterpret_cast<uint4*>(&Bs[buf][(c / KCH) * BKP + (c % KCH) * V]) = rb[i];
         }
     };
 
@@ -282,21 +289,26 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
             const T* A = As[cur];
             const T* B = Bs[cur];
             if constexpr (sizeof(T) == 2) {
-                bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
-                    af[i] = *reinterpret_cast<const bf16x8_t*>(&A[(wm0 + i * 16 + (lane & 15)) * BKP + (lane >> 4) * 8]);
+                for (int s = 0; s < BK / 32; ++s) {
+                    bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    bfr[j] = *reinterpret_cast<const bf16x8_t*>(&B[(wn0 + j * 16 + (lane & 15)) * BKP + (lane >> 4) * 8]);
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
+                    for (int i = 0; i < TM; ++i)
+                        af[i] = *reinterpret_cast<const bf16x8_t*>(
+                            &A[(wm0 + i * 16 + (lane & 15)) * BKP + s * 32 + (lane >> 4) * 8]);
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                        bfr[j] = *reinterpret_cast<const bf16x8_t*>(
+                            &B[(wn0 + j * 16 + (lane & 15)) * BKP + s * 32 + (lane >> 4) * 8]);
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                }
             } else {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
+                for (int s = 0; s < BK / 4; ++s) {
                     float af[TM], bfr[TN];
 #pragma unroll
                     for (int i = 0; i < TM; ++i) af[i] = A[(wm0 + i * 16 + (lane & 15)) * BKP + s * 4 + (lane >> 4)];
@@ -416,10 +428,10 @@ struct KRowConvS2 {
 
 // ============================================================================ TN main loop
 // Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_kernel).
-template <typename T, int BM, int BN, int WM, int WN, class LL, class HL>
+template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len) {
     constexpr int V = Vec16<T>::N;
-    constexpr int BK = 4 * V;              // k rows per tile (32 bf16 / 16 f32)
+    constexpr int BK = KCH * V;            // k rows per tile (KCH 16-byte chunks of one column)
     constexpr int LDA = BM + V;             // padded LDS row (elements)
     constexpr int LDB = BN + V;
     constexpr int WAVES_N = BN / WN;
@@ -492,29 +504,32 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
                 // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses row q, cols 4p..4p+3;
                 // lane i receives column i of the 4 rows.
                 const int q = li >> 2, p = li & 3;
-                bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const T* base = &A[(8 * g + q) * LDA + wm0 + i * 16 + 4 * p];
-                    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base));
-                    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + 4 * LDA));
-                    af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                for (int s = 0; s < BK / 32; ++s) {
+                    bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) {
+                        const T* base = &A[(32 * s + 8 * g + q) * LDA + wm0 + i * 16 + 4 * p];
+                        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base));
+                        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + 4 * LDA));
+                        af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    }
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        const T* base = &B[(32 * s + 8 * g + q) * LDB + wn0 + j * 16 + 4 * p];
+                        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base));
+                        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + 4 * LDB));
+                        bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    }
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
                 }
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const T* base = &B[(8 * g + q) * LDB + wn0 + j * 16 + 4 * p];
-                    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base));
-                    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + 4 * LDB));
-                    bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                }
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
             } else {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
+                for (int s = 0; s < BK / 4; ++s) {
                     float af[TM], bfr[TN];
 #pragma unroll
                     for (int i = 0; i < TM; ++i) af[i] = A[(s * 4 + g) * LDA + wm0 + i * 16 + li];

@@ -35,12 +35,17 @@ inline Plan plan_tn(int tiles, int K, int BK) {
 
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
 int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws) {
-    constexpr int BK = 4 * Vec16<T>::N;
+    constexpr int BK = gemm_bk<T>();
     const int tmn = cdiv(M, BM) * cdiv(N, BN);
     Plan pl = plan_nt(tmn * phases, Kmax, BK);
     dim3 grid(tmn, phases, pl.S);
+    // short reductions keep the 4-chunk K-step (more co-resident blocks); long ones use 8 chunks
+    const bool long_k = Kmax >= 1024;
     if (pl.S == 1) {
-        gemm_nt_kernel<T, BM, BN, WM, WN, AL, BL, EP><<<grid, 256, 0, s>>>(al, bl, ep, M, N, pl.ksl);
+        if (long_k)
+            gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, EP><<<grid, 256, 0, s>>>(al, bl, ep, M, N, pl.ksl);
+        else
+            gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, EP><<<grid, 256, 0, s>>>(al, bl, ep, M, N, pl.ksl);
         HLMC_LAUNCHED();
         return HLMC_OK;
     }
@@ -48,7 +53,10 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "split-K workspace too small");
     StorePartialZ part;
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
-    gemm_nt_kernel<T, BM, BN, WM, WN, AL, BL, StorePartialZ><<<grid, 256, 0, s>>>(al, bl, part, M, N, pl.ksl);
+    if (long_k)
+        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, StorePartialZ><<<grid, 256, 0, s>>>(al, bl, part, M, N, pl.ksl);
+    else
+        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, StorePartialZ><<<grid, 256, 0, s>>>(al, bl, part, M, N, pl.ksl);
     HLMC_LAUNCHED();
     int64_t total = (int64_t)phases * M * N;
     int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
@@ -73,7 +81,7 @@ int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, 
 }
 template <typename T>
 size_t dispatch_nt_ws(int M, int N, int Kmax, int phases) {
-    constexpr int BK = 4 * Vec16<T>::N;
+    constexpr int BK = gemm_bk<T>();
     if (N >= 128) return nt_ws<128, 128>(M, N, Kmax, phases, BK);
     if (N > 32) return nt_ws<128, 64>(M, N, Kmax, phases, BK);
     return nt_ws<128, 32>(M, N, Kmax, phases, BK);
@@ -87,7 +95,7 @@ int dispatch_linear(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int
 }
 template <typename T>
 size_t dispatch_linear_ws(int M, int N, int K) {
-    constexpr int BK = 4 * Vec16<T>::N;
+    constexpr int BK = gemm_bk<T>();
     if (M >= 1024 && N >= 128) return nt_ws<128, 128>(M, N, K, 1, BK);
     return nt_ws<64, 64>(M, N, K, 1, BK);
 }
@@ -109,13 +117,16 @@ struct StoreWgradConv {
 
 template <typename T, int BM, int BN, int WM, int WN, class LL, class HL, class EP>
 int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws) {
-    constexpr int BK = 4 * Vec16<T>::N;
+    constexpr int BK = gemm_bk<T>();
     const int tiles = cdiv(M, BM) * cdiv(N, BN);
     Plan pl = plan_tn(tiles, K, BK);
     size_t need = (size_t)pl.S * M * N * sizeof(float);
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "wgrad workspace too small");
     dim3 grid(tiles, 1, pl.S);
-    gemm_tn_kernel<T, BM, BN, WM, WN, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl);
+    if (pl.ksl >= 1024)
+        gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl);
+    else
+        gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl);
     HLMC_LAUNCHED();
     int64_t total = (int64_t)M * N;
     int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
@@ -137,7 +148,7 @@ int dispatch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, 
 }
 template <typename T>
 size_t dispatch_tn_ws(int M, int N, int K) {
-    constexpr int BK = 4 * Vec16<T>::N;
+    constexpr int BK = gemm_bk<T>();
     if (M >= 128) return tn_ws<128, 128>(M, N, K, BK);
     if (M > 32) return tn_ws<64, 128>(M, N, K, BK);
     return tn_ws<32, 128>(M, N, K, BK);
@@ -153,7 +164,7 @@ namespace ops {
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws) {
     constexpr int V = Vec16<T>::N;
-    HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % (4 * V) == 0, "conv_s2: need even H/W and Ci % BK == 0");
+    HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % V == 0, "conv_s2: need even H/W and Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "conv_s2: 16-byte alignment");
     const int Ho = Hi / 2, Wo = Wi / 2, M = B * Ho * Wo, K = 9 * Ci;
     ConvS2Loader<T> al{x, Hi, Wi, Ci, Ho, Wo, M, log2_exact(Ci)};
@@ -169,7 +180,7 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws) {
     constexpr int V = Vec16<T>::N;
-    HLMC_CHECK_ARG(Ci % (4 * V) == 0, "subpixel: Ci % BK == 0");
+    HLMC_CHECK_ARG(Ci % V == 0, "subpixel: Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "subpixel: 16-byte alignment");
     const int M = B * Hi * Wi;
     SubpixelLoader<T> al{x, Hi, Wi, Ci, M, log2_exact(Ci), 0, 0, 0, 0};

@@ -135,6 +135,20 @@ def mean_std_pool(feat):
     return out.cpu().numpy() if was_np else out
 
 
+def scaler_finalize(n_total, col_sum, corr, m2):
+    """sklearn StandardScaler statistics from the (globally reduced) pass outputs, float64 torch tensors:
+    mean = sum / n; var = (M2 - corr^2 / n) / n (the corrected two-pass of _incremental_mean_and_var);
+    scale = sqrt(var) with near-constant columns (var <= n eps var + (n mean eps)^2) -> 1."""
+    N = float(n_total)
+    mean = col_sum / N
+    var = (m2 - corr * corr / N) / N
+    eps = np.finfo(np.float64).eps
+    upper = N * eps * var + (N * mean * eps) ** 2
+    scale = torch.sqrt(var)
+    scale = torch.where(var <= upper, torch.ones_like(scale), scale)
+    return mean, var, scale
+
+
 class StandardScaler:
     """sklearn.preprocessing.StandardScaler (with_mean, with_std) with float64 accumulators on the GPU.
 
@@ -147,9 +161,8 @@ class StandardScaler:
         self.process_group = process_group
 
     def _allreduce(self, t):
-        if self.process_group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()
-                                              and self.process_group is not None):
-            torch.distributed.all_reduce(t, group=self.process_group)
+        if self.process_group is not None:
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.process_group)
         return t
 
     def fit(self, X):
@@ -158,26 +171,19 @@ class StandardScaler:
         n, cols = x.shape
         dev = x.device
         ws = torch.empty(max(16, int(L.lib().hlmc_colstats_workspace(n, cols))), dtype=torch.uint8, device=dev)
-        total = torch.tensor([float(n)], dtype=torch.float64, device=dev)
+        total = self._allreduce(torch.tensor([float(n)], dtype=torch.float64, device=dev))
         s = torch.empty(cols, dtype=torch.float64, device=dev)
         L.check(L.lib().hlmc_colstats_sum(L.stream(), x.data_ptr(), n, cols, s.data_ptr(), ws.data_ptr()))
-        if self.process_group is not None:
-            self._allreduce(s)
-            self._allreduce(total)
+        self._allreduce(s)
         N = float(total.item())
         mean = s / N
         corr = torch.empty_like(s)
         m2 = torch.empty_like(s)
         L.check(L.lib().hlmc_colstats_centered(L.stream(), x.data_ptr(), n, cols, mean.data_ptr(), corr.data_ptr(),
                                                m2.data_ptr(), ws.data_ptr()))
-        if self.process_group is not None:
-            self._allreduce(corr)
-            self._allreduce(m2)
-        var = (m2 - corr * corr / N) / N
-        eps = np.finfo(np.float64).eps
-        upper = N * eps * var + (N * mean * eps) ** 2
-        scale = torch.sqrt(var)
-        scale = torch.where(var <= upper, torch.ones_like(scale), scale)
+        self._allreduce(corr)
+        self._allreduce(m2)
+        mean, var, scale = scaler_finalize(N, s, corr, m2)
         self.mean_d, self.scale_d = mean.contiguous(), scale.contiguous()
         self.mean_ = mean.cpu().numpy()
         self.var_ = var.cpu().numpy()

@@ -1,0 +1,95 @@
+"""Data-parallel host logic on CPU with world_size-2 gloo (the GPU path uses the same code over RCCL).
+
+* Trainer.allreduce_grads: SUM of the flat gradient buffer across ranks.  With the reference's sum-reduced
+  loss, the DP gradient of the global batch is the sum of the per-shard gradients (BatchNorm statistics per
+  rank = DDP semantics, so each shard's gradient is that of the reference model run on the shard).  Checked
+  bit-exact against the single-process sum of the oracle model's per-shard gradients.
+* StandardScaler(process_group): the two f64 passes are all-reduced and finalised with scaler_finalize; the
+  result equals sklearn's StandardScaler on the concatenated shards.
+"""
+import os
+import tempfile
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import models_oracle as OM
+
+WORLD = 2
+
+
+def _shard_grads(rank):
+    """Flat fp32 gradient of the oracle audio-only HybridVAE (seed-42 init) on shard `rank` (2 clips)."""
+    torch.manual_seed(42)
+    model = OM.HybridVAE(128, 768, (128, 128), audio_only=True)
+    g = torch.Generator().manual_seed(100 + rank)
+    audio = torch.randn(2, 1, 128, 128, generator=g)
+    eps = torch.randn(2, 128, generator=g)
+    out = model(audio, None, eps=eps)
+    loss = OM.loss_function(out[0], audio, None, None, out[2], out[3])[0]
+    loss.backward()
+    return torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+
+
+def _scaler_shard(rank):
+    rng = np.random.default_rng(3)
+    X = (rng.standard_normal((61, 40)) * rng.uniform(0.1, 4, 40) + rng.uniform(-2, 2, 40)).astype(np.float32)
+    X[:, 3] = 0.75  # constant column -> scale 1
+    return X, np.array_split(X, WORLD)[rank]
+
+
+def _worker(rank, port, outdir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    import hlmc_amd
+    from hlmc_amd.features import scaler_finalize
+
+    # ---- gradient SUM all-reduce through Trainer.allreduce_grads (fp32 and bf16 wire formats)
+    flat = _shard_grads(rank)
+    ns = types.SimpleNamespace(gflat=flat.clone(), grad_dtype=torch.float32, process_group=None)
+    hlmc_amd.Trainer.allreduce_grads(ns)
+    ns16 = types.SimpleNamespace(gflat=flat.clone(), grad_dtype=torch.bfloat16, process_group=None)
+    hlmc_amd.Trainer.allreduce_grads(ns16)
+
+    # ---- distributed StandardScaler statistics (numpy stands in for the f64 column-sum kernels)
+    _, shard = _scaler_shard(rank)
+    n = torch.tensor([float(shard.shape[0])], dtype=torch.float64)
+    s = torch.from_numpy(shard.astype(np.float64).sum(0))
+    dist.all_reduce(n)
+    dist.all_reduce(s)
+    mean = s / float(n.item())
+    d = torch.from_numpy(shard.astype(np.float64)) - mean
+    corr, m2 = d.sum(0), (d * d).sum(0)
+    dist.all_reduce(corr)
+    dist.all_reduce(m2)
+    mean, var, scale = scaler_finalize(float(n.item()), s, corr, m2)
+    torch.save({"g32": ns.gflat, "g16": ns16.gflat, "mean": mean, "var": var, "scale": scale},
+               os.path.join(outdir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_allreduce_and_distributed_scaler():
+    from sklearn.preprocessing import StandardScaler as SkScaler
+    with tempfile.TemporaryDirectory() as outdir:
+        port = 29500 + (os.getpid() % 2000)
+        mp.spawn(_worker, args=(port, outdir), nprocs=WORLD, join=True)
+        res = [torch.load(os.path.join(outdir, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
+    ref = _shard_grads(0) + _shard_grads(1)
+    for r in res:
+        assert torch.equal(r["g32"], ref), "fp32 SUM all-reduce must equal the per-shard gradient sum exactly"
+        rel = float((r["g16"] - ref).norm() / ref.norm())
+        assert rel < 1e-2, rel
+    assert torch.equal(res[0]["g32"], res[1]["g32"])
+    X, _ = _scaler_shard(0)
+    sk = SkScaler().fit(X)
+    for r in res:
+        np.testing.assert_allclose(r["mean"].numpy(), sk.mean_, rtol=1e-12, atol=1e-15)
+        np.testing.assert_allclose(r["var"].numpy(), sk.var_, rtol=1e-9, atol=1e-15)
+        np.testing.assert_allclose(r["scale"].numpy(), sk.scale_, rtol=1e-9)
+    assert res[0]["scale"][3] == 1.0

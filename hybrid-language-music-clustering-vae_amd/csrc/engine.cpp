@@ -174,11 +174,15 @@ class NetT : public NetBase {
         size_t mean = 0, inv = 0;
     };
     BnBufs bn_plan(Arena& A, int C) { return BnBufs{A.take(C * 4), A.take(C * 4)}; }
+    // st: statistics already emitted by the producing GEMM's epilogue (nparts > 0), else a separate pass
     int bn_fwd(hipStream_t s, bool train, const T* y, int64_t R, int C, int bn, const BnBufs& bb, int g, int beta, int act,
-               const uint8_t* mask, float mscale, T* a, int lda) {
+               const uint8_t* mask, float mscale, T* a, int lda, const ops::ColStats* st = nullptr) {
         float* mean = AF(bb.mean);
         float* inv = AF(bb.inv);
-        if (train)
+        if (train && st && st->nparts > 0)
+            HLMC_TRY(ops::bn_stats_from_parts(s, st->part, st->nparts, R, C, mean, inv, RM[bn], RV[bn], NBT[bn],
+                                              kBnMomentum, kBnEps));
+        else if (train)
             HLMC_TRY(ops::bn_stats<T>(s, y, R, C, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps, scratch));
         else
             HLMC_TRY(ops::bn_eval_stats(s, RM[bn], RV[bn], C, kBnEps, mean, inv));
@@ -223,6 +227,7 @@ class NetT : public NetBase {
             }
             h /= 2;
             w /= 2;
+            need(ops::col_stats_bytes(B * h * w, 1, co));
             const size_t n = (size_t)B * h * w * co;
             enc.y[l] = A.take(n * sizeof(T));
             enc.a[l] = A.take(n * sizeof(T));
@@ -240,14 +245,16 @@ class NetT : public NetBase {
         for (int l = 0; l < 6; ++l) {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             T* y = AT(enc.y[l]);
+            ops::ColStats st{train ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
             if (l == 0)
                 HLMC_TRY(ops::conv_c1_s2<T>(s, audio, B, h, w, P[enc.w[0]], P[enc.b[0]], co, y));
             else
-                HLMC_TRY(ops::conv_s2<T>(s, AT(enc.a[l - 1]), B, h, w, ci, P0(enc.w[l]), P[enc.b[l]], co, y, scratch));
+                HLMC_TRY(ops::conv_s2<T>(s, AT(enc.a[l - 1]), B, h, w, ci, P0(enc.w[l]), P[enc.b[l]], co, y, scratch,
+                                         &st));
             h /= 2;
             w /= 2;
             HLMC_TRY(bn_fwd(s, train, y, (int64_t)B * h * w, co, enc.bn[l], enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f,
-                            AT(enc.a[l]), co));
+                            AT(enc.a[l]), co, &st));
         }
         return HLMC_OK;
     }
@@ -309,6 +316,7 @@ class NetT : public NetBase {
                 dec.a[l] = A.take(n * sizeof(T));
                 dec.bb[l] = bn_plan(A, co);
                 need(ops::bn_ws(B * 4 * h * w, co));
+                need(ops::col_stats_bytes(B * h * w, 4, co));
             } else {
                 need(ops::wgrad_c1_ws((int)B, h, w, ci));
                 need(ops::colsum_ws((int)(B * 4 * h * w), 1));
@@ -326,9 +334,10 @@ class NetT : public NetBase {
             const int ci = DEC_CH[l], co = DEC_CH[l + 1];
             if (l < 5) {
                 T* y = AT(dec.y[l]);
-                HLMC_TRY(ops::subpixel<T>(s, x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co, y, scratch));
+                ops::ColStats st{train ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
+                HLMC_TRY(ops::subpixel<T>(s, x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co, y, scratch, &st));
                 HLMC_TRY(bn_fwd(s, train, y, (int64_t)B * 4 * h * w, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0,
-                                nullptr, 1.f, AT(dec.a[l]), co));
+                                nullptr, 1.f, AT(dec.a[l]), co, &st));
                 x = AT(dec.a[l]);
             } else {
                 HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon));

@@ -162,12 +162,19 @@ struct SubpixelWeight {
 // act: 0 none, 1 relu
 template <typename OutT>
 struct StoreRM {
+    static constexpr bool kStats = false;
     OutT* out;
     const float* bias;
     int ld, act, accumulate;
     struct Row {
         OutT* r;
     };
+    // the value store() writes (without accumulate), as float: for the fused column statistics
+    __device__ float stored(int n, float v) const {
+        if (bias) v += bias[n];
+        if (act == 1) v = v > 0.f ? v : 0.f;
+        return to_f32<OutT>(from_f32<OutT>(v));
+    }
     __device__ void set_phase(int) {}
     __device__ Row row(int m) const { return Row{out + (int64_t)m * ld}; }
     __device__ void store(const Row& rw, int n, float v) const {
@@ -182,6 +189,7 @@ struct StoreRM {
 // Sub-pixel phase store into a high-res NHWC map [B, 2Hi, 2Wi, N]; m = (b, r, c) over the low grid.
 template <typename OutT>
 struct StoreSubpixel {
+    static constexpr bool kStats = false;
     OutT* out;
     const float* bias;
     int Hi, Wi, N;
@@ -189,6 +197,10 @@ struct StoreSubpixel {
     struct Row {
         OutT* r;
     };
+    __device__ float stored(int n, float v) const {
+        if (bias) v += bias[n];
+        return to_f32<OutT>(from_f32<OutT>(v));
+    }
     __device__ void set_phase(int p) { py = p >> 1; px = p & 1; }
     __device__ Row row(int m) const {
         const int c = m % Wi, t = m / Wi;
@@ -202,8 +214,19 @@ struct StoreSubpixel {
     }
 };
 
+// Any epilogue plus fused per-column statistics of the stored values (BatchNorm batch statistics):
+// block (phase, m-tile) writes part[(phase * mtiles + mtile) * 2N + n] = sum, [... + N + n] = sum of squares
+// (f64, fixed-order reduction) over its rows — the [nparts][2C] layout bn_finalize reduces.
+template <class Base>
+struct WithStats : Base {
+    static constexpr bool kStats = true;
+    double* part;
+    int mtiles;
+};
+
 // Split-K partial slab: ws[((phase * S + split) * M + m) * N + n]
 struct StorePartial {
+    static constexpr bool kStats = false;
     float* ws;
     int M, N, S;
     int phase, split;
@@ -339,6 +362,53 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
                 if (n < N) ep.store(er, n, acc[i][j][r]);
             }
         }
+    if constexpr (EP::kStats) {
+        // per-column sum / sum of squares of the stored values over the block's rows: lane sums over its
+        // 4*TM rows, xor-16/32 shuffles over the wave's row groups, then the waves of one column strip in order
+        constexpr int WAVES_M = BM / WM;
+        __shared__ double sred[WAVES_M][2][BN];
+        const int wmi = wave / WAVES_N;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 16 + (lane & 15);
+            double cs = 0.0, cq = 0.0;
+            if (n < N) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
+                        if (m < M) {
+                            const float v = ep.stored(n, acc[i][j][r]);
+                            cs += v;
+                            cq += (double)v * v;
+                        }
+                    }
+            }
+            cs += __shfl_xor(cs, 16, 64);
+            cq += __shfl_xor(cq, 16, 64);
+            cs += __shfl_xor(cs, 32, 64);
+            cq += __shfl_xor(cq, 32, 64);
+            if (lane < 16) {
+                sred[wmi][0][wn0 + j * 16 + lane] = cs;
+                sred[wmi][1][wn0 + j * 16 + lane] = cq;
+            }
+        }
+        __syncthreads();
+        const int row = phase * ep.mtiles + (int)(blockIdx.x / tiles_n);
+        for (int c = tid; c < BN; c += 256) {
+            const int n = n0 + c;
+            if (n >= N) continue;
+            double a = 0.0, q = 0.0;
+#pragma unroll
+            for (int w = 0; w < WAVES_M; ++w) {
+                a += sred[w][0][c];
+                q += sred[w][1][c];
+            }
+            ep.part[(int64_t)row * 2 * N + n] = a;
+            ep.part[(int64_t)row * 2 * N + N + n] = q;
+        }
+    }
 }
 
 // Split-K wrapper epilogue: the z-index of the grid selects the partial slab.

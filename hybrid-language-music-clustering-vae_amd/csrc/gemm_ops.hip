@@ -13,11 +13,13 @@ constexpr int kTargetBlocks = 512;  // 256 CUs x 2
 struct Plan {
     int S, ksl;
 };
+// BK = the largest K-step (split ranges are multiples of it); the minimum work per split is counted in
+// steps of the short (BK/2) K-step the kernel uses for short ranges
 inline Plan plan_nt(int tiles, int Kmax, int BK) {
     int S = 1;
     if (tiles < kTargetBlocks / 2) {
         S = cdiv(kTargetBlocks, tiles);
-        S = std::min(S, std::max(1, Kmax / (4 * BK)));
+        S = std::min(S, std::max(1, Kmax / (2 * BK)));
     }
     int ksl = cdiv(cdiv(Kmax, S), BK) * BK;
     S = cdiv(Kmax, ksl);
@@ -27,20 +29,35 @@ inline Plan plan_tn(int tiles, int K, int BK) {
     // weight gradients: long K (= batch x pixels), tiny M x N: split K until the grid fills the chip
     // (>= 8 k-tiles per split); the slab reduction keeps 4 loads in flight
     int S = cdiv(kTargetBlocks, tiles);
-    S = std::max(1, std::min(S, K / (8 * BK)));
+    S = std::max(1, std::min(S, K / (4 * BK)));
     int ksl = cdiv(cdiv(K, S), BK) * BK;
     S = cdiv(K, ksl);
     return {S, ksl};
 }
 
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
-int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws) {
+int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
+              ops::ColStats* st = nullptr) {
     constexpr int BK = gemm_bk<T>();
     const int tmn = cdiv(M, BM) * cdiv(N, BN);
     Plan pl = plan_nt(tmn * phases, Kmax, BK);
     dim3 grid(tmn, phases, pl.S);
     // short reductions keep the 4-chunk K-step (more co-resident blocks); long ones use 8 chunks
     const bool long_k = Kmax >= 1024;
+    if (st) st->nparts = 0;
+    if (pl.S == 1 && st && st->part) {  // single pass: the epilogue also emits the column statistics
+        WithStats<EP> eps;
+        static_cast<EP&>(eps) = ep;
+        eps.part = st->part;
+        eps.mtiles = cdiv(M, BM);
+        if (long_k)
+            gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, WithStats<EP>><<<grid, 256, 0, s>>>(al, bl, eps, M, N, pl.ksl);
+        else
+            gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, WithStats<EP>><<<grid, 256, 0, s>>>(al, bl, eps, M, N, pl.ksl);
+        HLMC_LAUNCHED();
+        st->nparts = phases * cdiv(M, BM);
+        return HLMC_OK;
+    }
     if (pl.S == 1) {
         if (long_k)
             gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, EP><<<grid, 256, 0, s>>>(al, bl, ep, M, N, pl.ksl);
@@ -74,10 +91,11 @@ size_t nt_ws(int M, int N, int Kmax, int phases, int BK) {
 
 // Dispatch on N for the NT family: 128x128 / 128x64 / 128x32 tiles.
 template <typename T, class AL, class BL, class EP>
-int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws) {
-    if (N >= 128) return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws);
-    if (N > 32) return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws);
-    return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws);
+int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
+                ops::ColStats* st = nullptr) {
+    if (N >= 128) return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+    if (N > 32) return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+    return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
 }
 template <typename T>
 size_t dispatch_nt_ws(int M, int N, int Kmax, int phases) {
@@ -162,7 +180,8 @@ inline int log2_exact(int c) { return (c > 0 && (c & (c - 1)) == 0) ? __builtin_
 namespace ops {
 
 template <typename T>
-int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws) {
+int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
+            ColStats* st) {
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % V == 0, "conv_s2: need even H/W and Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "conv_s2: 16-byte alignment");
@@ -170,15 +189,18 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     ConvS2Loader<T> al{x, Hi, Wi, Ci, Ho, Wo, M, log2_exact(Ci)};
     DenseLoader<T> bl{wp, K, Co, K, true};
     StoreRM<T> ep{y, bias, Co, 0, 0};
-    return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws);
+    return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
 }
+size_t col_stats_bytes(int64_t M, int phases, int C) { return (size_t)phases * cdiv((int)M, 128) * 2 * C * sizeof(double); }
+
 template <typename T>
 size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {
     return dispatch_nt_ws<T>(B * (Hi / 2) * (Wi / 2), Co, 9 * Ci, 1);
 }
 
 template <typename T>
-int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws) {
+int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
+             ColStats* st) {
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(Ci % V == 0, "subpixel: Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "subpixel: 16-byte alignment");
@@ -186,7 +208,7 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
     SubpixelLoader<T> al{x, Hi, Wi, Ci, M, log2_exact(Ci), 0, 0, 0, 0};
     SubpixelWeight<T> bl{wp, Ci, Co, log2_exact(Ci), 0, 0, 0, 0};
     StoreSubpixel<T> ep{y, bias, Hi, Wi, Co, 0, 0};
-    return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws);
+    return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
 }
 template <typename T>
 size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co) {
@@ -238,9 +260,11 @@ size_t linear_wgrad_ws(int Mb, int N, int K) {
 }
 
 #define INST(T)                                                                                                     \
-    template int conv_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws);        \
+    template int conv_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,         \
+                            ColStats*);                                                                              \
     template size_t conv_s2_ws<T>(int, int, int, int, int);                                                        \
-    template int subpixel<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws);       \
+    template int subpixel<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,        \
+                             ColStats*);                                                                             \
     template size_t subpixel_ws<T>(int, int, int, int, int);                                                       \
     template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws);                \
     template size_t wgrad_s2_ws<T>(int, int, int, int, int);                                                       \

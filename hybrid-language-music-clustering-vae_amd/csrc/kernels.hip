@@ -779,6 +779,14 @@ int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* in
     return HLMC_OK;
 }
 
+int bn_stats_from_parts(hipStream_t s, const double* part, int nparts, int64_t R, int C, float* mean, float* invstd,
+                        float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps) {
+    HLMC_CHECK_ARG(part && nparts > 0 && R > 0, "bn_stats_from_parts arguments");
+    bn_finalize_kernel<<<C, 256, 0, s>>>(part, nparts, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
 int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, int C, float eps, float* mean, float* invstd) {
     bn_eval_kernel<<<cdiv(C, 256), 256, 0, s>>>(run_mean, run_var, C, eps, mean, invstd);
     HLMC_LAUNCHED();

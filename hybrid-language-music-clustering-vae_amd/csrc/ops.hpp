@@ -13,16 +13,25 @@ struct Ws {  // split-K / reduction scratch handed down by the caller
 namespace ops {
 
 // ---------------------------------------------------------------- GEMM-shaped (gemm_ops.hip)
+// Optional fused BatchNorm statistics of a conv output: when the launch is single-pass the epilogue writes
+// nparts rows of [sum(C) | sum of squares(C)] f64 partials to part (else nparts = 0: compute them separately).
+struct ColStats {
+    double* part;
+    int nparts;
+};
+size_t col_stats_bytes(int64_t M, int phases, int C);  // bytes of part for M output rows x phases
 // y[B, Hi/2, Wi/2, Co] = conv3x3_s2_p1(x[B,Hi,Wi,Ci]) + bias ; wp packed [Co][3][3][Ci]
 template <typename T>
-int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws);
+int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
+            ColStats* st = nullptr);
 template <typename T>
 size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 
 // y[B, 2Hi, 2Wi, Co] = convT3x3_s2_p1_op1(x[B,Hi,Wi,Ci]) + bias ; wp packed [Co][3][3][Ci]
 // (also the data gradient of a stride-2 conv with the conv weight re-packed [Ci_conv][3][3][Co_conv])
 template <typename T>
-int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws);
+int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
+             ColStats* st = nullptr);
 template <typename T>
 size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -63,6 +72,9 @@ template <typename T>
 int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean, float* run_var,
              int64_t* nbt, float momentum, float eps, Ws ws);
 size_t bn_ws(int64_t R, int C);
+// Train-mode statistics from nparts fused partial rows ([nparts][2C] f64, ColStats) over R rows.
+int bn_stats_from_parts(hipStream_t s, const double* part, int nparts, int64_t R, int C, float* mean, float* invstd,
+                        float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps);
 // Eval-mode statistics from running buffers.
 int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, int C, float eps, float* mean, float* invstd);
 // a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale];  act: 0 lrelu(0.01), 1 relu, 2 none

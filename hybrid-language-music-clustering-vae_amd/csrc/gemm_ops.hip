@@ -89,20 +89,33 @@ size_t nt_ws(int M, int N, int Kmax, int phases, int BK) {
     return pl.S == 1 ? 0 : (size_t)phases * pl.S * M * N * sizeof(float);
 }
 
-// Dispatch on N for the NT family: 128x128 / 128x64 / 128x32 tiles.
+// Tile choice for the NT family by N: 128x128 / 128x64 / 128x32.  (Measured: stepping down to 64x64 to put
+// two blocks on every CU doubles operand re-reads and is slower on every layer of the step.)
+inline int nt_tile(int M, int N, int phases) {
+    (void)M; (void)phases;
+    if (N >= 128) return 0;
+    if (N > 32) return 1;
+    return 3;
+}
 template <typename T, class AL, class BL, class EP>
 int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
                 ops::ColStats* st = nullptr) {
-    if (N >= 128) return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
-    if (N > 32) return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
-    return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+    switch (nt_tile(M, N, phases)) {
+        case 0: return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+        case 1: return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+        case 2: return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+        default: return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+    }
 }
 template <typename T>
 size_t dispatch_nt_ws(int M, int N, int Kmax, int phases) {
     constexpr int BK = gemm_bk<T>();
-    if (N >= 128) return nt_ws<128, 128>(M, N, Kmax, phases, BK);
-    if (N > 32) return nt_ws<128, 64>(M, N, Kmax, phases, BK);
-    return nt_ws<128, 32>(M, N, Kmax, phases, BK);
+    switch (nt_tile(M, N, phases)) {
+        case 0: return nt_ws<128, 128>(M, N, Kmax, phases, BK);
+        case 1: return nt_ws<128, 64>(M, N, Kmax, phases, BK);
+        case 2: return nt_ws<64, 64>(M, N, Kmax, phases, BK);
+        default: return nt_ws<128, 32>(M, N, Kmax, phases, BK);
+    }
 }
 
 // Linear layers have small M (= batch): 64x64 tiles so more blocks exist before split-K.
@@ -191,7 +204,7 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     StoreRM<T> ep{y, bias, Co, 0, 0};
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
 }
-size_t col_stats_bytes(int64_t M, int phases, int C) { return (size_t)phases * cdiv((int)M, 128) * 2 * C * sizeof(double); }
+size_t col_stats_bytes(int64_t M, int phases, int C) { return (size_t)phases * cdiv((int)M, 64) * 2 * C * sizeof(double); }
 
 template <typename T>
 size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {

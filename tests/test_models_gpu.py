@@ -4,11 +4,15 @@ tests/golden/make_golden.py) on the golden fixture cases, from identical weights
 
 Tolerances (fp32, per step from shared state — SURVEY §0.6):
   * mu, logvar, reconstructions, ELBO terms: relative error <= 1e-4 (north_star), typically ~1e-6.
-  * parameter gradients: relative L2 <= 1e-3 per tensor; conv biases that feed train-mode BatchNorm
+  * parameter gradients: relative L2 error vs a float64 run of the oracle <= max(1e-3, 8 x the fp32 oracle's
+    own error) per tensor (sum-reduced losses leave a few gradients ill-conditioned in any fp32 order);
+    conv biases that feed train-mode BatchNorm
     have a mathematically-zero gradient (pure rounding noise) and are checked absolutely against the
     scale of their layer's weight gradient.
   * BatchNorm running statistics after the step: relative <= 1e-4.
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -108,6 +112,9 @@ def simple_masks(case, B, seed=5):
 def compare_step(case, ora, ours, tol_out=1e-4, tol_grad=1e-3):
     ins, eps = FX.inputs_fn(case)(0)
     masks, flat = (simple_masks(case, case["B"]) if case["kind"] == "simple" else (None, None))
+    # float64 run of the same oracle: the exact-arithmetic yardstick for the gradient check
+    ora64 = copy.deepcopy(ora).double()
+    run_oracle_step(case, ora64, [t.double() for t in ins], eps.double(), masks)
     o_out, o_loss = run_oracle_step(case, ora, ins, eps, masks)
     m_out, m_loss = run_ours_step(case, ours, ins, eps, flat)
     for i, (a, b) in enumerate(zip(m_out, o_out)):
@@ -118,6 +125,7 @@ def compare_step(case, ora, ours, tol_out=1e-4, tol_grad=1e-3):
         if float(b) != 0.0:
             assert abs(float(a) - float(b)) <= tol_out * abs(float(b)) + 1e-6, f"loss {i}: {float(a)} vs {float(b)}"
     onames = dict(ora.named_parameters())
+    o64 = dict(ora64.named_parameters())
     mparams = dict(ours.named_parameters())
     for name, po in onames.items():
         gm, go = mparams[name].grad, po.grad
@@ -127,7 +135,11 @@ def compare_step(case, ora, ours, tol_out=1e-4, tol_grad=1e-3):
             scale = float(onames[wname].grad.abs().max())
             assert float((gm.cpu() - go).abs().max()) <= 1e-4 * scale + 1e-6, name
         else:
-            assert rel(gm, go) < tol_grad, f"grad {name}: {rel(gm, go)}"
+            # as accurate as the reference's own fp32 computation: error vs the float64 gradient within
+            # max(tol_grad, 8 x the fp32 oracle's error) (sum-reduced losses make some gradients ill-conditioned)
+            g64 = o64[name].grad
+            e_ref, e_ours = rel(go, g64), rel(gm, g64)
+            assert e_ours <= max(tol_grad, 8 * e_ref), f"grad {name}: {e_ours:.3e} vs fp32 oracle {e_ref:.3e}"
     for (n, bo), (_, bm) in zip(ora.named_buffers(), ours.named_buffers()):
         if bo.dtype.is_floating_point:
             assert rel(bm, bo) < tol_out, f"buffer {n}: {rel(bm, bo)}"

@@ -33,9 +33,13 @@ struct FastDiv {
     __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, mul) + n) >> sh; }
 };
 
+// 16 zero bytes: the source of every out-of-range / padding chunk of the LDS-DMA (global_load_lds) loaders
+static __device__ __attribute__((aligned(16))) uint4 g_zero16 = {0u, 0u, 0u, 0u};
+
 // ============================================================================ A / B loaders (NT)
 // Loader contract: set_phase(p); int K() const; Row prep(int m) (once per tile row, outside the K loop);
-// uint4 load(const Row&, int k) (16 bytes = V consecutive k, zero-filled outside the operand).
+// uint4 load(const Row&, int k) (16 bytes = V consecutive k, zero-filled outside the operand);
+// const void* addr(const Row&, int k): the same chunk's global address, or g_zero16 (LDS-DMA path).
 
 template <typename T>
 struct DenseLoader {  // X[m * ld + k], m < M, k < K
@@ -48,6 +52,9 @@ struct DenseLoader {  // X[m * ld + k], m < M, k < K
     __device__ void set_phase(int) {}
     __device__ int K() const { return Kd; }
     __device__ Row prep(int m) const { return Row{m < M ? p + (int64_t)m * ld : nullptr}; }
+    __device__ const void* addr(const Row& rw, int k) const {  // DMA path: Kd % V == 0, 16-byte rows
+        return (rw.r && k < Kd) ? static_cast<const void*>(rw.r + k) : static_cast<const void*>(&g_zero16);
+    }
     __device__ uint4 load(const Row& rw, int k) const {
         constexpr int V = Vec16<T>::N;
         if (!rw.r) return make_uint4(0, 0, 0, 0);
@@ -88,6 +95,13 @@ struct ConvS2Loader {
             return make_uint4(0, 0, 0, 0);
         return *reinterpret_cast<const uint4*>(x + rw.base + ((int64_t)kh * Wi + kw) * C + ci);
     }
+    __device__ const void* addr(const Row& rw, int k) const {
+        const int tap = cshift >= 0 ? (k >> cshift) : k / C;
+        const int ci = k - tap * C;
+        const int kh = tap / 3, kw = tap - kh * 3;
+        if (!(rw.flags & 1) || tap >= 9 || (kh == 0 && (rw.flags & 2)) || (kw == 0 && (rw.flags & 4))) return &g_zero16;
+        return x + rw.base + ((int64_t)kh * Wi + kw) * C + ci;
+    }
 };
 
 // Sub-pixel phase of a stride-2 transposed 3x3 conv (pad 1, output_padding 1) / of the stride-2
@@ -127,6 +141,14 @@ struct SubpixelLoader {
         if (!(rw.flags & 1) || k >= Kd || (dr && (rw.flags & 2)) || (dc && (rw.flags & 4))) return make_uint4(0, 0, 0, 0);
         return *reinterpret_cast<const uint4*>(x + rw.base + ((int64_t)dr * Wi + dc) * C + ci);
     }
+    __device__ const void* addr(const Row& rw, int k) const {
+        const int tt = cshift >= 0 ? (k >> cshift) : k / C;
+        const int ci = k - tt * C;
+        const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
+        const int dr = sp_delta(py, ty), dc = sp_delta(px, tx);
+        if (!(rw.flags & 1) || k >= Kd || (dr && (rw.flags & 2)) || (dc && (rw.flags & 4))) return &g_zero16;
+        return x + rw.base + ((int64_t)dr * Wi + dc) * C + ci;
+    }
 };
 
 // B operand for a sub-pixel phase: packed P[n][kh][kw][C]; k = (ty,tx,ci) -> tap (kh,kw) of the phase.
@@ -153,6 +175,14 @@ struct SubpixelWeight {
         const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
         const int kh = sp_kidx(py, ty), kw = sp_kidx(px, tx);
         return *reinterpret_cast<const uint4*>(rw.r + (kh * 3 + kw) * C + ci);
+    }
+    __device__ const void* addr(const Row& rw, int k) const {
+        if (!rw.r || k >= Kd) return &g_zero16;
+        const int tt = cshift >= 0 ? (k >> cshift) : k / C;
+        const int ci = k - tt * C;
+        const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
+        const int kh = sp_kidx(py, ty), kw = sp_kidx(px, tx);
+        return rw.r + (kh * 3 + kw) * C + ci;
     }
 };
 
@@ -407,6 +437,195 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
             }
             ep.part[(int64_t)row * 2 * N + n] = a;
             ep.part[(int64_t)row * 2 * N + N + n] = q;
+        }
+    }
+}
+
+// ============================================================================ NT main loop, LDS-DMA pipeline
+// NS-stage ring of [rows][8 x 16-byte chunks] tiles in LDS, filled by global_load_lds_dwordx4 (no register
+// staging): one wave-instruction writes 1 KB = 8 rows; lane l of it writes physical chunk l & 7 of row l >> 3
+// and fetches logical chunk (l & 7) ^ (row & 7) (XOR swizzle on the SOURCE address keeps the LDS image
+// lane-linear and makes the MFMA fragment reads bank-conflict-free).  Per K-step: counted vmcnt wait for this
+// stage's DMA, raw barrier, issue the stage NS-1 ahead into the buffer everyone just finished, MFMAs.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int GPW, int NS>
+__device__ __forceinline__ void wait_stage(int ahead) {  // ahead = stages still allowed in flight (< NS-1)
+    if constexpr (NS >= 4) {
+        if (ahead >= 2) { wait_vmcnt<2 * GPW>(); return; }
+    }
+    if constexpr (NS >= 3) {
+        if (ahead >= 1) { wait_vmcnt<GPW>(); return; }
+    }
+    wait_vmcnt<0>();
+}
+__device__ __forceinline__ void glds16(const void* g, void* l) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NS, class AL, class BL, class EP>
+__global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len) {
+    constexpr int V = Vec16<T>::N;
+    constexpr int BK = 8 * V;                       // 128-byte tile rows
+    constexpr int ASZ = BM * 128, BSZ = BN * 128, STG = ASZ + BSZ;
+    constexpr int AI = BM / 8, BI = BN / 8;         // 1 KB DMA instructions per stage
+    static_assert(AI % 4 == 0 && BI >= 4 && BI % 4 == 0, "tile rows per stage must split over 4 waves");
+    constexpr int AIW = AI / 4, BIW = BI / 4, GPW = AIW + BIW;
+    constexpr int WAVES_N = BN / WN;
+    static_assert((BM / WM) * WAVES_N == 4, "4 waves per block");
+    constexpr int TM = WM / 16, TN = WN / 16;
+    __shared__ __attribute__((aligned(1024))) char smem[NS * STG];  // the only LDS object (see vmcnt traps)
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
+    const int tiles_n = (N + BN - 1) / BN;
+    const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
+    const int phase = blockIdx.y;
+    al.set_phase(phase); bl.set_phase(phase); ep.set_phase(phase);
+    const int K = al.K();
+    const int kb = blockIdx.z * ksplit_len;
+    const int ke = min(K, kb + ksplit_len);
+    const int nsteps = kb < ke ? (ke - kb + BK - 1) / BK : 0;
+
+    f32x4_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    const int lrow = lane >> 3;
+    const int lchunk = (lane & 7) ^ (lrow & 7);  // logical chunk fetched by this lane (row & 7 == lrow)
+    typename AL::Row arow[AIW];
+    typename BL::Row brow[BIW];
+#pragma unroll
+    for (int i = 0; i < AIW; ++i) arow[i] = al.prep(m0 + (wave * AIW + i) * 8 + lrow);
+#pragma unroll
+    for (int i = 0; i < BIW; ++i) brow[i] = bl.prep(n0 + (wave * BIW + i) * 8 + lrow);
+    auto issue = [&](int slot, int k0) {
+        char* sb = smem + slot * STG;
+        const int k = k0 + lchunk * V;
+#pragma unroll
+        for (int i = 0; i < AIW; ++i) glds16(al.addr(arow[i], k), sb + (wave * AIW + i) * 1024);
+#pragma unroll
+        for (int i = 0; i < BIW; ++i) glds16(bl.addr(brow[i], k), sb + ASZ + (wave * BIW + i) * 1024);
+    };
+
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+        if (p < nsteps) issue(p, kb + p * BK);
+    for (int t = 0; t < nsteps; ++t) {
+        wait_stage<GPW, NS>(min(NS - 2, nsteps - 1 - t));
+        __builtin_amdgcn_s_barrier();
+        if (t + NS - 1 < nsteps) issue((t + NS - 1) % NS, kb + (t + NS - 1) * BK);
+        const char* sa = smem + (t % NS) * STG;
+        const char* sbb = sa + ASZ;
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int s = 0; s < BK / 32; ++s) {
+                const int c = 4 * s + (lane >> 4);
+                bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = wm0 + i * 16 + (lane & 15);
+                    af[i] = *reinterpret_cast<const bf16x8_t*>(sa + row * 128 + ((c ^ (row & 7)) << 4));
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int row = wn0 + j * 16 + (lane & 15);
+                    bfr[j] = *reinterpret_cast<const bf16x8_t*>(sbb + row * 128 + ((c ^ (row & 7)) << 4));
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < BK / 4; ++s) {
+                float af[TM], bfr[TN];
+                const int q = lane >> 4;  // k = 4 s + q: chunk s, word q
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = wm0 + i * 16 + (lane & 15);
+                    af[i] = *reinterpret_cast<const float*>(sa + row * 128 + ((s ^ (row & 7)) << 4) + q * 4);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int row = wn0 + j * 16 + (lane & 15);
+                    bfr[j] = *reinterpret_cast<const float*>(sbb + row * 128 + ((s ^ (row & 7)) << 4) + q * 4);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+    // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
+            if (m >= M) continue;
+            const typename EP::Row er = ep.row(m);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = n0 + wn0 + j * 16 + (lane & 15);
+                if (n < N) ep.store(er, n, acc[i][j][r]);
+            }
+        }
+    if constexpr (EP::kStats) {
+        constexpr int WAVES_M = BM / WM;
+        static_assert(WAVES_M * 2 * BN * 8 <= NS * STG, "stats scratch fits the staging ring");
+        __syncthreads();  // every wave is done with the ring: reuse it for the column-sum scratch
+        double* sred = reinterpret_cast<double*>(smem);  // [WAVES_M][2][BN]
+        const int wmi = wave / WAVES_N;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn0 + j * 16 + (lane & 15);
+            double cs = 0.0, cq = 0.0;
+            if (n < N) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
+                        if (m < M) {
+                            const float v = ep.stored(n, acc[i][j][r]);
+                            cs += v;
+                            cq += (double)v * v;
+                        }
+                    }
+            }
+            cs += __shfl_xor(cs, 16, 64);
+            cq += __shfl_xor(cq, 16, 64);
+            cs += __shfl_xor(cs, 32, 64);
+            cq += __shfl_xor(cq, 32, 64);
+            if (lane < 16) {
+                sred[(wmi * 2 + 0) * BN + wn0 + j * 16 + lane] = cs;
+                sred[(wmi * 2 + 1) * BN + wn0 + j * 16 + lane] = cq;
+            }
+        }
+        __syncthreads();
+        const int prow = phase * ep.mtiles + (int)(blockIdx.x / tiles_n);
+        for (int c = tid; c < BN; c += 256) {
+            const int n = n0 + c;
+            if (n >= N) continue;
+            double a = 0.0, q = 0.0;
+#pragma unroll
+            for (int w = 0; w < WAVES_M; ++w) {
+                a += sred[(w * 2 + 0) * BN + c];
+                q += sred[(w * 2 + 1) * BN + c];
+            }
+            ep.part[(int64_t)prow * 2 * N + n] = a;
+            ep.part[(int64_t)prow * 2 * N + N + n] = q;
         }
     }
 }

@@ -3,6 +3,7 @@
 #include "ops.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace hlmc {
 namespace {
@@ -35,34 +36,55 @@ inline Plan plan_tn(int tiles, int K, int BK) {
     return {S, ksl};
 }
 
+// NT pipeline: 0 register-staged (gemm_nt_kernel), 3/4 = LDS-DMA ring of that many stages (gemm_nt_glds_kernel).
+// Measured (scripts/bench_gemm.py): the 4-stage DMA ring wins when a block reduces >= 1024 (16 K-steps),
+// the register path below that (short reductions: more co-resident blocks hide the pipeline prologue).
+// HLMC_GEMM_PIPE=0/3/4 forces one (A/B measurement aid).
+inline int nt_pipe_select(int ksl) {
+    static const int forced = [] {
+        const char* e = std::getenv("HLMC_GEMM_PIPE");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (forced >= 0) return forced;
+    return ksl >= 1024 ? 4 : 0;
+}
+
+template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class E>
+void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
+                      bool long_k, int pipe) {
+    if (pipe == 3)
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+    else if (pipe == 4)
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+    else if (long_k)
+        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+    else
+        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+}
+
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
 int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
-              ops::ColStats* st = nullptr) {
+              ops::ColStats* st = nullptr, bool dma_ok = true) {
     constexpr int BK = gemm_bk<T>();
     const int tmn = cdiv(M, BM) * cdiv(N, BN);
     Plan pl = plan_nt(tmn * phases, Kmax, BK);
     dim3 grid(tmn, phases, pl.S);
-    // short reductions keep the 4-chunk K-step (more co-resident blocks); long ones use 8 chunks
+    // register path: short reductions keep the 4-chunk K-step (more co-resident blocks), long ones 8 chunks
     const bool long_k = Kmax >= 1024;
+    const int pipe = (dma_ok && BN >= 32 && BM >= 64) ? nt_pipe_select(pl.ksl) : 0;
     if (st) st->nparts = 0;
     if (pl.S == 1 && st && st->part) {  // single pass: the epilogue also emits the column statistics
         WithStats<EP> eps;
         static_cast<EP&>(eps) = ep;
         eps.part = st->part;
         eps.mtiles = cdiv(M, BM);
-        if (long_k)
-            gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, WithStats<EP>><<<grid, 256, 0, s>>>(al, bl, eps, M, N, pl.ksl);
-        else
-            gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, WithStats<EP>><<<grid, 256, 0, s>>>(al, bl, eps, M, N, pl.ksl);
+        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, eps, M, N, pl.ksl, long_k, pipe);
         HLMC_LAUNCHED();
         st->nparts = phases * cdiv(M, BM);
         return HLMC_OK;
     }
     if (pl.S == 1) {
-        if (long_k)
-            gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, EP><<<grid, 256, 0, s>>>(al, bl, ep, M, N, pl.ksl);
-        else
-            gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, EP><<<grid, 256, 0, s>>>(al, bl, ep, M, N, pl.ksl);
+        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, ep, M, N, pl.ksl, long_k, pipe);
         HLMC_LAUNCHED();
         return HLMC_OK;
     }
@@ -70,10 +92,7 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "split-K workspace too small");
     StorePartialZ part;
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
-    if (long_k)
-        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, StorePartialZ><<<grid, 256, 0, s>>>(al, bl, part, M, N, pl.ksl);
-    else
-        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, StorePartialZ><<<grid, 256, 0, s>>>(al, bl, part, M, N, pl.ksl);
+    nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe);
     HLMC_LAUNCHED();
     int64_t total = (int64_t)phases * M * N;
     int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
@@ -121,8 +140,9 @@ size_t dispatch_nt_ws(int M, int N, int Kmax, int phases) {
 // Linear layers have small M (= batch): 64x64 tiles so more blocks exist before split-K.
 template <typename T, class AL, class BL, class EP>
 int dispatch_linear(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int K, Ws ws) {
-    if (M >= 1024 && N >= 128) return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, K, 1, ws);
-    return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, K, 1, ws);
+    // register path: arbitrary ld / K (the DMA path needs 16-byte chunks that never straddle K)
+    if (M >= 1024 && N >= 128) return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, K, 1, ws, nullptr, false);
+    return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, K, 1, ws, nullptr, false);
 }
 template <typename T>
 size_t dispatch_linear_ws(int M, int N, int K) {

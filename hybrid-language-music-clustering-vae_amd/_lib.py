@@ -12,7 +12,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhlmc.so")
+LIB_PATH = os.environ.get("HLMC_LIB") or os.path.join(_HERE, "libhlmc.so")  # HLMC_LIB: A/B builds
 
 c_int, c_i64, c_f32, c_f64, c_vp, c_char_p = C.c_int, C.c_int64, C.c_float, C.c_double, C.c_void_p, C.c_char_p
 P_vp = C.POINTER(c_vp)

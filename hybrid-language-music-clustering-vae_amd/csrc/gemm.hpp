@@ -37,9 +37,13 @@ struct FastDiv {
 static __device__ __attribute__((aligned(16))) uint4 g_zero16 = {0u, 0u, 0u, 0u};
 
 // ============================================================================ A / B loaders (NT)
-// Loader contract: set_phase(p); int K() const; Row prep(int m) (once per tile row, outside the K loop);
-// uint4 load(const Row&, int k) (16 bytes = V consecutive k, zero-filled outside the operand);
-// const void* addr(const Row&, int k): the same chunk's global address, or g_zero16 (LDS-DMA path).
+// Loader contract: set_phase(p); int K() const;
+//   Row prep(int m)  — once per tile row, outside the K loop;
+//   Ctx ctx(int k)   — once per (thread, K-step): everything that depends only on this thread's k;
+//   uint4 load(const Row&, const Ctx&)        — 16 bytes = V consecutive k, zero outside the operand;
+//   const void* addr(const Row&, const Ctx&)  — the same chunk's global address or g_zero16 (LDS-DMA path).
+// A thread's 16-byte chunk column is fixed for the whole kernel, so per row and step a load costs one
+// flag test and one 64-bit add.
 
 template <typename T>
 struct DenseLoader {  // X[m * ld + k], m < M, k < K
@@ -49,14 +53,21 @@ struct DenseLoader {  // X[m * ld + k], m < M, k < K
     struct Row {
         const T* r;
     };
+    struct Ctx {
+        int k;
+    };
     __device__ void set_phase(int) {}
     __device__ int K() const { return Kd; }
     __device__ Row prep(int m) const { return Row{m < M ? p + (int64_t)m * ld : nullptr}; }
-    __device__ const void* addr(const Row& rw, int k) const {  // DMA path: Kd % V == 0, 16-byte rows
-        return (rw.r && k < Kd) ? static_cast<const void*>(rw.r + k) : static_cast<const void*>(&g_zero16);
+    __device__ Ctx ctx(int k) const { return Ctx{k}; }
+    __device__ const void* addr(const Row& rw, const Ctx& cx) const {  // DMA path: Kd % V == 0, 16-byte rows
+        return (rw.r && cx.k < Kd) ? static_cast<const void*>(rw.r + cx.k) : static_cast<const void*>(&g_zero16);
     }
-    __device__ uint4 load(const Row& rw, int k) const {
+    __device__ uint4 load(const Row& rw, const Ctx& cx) const {
         constexpr int V = Vec16<T>::N;
+        const int k = cx.k;
+        // whole-chunk operand (Kd % V == 0, aligned rows: every conv weight): unconditional load, no tail path
+        if (vec && (Kd % V) == 0) return *reinterpret_cast<const uint4*>(addr(rw, cx));
         if (!rw.r) return make_uint4(0, 0, 0, 0);
         if (vec && k + V <= Kd) return *reinterpret_cast<const uint4*>(rw.r + k);
         union { uint4 u; T e[V]; } x;
@@ -68,8 +79,8 @@ struct DenseLoader {  // X[m * ld + k], m < M, k < K
 
 // Stride-2, pad-1, 3x3 window gather over an NHWC map: A(m = (b,oh,ow), k = (kh,kw,ci))
 //   = X[b, 2oh-1+kh, 2ow-1+kw, ci].  Requires C % VEC == 0 (a 16-byte chunk never straddles taps);
-// chunks past K = 9C read as zeros.
-// Only the top row (kh = 0, oh = 0) and left column (kw = 0, ow = 0) of the window can fall outside.
+// chunks past K = 9C read as zeros.  Row flags: bit0 row out of range, bit1 top row (oh = 0), bit2 left
+// column (ow = 0), bit3 always set; the step's Ctx rejects the rows whose flags meet its mask.
 template <typename T>
 struct ConvS2Loader {
     const T* x;
@@ -77,30 +88,31 @@ struct ConvS2Loader {
     int cshift;  // log2(C) when C is a power of two, else -1
     struct Row {
         int64_t base;  // element offset of (b, 2oh-1, 2ow-1, 0)
-        int flags;     // bit0 valid, bit1 top row, bit2 left column
+        int flags;
+    };
+    struct Ctx {
+        int64_t off;  // (kh*Wi + kw)*C + ci
+        int reject;   // bit0 always; bit1 if kh == 0; bit2 if kw == 0; bit3 if tap >= 9
     };
     __device__ void set_phase(int) {}
     __device__ int K() const { return 9 * C; }
     __device__ Row prep(int m) const {
-        if (m >= M) return Row{0, 0};
+        if (m >= M) return Row{0, 1 | 8};
         const int ow = m % Wo, t = m / Wo;
         const int oh = t % Ho, b = t / Ho;
-        return Row{(((int64_t)b * Hi + 2 * oh - 1) * Wi + 2 * ow - 1) * C, 1 | (oh == 0 ? 2 : 0) | (ow == 0 ? 4 : 0)};
+        return Row{(((int64_t)b * Hi + 2 * oh - 1) * Wi + 2 * ow - 1) * C, 8 | (oh == 0 ? 2 : 0) | (ow == 0 ? 4 : 0)};
     }
-    __device__ uint4 load(const Row& rw, int k) const {
+    __device__ Ctx ctx(int k) const {
         const int tap = cshift >= 0 ? (k >> cshift) : k / C;
         const int ci = k - tap * C;
         const int kh = tap / 3, kw = tap - kh * 3;
-        if (!(rw.flags & 1) || tap >= 9 || (kh == 0 && (rw.flags & 2)) || (kw == 0 && (rw.flags & 4)))
-            return make_uint4(0, 0, 0, 0);
-        return *reinterpret_cast<const uint4*>(x + rw.base + ((int64_t)kh * Wi + kw) * C + ci);
+        return Ctx{((int64_t)kh * Wi + kw) * C + ci, 1 | (kh == 0 ? 2 : 0) | (kw == 0 ? 4 : 0) | (tap >= 9 ? 8 : 0)};
     }
-    __device__ const void* addr(const Row& rw, int k) const {
-        const int tap = cshift >= 0 ? (k >> cshift) : k / C;
-        const int ci = k - tap * C;
-        const int kh = tap / 3, kw = tap - kh * 3;
-        if (!(rw.flags & 1) || tap >= 9 || (kh == 0 && (rw.flags & 2)) || (kw == 0 && (rw.flags & 4))) return &g_zero16;
-        return x + rw.base + ((int64_t)kh * Wi + kw) * C + ci;
+    // unconditional load from a selected address (no branch around the load: hipcc would wait per chunk)
+    __device__ uint4 load(const Row& rw, const Ctx& cx) const { return *reinterpret_cast<const uint4*>(addr(rw, cx)); }
+    __device__ const void* addr(const Row& rw, const Ctx& cx) const {
+        if (rw.flags & cx.reject) return &g_zero16;
+        return x + rw.base + cx.off;
     }
 };
 
@@ -111,6 +123,7 @@ __device__ __forceinline__ int sp_ntaps(int par) { return par ? 2 : 1; }
 __device__ __forceinline__ int sp_kidx(int par, int t) { return par ? (t ? 2 : 0) : 1; }
 __device__ __forceinline__ int sp_delta(int par, int t) { return (par && t == 0) ? 1 : 0; }
 
+// Row flags: bit0 row out of range, bit1 last low-res row (r+1 outside), bit2 last column, bit3 always.
 template <typename T>
 struct SubpixelLoader {
     const T* x;  // low-res NHWC [B, Hi, Wi, C]
@@ -119,7 +132,11 @@ struct SubpixelLoader {
     int py, px, ntx, Kd;
     struct Row {
         int64_t base;  // offset of (b, r, c, 0)
-        int flags;     // bit0 valid, bit1 last row (r+1 out), bit2 last column
+        int flags;
+    };
+    struct Ctx {
+        int64_t off;  // (dr*Wi + dc)*C + ci
+        int reject;   // bit0 always; bit1 if dr; bit2 if dc; bit3 if k >= K
     };
     __device__ void set_phase(int p) {
         py = p >> 1; px = p & 1;
@@ -128,26 +145,23 @@ struct SubpixelLoader {
     }
     __device__ int K() const { return Kd; }
     __device__ Row prep(int m) const {
-        if (m >= M) return Row{0, 0};
+        if (m >= M) return Row{0, 1 | 8};
         const int c = m % Wi, t = m / Wi;
         const int r = t % Hi, b = t / Hi;
-        return Row{(((int64_t)b * Hi + r) * Wi + c) * C, 1 | (r == Hi - 1 ? 2 : 0) | (c == Wi - 1 ? 4 : 0)};
+        return Row{(((int64_t)b * Hi + r) * Wi + c) * C, 8 | (r == Hi - 1 ? 2 : 0) | (c == Wi - 1 ? 4 : 0)};
     }
-    __device__ uint4 load(const Row& rw, int k) const {
+    __device__ Ctx ctx(int k) const {
         const int tt = cshift >= 0 ? (k >> cshift) : k / C;
         const int ci = k - tt * C;
         const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
         const int dr = sp_delta(py, ty), dc = sp_delta(px, tx);
-        if (!(rw.flags & 1) || k >= Kd || (dr && (rw.flags & 2)) || (dc && (rw.flags & 4))) return make_uint4(0, 0, 0, 0);
-        return *reinterpret_cast<const uint4*>(x + rw.base + ((int64_t)dr * Wi + dc) * C + ci);
+        return Ctx{((int64_t)dr * Wi + dc) * C + ci, 1 | (dr ? 2 : 0) | (dc ? 4 : 0) | (k >= Kd ? 8 : 0)};
     }
-    __device__ const void* addr(const Row& rw, int k) const {
-        const int tt = cshift >= 0 ? (k >> cshift) : k / C;
-        const int ci = k - tt * C;
-        const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
-        const int dr = sp_delta(py, ty), dc = sp_delta(px, tx);
-        if (!(rw.flags & 1) || k >= Kd || (dr && (rw.flags & 2)) || (dc && (rw.flags & 4))) return &g_zero16;
-        return x + rw.base + ((int64_t)dr * Wi + dc) * C + ci;
+    // unconditional load from a selected address (no branch around the load: hipcc would wait per chunk)
+    __device__ uint4 load(const Row& rw, const Ctx& cx) const { return *reinterpret_cast<const uint4*>(addr(rw, cx)); }
+    __device__ const void* addr(const Row& rw, const Ctx& cx) const {
+        if (rw.flags & cx.reject) return &g_zero16;
+        return x + rw.base + cx.off;
     }
 };
 
@@ -161,6 +175,9 @@ struct SubpixelWeight {
     struct Row {
         const T* r;
     };
+    struct Ctx {
+        int off;  // (kh*3 + kw)*C + ci, or -1 past K
+    };
     __device__ void set_phase(int p) {
         py = p >> 1; px = p & 1;
         ntx = sp_ntaps(px);
@@ -168,21 +185,17 @@ struct SubpixelWeight {
     }
     __device__ int K() const { return Kd; }
     __device__ Row prep(int n) const { return Row{n < N ? w + (int64_t)n * 9 * C : nullptr}; }
-    __device__ uint4 load(const Row& rw, int k) const {
-        if (!rw.r || k >= Kd) return make_uint4(0, 0, 0, 0);
+    __device__ Ctx ctx(int k) const {
+        if (k >= Kd) return Ctx{-1};
         const int tt = cshift >= 0 ? (k >> cshift) : k / C;
         const int ci = k - tt * C;
         const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
-        const int kh = sp_kidx(py, ty), kw = sp_kidx(px, tx);
-        return *reinterpret_cast<const uint4*>(rw.r + (kh * 3 + kw) * C + ci);
+        return Ctx{(sp_kidx(py, ty) * 3 + sp_kidx(px, tx)) * C + ci};
     }
-    __device__ const void* addr(const Row& rw, int k) const {
-        if (!rw.r || k >= Kd) return &g_zero16;
-        const int tt = cshift >= 0 ? (k >> cshift) : k / C;
-        const int ci = k - tt * C;
-        const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
-        const int kh = sp_kidx(py, ty), kw = sp_kidx(px, tx);
-        return rw.r + (kh * 3 + kw) * C + ci;
+    __device__ uint4 load(const Row& rw, const Ctx& cx) const { return *reinterpret_cast<const uint4*>(addr(rw, cx)); }
+    __device__ const void* addr(const Row& rw, const Ctx& cx) const {
+        if (!rw.r || cx.off < 0) return &g_zero16;
+        return rw.r + cx.off;
     }
 };
 
@@ -305,28 +318,31 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
     for (int i = 0; i < AR; ++i) arow[i] = al.prep(m0 + ((tid + i * 256) / KCH));
 #pragma unroll
     for (int i = 0; i < BR; ++i) brow[i] = bl.prep(n0 + ((tid + i * 256) / KCH));
+    const int kc = (tid % KCH) * V;  // this thread's chunk column (256 % KCH == 0: the same for every i)
     auto gload = [&](int k0) {
+        const typename AL::Ctx ax = al.ctx(k0 + kc);
+        const typename BL::Ctx bx = bl.ctx(k0 + kc);
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) ra[i] = al.load(arow[i], k0 + (c % KCH) * V);
+            if (ACH % 256 == 0 || c < ACH) ra[i] = al.load(arow[i], ax);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) rb[i] = bl.load(brow[i], k0 + (c % KCH) * V);
+            if (BCH % 256 == 0 || c < BCH) rb[i] = bl.load(brow[i], bx);
         }
     };
     auto lstore = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) *reinterpret_cast<uint4*>(&As[buf][(c / KCH) * BKP + (c % KCH) * V]) = ra[i];
+            if (ACH % 256 == 0 || c < ACH) *reinterpret_cast<uint4*>(&As[buf][(c / KCH) * BKP + (c % KCH) * V]) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) *reinterpret_cast<uint4*>(&Bs[buf][(c / KCH) * BKP + (c % KCH) * V]) = rb[i];
+            if (BCH % 256 == 0 || c < BCH) *reinterpret_cast<uint4*>(&Bs[buf][(c / KCH) * BKP + (c % KCH) * V]) = rb[i];
         }
     };
 
@@ -508,10 +524,12 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
     auto issue = [&](int slot, int k0) {
         char* sb = smem + slot * STG;
         const int k = k0 + lchunk * V;
+        const typename AL::Ctx ax = al.ctx(k);
+        const typename BL::Ctx bx = bl.ctx(k);
 #pragma unroll
-        for (int i = 0; i < AIW; ++i) glds16(al.addr(arow[i], k), sb + (wave * AIW + i) * 1024);
+        for (int i = 0; i < AIW; ++i) glds16(al.addr(arow[i], ax), sb + (wave * AIW + i) * 1024);
 #pragma unroll
-        for (int i = 0; i < BIW; ++i) glds16(bl.addr(brow[i], k), sb + ASZ + (wave * BIW + i) * 1024);
+        for (int i = 0; i < BIW; ++i) glds16(bl.addr(brow[i], bx), sb + ASZ + (wave * BIW + i) * 1024);
     };
 
 #pragma unroll

@@ -5,7 +5,10 @@ tests/golden/make_golden.py) on the golden fixture cases, from identical weights
 Tolerances (fp32, per step from shared state — SURVEY §0.6):
   * mu, logvar, reconstructions, ELBO terms: relative error <= 1e-4 (north_star), typically ~1e-6.
   * parameter gradients: relative L2 error vs a float64 run of the oracle <= max(1e-3, 8 x the fp32 oracle's
-    own error) per tensor (sum-reduced losses leave a few gradients ill-conditioned in any fp32 order);
+    own error) per tensor (sum-reduced losses leave a few gradients ill-conditioned in any fp32 order), plus
+    a kink envelope: pre-activations within ~8 fp32 ulps of a (Leaky)ReLU kink (|z| <= 1e-6 max|z|; several
+    per layer at these sizes) have a rounding-decided derivative, so the allowance adds 1.5 x the change a
+    float64 run shows when those derivatives are flipped;
     conv biases that feed train-mode BatchNorm
     have a mathematically-zero gradient (pure rounding noise) and are checked absolutely against the
     scale of their layer's weight gradient.
@@ -109,12 +112,51 @@ def simple_masks(case, B, seed=5):
     return masks, flat
 
 
+KINK_REL = 1e-6  # |z| <= KINK_REL * max|z| of its layer: within ~8 fp32 ulps of a (Leaky)ReLU kink
+
+
+def _act_modules(model):
+    return [m for m in model.modules() if isinstance(m, (torch.nn.LeakyReLU, torch.nn.ReLU))]
+
+
+def oracle64_with_kink_envelope(case, ora, ins, eps, masks):
+    """float64 oracle step, plus a second float64 step with the activation derivative flipped at every
+    pre-activation within rounding distance of the kink (where an fp32 implementation's derivative is
+    decided by rounding, e.g. |z| = 7e-8 max|z|).  Returns (model64, model64_flipped)."""
+    base = copy.deepcopy(ora).double()
+    flip = copy.deepcopy(ora).double()
+    zs = {}
+    hooks = []
+    for i, m in enumerate(_act_modules(base)):
+        hooks.append(m.register_forward_hook(lambda mod, inp, out, i=i: zs.__setitem__(i, inp[0].detach())))
+    run_oracle_step(case, base, [t.double() for t in ins], eps.double(), masks)
+    for h in hooks:
+        h.remove()
+    for i, m in enumerate(_act_modules(flip)):
+        z = zs.get(i)
+        if z is None:
+            continue
+        amb = z.abs() <= KINK_REL * z.abs().max()
+        if not bool(amb.any()):
+            continue
+        slope = getattr(m, "negative_slope", 0.0)
+        other = torch.where(z > 0, torch.full_like(z, slope), torch.ones_like(z))
+
+        def bhook(mod, gin, gout, amb=amb, other=other):
+            g = gin[0].clone()
+            g[amb] = gout[0][amb] * other[amb]
+            return (g,)
+        m.register_full_backward_hook(bhook)
+    run_oracle_step(case, flip, [t.double() for t in ins], eps.double(), masks)
+    return base, flip
+
+
 def compare_step(case, ora, ours, tol_out=1e-4, tol_grad=1e-3):
     ins, eps = FX.inputs_fn(case)(0)
     masks, flat = (simple_masks(case, case["B"]) if case["kind"] == "simple" else (None, None))
-    # float64 run of the same oracle: the exact-arithmetic yardstick for the gradient check
-    ora64 = copy.deepcopy(ora).double()
-    run_oracle_step(case, ora64, [t.double() for t in ins], eps.double(), masks)
+    # float64 runs of the same oracle: the exact-arithmetic yardstick for the gradient check, and its
+    # kink envelope (derivatives flipped where fp32 rounding decides the side of a (Leaky)ReLU kink)
+    ora64, ora64f = oracle64_with_kink_envelope(case, ora, ins, eps, masks)
     o_out, o_loss = run_oracle_step(case, ora, ins, eps, masks)
     m_out, m_loss = run_ours_step(case, ours, ins, eps, flat)
     for i, (a, b) in enumerate(zip(m_out, o_out)):
@@ -126,6 +168,7 @@ def compare_step(case, ora, ours, tol_out=1e-4, tol_grad=1e-3):
             assert abs(float(a) - float(b)) <= tol_out * abs(float(b)) + 1e-6, f"loss {i}: {float(a)} vs {float(b)}"
     onames = dict(ora.named_parameters())
     o64 = dict(ora64.named_parameters())
+    o64f = dict(ora64f.named_parameters())
     mparams = dict(ours.named_parameters())
     for name, po in onames.items():
         gm, go = mparams[name].grad, po.grad
@@ -136,10 +179,12 @@ def compare_step(case, ora, ours, tol_out=1e-4, tol_grad=1e-3):
             assert float((gm.cpu() - go).abs().max()) <= 1e-4 * scale + 1e-6, name
         else:
             # as accurate as the reference's own fp32 computation: error vs the float64 gradient within
-            # max(tol_grad, 8 x the fp32 oracle's error) (sum-reduced losses make some gradients ill-conditioned)
+            # max(tol_grad, 8 x the fp32 oracle's error) (sum-reduced losses make some gradients ill-conditioned),
+            # plus the kink envelope (1.5 x the change from flipping the rounding-decided derivatives)
             g64 = o64[name].grad
-            e_ref, e_ours = rel(go, g64), rel(gm, g64)
-            assert e_ours <= max(tol_grad, 8 * e_ref), f"grad {name}: {e_ours:.3e} vs fp32 oracle {e_ref:.3e}"
+            e_ref, e_ours, e_kink = rel(go, g64), rel(gm, g64), rel(o64f[name].grad, g64)
+            assert e_ours <= max(tol_grad, 8 * e_ref) + 1.5 * e_kink, \
+                f"grad {name}: {e_ours:.3e} vs fp32 oracle {e_ref:.3e}, kink envelope {e_kink:.3e}"
     for (n, bo), (_, bm) in zip(ora.named_buffers(), ours.named_buffers()):
         if bo.dtype.is_floating_point:
             assert rel(bm, bo) < tol_out, f"buffer {n}: {rel(bm, bo)}"

@@ -109,7 +109,8 @@ def test_wgrad_s2_convT(cuda, ws, dt):
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 @pytest.mark.parametrize("M,K,N,ldx,act,acc", [(4, 768, 256, 768, 0, 0), (256, 2048, 1024, 2048, 0, 0),
                                               (5, 370, 128, 376, 1, 0), (256, 2314, 64, 2320, 0, 1),
-                                              (33, 128, 1152, 136, 1, 0), (256, 74, 2304, 80, 0, 0)])
+                                              (33, 128, 1152, 136, 1, 0), (256, 74, 2304, 80, 0, 0),
+                                              (2, 1024, 16384, 1152, 0, 0), (2, 1024, 16384, 1152, 0, 1)])
 def test_linear(cuda, ws, dt, M, K, N, ldx, act, acc):
     code, tdt, tol = DT[dt]
     g = torch.Generator().manual_seed(M + K + N)

@@ -12,6 +12,7 @@ N > 1 is launched by torch.distributed.run (one process per GPU); rank 0 prints 
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -66,55 +67,55 @@ class MelStage:
         return self.audio
 
 
-def conv_layers(batch, hw=(128, 128)):
-    """(name, M, N, K) of every MFMA implicit-GEMM launch family in one train step (encoder + decoder)."""
-    enc = (1, 32, 64, 128, 256, 512, 512)
-    dec = (512, 512, 256, 128, 64, 32, 1)
-    H, W = hw
-    out = []
-    h, w = H, W
-    for l in range(6):
-        h, w = h // 2, w // 2
-        if l > 0:
-            out.append((f"enc{l}_fwd", batch * h * w, enc[l + 1], 9 * enc[l], ("conv_s2", batch, 2 * h, 2 * w,
-                                                                               enc[l], enc[l + 1])))
-    h, w = H // 64, W // 64
-    for l in range(5):
-        # 4 sub-pixel phases with 1/2/2/4 taps: K summed over phases = 9 * Ci per low-res position
-        out.append((f"dec{l}_fwd", batch * h * w, dec[l + 1], 9 * dec[l], ("subpixel", batch, h, w, dec[l], dec[l + 1])))
-        h, w = 2 * h, 2 * w
-    return out
+# Op kinds of the live kernel probe (include/hlmc.h hlmc_probe_arm) and the kernel each one launches
+PROBE_KINDS = {
+    1: ("conv_s2", "gemm_nt ConvS2Loader (conv fwd / convT dgrad)", "mfma"),
+    2: ("subpixel", "gemm_nt SubpixelLoader (convT fwd / conv dgrad)", "mfma"),
+    4: ("wgrad_s2", "gemm_tn KRowConvS2 (conv / convT weight gradient)", "mfma"),
+    8: ("linear", "gemm_nt DenseLoader (Linear fwd / dgrad)", "mfma"),
+    16: ("linear_wgrad", "gemm_tn KRowDense (Linear weight gradient)", "mfma"),
+    32: ("stft_mel", "stft_mel_kernel (STFT + mel)", "hbm"),
+}
 
 
-def time_op(spec, device, reps=20):
-    """Average duration (ms) of one launch of an op-level kernel, HIP events on the launch stream."""
-    kind, B, Hi, Wi, Ci, Co = spec
-    ws_bytes = 512 << 20
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
-    x = torch.randn(B, Hi, Wi, Ci, device=device).to(torch.bfloat16)
-    wp = (torch.randn(Co, 3, 3, Ci, device=device) * 0.05).to(torch.bfloat16)
-    bias = torch.zeros(Co, device=device)
-    if kind == "conv_s2":
-        y = torch.empty(B, Hi // 2, Wi // 2, Co, device=device, dtype=torch.bfloat16)
-        fn = lambda: L.lib().hlmc_op_conv_s2(L.stream(), L.HLMC_BF16, x.data_ptr(), B, Hi, Wi, Ci, wp.data_ptr(),  # noqa
-                                              bias.data_ptr(), Co, y.data_ptr(), ws.data_ptr(), ws_bytes)
+def probe_read(cap=4096):
+    n = L.c_int()
+    tot, fl, by = L.c_f64(), L.c_f64(), L.c_f64()
+    each = (L.c_f32 * cap)()
+    L.check(L.lib().hlmc_probe_read(C.byref(n), C.byref(tot), C.byref(fl), C.byref(by), each, cap), "hlmc_probe_read")
+    return {"launches": n.value, "ms": tot.value, "flops": fl.value, "bytes": by.value,
+            "each_ms": list(each)[: min(n.value, cap)]}
+
+
+def kind_roofline(kind, st):
+    """Achieved rate of one probed kernel kind: algorithmic work per launch / its average launch duration."""
+    name, kernel, bound = PROBE_KINDS[kind]
+    n = max(1, st["launches"])
+    avg_s = st["ms"] / n * 1e-3
+    if bound == "mfma":
+        ach = st["flops"] / n / avg_s / 1e12
+        peak, unit = PEAK_BF16_TFLOPS, "TFLOP/s"
     else:
-        y = torch.empty(B, 2 * Hi, 2 * Wi, Co, device=device, dtype=torch.bfloat16)
-        fn = lambda: L.lib().hlmc_op_subpixel(L.stream(), L.HLMC_BF16, x.data_ptr(), B, Hi, Wi, Ci, wp.data_ptr(),  # noqa
-                                               bias.data_ptr(), Co, y.data_ptr(), ws.data_ptr(), ws_bytes)
-    for _ in range(3):
-        L.check(fn())
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / reps
+        ach = st["bytes"] / n / avg_s / 1e9
+        peak, unit = PEAK_HBM_GBS, "GB/s"
+    return {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+            "kernel": kernel, "op": name, "launches": st["launches"], "avg_us_per_launch": round(avg_s * 1e6, 2),
+            "flops_per_launch": st["flops"] / n, "bytes_per_launch": st["bytes"] / n}
 
 
-def cpu_baseline(batch=64, steps=3):
+def pmc_traffic(kind):
+    """HBM bytes per launch of this kind from the committed rocprofv3 PMC summary (scripts/pmc_traffic.py:
+    2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes, per the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["kinds"][PROBE_KINDS[kind][0]]["hbm_bytes_per_launch"], d.get("source")
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def cpu_baseline(batch=256, steps=5):
     """Oracle (torch-CPU restatement of the reference model + numpy restatement of librosa) on host cores."""
     from multiprocessing import Pool
 
@@ -189,6 +190,20 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    breakdown, dominant = {}, None
+    if not args.no_roofline:
+        # untimed calibration: kernel time per step of every probed kind (one extra step each); the kind with
+        # the most time is the dominant kernel whose launches are then timed live inside the timed region
+        for kind in PROBE_KINDS:
+            L.check(L.lib().hlmc_probe_arm(kind, 256), "hlmc_probe_arm")
+            step()
+            st = probe_read()
+            if st["launches"]:
+                r = kind_roofline(kind, st)
+                breakdown[r["op"]] = {"us_per_step": round(st["ms"] * 1e3, 1), "launches_per_step": st["launches"],
+                                      "achieved": r["achieved"], "unit": r["unit"], "frac": r["frac"]}
+        dominant = max(PROBE_KINDS, key=lambda k: breakdown.get(PROBE_KINDS[k][0], {}).get("us_per_step", 0.0))
+        L.check(L.lib().hlmc_probe_arm(dominant, 64 * args.steps), "hlmc_probe_arm")
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
@@ -198,6 +213,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    live = probe_read() if not args.no_roofline else None
     if dist:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -221,16 +237,15 @@ def main():
                               p.numel() for p in model.parameters()), "parallelism": f"dp{world}",
                           "final_loss": round(loss, 3),
                           "step_mfma_frac": round(value / world * flops_clip / 1e12 / PEAK_BF16_TFLOPS, 4)}}
-        if not args.no_roofline:
-            # dominant MFMA kernel family: the stride-2 conv GEMM with the most FLOPs per launch
-            layers = conv_layers(B)
-            name, M, N, K, spec = max(layers, key=lambda t: t[1] * t[2] * t[3])
-            ms_k = time_op(spec, device)
-            flops = 2.0 * M * N * K
-            ach = flops / (ms_k * 1e-3) / 1e12
-            rec["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                               "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                               "kernel": f"gemm_nt_kernel {name} M={M} N={N} K={K} (bf16, avg {ms_k * 1e3:.1f} us/launch)"}
+        if live is not None:
+            roof = kind_roofline(dominant, live)
+            traffic, src = pmc_traffic(dominant)
+            roof["traffic"] = traffic
+            roof["traffic_source"] = src
+            roof["timing"] = (f"HIP events around each launch on its stream, inside the timed region "
+                              f"({live['launches']} launches over {args.steps} steps)")
+            roof["per_kind_untimed"] = breakdown  # concurrent streams: kernel times overlap
+            rec["roofline"] = roof
         if not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline()
         print(json.dumps(rec), flush=True)

@@ -52,6 +52,12 @@ _SIGS = {
     "hlmc_net_backward": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hlmc_net_adam_step": (c_int, [c_vp, c_vp, P_vp, P_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_int]),
     "hlmc_net_set_trust_packs": (c_int, [c_vp, c_int]),
+    "hlmc_net_grad_buckets": (c_int, [c_vp, C.POINTER(c_int), c_int]),
+    "hlmc_net_set_bucket_sync": (c_int, [c_vp, c_int]),
+    "hlmc_net_bucket_wait": (c_int, [c_vp, c_int, c_vp]),
+    "hlmc_probe_arm": (c_int, [c_int, c_int]),
+    "hlmc_probe_read": (c_int, [C.POINTER(c_int), C.POINTER(c_f64), C.POINTER(c_f64), C.POINTER(c_f64),
+                                C.POINTER(c_f32), c_int]),
     "hlmc_loss_workspace": (c_i64, [c_i64, c_i64, c_i64]),
     "hlmc_loss_sums": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hlmc_loss_backward": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,

@@ -13,6 +13,24 @@ static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 const char* get_error() { return g_err.c_str(); }
 
+namespace probe {
+int g_mask = 0;
+Site g_site{0, 0.0, 0.0};
+static std::vector<hipEvent_t> g_ev;  // start/stop pairs
+static int g_cap = 0, g_n = 0;
+static double g_flops = 0.0, g_bytes = 0.0;
+void begin(hipStream_t s) {
+    if (g_n < g_cap) (void)hipEventRecord(g_ev[2 * g_n], s);
+}
+void end(hipStream_t s) {
+    if (g_n >= g_cap) return;
+    (void)hipEventRecord(g_ev[2 * g_n + 1], s);
+    g_flops += g_site.flops;
+    g_bytes += g_site.bytes;
+    ++g_n;
+}
+}  // namespace probe
+
 
 
 }  // namespace hlmc
@@ -33,6 +51,38 @@ struct hlmc_net {
 extern "C" {
 
 int hlmc_version(void) { return 1; }
+
+int hlmc_probe_arm(int mask, int max_launches) {
+    HLMC_CHECK_ARG(mask >= 0 && max_launches >= 0, "bad arguments");
+    const size_t need = 2 * (size_t)max_launches;
+    while (probe::g_ev.size() < need) {
+        hipEvent_t e;
+        HLMC_HIP(hipEventCreate(&e));
+        probe::g_ev.push_back(e);
+    }
+    probe::g_cap = max_launches;
+    probe::g_n = 0;
+    probe::g_flops = probe::g_bytes = 0.0;
+    probe::g_mask = max_launches > 0 ? mask : 0;
+    return HLMC_OK;
+}
+int hlmc_probe_read(int* launches, double* total_ms, double* flops, double* bytes, float* ms_each, int cap_each) {
+    HLMC_CHECK_ARG(launches && total_ms && flops && bytes, "NULL argument");
+    double tot = 0.0;
+    for (int i = 0; i < probe::g_n; ++i) {
+        float ms = 0.f;
+        HLMC_HIP(hipEventSynchronize(probe::g_ev[2 * i + 1]));
+        HLMC_HIP(hipEventElapsedTime(&ms, probe::g_ev[2 * i], probe::g_ev[2 * i + 1]));
+        if (ms_each && i < cap_each) ms_each[i] = ms;
+        tot += ms;
+    }
+    *launches = probe::g_n;
+    *total_ms = tot;
+    *flops = probe::g_flops;
+    *bytes = probe::g_bytes;
+    probe::g_mask = 0;
+    return HLMC_OK;
+}
 const char* hlmc_last_error(void) { return get_error(); }
 
 // ------------------------------------------------------------------------------------ features
@@ -193,6 +243,25 @@ int hlmc_net_set_trust_packs(hlmc_net* h, int trust) {
     HLMC_CHECK_ARG(h, "net is NULL");
     h->impl->trust_packs = trust != 0;
     if (!trust) h->impl->packs_valid = false;
+    return HLMC_OK;
+}
+int hlmc_net_grad_buckets(const hlmc_net* h, int* starts, int cap) {
+    HLMC_CHECK_ARG(h && starts && cap > 0, "NULL argument");
+    const auto& b = h->impl->bucket_starts;
+    for (int k = 0; k < (int)b.size() && k < cap; ++k) starts[k] = b[k];
+    return (int)b.size();
+}
+int hlmc_net_set_bucket_sync(hlmc_net* h, int enable) {
+    HLMC_CHECK_ARG(h, "net is NULL");
+    h->impl->bucket_sync = enable != 0;
+    return HLMC_OK;
+}
+int hlmc_net_bucket_wait(hlmc_net* h, int k, void* stream) {
+    HLMC_CHECK_ARG(h, "net is NULL");
+    auto& ev = h->impl->bucket_ev;
+    HLMC_CHECK_ARG(h->impl->bucket_sync && k >= 0 && k < (int)ev.size() && ev[k],
+                   "bucket events not recorded (hlmc_net_set_bucket_sync + hlmc_net_backward first)");
+    HLMC_HIP(hipStreamWaitEvent(S(stream), ev[k], 0));
     return HLMC_OK;
 }
 

@@ -52,6 +52,27 @@ const char* get_error();
         if (s__ != HLMC_OK) return s__;                                    \
     } while (0)
 
+// ------------------------------------------------------------------ live kernel timing (bench.py roofline)
+// An op sets the site (its kind and ALGORITHMIC flops / HBM bytes) before its launcher runs; when the kind is
+// in the armed mask (hlmc_probe_arm) the launcher brackets its main kernel with a HIP event pair on the launch
+// stream.  Off (mask 0) it costs one branch per launch.
+namespace probe {
+enum : int { kConvS2 = 1, kSubpixel = 2, kWgradS2 = 4, kLinear = 8, kLinearWgrad = 16, kStftMel = 32 };
+struct Site {
+    int kind;
+    double flops, bytes;
+};
+extern int g_mask;
+extern Site g_site;
+void begin(hipStream_t s);
+void end(hipStream_t s);
+inline void site(int kind, double flops, double bytes) { g_site = Site{kind, flops, bytes}; }
+}  // namespace probe
+#define HLMC_PROBE_BEGIN(s) \
+    do { if (::hlmc::probe::g_mask & ::hlmc::probe::g_site.kind) ::hlmc::probe::begin(s); } while (0)
+#define HLMC_PROBE_END(s) \
+    do { if (::hlmc::probe::g_mask & ::hlmc::probe::g_site.kind) ::hlmc::probe::end(s); ::hlmc::probe::g_site.kind = 0; } while (0)
+
 // ------------------------------------------------------------------ scalar conversions
 template <typename T> __device__ __forceinline__ float to_f32(T v);
 template <> __device__ __forceinline__ float to_f32<float>(float v) { return v; }

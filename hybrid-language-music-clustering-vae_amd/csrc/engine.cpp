@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 namespace hlmc {
 namespace {
@@ -120,7 +121,8 @@ class NetT : public NetBase {
     // ---------------------------------------------------------------- workspace
     char* ws = nullptr;
     Ws scratch{nullptr, 0};
-    size_t scratch_off = 0, scratch_bytes = 0;
+    Ws scratch2{nullptr, 0};  // split-K / reduction scratch of the weight-gradient stream
+    size_t scratch_off = 0, scratch2_off = 0, scratch_bytes = 0;
     int64_t planned_B = -1;
     size_t ws_total = 0;
 
@@ -137,6 +139,7 @@ class NetT : public NetBase {
             scratch_bytes = 0;
             plan(A, B);
             scratch_off = A.take(scratch_bytes + 256);
+            scratch2_off = A.take(scratch_bytes + 256);
             ws_total = A.used;
             planned_B = B;
         }
@@ -145,6 +148,79 @@ class NetT : public NetBase {
     void set_ws(void* w) {
         ws = reinterpret_cast<char*>(w);
         scratch = Ws{reinterpret_cast<float*>(ws + scratch_off), scratch_bytes + 256};
+        scratch2 = Ws{reinterpret_cast<float*>(ws + scratch2_off), scratch_bytes + 256};
+    }
+
+    // ---------------------------------------------------------------- weight-gradient stream
+    // Weight and bias gradients have no consumer before Adam.  backward() forks them onto a second stream
+    // (own split-K scratch) right after the data gradient they read is written, so the critical path stays
+    // dgrad -> BN-backward -> dgrad and the wgrad GEMMs / reduces fill the CUs it leaves idle.  Every buffer
+    // a forked op reads is written once per backward; backward() joins the stream before returning.
+    // HLMC_SIDE_STREAM=0 keeps everything on the caller's stream (A/B measurement aid).
+    hipStream_t s2 = nullptr;
+    std::vector<hipEvent_t> evs;
+    int ev_next = 0;
+    bool use_side = true;
+    ~NetT() override {
+        if (s2) (void)hipStreamDestroy(s2);
+        for (auto e : evs) (void)hipEventDestroy(e);
+        for (auto e : this->bucket_ev) (void)hipEventDestroy(e);
+    }
+    int side_init() {
+        static const bool env_off = [] {
+            const char* e = std::getenv("HLMC_SIDE_STREAM");
+            return e && e[0] == '0';
+        }();
+        use_side = !env_off;
+        if (use_side && !s2) {
+            HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+            evs.resize(32);
+            for (auto& e : evs) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        if (this->bucket_sync && this->bucket_ev.size() != this->bucket_starts.size()) {
+            for (auto e : this->bucket_ev) (void)hipEventDestroy(e);
+            this->bucket_ev.assign(this->bucket_starts.size(), nullptr);
+            for (auto& e : this->bucket_ev) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        return HLMC_OK;
+    }
+    hipEvent_t next_ev() {
+        hipEvent_t e = evs[ev_next];
+        ev_next = (ev_next + 1) % (int)evs.size();
+        return e;
+    }
+    // the weight-gradient stream continues after everything issued so far on s
+    int fork(hipStream_t s) {
+        hipEvent_t e = next_ev();
+        HLMC_HIP(hipEventRecord(e, s));
+        HLMC_HIP(hipStreamWaitEvent(s2, e, 0));
+        return HLMC_OK;
+    }
+    int join(hipStream_t s) {
+        if (!use_side) return HLMC_OK;
+        hipEvent_t e = next_ev();
+        HLMC_HIP(hipEventRecord(e, s2));
+        HLMC_HIP(hipStreamWaitEvent(s, e, 0));
+        return HLMC_OK;
+    }
+    // run f(stream, scratch) on the weight-gradient stream, ordered after the work issued so far on s
+    template <class F>
+    int side(hipStream_t s, F&& f) {
+        if (!use_side) return f(s, scratch);
+        HLMC_TRY(fork(s));
+        return f(s2, scratch2);
+    }
+    // bucket k of the data-parallel all-reduce is final once both streams pass this point
+    int mark(hipStream_t s, int k) {
+        if (!this->bucket_sync) return HLMC_OK;
+        HLMC_CHECK_ARG(k >= 0 && k < (int)this->bucket_ev.size(), "bucket index");
+        if (use_side && k + 1 < (int)this->bucket_ev.size()) {
+            HLMC_TRY(fork(s));
+            HLMC_HIP(hipEventRecord(this->bucket_ev[k], s2));
+        } else {  // the last bucket: the caller has joined the weight-gradient stream
+            HLMC_HIP(hipEventRecord(this->bucket_ev[k], s));
+        }
+        return HLMC_OK;
     }
 
     // ---------------------------------------------------------------- layer helpers
@@ -161,13 +237,29 @@ class NetT : public NetBase {
         need(ops::linear_wgrad_ws<T>(B, N, K));
         need(ops::colsum_ws(B, N));
     }
-    // grads of a linear layer from dy (pre-activation grad): dW, db, and optionally dx (+=)
+    // grads of a linear layer from dy (pre-activation grad): dW, db (weight-gradient stream), optionally dx (+=)
     int lin_bwd(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int B, int w, int b, T* dx, int lddx, int acc = 0) {
         const int N = (int)params[w].shape[0], K = (int)params[w].shape[1];
-        HLMC_TRY(ops::linear_wgrad<T>(s, dy, lddy, x, ldx, B, N, K, G[w], scratch));
-        if (b >= 0) HLMC_TRY(ops::colsum<T>(s, dy, lddy, B, N, G[b], scratch));
+        float* gw = G[w];
+        float* gb = b >= 0 ? G[b] : nullptr;
+        HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) {
+            HLMC_TRY(ops::linear_wgrad<T>(q, dy, lddy, x, ldx, B, N, K, gw, sc));
+            if (gb) HLMC_TRY(ops::colsum<T>(q, dy, lddy, B, N, gb, sc));
+            return (int)HLMC_OK;
+        }));
         if (dx) HLMC_TRY(ops::linear<T, T>(s, dy, lddy, B, N, P1(w), ld1(w), nullptr, K, dx, lddx, 0, acc, scratch));
         return HLMC_OK;
+    }
+
+    // latent heads: dW = dyT^T x (dyT = T copy of the f32 grad dyF), db = column sums of dyF (weight-gradient stream)
+    int head_wgrad(hipStream_t s, const T* dyT, const float* dyF, int L, const T* x, int ldx, int B, int K, int w, int b) {
+        float* gw = G[w];
+        float* gb = G[b];
+        return side(s, [&](hipStream_t q, Ws sc) {
+            HLMC_TRY(ops::linear_wgrad<T>(q, dyT, L, x, ldx, B, L, K, gw, sc));
+            HLMC_TRY(ops::colsum<float>(q, dyF, L, B, L, gb, sc));
+            return (int)HLMC_OK;
+        });
     }
 
     struct BnBufs {
@@ -198,7 +290,7 @@ class NetT : public NetBase {
     struct Enc {
         int w[6], b[6], g[6], beta[6], bn[6];
         int H = 0, W = 0;
-        size_t y[6], a[6], audio = 0;
+        size_t y[6], a[6], dy[6], audio = 0;  // dy: grad wrt the conv output (read by the forked wgrad)
         BnBufs bb[6];
     };
     Enc enc;
@@ -231,6 +323,7 @@ class NetT : public NetBase {
             const size_t n = (size_t)B * h * w * co;
             enc.y[l] = A.take(n * sizeof(T));
             enc.a[l] = A.take(n * sizeof(T));
+            enc.dy[l] = A.take(n * sizeof(T));
             enc.bb[l] = bn_plan(A, co);
             need(ops::bn_ws(B * h * w, co));
         }
@@ -258,8 +351,9 @@ class NetT : public NetBase {
         }
         return HLMC_OK;
     }
-    // da5: grad of the last activation in gA; uses gA/gB ping-pong
-    int enc_bwd(hipStream_t s, int B, T* gA, T* gB) {
+    // gA: grad of the last activation on entry (overwritten: data-gradient chain buffer).  Bucket
+    // `bucket_hi` (layers 3..5) is marked final after layer 3 (-1: no mark).
+    int enc_bwd(hipStream_t s, int B, T* gA, int bucket_hi = -1) {
         const float* audio = AF(enc.audio);
         int hs[7], ws_[7];
         hs[0] = enc.H;
@@ -269,13 +363,17 @@ class NetT : public NetBase {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             const int ho = hs[l + 1], wo = ws_[l + 1];
             const int64_t R = (int64_t)B * ho * wo;
-            HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, gB, enc.b[l]));
+            T* dy = AT(enc.dy[l]);
+            HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l]));
+            float* gw = G[enc.w[l]];
             if (l == 0) {
-                HLMC_TRY(ops::wgrad_c1<T>(s, gB, B, ho, wo, co, audio, G[enc.w[0]], scratch));
+                HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
             } else {
-                HLMC_TRY(ops::wgrad_s2<T>(s, gB, B, ho, wo, co, AT(enc.a[l - 1]), ci, G[enc.w[l]], scratch));
-                HLMC_TRY(ops::subpixel<T>(s, gB, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));
+                const T* xin = AT(enc.a[l - 1]);
+                HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
+                HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));
             }
+            if (l == 3 && bucket_hi >= 0) HLMC_TRY(mark(s, bucket_hi));
         }
         return HLMC_OK;
     }
@@ -284,7 +382,7 @@ class NetT : public NetBase {
     struct Dec {
         int w[6], b[6], g[5], beta[5], bn[5];
         int h0 = 0, w0 = 0;  // low-res input grid (H/64, W/64)
-        size_t y[5], a[5];
+        size_t y[5], a[5], dy[5];
         BnBufs bb[5];
     };
     Dec dec;
@@ -314,6 +412,7 @@ class NetT : public NetBase {
                 const size_t n = (size_t)B * 4 * h * w * co;
                 dec.y[l] = A.take(n * sizeof(T));
                 dec.a[l] = A.take(n * sizeof(T));
+                dec.dy[l] = A.take(n * sizeof(T));
                 dec.bb[l] = bn_plan(A, co);
                 need(ops::bn_ws(B * 4 * h * w, co));
                 need(ops::col_stats_bytes(B * h * w, 4, co));
@@ -347,8 +446,8 @@ class NetT : public NetBase {
         }
         return HLMC_OK;
     }
-    // returns grad wrt u in *out (one of gA/gB)
-    int dec_bwd(hipStream_t s, const T* u, int B, const float* d_recon, T* gA, T* gB, T** out) {
+    // gA: data-gradient chain buffer; returns the grad wrt u in *out (= gA)
+    int dec_bwd(hipStream_t s, const T* u, int B, const float* d_recon, T* gA, T** out) {
         int hs[7], ws_[7];
         hs[0] = dec.h0;
         ws_[0] = dec.w0;
@@ -356,18 +455,26 @@ class NetT : public NetBase {
         // last layer (1 output channel): input a4 [B, hs5, ws5, 32]
         {
             const int hl = hs[5], wl = ws_[5];
-            HLMC_TRY(ops::wgrad_c1<T>(s, AT(dec.a[4]), B, hl, wl, DEC_CH[5], d_recon, G[dec.w[5]], scratch));
-            HLMC_TRY(ops::colsum<float>(s, d_recon, 1, B * hs[6] * ws_[6], 1, G[dec.b[5]], scratch));
+            const T* a4 = AT(dec.a[4]);
+            float* gw = G[dec.w[5]];
+            float* gb = G[dec.b[5]];
+            const int npix = B * hs[6] * ws_[6];
+            HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) {
+                HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
+                return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
+            }));
             HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA));
         }
         for (int l = 4; l >= 0; --l) {
             const int ci = DEC_CH[l], co = DEC_CH[l + 1];
             const int hl = hs[l], wl = ws_[l];
             const int64_t R = (int64_t)B * 4 * hl * wl;
-            HLMC_TRY(bn_bwd(s, gA, co, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f, gB, dec.b[l]));
+            T* dy = AT(dec.dy[l]);
+            HLMC_TRY(bn_bwd(s, gA, co, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f, dy, dec.b[l]));
             const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
-            HLMC_TRY(ops::wgrad_s2<T>(s, xin, B, hl, wl, ci, gB, co, G[dec.w[l]], scratch));
-            HLMC_TRY(ops::conv_s2<T>(s, gB, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
+            float* gw = G[dec.w[l]];
+            HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
+            HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
         }
         *out = gA;
         return HLMC_OK;
@@ -395,7 +502,7 @@ class HybridNet : public NetT<T> {
     // workspace
     size_t flat_, fuse_, tin_, te_y[2], te_a0, h_, mu_, lv_, eps_, z_, d1_, s_, ah_, u_, td_y, td_a, rt_;
     BnBufs te_bb[2], td_bb;
-    size_t gA_, gB_, gflat_, gfuse_, gh_, gz_, gd1_, gs_, gah_, gte_, gte2_, gtd_, gdmu_, gdlv_, gmuT_, glvT_, grt_;
+    size_t gA_, gflat_, gfuse_, gh_, gz_, gd1_, gs_, gah_, gte_, gte1_, gte2_, gtd_, gtd2_, gdmu_, gdlv_, gmuT_, glvT_, grt_;
     int ldF = 0, ldT = 0, ldFU = 0, ldSP = 0;
 
     HybridNet(int latent, int text_dim, int h, int w) : L(latent), TD(text_dim), H(h), W(w) {
@@ -448,6 +555,8 @@ class HybridNet : public NetT<T> {
             this->register_pack(td_w[1], 1);
         }
         this->finalize_state();
+        // backward finishes: audio + text decoder | audio_fc .. audio_decoder_fc | encoder layers 3-5 | layers 0-2
+        this->bucket_starts = {this->dec.w[0], afc_w, this->enc.w[3], 0};
     }
 
     void plan(Arena& A, int64_t B) override {
@@ -481,8 +590,10 @@ class HybridNet : public NetT<T> {
             td_bb = this->bn_plan(A, 256);
             rt_ = A.take(B * ldT * t);
             gte_ = A.take(B * 256 * t);
+            gte1_ = A.take(B * 128 * t);
             gte2_ = A.take(B * 256 * t);
             gtd_ = A.take(B * 256 * t);
+            gtd2_ = A.take(B * 256 * t);
             grt_ = A.take(B * ldT * t);
             this->need(ops::bn_ws(B, 256));
             for (int i = 0; i < 2; ++i) this->lin_need((int)B, te_w[i]);
@@ -491,7 +602,6 @@ class HybridNet : public NetT<T> {
         }
         const size_t gmax = std::max(this->enc_max_elems(B), this->dec_max_elems(B));
         gA_ = A.take(gmax * t);
-        gB_ = A.take(gmax * t);
         gflat_ = A.take(B * ldF * t);
         gfuse_ = A.take(B * ldFU * t);
         gh_ = A.take(B * 512 * t);
@@ -561,22 +671,21 @@ class HybridNet : public NetT<T> {
         const int B = (int)a.B;
         HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
         this->set_ws(a.ws);
+        HLMC_TRY(this->side_init());
         T* gA = AT(gA_);
-        T* gB = AT(gB_);
         // ---- text decoder
         if (text) {
             HLMC_CHECK_ARG(a.d_recon_text, "d_recon_text required");
             HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon_text, TD, AT(grt_), ldT, B, TD));
             HLMC_TRY(this->lin_bwd(s, AT(grt_), ldT, AT(td_a), 256, B, td_w[1], td_b[1], AT(gtd_), 256));
             HLMC_TRY(this->bn_bwd(s, AT(gtd_), 256, AT(td_y), B, 256, td_bb, td_g, td_beta, 0, nullptr, 1.f,
-                                  AT(gte2_), td_b[0]));
-            HLMC_TRY(ops::linear_wgrad<T>(s, AT(gte2_), 256, AT(s_) + 1024, ldSP, B, 256, 128, G[td_w[0]], this->scratch));
-            HLMC_TRY(ops::linear<T, T>(s, AT(gte2_), 256, B, 256, this->P1(td_w[0]), this->ld1(td_w[0]), nullptr, 128,
-                                       AT(gs_) + 1024, ldSP, 0, 0, this->scratch));
+                                  AT(gtd2_), td_b[0]));
+            HLMC_TRY(this->lin_bwd(s, AT(gtd2_), 256, AT(s_) + 1024, ldSP, B, td_w[0], -1, AT(gs_) + 1024, ldSP));
         }
         // ---- audio decoder
         T* gu = nullptr;
-        HLMC_TRY(this->dec_bwd(s, AT(u_), B, a.d_recon, gA, gB, &gu));
+        HLMC_TRY(this->dec_bwd(s, AT(u_), B, a.d_recon, gA, &gu));
+        HLMC_TRY(this->mark(s, 0));
         HLMC_TRY(ops::nhwc_to_flat<T>(s, gu, B, H / 64, W / 64, 512, AT(gah_), ldF));
         HLMC_TRY(ops::relu_bwd<T>(s, AT(gah_), ldF, AT(ah_), ldF, B, F));
         HLMC_TRY(this->lin_bwd(s, AT(gah_), ldF, AT(s_), ldSP, B, adf_w, adf_b, AT(gs_), ldSP));
@@ -590,10 +699,8 @@ class HybridNet : public NetT<T> {
         HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), L, AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
-        HLMC_TRY(ops::linear_wgrad<T>(s, AT(gmuT_), L, AT(h_), 512, B, L, 512, G[mu_w], this->scratch));
-        HLMC_TRY(ops::colsum<float>(s, AF(gdmu_), L, B, L, G[mu_b], this->scratch));
-        HLMC_TRY(ops::linear_wgrad<T>(s, AT(glvT_), L, AT(h_), 512, B, L, 512, G[lv_w], this->scratch));
-        HLMC_TRY(ops::colsum<float>(s, AF(gdlv_), L, B, L, G[lv_b], this->scratch));
+        HLMC_TRY(this->head_wgrad(s, AT(gmuT_), AF(gdmu_), L, AT(h_), 512, B, 512, mu_w, mu_b));
+        HLMC_TRY(this->head_wgrad(s, AT(glvT_), AF(gdlv_), L, AT(h_), 512, B, 512, lv_w, lv_b));
         HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, 512, AT(gh_), 512, 0, 0, this->scratch));
         HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, 512, AT(gh_), 512, 0, 1, this->scratch));
         HLMC_TRY(ops::relu_bwd<T>(s, AT(gh_), 512, AT(h_), 512, B, 512));
@@ -601,17 +708,19 @@ class HybridNet : public NetT<T> {
         // ---- text encoder
         if (text) {
             HLMC_TRY(this->bn_bwd(s, AT(gfuse_) + 1024, ldFU, AT(te_y[1]), B, 128, te_bb[1], te_g[1], te_beta[1], 0,
-                                  nullptr, 1.f, AT(gte2_), te_b[1]));
-            HLMC_TRY(this->lin_bwd(s, AT(gte2_), 128, AT(te_a0), 256, B, te_w[1], -1, AT(gte_), 256));
+                                  nullptr, 1.f, AT(gte1_), te_b[1]));
+            HLMC_TRY(this->lin_bwd(s, AT(gte1_), 128, AT(te_a0), 256, B, te_w[1], -1, AT(gte_), 256));
             HLMC_TRY(this->bn_bwd(s, AT(gte_), 256, AT(te_y[0]), B, 256, te_bb[0], te_g[0], te_beta[0], 0, nullptr, 1.f,
                                   AT(gte2_), te_b[0]));
             HLMC_TRY(this->lin_bwd(s, AT(gte2_), 256, AT(tin_), ldT, B, te_w[0], -1, nullptr, 0));
         }
         // ---- audio encoder
         HLMC_TRY(this->lin_bwd(s, AT(gfuse_), ldFU, AT(flat_), ldF, B, afc_w, afc_b, AT(gflat_), ldF));
+        HLMC_TRY(this->mark(s, 1));
         HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(gflat_), ldF, B, H / 64, W / 64, 512, gA));
-        HLMC_TRY(this->enc_bwd(s, B, gA, gB));
-        return HLMC_OK;
+        HLMC_TRY(this->enc_bwd(s, B, gA, 2));
+        HLMC_TRY(this->join(s));
+        return this->mark(s, 3);
     }
 };
 
@@ -633,7 +742,7 @@ class CvaeNet : public NetT<T> {
     int ldF = 0, ldT = 0, ldX = 0, ldZ = 0, ldS = 0;
     size_t tin_, te_y, X_, mu_, lv_, eps_, Z_, S_, u_, td_y, td_a;
     BnBufs te_bb, td_bb;
-    size_t gA_, gB_, grt_, gtd_, gt2_, gS_, gZ_, gX_, gdmu_, gdlv_, gmuT_, glvT_;
+    size_t gA_, grt_, gtd_, gt2_, gt3_, gS_, gZ_, gX_, gdmu_, gdlv_, gmuT_, glvT_;
 
     CvaeNet(int latent, int text_dim, int ncls, int h, int w) : L(latent), TD(text_dim), C(ncls), H(h), W(w) {
         F = 512 * (H / 64) * (W / 64);
@@ -664,6 +773,8 @@ class CvaeNet : public NetT<T> {
         for (int w_ : {te_w, mu_w, lv_w, dfc_w, td_w[0], td_w[1]}) this->register_pack(w_, 1);
         this->dec_register("audio_decoder", 0);
         this->finalize_state();
+        // backward finishes: text + audio decoder | text_encoder .. decoder_fc | encoder layers 3-5 | layers 0-2
+        this->bucket_starts = {td_w[0], te_w, this->enc.w[3], 0};
     }
 
     void plan(Arena& A, int64_t B) override {
@@ -690,10 +801,10 @@ class CvaeNet : public NetT<T> {
         td_bb = this->bn_plan(A, 512);
         const size_t gmax = std::max(this->enc_max_elems(B), this->dec_max_elems(B));
         gA_ = A.take(gmax * t);
-        gB_ = A.take(gmax * t);
         grt_ = A.take(B * ldT * t);
         gtd_ = A.take(B * 512 * t);
         gt2_ = A.take(B * 512 * t);
+        gt3_ = A.take(B * 256 * t);
         gS_ = A.take(B * ldS * t);
         gZ_ = A.take(B * ldZ * t);
         gX_ = A.take(B * ldX * t);
@@ -748,8 +859,8 @@ class CvaeNet : public NetT<T> {
         HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
         HLMC_CHECK_ARG(a.d_recon_text, "d_recon_text required");
         this->set_ws(a.ws);
+        HLMC_TRY(this->side_init());
         T* gA = AT(gA_);
-        T* gB = AT(gB_);
         // text decoder
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon_text, TD, AT(grt_), ldT, B, TD));
         HLMC_TRY(this->lin_bwd(s, AT(grt_), ldT, AT(td_a), 512, B, td_w[1], td_b[1], AT(gtd_), 512));
@@ -757,7 +868,8 @@ class CvaeNet : public NetT<T> {
         HLMC_TRY(this->lin_bwd(s, AT(gt2_), 512, AT(S_) + F, ldS, B, td_w[0], -1, AT(gS_) + F, ldS));
         // audio decoder
         T* gu = nullptr;
-        HLMC_TRY(this->dec_bwd(s, AT(u_), B, a.d_recon, gA, gB, &gu));
+        HLMC_TRY(this->dec_bwd(s, AT(u_), B, a.d_recon, gA, &gu));
+        HLMC_TRY(this->mark(s, 0));
         HLMC_TRY(ops::nhwc_to_flat<T>(s, gu, B, H / 64, W / 64, 512, AT(gS_), ldS));
         // decoder_fc (no activation)
         HLMC_TRY(this->lin_bwd(s, AT(gS_), ldS, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(gZ_), ldZ));
@@ -768,19 +880,19 @@ class CvaeNet : public NetT<T> {
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
         const int K = F + 256 + C;
-        HLMC_TRY(ops::linear_wgrad<T>(s, AT(gmuT_), L, AT(X_), ldX, B, L, K, G[mu_w], this->scratch));
-        HLMC_TRY(ops::colsum<float>(s, AF(gdmu_), L, B, L, G[mu_b], this->scratch));
-        HLMC_TRY(ops::linear_wgrad<T>(s, AT(glvT_), L, AT(X_), ldX, B, L, K, G[lv_w], this->scratch));
-        HLMC_TRY(ops::colsum<float>(s, AF(gdlv_), L, B, L, G[lv_b], this->scratch));
+        HLMC_TRY(this->head_wgrad(s, AT(gmuT_), AF(gdmu_), L, AT(X_), ldX, B, K, mu_w, mu_b));
+        HLMC_TRY(this->head_wgrad(s, AT(glvT_), AF(gdlv_), L, AT(X_), ldX, B, K, lv_w, lv_b));
         HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, K, AT(gX_), ldX, 0, 0, this->scratch));
         HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, K, AT(gX_), ldX, 0, 1, this->scratch));
         // text encoder
-        HLMC_TRY(this->bn_bwd(s, AT(gX_) + F, ldX, AT(te_y), B, 256, te_bb, te_g, te_beta, 0, nullptr, 1.f, AT(gt2_), te_b));
-        HLMC_TRY(this->lin_bwd(s, AT(gt2_), 256, AT(tin_), ldT, B, te_w, -1, nullptr, 0));
+        HLMC_TRY(this->bn_bwd(s, AT(gX_) + F, ldX, AT(te_y), B, 256, te_bb, te_g, te_beta, 0, nullptr, 1.f, AT(gt3_), te_b));
+        HLMC_TRY(this->lin_bwd(s, AT(gt3_), 256, AT(tin_), ldT, B, te_w, -1, nullptr, 0));
+        HLMC_TRY(this->mark(s, 1));
         // audio encoder
         HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(gX_), ldX, B, H / 64, W / 64, 512, gA));
-        HLMC_TRY(this->enc_bwd(s, B, gA, gB));
-        return HLMC_OK;
+        HLMC_TRY(this->enc_bwd(s, B, gA, 2));
+        HLMC_TRY(this->join(s));
+        return this->mark(s, 3);
     }
 };
 
@@ -800,14 +912,14 @@ class SimpleNet : public NetT<T> {
     std::vector<int> hid;
     struct Blk {
         int w, b, g, beta, bn, din, dout;
-        size_t y, a;
+        size_t y, a, dy;
         BnBufs bb;
         int64_t mask_off;
     };
     std::vector<Blk> encb, decb;
     int mu_w, mu_b, lv_w, lv_b, out_w, out_b;
     int ldD = 0;
-    size_t x_, mu_, lv_, eps_, z_, gx1_, gx2_, gdmu_, gdlv_, gmuT_, glvT_, gz_, grec_, mask_;
+    size_t x_, mu_, lv_, eps_, z_, gx1_, gdmu_, gdlv_, gmuT_, glvT_, gz_, grec_, mask_;
     int64_t mask_total = 0;
 
     SimpleNet(int input_dim, int latent, std::vector<int> hidden) : D(input_dim), L(latent), hid(std::move(hidden)) {
@@ -865,6 +977,7 @@ class SimpleNet : public NetT<T> {
             for (auto& b : *v) {
                 b.y = A.take(B * b.dout * t);
                 b.a = A.take(B * b.dout * t);
+                b.dy = A.take(B * b.dout * t);
                 b.bb = this->bn_plan(A, b.dout);
                 b.mask_off = moff;
                 moff += B * b.dout;
@@ -879,7 +992,6 @@ class SimpleNet : public NetT<T> {
         eps_ = A.take(B * L * 4);
         z_ = A.take(B * pad8(L) * t);
         gx1_ = A.take(B * widest * t);
-        gx2_ = A.take(B * widest * t);
         gdmu_ = A.take(B * L * 4);
         gdlv_ = A.take(B * L * 4);
         gmuT_ = A.take(B * L * t);
@@ -946,19 +1058,20 @@ class SimpleNet : public NetT<T> {
         const int B = (int)a.B;
         HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
         this->set_ws(a.ws);
+        HLMC_TRY(this->side_init());
         T* g1 = AT(gx1_);
-        T* g2 = AT(gx2_);
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon, D, AT(grec_), ldD, B, D));
         const Blk& last = decb.back();
         HLMC_TRY(this->lin_bwd(s, AT(grec_), ldD, AT(last.a), last.dout, B, out_w, out_b, g1, last.dout));
         for (int i = (int)decb.size() - 1; i >= 0; --i) {
             const Blk& b = decb[i];
-            HLMC_TRY(this->bn_bwd(s, g1, b.dout, AT(b.y), B, b.dout, b.bb, b.g, b.beta, 1, mask_of(b), kKeepScale, g2, b.b));
+            T* dy = AT(b.dy);
+            HLMC_TRY(this->bn_bwd(s, g1, b.dout, AT(b.y), B, b.dout, b.bb, b.g, b.beta, 1, mask_of(b), kKeepScale, dy, b.b));
             const T* xin = i == 0 ? AT(z_) : AT(decb[i - 1].a);
             const int ldx = i == 0 ? pad8(L) : decb[i - 1].dout;
             T* gin = i == 0 ? AT(gz_) : g1;
             const int ldg = i == 0 ? pad8(L) : b.din;
-            HLMC_TRY(this->lin_bwd(s, g2, b.dout, xin, ldx, B, b.w, -1, gin, ldg));
+            HLMC_TRY(this->lin_bwd(s, dy, b.dout, xin, ldx, B, b.w, -1, gin, ldg));
         }
         HLMC_HIP(hipMemcpyAsync(AF(gdmu_), a.d_mu, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
         HLMC_HIP(hipMemcpyAsync(AF(gdlv_), a.d_logvar, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
@@ -966,20 +1079,20 @@ class SimpleNet : public NetT<T> {
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
         const Blk& top = encb.back();
-        HLMC_TRY(ops::linear_wgrad<T>(s, AT(gmuT_), L, AT(top.a), top.dout, B, L, top.dout, G[mu_w], this->scratch));
-        HLMC_TRY(ops::colsum<float>(s, AF(gdmu_), L, B, L, G[mu_b], this->scratch));
-        HLMC_TRY(ops::linear_wgrad<T>(s, AT(glvT_), L, AT(top.a), top.dout, B, L, top.dout, G[lv_w], this->scratch));
-        HLMC_TRY(ops::colsum<float>(s, AF(gdlv_), L, B, L, G[lv_b], this->scratch));
+        HLMC_TRY(this->head_wgrad(s, AT(gmuT_), AF(gdmu_), L, AT(top.a), top.dout, B, top.dout, mu_w, mu_b));
+        HLMC_TRY(this->head_wgrad(s, AT(glvT_), AF(gdlv_), L, AT(top.a), top.dout, B, top.dout, lv_w, lv_b));
         HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, top.dout, g1, top.dout, 0, 0, this->scratch));
         HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, top.dout, g1, top.dout, 0, 1, this->scratch));
         for (int i = (int)encb.size() - 1; i >= 0; --i) {
             const Blk& b = encb[i];
-            HLMC_TRY(this->bn_bwd(s, g1, b.dout, AT(b.y), B, b.dout, b.bb, b.g, b.beta, 1, mask_of(b), kKeepScale, g2, b.b));
+            T* dy = AT(b.dy);
+            HLMC_TRY(this->bn_bwd(s, g1, b.dout, AT(b.y), B, b.dout, b.bb, b.g, b.beta, 1, mask_of(b), kKeepScale, dy, b.b));
             const T* xin = i == 0 ? AT(x_) : AT(encb[i - 1].a);
             const int ldx = i == 0 ? ldD : encb[i - 1].dout;
-            HLMC_TRY(this->lin_bwd(s, g2, b.dout, xin, ldx, B, b.w, -1, i == 0 ? nullptr : g1, b.din));
+            HLMC_TRY(this->lin_bwd(s, dy, b.dout, xin, ldx, B, b.w, -1, i == 0 ? nullptr : g1, b.din));
         }
-        return HLMC_OK;
+        HLMC_TRY(this->join(s));
+        return this->mark(s, 0);
     }
 };
 

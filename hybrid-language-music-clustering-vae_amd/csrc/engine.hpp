@@ -81,6 +81,14 @@ class NetBase {
     virtual int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a) = 0;
     bool trust_packs = false;  // forward skips re-packing when packs are known current
     bool packs_valid = false;
+
+    // Gradient buckets of the data-parallel all-reduce, in the order backward() finishes them:
+    // bucket k = params[bucket_starts[k] .. bucket_starts[k-1]) (bucket_starts[-1] = params.size();
+    // strictly decreasing, last = 0).  With bucket_sync set, backward() records bucket_ev[k] once every
+    // gradient of bucket k is written (on any stream), so an all-reduce can start before backward ends.
+    std::vector<int> bucket_starts{0};
+    std::vector<hipEvent_t> bucket_ev;
+    bool bucket_sync = false;
 };
 
 // factory: kind 0 hybrid, 1 cvae, 2 simple; cfg per hlmc.h

@@ -511,8 +511,15 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
     HLMC_CHECK_ARG(p->n_mels <= 2 * kMelLanes, "n_mels <= 128");
     dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
     const size_t dyn = ((size_t)p->nnz + 4 * kMelLanes + (size_t)kFpb * (p->n_mels + 1)) * 4;
+    {  // algorithmic work: radix-2-equivalent FFT 2.5 N log2 N + window + |X|^2 + banded mel; PCM in, mel out
+        const double nf = p->n_fft, lg = std::log2(nf);
+        probe::site(probe::kStftMel, (double)B * T * (2.5 * nf * lg + nf + 3.0 * (nf / 2 + 1) + 2.0 * p->nnz),
+                    (double)B * ((double)n * 4 + (double)p->n_mels * T * 4));
+    }
+    HLMC_PROBE_BEGIN(s);
     stft_mel_kernel<<<grid, 256, dyn, s>>>(
         pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff, p->d_w, p->n_mels, p->nnz, out, cmax, cmin);
+    HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -52,6 +52,7 @@ inline int nt_pipe_select(int ksl) {
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class E>
 void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
                       bool long_k, int pipe) {
+    HLMC_PROBE_BEGIN(s);
     if (pipe == 3)
         gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
     else if (pipe == 4)
@@ -60,6 +61,7 @@ void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, cons
         gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
     else
         gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+    HLMC_PROBE_END(s);
 }
 
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
@@ -174,10 +176,12 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
     size_t need = (size_t)pl.S * M * N * sizeof(float);
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "wgrad workspace too small");
     dim3 grid(tiles, 1, pl.S);
+    HLMC_PROBE_BEGIN(s);
     if (pl.ksl >= 1024)
         gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl);
     else
         gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl);
+    HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     int64_t total = (int64_t)M * N;
     int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
@@ -222,6 +226,8 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     ConvS2Loader<T> al{x, Hi, Wi, Ci, Ho, Wo, M, log2_exact(Ci)};
     DenseLoader<T> bl{wp, K, Co, K, true};
     StoreRM<T> ep{y, bias, Co, 0, 0};
+    probe::site(probe::kConvS2, 2.0 * M * Co * K,
+                (double)sizeof(T) * ((double)B * Hi * Wi * Ci + (double)Co * K + (double)M * Co));
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
 }
 size_t col_stats_bytes(int64_t M, int phases, int C) { return (size_t)phases * cdiv((int)M, 64) * 2 * C * sizeof(double); }
@@ -241,6 +247,9 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
     SubpixelLoader<T> al{x, Hi, Wi, Ci, M, log2_exact(Ci), 0, 0, 0, 0};
     SubpixelWeight<T> bl{wp, Ci, Co, log2_exact(Ci), 0, 0, 0, 0};
     StoreSubpixel<T> ep{y, bias, Hi, Wi, Co, 0, 0};
+    // the 4 phases hold 1 + 2 + 2 + 4 = 9 taps: 9 Ci MACs per (low-res pixel, output channel)
+    probe::site(probe::kSubpixel, 2.0 * M * Co * 9.0 * Ci,
+                (double)sizeof(T) * ((double)M * Ci + 9.0 * Ci * Co + 4.0 * M * Co));
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
 }
 template <typename T>
@@ -256,6 +265,8 @@ int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* X
     KRowDense<T> ll{L, M, K, M, aligned16(L)};
     KRowConvS2<T> hl{Xh, Hl, Wl, C, K, FastDiv((uint32_t)Wl), FastDiv((uint32_t)Hl)};
     StoreWgradConv ep{dW, C};
+    probe::site(probe::kWgradS2, 2.0 * M * N * K,
+                (double)sizeof(T) * ((double)K * M + 4.0 * K * C) + 4.0 * M * N);
     return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
 }
 template <typename T>
@@ -272,6 +283,7 @@ int linear(hipStream_t s, const T* x, int ldx, int M, int K, const T* w, int ldw
     DenseLoader<T> al{x, ldx, M, K, vx};
     DenseLoader<T> bl{w, ldw, N, K, vw};
     StoreRM<OutT> ep{y, bias, ldy, act, accumulate};
+    probe::site(probe::kLinear, 2.0 * M * N * K, (double)sizeof(T) * ((double)M * K + (double)N * K) + (double)sizeof(OutT) * M * N);
     return dispatch_linear<T>(s, al, bl, ep, M, N, K, ws);
 }
 template <typename T>
@@ -285,6 +297,7 @@ int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int 
     KRowDense<T> ll{dy, lddy, Mb, N, (lddy % V == 0) && aligned16(dy)};
     KRowDense<T> hl{x, ldx, Mb, K, (ldx % V == 0) && aligned16(x)};
     StoreRM<float> ep{dW, nullptr, K, 0, 0};
+    probe::site(probe::kLinearWgrad, 2.0 * N * K * Mb, (double)sizeof(T) * ((double)Mb * N + (double)Mb * K) + 4.0 * N * K);
     return dispatch_tn<T>(s, ll, hl, ep, N, K, Mb, ws);
 }
 template <typename T>

@@ -8,7 +8,10 @@ per-batch ``loss.item()`` is replaced by device-side loss sums that the caller m
 Data parallel: one process per GPU; the flat fp32 gradient buffer is all-reduced with SUM over
 ``torch.distributed`` (backend "nccl" = RCCL over xGMI on MI355X), i.e. gradients of the loss summed
 over the global batch — the reference's sum-reduced losses make SUM the matching reduction.
-BatchNorm statistics stay per rank (DDP semantics).
+BatchNorm statistics stay per rank (DDP semantics).  The buffer is reduced in the engine's gradient
+buckets (hlmc_net_grad_buckets: contiguous parameter ranges in the order backward finishes them); on a
+GPU each bucket's all-reduce is issued on a communication stream that waits on the bucket's event, so
+RCCL overlaps the rest of the backward pass, and Adam waits for all of them.
 """
 from __future__ import annotations
 
@@ -47,6 +50,11 @@ class Trainer:
         self.distributed = distributed or process_group is not None
         self.process_group = process_group
         self.grad_dtype = grad_dtype
+        self.buckets = self._bucket_ranges()
+        self._comm = None
+        if self.distributed and dev.type == "cuda":
+            L.check(L.lib().hlmc_net_set_bucket_sync(self.net.h, 1), "hlmc_net_set_bucket_sync")
+            self._comm = torch.cuda.Stream(device=dev)
         self._mv = (L.vp_array([t.data_ptr() for t in mv]), L.vp_array([t.data_ptr() for t in vv]))
         # weights change only through hlmc_net_adam_step (which refreshes the packed GEMM layouts)
         L.check(L.lib().hlmc_net_set_trust_packs(self.net.h, 1))
@@ -97,7 +105,10 @@ class Trainer:
         L.check(lib.hlmc_net_backward(self.net.h, s, B, L.ptr(d["recon"]), L.ptr(d.get("recon_text")), L.ptr(d["mu"]),
                                       L.ptr(d["logvar"]), c["ws"].data_ptr()), "hlmc_net_backward")
         if self.distributed:
-            self.allreduce_grads()
+            if self._comm is not None:
+                self._allreduce_overlapped()
+            else:
+                self.allreduce_grads()
         self.step_count += 1
         b1, b2 = self.betas
         L.check(lib.hlmc_net_adam_step(self.net.h, s, *self._mv, float(self.lr), float(b1), float(b2), float(self.eps),
@@ -108,15 +119,35 @@ class Trainer:
         """Hand the model back to the nn.Module path (forward re-packs weights every call again)."""
         L.check(L.lib().hlmc_net_set_trust_packs(self.net.h, 0))
 
-    def allreduce_grads(self):
-        """SUM all-reduce of the flat gradient buffer (RCCL under backend 'nccl')."""
+    def _bucket_ranges(self):
+        """[(lo, hi)] element ranges of the flat gradient buffer, one per engine bucket, in backward order."""
+        offs = [0]
+        for p in self.params:
+            offs.append(offs[-1] + p.numel())
+        cap = 64
+        starts = (L.c_int * cap)()
+        nb = L.lib().hlmc_net_grad_buckets(self.net.h, starts, cap)
+        if nb < 0:
+            L.check(nb, "hlmc_net_grad_buckets")
+        return bucket_ranges(list(starts)[:nb], offs)
+
+    def _allreduce_overlapped(self):
+        """Per-bucket SUM all-reduces on the comm stream, each gated on its bucket's backward event;
+        the current stream (Adam) waits for all of them."""
         import torch.distributed as dist
-        if self.grad_dtype == torch.float32:
-            dist.all_reduce(self.gflat, op=dist.ReduceOp.SUM, group=self.process_group)
-        else:
-            g = self.gflat.to(self.grad_dtype)
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.process_group)
-            self.gflat.copy_(g)
+        lib = L.lib()
+        works = []
+        with torch.cuda.stream(self._comm):
+            for k, (lo, hi) in enumerate(self.buckets):
+                L.check(lib.hlmc_net_bucket_wait(self.net.h, k, self._comm.cuda_stream), "hlmc_net_bucket_wait")
+                works.append(_allreduce_sum(self.gflat[lo:hi], self.grad_dtype, self.process_group, async_op=True))
+        for w in works:
+            w.wait()
+
+    def allreduce_grads(self):
+        """SUM all-reduce of the flat gradient buffer, bucket by bucket (RCCL under 'nccl', gloo on CPU)."""
+        for lo, hi in getattr(self, "buckets", None) or [(0, self.gflat.numel())]:
+            _allreduce_sum(self.gflat[lo:hi], self.grad_dtype, self.process_group)
 
     def loss_tuple(self, sums, batch=None):
         """Host floats (total, l_audio, l_text, kld) from device sums (synchronises)."""
@@ -127,3 +158,32 @@ class Trainer:
             return la + self.beta * kl, la, 0.0, kl
         kld = -0.5 * s[2]
         return s[0] + self.text_weight * s[1] + self.beta * kld, s[0], s[1], kld
+
+
+def bucket_ranges(starts, offsets):
+    """Flat-buffer element ranges of engine gradient buckets.  starts: first parameter index of each bucket in
+    backward order (strictly decreasing, last 0); offsets: element offset of every parameter (+ the total)."""
+    if not starts or starts[-1] != 0 or any(a <= b for a, b in zip(starts, starts[1:])):
+        raise ValueError(f"bucket starts must decrease strictly to 0: {starts}")
+    hi_idx = len(offsets) - 1
+    out = []
+    for st in starts:
+        out.append((offsets[st], offsets[hi_idx]))
+        hi_idx = st
+    return out
+
+
+def _allreduce_sum(buf, grad_dtype, group, async_op=False):
+    """SUM all-reduce of a contiguous fp32 gradient slice (optionally on a bf16 wire copy, synchronous)."""
+    import torch.distributed as dist
+    if grad_dtype == torch.float32:
+        return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+    g = buf.to(grad_dtype)
+    dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+    buf.copy_(g)
+    return _Done()
+
+
+class _Done:
+    def wait(self):
+        return True

@@ -124,6 +124,26 @@ int hlmc_net_adam_step(hlmc_net* net, void* stream, float* const* exp_avg, float
  * writes parameters any other way must pass 0, the default, so forward always re-packs). */
 int hlmc_net_set_trust_packs(hlmc_net* net, int trust);
 
+/* Data-parallel gradient buckets (the reference trains on one device; its DDP counterpart is the gradient
+ * all-reduce of SURVEY.md §8e).  Bucket k = parameters [starts[k], starts[k-1]) in registration order
+ * (starts[-1] = num_params), listed in the order hlmc_net_backward finishes them; the last start is 0.
+ * Returns the bucket count (<= cap entries written) or a negative status. */
+int hlmc_net_grad_buckets(const hlmc_net* net, int* starts, int cap);
+/* enable != 0: every later hlmc_net_backward records one event per bucket once all of its gradients are
+ * written (backward internally runs weight gradients on a second stream). */
+int hlmc_net_set_bucket_sync(hlmc_net* net, int enable);
+/* Make `stream` wait until bucket k of the last hlmc_net_backward is final (enqueue-only, no host sync). */
+int hlmc_net_bucket_wait(hlmc_net* net, int k, void* stream);
+
+/* ============================================================== live kernel timing (measurement only)
+ * Arm: launches of the op kinds in `mask` (1 conv_s2 GEMM, 2 sub-pixel GEMM, 4 conv weight-gradient GEMM,
+ * 8 linear GEMM, 16 linear weight-gradient GEMM, 32 STFT-mel) are bracketed by HIP events on their launch
+ * stream (up to max_launches; their algorithmic flops / bytes are summed).  Read: synchronises on the last
+ * event, returns the count, the summed kernel time and work (and per-launch ms into ms_each[cap_each]), and
+ * disarms.  bench.py uses this for the roofline of its dominant kernel inside the timed region. */
+int hlmc_probe_arm(int mask, int max_launches);
+int hlmc_probe_read(int* launches, double* total_ms, double* flops, double* bytes, float* ms_each, int cap_each);
+
 /* ============================================================== losses
  * loss_function (src/Convolutional_VAE.py:187-194), cvae_loss_function (src/Conditional_VAE.py:233-246),
  * vae_loss (src/Simple_VAE.py:108-114).  sums3 (device, double[3]) receives

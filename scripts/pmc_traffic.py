@@ -1,0 +1,82 @@
+"""HBM traffic per launch of every probed kernel kind from rocprofv3 PMC passes over bench.py, and the
+rocprofv3 kernel-trace average duration of the same kinds (the check on bench.py's live HIP-event timing).
+
+    python scripts/pmc_traffic.py OUT_JSON FETCH_DIR WRITE_DIR TRACE_DIR [--steps N]
+
+FETCH_DIR / WRITE_DIR: `rocprofv3 --kernel-trace --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` output directories;
+TRACE_DIR: a `--kernel-trace --stats` run of the bench command.  HBM bytes per dispatch =
+(2 x FETCH_SIZE + WRITE_SIZE) x 1024: rocprofv3 reports both in KiB, and on gfx950 FETCH_SIZE counts half the
+bytes of 16-B-per-lane streaming reads (/opt/skills/guides/MI355X_MICROARCH.md, HBM section).
+"""
+import csv
+import glob
+import json
+import re
+import sys
+
+KINDS = {  # op kind of include/hlmc.h hlmc_probe_arm -> kernel-name pattern
+    "conv_s2": r"gemm_nt\w*<.*ConvS2Loader",
+    "subpixel": r"gemm_nt\w*<.*SubpixelLoader",
+    "wgrad_s2": r"gemm_tn_kernel<.*KRowConvS2",
+    "linear": r"gemm_nt\w*<[^<>]*, hlmc::DenseLoader<",
+    "linear_wgrad": r"gemm_tn_kernel<[^<>]*, hlmc::(\(anonymous namespace\)::)?KRowDenseV?<[^<>]*>, hlmc::(\(anonymous namespace\)::)?KRowDenseV?<",
+    "stft_mel": r"stft_mel_kernel",
+}
+
+
+def kind_of(name):
+    for k, pat in KINDS.items():
+        if re.search(pat, name):
+            return k
+    return None
+
+
+def counters(d, counter):
+    vals = {}
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = kind_of(r["Kernel_Name"])
+            if k:
+                vals.setdefault(k, {}).setdefault(r["Dispatch_Id"], 0.0)
+                vals[k][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+def trace_avg(d):
+    durs = {}
+    for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = kind_of(r["Kernel_Name"])
+            if k:
+                durs.setdefault(k, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return {k: (sum(v) / len(v) / 1e3, len(v)) for k, v in durs.items()}
+
+
+def main():
+    out, fdir, wdir, tdir = sys.argv[1:5]
+    fetch, nf = counters(fdir, "FETCH_SIZE")
+    write, nw = counters(wdir, "WRITE_SIZE")
+    tr = trace_avg(tdir)
+    kinds = {}
+    for k in KINDS:
+        e = {}
+        if k in fetch and k in write:
+            e["fetch_kib_raw"] = round(fetch[k], 1)
+            e["write_kib"] = round(write[k], 1)
+            e["hbm_bytes_per_launch"] = (2.0 * fetch[k] + write[k]) * 1024.0
+            e["pmc_dispatches"] = min(nf[k], nw[k])
+        if k in tr:
+            e["trace_avg_us"] = round(tr[k][0], 2)
+            e["trace_dispatches"] = tr[k][1]
+        if e:
+            kinds[k] = e
+    res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py ({fdir}, {wdir}); "
+                     f"2*FETCH_SIZE+WRITE_SIZE KiB per dispatch (gfx950 correction)", "kinds": kinds}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

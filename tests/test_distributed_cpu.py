@@ -35,6 +35,36 @@ def _shard_grads(rank):
     return torch.cat([p.grad.reshape(-1) for p in model.parameters()])
 
 
+def _engine_buckets(total):
+    """Flat ranges of libhlmc's gradient buckets for the audio-only HybridVAE (host-only C-ABI calls)."""
+    import ctypes
+    from hlmc_amd import _lib as L
+    from hlmc_amd.train import bucket_ranges
+    lib = L.lib()
+    h = ctypes.c_void_p()
+    L.check(lib.hlmc_net_create(L.NET_HYBRID, L.i64_array([128, 0, 128, 128]), 4, L.HLMC_F32, ctypes.byref(h)))
+    try:
+        offs = [0]
+        shape = (L.c_i64 * 8)()
+        nd = ctypes.c_int()
+        name = ctypes.create_string_buffer(256)
+        for i in range(lib.hlmc_net_num_params(h)):
+            L.check(lib.hlmc_net_param_info(h, i, name, 256, ctypes.byref(nd), shape))
+            n = 1
+            for d in shape[:nd.value]:
+                n *= d
+            offs.append(offs[-1] + n)
+        starts = (ctypes.c_int * 16)()
+        nb = lib.hlmc_net_grad_buckets(h, starts, 16)
+        assert nb >= 2, nb
+        ranges = bucket_ranges(list(starts)[:nb], offs)
+    finally:
+        lib.hlmc_net_destroy(h)
+    assert offs[-1] == total
+    assert sorted(ranges) == [(a, b) for a, b in sorted(ranges)] and sum(b - a for a, b in ranges) == total
+    return ranges
+
+
 def _scaler_shard(rank):
     rng = np.random.default_rng(3)
     X = (rng.standard_normal((61, 40)) * rng.uniform(0.1, 4, 40) + rng.uniform(-2, 2, 40)).astype(np.float32)
@@ -49,11 +79,13 @@ def _worker(rank, port, outdir):
     import hlmc_amd
     from hlmc_amd.features import scaler_finalize
 
-    # ---- gradient SUM all-reduce through Trainer.allreduce_grads (fp32 and bf16 wire formats)
+    # ---- gradient SUM all-reduce through Trainer.allreduce_grads, bucket by bucket over the engine's own
+    #      gradient buckets (fp32 and bf16 wire formats)
     flat = _shard_grads(rank)
-    ns = types.SimpleNamespace(gflat=flat.clone(), grad_dtype=torch.float32, process_group=None)
+    buckets = _engine_buckets(flat.numel())
+    ns = types.SimpleNamespace(gflat=flat.clone(), grad_dtype=torch.float32, process_group=None, buckets=buckets)
     hlmc_amd.Trainer.allreduce_grads(ns)
-    ns16 = types.SimpleNamespace(gflat=flat.clone(), grad_dtype=torch.bfloat16, process_group=None)
+    ns16 = types.SimpleNamespace(gflat=flat.clone(), grad_dtype=torch.bfloat16, process_group=None, buckets=buckets)
     hlmc_amd.Trainer.allreduce_grads(ns16)
 
     # ---- distributed StandardScaler statistics (numpy stands in for the f64 column-sum kernels)

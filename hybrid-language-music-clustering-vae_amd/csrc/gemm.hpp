@@ -33,6 +33,17 @@ struct FastDiv {
     __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, mul) + n) >> sh; }
 };
 
+// XCD-aware block order (cdna_hip_programming.md T1): the dispatcher deals linear block ids round-robin over
+// the 8 XCDs (ids b and b+8 share an L2), so map them to logical ids that run consecutively on one XCD; blocks
+// that share operand rows (the N-tiles / phases of one M-tile, the tiles of one K-split) then share an L2.
+// Bijective for any total (q = total / 8 logical ids per XCD, the first total % 8 XCD labels get one more).
+// Placement is a speed hint only: every logical id is still computed exactly once.
+__device__ __forceinline__ int xcd_logical_block(int lin, int total) {
+    const int xcd = lin & 7, idx = lin >> 3;
+    const int q = total >> 3, r = total & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
 // 16 zero bytes: the source of every out-of-range / padding chunk of the LDS-DMA (global_load_lds) loaders
 static __device__ __attribute__((aligned(16))) uint4 g_zero16 = {0u, 0u, 0u, 0u};
 
@@ -86,6 +97,7 @@ struct ConvS2Loader {
     const T* x;
     int Hi, Wi, C, Ho, Wo, M;
     int cshift;  // log2(C) when C is a power of two, else -1
+    FastDiv dWo, dHo;
     struct Row {
         int64_t base;  // element offset of (b, 2oh-1, 2ow-1, 0)
         int flags;
@@ -98,8 +110,8 @@ struct ConvS2Loader {
     __device__ int K() const { return 9 * C; }
     __device__ Row prep(int m) const {
         if (m >= M) return Row{0, 1 | 8};
-        const int ow = m % Wo, t = m / Wo;
-        const int oh = t % Ho, b = t / Ho;
+        const int t = (int)dWo.div((uint32_t)m), ow = m - t * Wo;
+        const int b = (int)dHo.div((uint32_t)t), oh = t - b * Ho;
         return Row{(((int64_t)b * Hi + 2 * oh - 1) * Wi + 2 * ow - 1) * C, 8 | (oh == 0 ? 2 : 0) | (ow == 0 ? 4 : 0)};
     }
     __device__ Ctx ctx(int k) const {
@@ -130,6 +142,7 @@ struct SubpixelLoader {
     int Hi, Wi, C, M;  // M = B*Hi*Wi
     int cshift;
     int py, px, ntx, Kd;
+    FastDiv dWi, dHi;
     struct Row {
         int64_t base;  // offset of (b, r, c, 0)
         int flags;
@@ -146,8 +159,8 @@ struct SubpixelLoader {
     __device__ int K() const { return Kd; }
     __device__ Row prep(int m) const {
         if (m >= M) return Row{0, 1 | 8};
-        const int c = m % Wi, t = m / Wi;
-        const int r = t % Hi, b = t / Hi;
+        const int t = (int)dWi.div((uint32_t)m), c = m - t * Wi;
+        const int b = (int)dHi.div((uint32_t)t), r = t - b * Hi;
         return Row{(((int64_t)b * Hi + r) * Wi + c) * C, 8 | (r == Hi - 1 ? 2 : 0) | (c == Wi - 1 ? 4 : 0)};
     }
     __device__ Ctx ctx(int k) const {
@@ -200,7 +213,11 @@ struct SubpixelWeight {
 };
 
 // ============================================================================ epilogues
-// Epilogue contract: set_phase(p); Row row(int m) (once per output row); store(const Row&, int n, float v).
+// Epilogue contract (two access forms):
+//   GEMM tiles:  float colbias(n) (hoisted per column); Quad quad(m) once per 4 consecutive rows m..m+3
+//                (m % 4 == 0, the MFMA C/D row group of a lane); float put(const Quad&, r, n, v) stores
+//                row m+r, column n of v (= accumulator + colbias) and returns the stored value as float.
+//   split-K reduce (per element): set_phase(p); Row row(int m); store(const Row&, int n, float v).
 // Row-major store with bias, activation, optional accumulate:  out[m*ld + n] (+)= act(v + bias[n])
 // act: 0 none, 1 relu
 template <typename OutT>
@@ -212,6 +229,20 @@ struct StoreRM {
     struct Row {
         OutT* r;
     };
+    struct Quad {
+        OutT* r0;
+    };
+    __device__ void set_split(int) {}
+    __device__ float colbias(int n) const { return bias ? bias[n] : 0.f; }
+    __device__ Quad quad(int m) const { return Quad{out + (int64_t)m * ld}; }
+    __device__ float put(const Quad& q, int r, int n, float v) const {
+        if (act == 1) v = v > 0.f ? v : 0.f;
+        OutT* o = q.r0 + (int64_t)r * ld + n;
+        if (accumulate) v += to_f32<OutT>(*o);
+        const OutT t = from_f32<OutT>(v);
+        *o = t;
+        return to_f32<OutT>(t);
+    }
     // the value store() writes (without accumulate), as float: for the fused column statistics
     __device__ float stored(int n, float v) const {
         if (bias) v += bias[n];
@@ -237,9 +268,28 @@ struct StoreSubpixel {
     const float* bias;
     int Hi, Wi, N;
     int py, px;
+    FastDiv dWi, dHi;
     struct Row {
         OutT* r;
     };
+    struct Quad {
+        OutT* p0;  // row m (Wi % 4 == 0: rows m+1..m+3 are the next low-res columns of the same image row)
+        int m;
+    };
+    __device__ OutT* pix_ptr(int m) const {
+        const int t = (int)dWi.div((uint32_t)m), c = m - t * Wi;
+        const int b = (int)dHi.div((uint32_t)t), r = t - b * Hi;
+        return out + (((int64_t)b * 2 * Hi + 2 * r + py) * (2 * Wi) + 2 * c + px) * N;
+    }
+    __device__ void set_split(int) {}
+    __device__ float colbias(int n) const { return bias ? bias[n] : 0.f; }
+    __device__ Quad quad(int m) const { return Quad{pix_ptr(m), m}; }
+    __device__ float put(const Quad& q, int r, int n, float v) const {
+        OutT* p = (Wi & 3) == 0 ? q.p0 + (int64_t)2 * r * N : pix_ptr(q.m + r);
+        const OutT t = from_f32<OutT>(v);
+        p[n] = t;
+        return to_f32<OutT>(t);
+    }
     __device__ float stored(int n, float v) const {
         if (bias) v += bias[n];
         return to_f32<OutT>(from_f32<OutT>(v));
@@ -279,11 +329,69 @@ struct StorePartial {
     __device__ void set_phase(int p) { phase = p; }
     __device__ Row row(int m) const { return Row{ws + (((int64_t)phase * S + split) * M + m) * N}; }
     __device__ void store(const Row& rw, int n, float v) const { rw.r[n] = v; }
+    struct Quad {
+        float* r0;
+    };
+    __device__ void set_split(int z) { split = z; }
+    __device__ float colbias(int) const { return 0.f; }
+    __device__ Quad quad(int m) const { return Quad{ws + (((int64_t)phase * S + split) * M + m) * N}; }
+    __device__ float put(const Quad& q, int r, int n, float v) const {
+        q.r0[(int64_t)r * N + n] = v;
+        return v;
+    }
 };
+
+// Store one wave's TM x TN grid of 16x16 accumulator tiles through the epilogue (C/D map: col = lane & 15,
+// rows (lane >> 4) * 4 + 0..3), bias hoisted per column, one quad() per 4-row group; with EP::kStats the
+// per-column sum / sum of squares of the stored values over this lane's rows go to cs / cq (f64).
+template <int TM, int TN, class EP>
+__device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)[TM][TN], int mb, int nb, int lane,
+                                              int M, int N, double (&cs)[TN], double (&cq)[TN]) {
+    float bias[TN];
+    int ncol[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        ncol[j] = nb + j * 16 + (lane & 15);
+        bias[j] = ncol[j] < N ? ep.colbias(ncol[j]) : 0.f;
+        cs[j] = 0.0;
+        cq[j] = 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + (lane >> 4) * 4;
+        if (m >= M) continue;
+        const typename EP::Quad q = ep.quad(m);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            if (m + r >= M) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if (ncol[j] >= N) continue;
+                const float v = ep.put(q, r, ncol[j], acc[i][j][r] + bias[j]);
+                if constexpr (EP::kStats) {
+                    cs[j] += v;
+                    cq[j] += (double)v * v;
+                }
+            }
+        }
+    }
+}
+
+// Block coordinates of the NT kernels after the XCD remap: logical id -> (phase fastest, then tile, then
+// K-split), so the phases and N-tiles of one M-tile (which gather the same A rows) run on one XCD.
+#define NT_BLOCK_COORDS()                                                                                  \
+    const int gx_ = (int)gridDim.x, gy_ = (int)gridDim.y;                                                  \
+    const int lin_ = (int)blockIdx.x + gx_ * ((int)blockIdx.y + gy_ * (int)blockIdx.z);                     \
+    const int lg_ = remap ? xcd_logical_block(lin_, gx_ * gy_ * (int)gridDim.z) : 0;                       \
+    const int phase = remap ? lg_ % gy_ : (int)blockIdx.y;                                                 \
+    const int tile_ = remap ? (lg_ / gy_) % gx_ : (int)blockIdx.x;                                         \
+    const int bz = remap ? lg_ / (gx_ * gy_) : (int)blockIdx.z;                                            \
+    const int m0 = (tile_ / tiles_n) * BM, n0 = (tile_ % tiles_n) * BN;                                     \
+    const int tile_m_ = tile_ / tiles_n
 
 // ============================================================================ NT main loop
 template <typename T, int BM, int BN, int WM, int WN, int KCH, class AL, class BL, class EP>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len) {
+__global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;
     constexpr int BKP = BK + V;  // rows padded by one 16-byte chunk
@@ -298,11 +406,10 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
     const int tiles_n = (N + BN - 1) / BN;
-    const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
-    const int phase = blockIdx.y;
-    al.set_phase(phase); bl.set_phase(phase); ep.set_phase(phase);
+    NT_BLOCK_COORDS();
+    al.set_phase(phase); bl.set_phase(phase); ep.set_phase(phase); ep.set_split(bz);
     const int K = al.K();
-    const int kb = blockIdx.z * ksplit_len;
+    const int kb = bz * ksplit_len;
     const int ke = min(K, kb + ksplit_len);
 
     f32x4_t acc[TM][TN];
@@ -394,54 +501,29 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
             __syncthreads();
         }
     }
-    // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
-            if (m >= M) continue;
-            const typename EP::Row er = ep.row(m);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n = n0 + wn0 + j * 16 + (lane & 15);
-                if (n < N) ep.store(er, n, acc[i][j][r]);
-            }
-        }
+    double cs[TN], cq[TN];
+    epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
     if constexpr (EP::kStats) {
         // per-column sum / sum of squares of the stored values over the block's rows: lane sums over its
-        // 4*TM rows, xor-16/32 shuffles over the wave's row groups, then the waves of one column strip in order
+        // 4*TM rows (epilogue_tile), xor-16/32 shuffles over the wave's row groups, then the waves of one
+        // column strip in order
         constexpr int WAVES_M = BM / WM;
         __shared__ double sred[WAVES_M][2][BN];
         const int wmi = wave / WAVES_N;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wn0 + j * 16 + (lane & 15);
-            double cs = 0.0, cq = 0.0;
-            if (n < N) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
-                        if (m < M) {
-                            const float v = ep.stored(n, acc[i][j][r]);
-                            cs += v;
-                            cq += (double)v * v;
-                        }
-                    }
-            }
-            cs += __shfl_xor(cs, 16, 64);
-            cq += __shfl_xor(cq, 16, 64);
-            cs += __shfl_xor(cs, 32, 64);
-            cq += __shfl_xor(cq, 32, 64);
+            double a = cs[j], q = cq[j];
+            a += __shfl_xor(a, 16, 64);
+            q += __shfl_xor(q, 16, 64);
+            a += __shfl_xor(a, 32, 64);
+            q += __shfl_xor(q, 32, 64);
             if (lane < 16) {
-                sred[wmi][0][wn0 + j * 16 + lane] = cs;
-                sred[wmi][1][wn0 + j * 16 + lane] = cq;
+                sred[wmi][0][wn0 + j * 16 + lane] = a;
+                sred[wmi][1][wn0 + j * 16 + lane] = q;
             }
         }
         __syncthreads();
-        const int row = phase * ep.mtiles + (int)(blockIdx.x / tiles_n);
+        const int row = phase * ep.mtiles + tile_m_;
         for (int c = tid; c < BN; c += 256) {
             const int n = n0 + c;
             if (n >= N) continue;
@@ -484,7 +566,7 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int NS, class AL, class BL, class EP>
-__global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len) {
+__global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = 8 * V;                       // 128-byte tile rows
     constexpr int ASZ = BM * 128, BSZ = BN * 128, STG = ASZ + BSZ;
@@ -499,11 +581,10 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
     const int tiles_n = (N + BN - 1) / BN;
-    const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
-    const int phase = blockIdx.y;
-    al.set_phase(phase); bl.set_phase(phase); ep.set_phase(phase);
+    NT_BLOCK_COORDS();
+    al.set_phase(phase); bl.set_phase(phase); ep.set_phase(phase); ep.set_split(bz);
     const int K = al.K();
-    const int kb = blockIdx.z * ksplit_len;
+    const int kb = bz * ksplit_len;
     const int ke = min(K, kb + ksplit_len);
     const int nsteps = kb < ke ? (ke - kb + BK - 1) / BK : 0;
 
@@ -585,20 +666,8 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
             }
         }
     }
-    // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
-            if (m >= M) continue;
-            const typename EP::Row er = ep.row(m);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n = n0 + wn0 + j * 16 + (lane & 15);
-                if (n < N) ep.store(er, n, acc[i][j][r]);
-            }
-        }
+    double cs[TN], cq[TN];
+    epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
     if constexpr (EP::kStats) {
         constexpr int WAVES_M = BM / WM;
         static_assert(WAVES_M * 2 * BN * 8 <= NS * STG, "stats scratch fits the staging ring");
@@ -607,32 +676,18 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
         const int wmi = wave / WAVES_N;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wn0 + j * 16 + (lane & 15);
-            double cs = 0.0, cq = 0.0;
-            if (n < N) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
-                        if (m < M) {
-                            const float v = ep.stored(n, acc[i][j][r]);
-                            cs += v;
-                            cq += (double)v * v;
-                        }
-                    }
-            }
-            cs += __shfl_xor(cs, 16, 64);
-            cq += __shfl_xor(cq, 16, 64);
-            cs += __shfl_xor(cs, 32, 64);
-            cq += __shfl_xor(cq, 32, 64);
+            double a = cs[j], q = cq[j];
+            a += __shfl_xor(a, 16, 64);
+            q += __shfl_xor(q, 16, 64);
+            a += __shfl_xor(a, 32, 64);
+            q += __shfl_xor(q, 32, 64);
             if (lane < 16) {
-                sred[(wmi * 2 + 0) * BN + wn0 + j * 16 + lane] = cs;
-                sred[(wmi * 2 + 1) * BN + wn0 + j * 16 + lane] = cq;
+                sred[(wmi * 2 + 0) * BN + wn0 + j * 16 + lane] = a;
+                sred[(wmi * 2 + 1) * BN + wn0 + j * 16 + lane] = q;
             }
         }
         __syncthreads();
-        const int prow = phase * ep.mtiles + (int)(blockIdx.x / tiles_n);
+        const int prow = phase * ep.mtiles + tile_m_;
         for (int c = tid; c < BN; c += 256) {
             const int n = n0 + c;
             if (n >= N) continue;
@@ -650,7 +705,7 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
 
 // Split-K wrapper epilogue: the z-index of the grid selects the partial slab.
 struct StorePartialZ : StorePartial {
-    __device__ void set_phase(int p) { phase = p; split = blockIdx.z; }
+    __device__ void set_split(int z) { split = z; }  // the block's (XCD-remapped) K-split index
 };
 
 // Reduce split-K partials (fixed order => deterministic) then apply the final epilogue.
@@ -736,7 +791,7 @@ struct KRowConvS2 {
 // ============================================================================ TN main loop
 // Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_kernel).
 template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL>
-__global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len) {
+__global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;            // k rows per tile (KCH 16-byte chunks of one column)
     constexpr int LDA = BM + V;             // padded LDS row (elements)
@@ -752,8 +807,12 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
     const int tiles_n = (N + BN - 1) / BN;
-    const int m0 = (blockIdx.x / tiles_n) * BM, n0 = (blockIdx.x % tiles_n) * BN;
-    const int kb = blockIdx.z * ksplit_len;
+    // XCD remap: the tiles of one K-split (which share L and H rows) run consecutively on one XCD
+    const int gx_ = (int)gridDim.x;
+    const int lg_ = remap ? xcd_logical_block((int)blockIdx.x + gx_ * (int)blockIdx.z, gx_ * (int)gridDim.z) : 0;
+    const int tile_ = remap ? lg_ % gx_ : (int)blockIdx.x, bz = remap ? lg_ / gx_ : (int)blockIdx.z;
+    const int m0 = (tile_ / tiles_n) * BM, n0 = (tile_ % tiles_n) * BN;
+    const int kb = bz * ksplit_len;
     const int ke = min(K, kb + ksplit_len);
 
     f32x4_t acc[TM][TN];
@@ -853,7 +912,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
             __syncthreads();
         }
     }
-    float* slab = ws + (int64_t)blockIdx.z * M * N;
+    float* slab = ws + (int64_t)bz * M * N;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll

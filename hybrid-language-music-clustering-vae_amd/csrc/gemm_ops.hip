@@ -9,6 +9,7 @@ namespace hlmc {
 namespace {
 
 constexpr int kTargetBlocks = 512;  // 256 CUs x 2
+constexpr int kXcdRemapDefault = probe::kWgradS2 | probe::kLinearWgrad;  // measured: helps the TN (wgrad) family, hurts sub-pixel
 
 // Split-K plan shared by the launcher and the workspace query (must agree).
 struct Plan {
@@ -49,18 +50,29 @@ inline int nt_pipe_select(int ksl) {
     return ksl >= 1024 ? 4 : 0;
 }
 
+// XCD-aware block order per op kind (bit = probe::k* kind; gemm.hpp xcd_logical_block).  Default from the
+// per-layer A/B of scripts/bench_gemm.py; HLMC_XCD_REMAP=<mask> overrides (measurement aid).
+inline int xcd_remap_for_site() {
+    static const int mask = [] {
+        const char* e = std::getenv("HLMC_XCD_REMAP");
+        return e ? std::atoi(e) : kXcdRemapDefault;
+    }();
+    return (mask & probe::g_site.kind) ? 1 : 0;
+}
+
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class E>
 void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
                       bool long_k, int pipe) {
+    const int rm = xcd_remap_for_site();
     HLMC_PROBE_BEGIN(s);
     if (pipe == 3)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (pipe == 4)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (long_k)
-        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else
-        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     HLMC_PROBE_END(s);
 }
 
@@ -176,11 +188,12 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
     size_t need = (size_t)pl.S * M * N * sizeof(float);
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "wgrad workspace too small");
     dim3 grid(tiles, 1, pl.S);
+    const int rm = xcd_remap_for_site();
     HLMC_PROBE_BEGIN(s);
     if (pl.ksl >= 1024)
-        gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl);
+        gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
     else
-        gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl);
+        gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     int64_t total = (int64_t)M * N;
@@ -223,7 +236,7 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % V == 0, "conv_s2: need even H/W and Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "conv_s2: 16-byte alignment");
     const int Ho = Hi / 2, Wo = Wi / 2, M = B * Ho * Wo, K = 9 * Ci;
-    ConvS2Loader<T> al{x, Hi, Wi, Ci, Ho, Wo, M, log2_exact(Ci)};
+    ConvS2Loader<T> al{x, Hi, Wi, Ci, Ho, Wo, M, log2_exact(Ci), FastDiv((uint32_t)Wo), FastDiv((uint32_t)Ho)};
     DenseLoader<T> bl{wp, K, Co, K, true};
     StoreRM<T> ep{y, bias, Co, 0, 0};
     probe::site(probe::kConvS2, 2.0 * M * Co * K,
@@ -244,9 +257,9 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
     HLMC_CHECK_ARG(Ci % V == 0, "subpixel: Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "subpixel: 16-byte alignment");
     const int M = B * Hi * Wi;
-    SubpixelLoader<T> al{x, Hi, Wi, Ci, M, log2_exact(Ci), 0, 0, 0, 0};
+    SubpixelLoader<T> al{x, Hi, Wi, Ci, M, log2_exact(Ci), 0, 0, 0, 0, FastDiv((uint32_t)Wi), FastDiv((uint32_t)Hi)};
     SubpixelWeight<T> bl{wp, Ci, Co, log2_exact(Ci), 0, 0, 0, 0};
-    StoreSubpixel<T> ep{y, bias, Hi, Wi, Co, 0, 0};
+    StoreSubpixel<T> ep{y, bias, Hi, Wi, Co, 0, 0, FastDiv((uint32_t)Wi), FastDiv((uint32_t)Hi)};
     // the 4 phases hold 1 + 2 + 2 + 4 = 9 taps: 9 Ci MACs per (low-res pixel, output channel)
     probe::site(probe::kSubpixel, 2.0 * M * Co * 9.0 * Ci,
                 (double)sizeof(T) * ((double)M * Ci + 9.0 * Ci * Co + 4.0 * M * Co));

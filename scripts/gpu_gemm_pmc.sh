@@ -1,0 +1,6 @@
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 300 python scripts/bench_gemm.py > gpurun_out/bench_gemm.log 2>&1 || exit $?
+timeout -k 10 400 bash scripts/pmc_op.sh sp4 subpixel 256 32 32 64 32 > gpurun_out/pmc_sp4.log 2>&1 || exit $?
+timeout -k 10 400 bash scripts/pmc_op.sh cv1 conv 256 64 64 32 64 > gpurun_out/pmc_cv1.log 2>&1 || exit $?
+timeout -k 10 400 bash scripts/pmc_op.sh wg1 wgrad 256 32 32 64 32 > gpurun_out/pmc_wg1.log 2>&1 || exit $?
+echo done

@@ -45,3 +45,45 @@ def test_trainer_bf16_loss_decreases(cuda):
         first = tot if first is None else first
         last = tot
     assert last < 0.9 * first
+
+
+@pytest.mark.parametrize("kind", ["hybrid", "cvae"])
+def test_trainer_dp_overlapped_allreduce_world1(cuda, kind):
+    """The DP path (per-bucket RCCL all-reduces on a comm stream gated on backward's bucket events, Adam
+    waiting on them) in a 1-rank NCCL group: parameters must equal the non-distributed Trainer's exactly."""
+    import os
+    import torch.distributed as dist
+    own = not dist.is_initialized()
+    if own:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29600 + os.getpid() % 1000))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=cuda)
+    try:
+        def make():
+            torch.manual_seed(42)
+            if kind == "hybrid":
+                m = hlmc_amd.HybridVAE(128, 384, (128, 128), compute_dtype="bf16").cuda()
+            else:
+                m = hlmc_amd.ConditionalVAE(64, 384, 10, (128, 128), compute_dtype="bf16").cuda()
+            return m
+        a, b = make(), make()
+        ta = hlmc_amd.Trainer(a, lr=1e-3)
+        tb = hlmc_amd.Trainer(b, lr=1e-3, distributed=True)
+        assert len(tb.buckets) >= 3
+        g = torch.Generator().manual_seed(0)
+        for _ in range(3):
+            audio = torch.randn(16, 1, 128, 128, generator=g).cuda()
+            text = (torch.randn(16, 384, generator=g) / 384 ** 0.5).cuda()
+            eps = torch.randn(16, a.latent_dim, generator=g).cuda()
+            extra = ()
+            if kind == "cvae":
+                extra = (torch.nn.functional.one_hot(torch.arange(16) % 10, 10).float().cuda(),)
+            sa = ta.step(audio, text, *extra, eps=eps)
+            sb = tb.step(audio, text, *extra, eps=eps)
+            assert torch.equal(sa, sb)
+        torch.cuda.synchronize()
+        for (n, p), q in zip(a.named_parameters(), b.parameters()):
+            assert torch.equal(p, q), n
+    finally:
+        if own:
+            dist.destroy_process_group()

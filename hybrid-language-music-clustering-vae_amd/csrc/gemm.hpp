@@ -389,19 +389,29 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
     const int m0 = (tile_ / tiles_n) * BM, n0 = (tile_ % tiles_n) * BN;                                     \
     const int tile_m_ = tile_ / tiles_n
 
+// Physical 16-byte chunk of logical chunk c in LDS tile row `row` (rows of KCH chunks, unpadded).  The bf16
+// A/B fragment read (ds_read_b128: lane l -> row l & 15, chunk 4s + (l >> 4)) is then conflict-free in all
+// four 16-lane bank groups (cdna_hip_programming.md §2 bank rule): 128-B rows XOR the chunk with row & 7;
+// 64-B rows (4 per 256-B bank row) XOR it with f((row >> 2) & 3), f = {0, 2, 3, 1}.  The ds_write_b128 fill
+// (8 consecutive lanes = 2 or 1 whole rows) stays conflict-free under any per-row chunk permutation.
+template <int KCH>
+__device__ __forceinline__ int nt_lds_chunk(int row, int c) {
+    if constexpr (KCH == 8) return c ^ (row & 7);
+    else return c ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3);
+}
+
 // ============================================================================ NT main loop
 template <typename T, int BM, int BN, int WM, int WN, int KCH, class AL, class BL, class EP>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
-    constexpr int BK = KCH * V;
-    constexpr int BKP = BK + V;  // rows padded by one 16-byte chunk
+    constexpr int BK = KCH * V;  // LDS rows of KCH 16-byte chunks, chunk positions swizzled (nt_lds_chunk)
     constexpr int WAVES_N = BN / WN;
     static_assert((BM / WM) * WAVES_N == 4, "4 waves per block");
     constexpr int TM = WM / 16, TN = WN / 16;
     constexpr int ACH = BM * KCH, BCH = BN * KCH;     // 16-byte chunks per tile
     constexpr int AR = (ACH + 255) / 256, BR = (BCH + 255) / 256;
-    __shared__ __attribute__((aligned(16))) T As[2][BM * BKP];
-    __shared__ __attribute__((aligned(16))) T Bs[2][BN * BKP];
+    __shared__ __attribute__((aligned(16))) T As[2][BM * BK];
+    __shared__ __attribute__((aligned(16))) T Bs[2][BN * BK];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
@@ -444,12 +454,14 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (ACH % 256 == 0 || c < ACH) *reinterpret_cast<uint4*>(&As[buf][(c / KCH) * BKP + (c % KCH) * V]) = ra[i];
+            if (ACH % 256 == 0 || c < ACH)
+                *reinterpret_cast<uint4*>(&As[buf][(c / KCH) * BK + nt_lds_chunk<KCH>(c / KCH, c % KCH) * V]) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (BCH % 256 == 0 || c < BCH) *reinterpret_cast<uint4*>(&Bs[buf][(c / KCH) * BKP + (c % KCH) * V]) = rb[i];
+            if (BCH % 256 == 0 || c < BCH)
+                *reinterpret_cast<uint4*>(&Bs[buf][(c / KCH) * BK + nt_lds_chunk<KCH>(c / KCH, c % KCH) * V]) = rb[i];
         }
     };
 
@@ -468,14 +480,17 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
 #pragma unroll
                 for (int s = 0; s < BK / 32; ++s) {
                     bf16x8_t af[TM], bfr[TN];
+                    const int c = s * 4 + (lane >> 4);
 #pragma unroll
-                    for (int i = 0; i < TM; ++i)
-                        af[i] = *reinterpret_cast<const bf16x8_t*>(
-                            &A[(wm0 + i * 16 + (lane & 15)) * BKP + s * 32 + (lane >> 4) * 8]);
+                    for (int i = 0; i < TM; ++i) {
+                        const int row = wm0 + i * 16 + (lane & 15);
+                        af[i] = *reinterpret_cast<const bf16x8_t*>(&A[row * BK + nt_lds_chunk<KCH>(row, c) * 8]);
+                    }
 #pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        bfr[j] = *reinterpret_cast<const bf16x8_t*>(
-                            &B[(wn0 + j * 16 + (lane & 15)) * BKP + s * 32 + (lane >> 4) * 8]);
+                    for (int j = 0; j < TN; ++j) {
+                        const int row = wn0 + j * 16 + (lane & 15);
+                        bfr[j] = *reinterpret_cast<const bf16x8_t*>(&B[row * BK + nt_lds_chunk<KCH>(row, c) * 8]);
+                    }
 #pragma unroll
                     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -487,9 +502,15 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
                 for (int s = 0; s < BK / 4; ++s) {
                     float af[TM], bfr[TN];
 #pragma unroll
-                    for (int i = 0; i < TM; ++i) af[i] = A[(wm0 + i * 16 + (lane & 15)) * BKP + s * 4 + (lane >> 4)];
+                    for (int i = 0; i < TM; ++i) {
+                        const int row = wm0 + i * 16 + (lane & 15);
+                        af[i] = A[row * BK + nt_lds_chunk<KCH>(row, s) * 4 + (lane >> 4)];
+                    }
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) bfr[j] = B[(wn0 + j * 16 + (lane & 15)) * BKP + s * 4 + (lane >> 4)];
+                    for (int j = 0; j < TN; ++j) {
+                        const int row = wn0 + j * 16 + (lane & 15);
+                        bfr[j] = B[row * BK + nt_lds_chunk<KCH>(row, s) * 4 + (lane >> 4)];
+                    }
 #pragma unroll
                     for (int i = 0; i < TM; ++i)
 #pragma unroll

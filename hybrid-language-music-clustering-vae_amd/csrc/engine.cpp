@@ -137,9 +137,11 @@ class NetT : public NetBase {
         if (B != planned_B) {
             Arena A;
             scratch_bytes = 0;
+            bnb_part_bytes = 0;
             plan(A, B);
             scratch_off = A.take(scratch_bytes + 256);
             scratch2_off = A.take(scratch_bytes + 256);
+            bnb_part_off = A.take(bnb_part_bytes + 256);
             ws_total = A.used;
             planned_B = B;
         }
@@ -280,17 +282,41 @@ class NetT : public NetBase {
             HLMC_TRY(ops::bn_eval_stats(s, RM[bn], RV[bn], C, kBnEps, mean, inv));
         return ops::bn_act<T>(s, y, R, C, mean, inv, P[g], P[beta], act, mask, mscale, a, lda);
     }
+    // fused: moments emitted by the GEMM that wrote da (nullable); bias_part: per-layer buffer of the conv bias
+    // column partials, reduced on the weight-gradient stream (nullable: reduced here)
     int bn_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const BnBufs& bb, int g, int beta,
-               int act, const uint8_t* mask, float mscale, T* dy, int bias) {
-        return ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask,
-                                  mscale, dy, G[g], G[beta], bias >= 0 ? G[bias] : nullptr, scratch);
+               int act, const uint8_t* mask, float mscale, T* dy, int bias, const ops::BnBwdFuse* fused = nullptr,
+               double* bias_part = nullptr) {
+        double* bp = (bias >= 0 && use_side) ? bias_part : nullptr;
+        HLMC_TRY(ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask, mscale, dy,
+                                    G[g], G[beta], bias >= 0 ? G[bias] : nullptr, scratch, fused, bp));
+        if (bp) {
+            float* gb = G[bias];
+            const int np = ops::bn_bias_parts(R);
+            HLMC_TRY(side(s, [&](hipStream_t q, Ws) { return ops::colsum_finalize(q, bp, np, C, gb); }));
+        }
+        return HLMC_OK;
     }
+    // fused BN-backward moments request for the GEMM that writes the grad of a BN layer's output
+    // Off by default: measured on MI355X (scripts/gpu_ab_env.sh, 3 alternating rounds) the epilogue's extra
+    // y reads in the low-occupancy DMA GEMMs plus the finalize over phases x M-tiles partial rows cost more
+    // than the moments pass they replace (87.4k vs 90.5k clips/s).  HLMC_BN_FUSE=1 enables it.
+    ops::BnBwdFuse bn_fuse(const T* y, const BnBufs& bb, int g, int beta) {
+        static const bool on = [] {
+            const char* e = std::getenv("HLMC_BN_FUSE");
+            return e && e[0] == '1';
+        }();
+        return ops::BnBwdFuse{y, AF(bb.mean), AF(bb.inv), P[g], P[beta],
+                              on ? reinterpret_cast<double*>(ws + bnb_part_off) : nullptr, 0};
+    }
+    size_t bnb_part_off = 0, bnb_part_bytes = 0;
+    void need_bnb(size_t b) { bnb_part_bytes = std::max(bnb_part_bytes, b); }
 
     // ---------------------------------------------------------------- conv encoder (6 x conv-BN-LReLU)
     struct Enc {
         int w[6], b[6], g[6], beta[6], bn[6];
         int H = 0, W = 0;
-        size_t y[6], a[6], dy[6], audio = 0;  // dy: grad wrt the conv output (read by the forked wgrad)
+        size_t y[6], a[6], dy[6], bpart[6], audio = 0;  // dy: grad wrt the conv output (read by the forked wgrad)
         BnBufs bb[6];
     };
     Enc enc;
@@ -324,6 +350,9 @@ class NetT : public NetBase {
             enc.y[l] = A.take(n * sizeof(T));
             enc.a[l] = A.take(n * sizeof(T));
             enc.dy[l] = A.take(n * sizeof(T));
+            enc.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * h * w) * co * sizeof(double));
+            // the sub-pixel data-gradient GEMM writing this layer's output grad (4 phases over the low grid)
+            need_bnb(ops::col_stats_bytes(B * (h / 2) * (w / 2), 4, co));
             enc.bb[l] = bn_plan(A, co);
             need(ops::bn_ws(B * h * w, co));
         }
@@ -359,19 +388,23 @@ class NetT : public NetBase {
         hs[0] = enc.H;
         ws_[0] = enc.W;
         for (int l = 0; l < 6; ++l) { hs[l + 1] = hs[l] / 2; ws_[l + 1] = ws_[l] / 2; }
+        ops::BnBwdFuse fuse{};  // nparts 0: layer 5's output grad comes from flat_to_nhwc (separate moments pass)
         for (int l = 5; l >= 0; --l) {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             const int ho = hs[l + 1], wo = ws_[l + 1];
             const int64_t R = (int64_t)B * ho * wo;
             T* dy = AT(enc.dy[l]);
-            HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l]));
+            HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
+                            &fuse, reinterpret_cast<double*>(ws + enc.bpart[l])));
             float* gw = G[enc.w[l]];
             if (l == 0) {
                 HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
             } else {
                 const T* xin = AT(enc.a[l - 1]);
                 HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
-                HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));
+                // grad of layer l-1's activation, with layer l-1's BN-backward moments from the epilogue
+                fuse = bn_fuse(AT(enc.y[l - 1]), enc.bb[l - 1], enc.g[l - 1], enc.beta[l - 1]);
+                HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch, nullptr, &fuse));
             }
             if (l == 3 && bucket_hi >= 0) HLMC_TRY(mark(s, bucket_hi));
         }
@@ -382,7 +415,7 @@ class NetT : public NetBase {
     struct Dec {
         int w[6], b[6], g[5], beta[5], bn[5];
         int h0 = 0, w0 = 0;  // low-res input grid (H/64, W/64)
-        size_t y[5], a[5], dy[5];
+        size_t y[5], a[5], dy[5], bpart[5];
         BnBufs bb[5];
     };
     Dec dec;
@@ -413,6 +446,9 @@ class NetT : public NetBase {
                 dec.y[l] = A.take(n * sizeof(T));
                 dec.a[l] = A.take(n * sizeof(T));
                 dec.dy[l] = A.take(n * sizeof(T));
+                dec.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * 4 * h * w) * co * sizeof(double));
+                // the stride-2 conv data-gradient GEMM writing this layer's output grad (output grid 2h x 2w)
+                need_bnb(ops::col_stats_bytes(B * 4 * h * w, 1, co));
                 dec.bb[l] = bn_plan(A, co);
                 need(ops::bn_ws(B * 4 * h * w, co));
                 need(ops::col_stats_bytes(B * h * w, 4, co));
@@ -465,16 +501,23 @@ class NetT : public NetBase {
             }));
             HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA));
         }
+        ops::BnBwdFuse fuse{};  // layer 4's output grad comes from the single-channel edge conv (separate pass)
         for (int l = 4; l >= 0; --l) {
             const int ci = DEC_CH[l], co = DEC_CH[l + 1];
             const int hl = hs[l], wl = ws_[l];
             const int64_t R = (int64_t)B * 4 * hl * wl;
             T* dy = AT(dec.dy[l]);
-            HLMC_TRY(bn_bwd(s, gA, co, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f, dy, dec.b[l]));
+            HLMC_TRY(bn_bwd(s, gA, co, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f, dy, dec.b[l],
+                            &fuse, reinterpret_cast<double*>(ws + dec.bpart[l])));
             const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
             float* gw = G[dec.w[l]];
             HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
-            HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
+            if (l > 0) {
+                fuse = bn_fuse(AT(dec.y[l - 1]), dec.bb[l - 1], dec.g[l - 1], dec.beta[l - 1]);
+                HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch, nullptr, &fuse));
+            } else {
+                HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
+            }
         }
         *out = gA;
         return HLMC_OK;

@@ -222,7 +222,7 @@ struct SubpixelWeight {
 // act: 0 none, 1 relu
 template <typename OutT>
 struct StoreRM {
-    static constexpr bool kStats = false;
+    static constexpr int kStatMode = 0;
     OutT* out;
     const float* bias;
     int ld, act, accumulate;
@@ -230,14 +230,15 @@ struct StoreRM {
         OutT* r;
     };
     struct Quad {
-        OutT* r0;
+        int64_t off;  // element offset of row m
     };
     __device__ void set_split(int) {}
     __device__ float colbias(int n) const { return bias ? bias[n] : 0.f; }
-    __device__ Quad quad(int m) const { return Quad{out + (int64_t)m * ld}; }
-    __device__ float put(const Quad& q, int r, int n, float v) const {
+    __device__ Quad quad(int m) const { return Quad{(int64_t)m * ld}; }
+    __device__ int64_t row_off(const Quad& q, int r) const { return q.off + (int64_t)r * ld; }
+    __device__ float put(int64_t ro, int n, float v) const {
         if (act == 1) v = v > 0.f ? v : 0.f;
-        OutT* o = q.r0 + (int64_t)r * ld + n;
+        OutT* o = out + ro + n;
         if (accumulate) v += to_f32<OutT>(*o);
         const OutT t = from_f32<OutT>(v);
         *o = t;
@@ -263,7 +264,7 @@ struct StoreRM {
 // Sub-pixel phase store into a high-res NHWC map [B, 2Hi, 2Wi, N]; m = (b, r, c) over the low grid.
 template <typename OutT>
 struct StoreSubpixel {
-    static constexpr bool kStats = false;
+    static constexpr int kStatMode = 0;
     OutT* out;
     const float* bias;
     int Hi, Wi, N;
@@ -273,21 +274,23 @@ struct StoreSubpixel {
         OutT* r;
     };
     struct Quad {
-        OutT* p0;  // row m (Wi % 4 == 0: rows m+1..m+3 are the next low-res columns of the same image row)
+        int64_t off;  // element offset of row m (Wi % 4 == 0: rows m+1..m+3 are the next low-res columns)
         int m;
     };
-    __device__ OutT* pix_ptr(int m) const {
+    __device__ int64_t pix_off(int m) const {
         const int t = (int)dWi.div((uint32_t)m), c = m - t * Wi;
         const int b = (int)dHi.div((uint32_t)t), r = t - b * Hi;
-        return out + (((int64_t)b * 2 * Hi + 2 * r + py) * (2 * Wi) + 2 * c + px) * N;
+        return (((int64_t)b * 2 * Hi + 2 * r + py) * (2 * Wi) + 2 * c + px) * N;
     }
     __device__ void set_split(int) {}
     __device__ float colbias(int n) const { return bias ? bias[n] : 0.f; }
-    __device__ Quad quad(int m) const { return Quad{pix_ptr(m), m}; }
-    __device__ float put(const Quad& q, int r, int n, float v) const {
-        OutT* p = (Wi & 3) == 0 ? q.p0 + (int64_t)2 * r * N : pix_ptr(q.m + r);
+    __device__ Quad quad(int m) const { return Quad{pix_off(m), m}; }
+    __device__ int64_t row_off(const Quad& q, int r) const {
+        return (Wi & 3) == 0 ? q.off + (int64_t)2 * r * N : pix_off(q.m + r);
+    }
+    __device__ float put(int64_t ro, int n, float v) const {
         const OutT t = from_f32<OutT>(v);
-        p[n] = t;
+        out[ro + n] = t;
         return to_f32<OutT>(t);
     }
     __device__ float stored(int n, float v) const {
@@ -312,14 +315,27 @@ struct StoreSubpixel {
 // (f64, fixed-order reduction) over its rows — the [nparts][2C] layout bn_finalize reduces.
 template <class Base>
 struct WithStats : Base {
-    static constexpr bool kStats = true;
+    static constexpr int kStatMode = 1;
     double* part;
     int mtiles;
 };
 
+// Any epilogue whose output is the gradient da of a BatchNorm(+LeakyReLU 0.01) layer's output, plus that
+// layer's fused backward moments (what bn_bwd_moments_kernel computes): with y the layer's BN input at the
+// same NHWC position, xhat = (y - mean) * invstd, z = gamma * xhat + beta, dz = da * lrelu'(z):
+// part[(phase * mtiles + mtile) * 2N + n] = sum dz, [... + N + n] = sum dz * xhat  (f64, fixed order).
+template <class Base, typename YT>
+struct WithBnBwd : Base {
+    static constexpr int kStatMode = 2;
+    double* part;
+    int mtiles;
+    const YT* y;
+    const float *mean, *invstd, *gamma, *beta;
+};
+
 // Split-K partial slab: ws[((phase * S + split) * M + m) * N + n]
 struct StorePartial {
-    static constexpr bool kStats = false;
+    static constexpr int kStatMode = 0;
     float* ws;
     int M, N, S;
     int phase, split;
@@ -330,31 +346,41 @@ struct StorePartial {
     __device__ Row row(int m) const { return Row{ws + (((int64_t)phase * S + split) * M + m) * N}; }
     __device__ void store(const Row& rw, int n, float v) const { rw.r[n] = v; }
     struct Quad {
-        float* r0;
+        int64_t off;
     };
     __device__ void set_split(int z) { split = z; }
     __device__ float colbias(int) const { return 0.f; }
-    __device__ Quad quad(int m) const { return Quad{ws + (((int64_t)phase * S + split) * M + m) * N}; }
-    __device__ float put(const Quad& q, int r, int n, float v) const {
-        q.r0[(int64_t)r * N + n] = v;
+    __device__ Quad quad(int m) const { return Quad{(((int64_t)phase * S + split) * M + m) * N}; }
+    __device__ int64_t row_off(const Quad& q, int r) const { return q.off + (int64_t)r * N; }
+    __device__ float put(int64_t ro, int n, float v) const {
+        ws[ro + n] = v;
         return v;
     }
 };
 
 // Store one wave's TM x TN grid of 16x16 accumulator tiles through the epilogue (C/D map: col = lane & 15,
-// rows (lane >> 4) * 4 + 0..3), bias hoisted per column, one quad() per 4-row group; with EP::kStats the
-// per-column sum / sum of squares of the stored values over this lane's rows go to cs / cq (f64).
+// rows (lane >> 4) * 4 + 0..3), bias hoisted per column, one quad() per 4-row group.  EP::kStatMode 1: per-column
+// sum / sum of squares of the stored values over this lane's rows into cs / cq (f64); 2: the fused BatchNorm
+// backward moments (WithBnBwd) of the stored gradient.
 template <int TM, int TN, class EP>
 __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)[TM][TN], int mb, int nb, int lane,
                                               int M, int N, double (&cs)[TN], double (&cq)[TN]) {
     float bias[TN];
     int ncol[TN];
+    float mu[TN], is[TN], ga[TN], be[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         ncol[j] = nb + j * 16 + (lane & 15);
-        bias[j] = ncol[j] < N ? ep.colbias(ncol[j]) : 0.f;
+        const bool ok = ncol[j] < N;
+        bias[j] = ok ? ep.colbias(ncol[j]) : 0.f;
         cs[j] = 0.0;
         cq[j] = 0.0;
+        if constexpr (EP::kStatMode == 2) {
+            mu[j] = ok ? ep.mean[ncol[j]] : 0.f;
+            is[j] = ok ? ep.invstd[ncol[j]] : 0.f;
+            ga[j] = ok ? ep.gamma[ncol[j]] : 0.f;
+            be[j] = ok ? ep.beta[ncol[j]] : 0.f;
+        }
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -364,13 +390,20 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             if (m + r >= M) continue;
+            const int64_t ro = ep.row_off(q, r);
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 if (ncol[j] >= N) continue;
-                const float v = ep.put(q, r, ncol[j], acc[i][j][r] + bias[j]);
-                if constexpr (EP::kStats) {
+                const float v = ep.put(ro, ncol[j], acc[i][j][r] + bias[j]);
+                if constexpr (EP::kStatMode == 1) {
                     cs[j] += v;
                     cq[j] += (double)v * v;
+                } else if constexpr (EP::kStatMode == 2) {
+                    const float xh = (to_f32(ep.y[ro + ncol[j]]) - mu[j]) * is[j];
+                    const float z = xh * ga[j] + be[j];
+                    const float dz = v * (z > 0.f ? 1.f : 0.01f);
+                    cs[j] += dz;
+                    cq[j] += (double)dz * xh;
                 }
             }
         }
@@ -524,7 +557,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
     }
     double cs[TN], cq[TN];
     epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
-    if constexpr (EP::kStats) {
+    if constexpr (EP::kStatMode != 0) {
         // per-column sum / sum of squares of the stored values over the block's rows: lane sums over its
         // 4*TM rows (epilogue_tile), xor-16/32 shuffles over the wave's row groups, then the waves of one
         // column strip in order
@@ -689,7 +722,7 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
     }
     double cs[TN], cq[TN];
     epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
-    if constexpr (EP::kStats) {
+    if constexpr (EP::kStatMode != 0) {
         constexpr int WAVES_M = BM / WM;
         static_assert(WAVES_M * 2 * BN * 8 <= NS * STG, "stats scratch fits the staging ring");
         __syncthreads();  // every wave is done with the ring: reuse it for the column-sum scratch

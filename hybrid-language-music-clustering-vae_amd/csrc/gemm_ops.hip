@@ -78,7 +78,7 @@ void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, cons
 
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
 int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
-              ops::ColStats* st = nullptr, bool dma_ok = true) {
+              ops::ColStats* st = nullptr, bool dma_ok = true, ops::BnBwdFuse* bf = nullptr) {
     constexpr int BK = gemm_bk<T>();
     const int tmn = cdiv(M, BM) * cdiv(N, BN);
     Plan pl = plan_nt(tmn * phases, Kmax, BK);
@@ -87,6 +87,19 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     const bool long_k = Kmax >= 1024;
     const int pipe = (dma_ok && BN >= 32 && BM >= 64) ? nt_pipe_select(pl.ksl) : 0;
     if (st) st->nparts = 0;
+    if (bf) bf->nparts = 0;
+    if (pl.S == 1 && bf && bf->part) {  // single pass: the epilogue also emits the BN-backward moments
+        WithBnBwd<EP, T> epb;
+        static_cast<EP&>(epb) = ep;
+        epb.part = bf->part;
+        epb.mtiles = cdiv(M, BM);
+        epb.y = static_cast<const T*>(bf->y);
+        epb.mean = bf->mean; epb.invstd = bf->invstd; epb.gamma = bf->gamma; epb.beta = bf->beta;
+        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, epb, M, N, pl.ksl, long_k, pipe);
+        HLMC_LAUNCHED();
+        bf->nparts = phases * cdiv(M, BM);
+        return HLMC_OK;
+    }
     if (pl.S == 1 && st && st->part) {  // single pass: the epilogue also emits the column statistics
         WithStats<EP> eps;
         static_cast<EP&>(eps) = ep;
@@ -132,12 +145,12 @@ inline int nt_tile(int M, int N, int phases) {
 }
 template <typename T, class AL, class BL, class EP>
 int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
-                ops::ColStats* st = nullptr) {
+                ops::ColStats* st = nullptr, ops::BnBwdFuse* bf = nullptr) {
     switch (nt_tile(M, N, phases)) {
-        case 0: return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
-        case 1: return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
-        case 2: return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
-        default: return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+        case 0: return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, bf);
+        case 1: return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, bf);
+        case 2: return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, bf);
+        default: return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, bf);
     }
 }
 template <typename T>
@@ -231,7 +244,7 @@ namespace ops {
 
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-            ColStats* st) {
+            ColStats* st, BnBwdFuse* bf) {
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % V == 0, "conv_s2: need even H/W and Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "conv_s2: 16-byte alignment");
@@ -241,7 +254,7 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     StoreRM<T> ep{y, bias, Co, 0, 0};
     probe::site(probe::kConvS2, 2.0 * M * Co * K,
                 (double)sizeof(T) * ((double)B * Hi * Wi * Ci + (double)Co * K + (double)M * Co));
-    return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
+    return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st, bf);
 }
 size_t col_stats_bytes(int64_t M, int phases, int C) { return (size_t)phases * cdiv((int)M, 64) * 2 * C * sizeof(double); }
 
@@ -252,7 +265,7 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {
 
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-             ColStats* st) {
+             ColStats* st, BnBwdFuse* bf) {
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(Ci % V == 0, "subpixel: Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "subpixel: 16-byte alignment");
@@ -263,7 +276,7 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
     // the 4 phases hold 1 + 2 + 2 + 4 = 9 taps: 9 Ci MACs per (low-res pixel, output channel)
     probe::site(probe::kSubpixel, 2.0 * M * Co * 9.0 * Ci,
                 (double)sizeof(T) * ((double)M * Ci + 9.0 * Ci * Co + 4.0 * M * Co));
-    return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
+    return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st, bf);
 }
 template <typename T>
 size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co) {
@@ -320,10 +333,10 @@ size_t linear_wgrad_ws(int Mb, int N, int K) {
 
 #define INST(T)                                                                                                     \
     template int conv_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,         \
-                            ColStats*);                                                                              \
+                            ColStats*, BnBwdFuse*);                                                                  \
     template size_t conv_s2_ws<T>(int, int, int, int, int);                                                        \
     template int subpixel<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,        \
-                             ColStats*);                                                                             \
+                             ColStats*, BnBwdFuse*);                                                                 \
     template size_t subpixel_ws<T>(int, int, int, int, int);                                                       \
     template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws);                \
     template size_t wgrad_s2_ws<T>(int, int, int, int, int);                                                       \

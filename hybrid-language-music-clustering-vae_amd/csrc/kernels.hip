@@ -807,7 +807,7 @@ int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
-               float* dbeta, float* dbias, Ws ws) {
+               float* dbeta, float* dbias, Ws ws, const BnBwdFuse* fused, double* bias_part) {
     HLMC_TRY(check_bn_shape<T>(C));
     HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act_bwd: grad row stride must be a multiple of 16 bytes");
     const int nblk = col_blocks(R);
@@ -815,17 +815,32 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
     const int64_t rpb = (R + nblk - 1) / nblk;
     double* part = reinterpret_cast<double*>(ws.p);
     float* sums = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
-    bn_bwd_moments_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb, part);
-    HLMC_LAUNCHED();
-    bn_bwd_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, dgamma, dbeta, sums);
-    HLMC_LAUNCHED();
+    if (fused && fused->nparts > 0) {  // moments came with the producing GEMM's epilogue
+        HLMC_CHECK_ARG(lda == C && !mask && act == 0, "bn_act_bwd: fused moments need a dense lrelu layer");
+        bn_bwd_finalize_kernel<<<C, 256, 0, s>>>(fused->part, fused->nparts, C, dgamma, dbeta, sums);
+        HLMC_LAUNCHED();
+    } else {
+        bn_bwd_moments_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale,
+                                                           rpb, part);
+        HLMC_LAUNCHED();
+        bn_bwd_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, dgamma, dbeta, sums);
+        HLMC_LAUNCHED();
+    }
+    double* bpart = bias_part ? bias_part : part;
     bn_bwd_apply_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
-                                                     dy, rpb, part);
+                                                     dy, rpb, bpart);
     HLMC_LAUNCHED();
-    if (dbias) {
+    if (dbias && !bias_part) {
         colsum_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, dbias);
         HLMC_LAUNCHED();
     }
+    return HLMC_OK;
+}
+int bn_bias_parts(int64_t R) { return col_blocks(R); }
+int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out) {
+    HLMC_CHECK_ARG(part && out && nparts > 0 && C > 0, "colsum_finalize: bad arguments");
+    colsum_finalize_kernel<<<C, 256, 0, s>>>(part, nparts, C, out);
+    HLMC_LAUNCHED();
     return HLMC_OK;
 }
 
@@ -1049,7 +1064,8 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
     template int bn_act<T>(hipStream_t, const T*, int64_t, int, const float*, const float*, const float*, const float*, \
                            int, const uint8_t*, float, T*, int);                                                      \
     template int bn_act_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,          \
-                               const float*, const float*, int, const uint8_t*, float, T*, float*, float*, float*, Ws);\
+                               const float*, const float*, int, const uint8_t*, float, T*, float*, float*, float*, Ws, \
+                               const BnBwdFuse*, double*);                                                           \
     template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*);        \
     template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);          \
     template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws);                    \

@@ -20,10 +20,19 @@ struct ColStats {
     int nparts;
 };
 size_t col_stats_bytes(int64_t M, int phases, int C);  // bytes of part for M output rows x phases
+// Optional fused BatchNorm(+LeakyReLU 0.01) backward moments of a data-gradient GEMM's output da (see
+// WithBnBwd): y / mean / invstd / gamma / beta of the BN layer whose output gradient the GEMM writes.  When
+// the launch is single-pass, part receives nparts rows of [sum dz | sum dz*xhat] (else nparts = 0).
+struct BnBwdFuse {
+    const void* y;
+    const float *mean, *invstd, *gamma, *beta;
+    double* part;
+    int nparts;
+};
 // y[B, Hi/2, Wi/2, Co] = conv3x3_s2_p1(x[B,Hi,Wi,Ci]) + bias ; wp packed [Co][3][3][Ci]
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-            ColStats* st = nullptr);
+            ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
 template <typename T>
 size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -31,7 +40,7 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 // (also the data gradient of a stride-2 conv with the conv weight re-packed [Ci_conv][3][3][Co_conv])
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-             ColStats* st = nullptr);
+             ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
 template <typename T>
 size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -81,11 +90,17 @@ int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, in
 template <typename T>
 int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const float* invstd, const float* gamma,
            const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda);
-// backward through act+BN: dy from da (ld lda); dgamma, dbeta, dbias(sum of dy; nullable)
+// backward through act+BN: dy from da (ld lda); dgamma, dbeta, dbias(sum of dy; nullable).
+// fused (nullable): moments already emitted by the producing GEMM (BnBwdFuse with nparts > 0) -> no moments pass.
+// bias_part (nullable): write the dbias column partials there (bn_bias_parts(R) rows of C) and leave their
+// reduction to the caller (colsum_finalize) instead of reducing into dbias here.
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
-               float* dbeta, float* dbias, Ws ws);
+               float* dbeta, float* dbias, Ws ws, const BnBwdFuse* fused = nullptr, double* bias_part = nullptr);
+int bn_bias_parts(int64_t R);  // partial rows of bn_act_bwd's bias column sums
+// out[c] = sum_k part[k * C + c], k < nparts (fixed order, f64)
+int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out);
 
 // ---------------------------------------------------------------- misc elementwise (kernels.hip)
 template <typename T> int cast_from_f32(hipStream_t s, const float* x, T* y, int64_t n);

@@ -18,8 +18,8 @@ from .features import (StandardScaler, extract_mel_spectrogram, mean_std_pool, m
 from .losses import cvae_loss_function, loss_function, vae_loss
 from .models import VAE, ConditionalVAE, HybridVAE
 from .optim import Adam
-from .train import Trainer
+from .train import GraphedStep, Trainer
 
 __all__ = ["HybridVAE", "ConditionalVAE", "VAE", "loss_function", "cvae_loss_function", "vae_loss", "melspectrogram",
            "power_to_db", "mfcc", "extract_mel_spectrogram", "mean_std_pool", "mel_filterbank", "StandardScaler",
-           "KMeans", "Adam", "Trainer"]
+           "KMeans", "Adam", "Trainer", "GraphedStep"]

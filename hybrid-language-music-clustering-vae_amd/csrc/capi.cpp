@@ -239,6 +239,17 @@ int hlmc_net_adam_step(hlmc_net* h, void* stream, float* const* exp_avg, float* 
     HLMC_CHECK_ARG(!h->impl->P.empty(), "net is not bound");
     return h->impl->adam_step(S(stream), exp_avg, exp_avg_sq, ops::AdamArgs{lr, b1, b2, eps, wd, step});
 }
+int hlmc_net_adam_step_dev(hlmc_net* h, void* stream, float* const* exp_avg, float* const* exp_avg_sq,
+                           const float* coef_dev) {
+    HLMC_CHECK_ARG(h && exp_avg && exp_avg_sq && coef_dev, "bad arguments");
+    HLMC_CHECK_ARG(!h->impl->P.empty(), "net is not bound");
+    return h->impl->adam_step(S(stream), exp_avg, exp_avg_sq, ops::AdamArgs{0.f, 0.f, 0.f, 0.f, 0.f, 1}, coef_dev);
+}
+int hlmc_adam_coef(float lr, float b1, float b2, float eps, float wd, int step, float* out6) {
+    HLMC_CHECK_ARG(out6 && step >= 1, "bad arguments");
+    ops::adam_coef_host(ops::AdamArgs{lr, b1, b2, eps, wd, step}, out6);
+    return HLMC_OK;
+}
 int hlmc_net_set_trust_packs(hlmc_net* h, int trust) {
     HLMC_CHECK_ARG(h, "net is NULL");
     h->impl->trust_packs = trust != 0;

@@ -91,7 +91,7 @@ class NetT : public NetBase {
         packs_valid = true;
         return HLMC_OK;
     }
-    int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a) override {
+    int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a, const float* coef_dev) override {
         // one launch: torch-Adam update of every parameter + refresh of the packed GEMM weights
         const size_t np = params.size();
         if (ajobs_m.size() != np || !std::equal(ajobs_m.begin(), ajobs_m.end(), m) ||
@@ -109,7 +109,8 @@ class NetT : public NetBase {
             HLMC_HIP(hipMemcpyAsync(state + ajobs_off, ajobs.data(), ajobs.size() * sizeof(ops::AdamJob),
                                     hipMemcpyHostToDevice, s));
         }
-        HLMC_TRY(ops::adam_pack<T>(s, reinterpret_cast<const ops::AdamJob*>(state + ajobs_off), (int)np, adam_tiles, a));
+        HLMC_TRY(ops::adam_pack<T>(s, reinterpret_cast<const ops::AdamJob*>(state + ajobs_off), (int)np, adam_tiles, a,
+                                   coef_dev));
         packs_valid = true;
         return HLMC_OK;
     }

@@ -78,7 +78,9 @@ class NetBase {
     virtual int forward(hipStream_t s, const ForwardArgs& a) = 0;
     virtual int backward(hipStream_t s, const BackwardArgs& a) = 0;
     // Adam over all bound parameters with the packed GEMM weights refreshed in the same pass
-    virtual int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a) = 0;
+    // coef_dev (nullable): device coefficients (ops::adam_coef_host layout) instead of a's step-dependent ones
+    virtual int adam_step(hipStream_t s, float* const* m, float* const* v, const ops::AdamArgs& a,
+                          const float* coef_dev = nullptr) = 0;
     bool trust_packs = false;  // forward skips re-packing when packs are known current
     bool packs_valid = false;
 

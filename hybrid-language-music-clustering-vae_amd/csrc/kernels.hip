@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <vector>
 
 namespace hlmc {
@@ -661,7 +662,10 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, AdamCoef c) {
 // writes each (i0, tap) segment of P0 and each (i1, tap) segment of P1 as 32 consecutive elements.
 // Unpacked tensors (BatchNorm affine, biases) are 4096-element chunks of the same launch.
 template <typename T>
-__global__ __launch_bounds__(256) void adam_pack_kernel(const ops::AdamJob* __restrict__ jobs, int njobs, AdamCoef c) {
+// cdev (nullable): coefficients read from device memory (graph replays: the host refreshes them per step)
+__global__ __launch_bounds__(256) void adam_pack_kernel(const ops::AdamJob* __restrict__ jobs, int njobs, AdamCoef cv,
+                                                        const AdamCoef* __restrict__ cdev) {
+    const AdamCoef c = cdev ? *cdev : cv;
     const int bid = blockIdx.x;
     int lo = 0, hi = njobs - 1;
     while (lo < hi) {
@@ -1042,10 +1046,17 @@ int adam_job_tiles(AdamJob& j) {
     return ((j.d0 + 31) / 32) * j.nt1;
 }
 
+void adam_coef_host(const AdamArgs& a, float* out6) {
+    const AdamCoef c = adam_coef(a);
+    static_assert(sizeof(AdamCoef) == 6 * sizeof(float), "AdamCoef layout");
+    std::memcpy(out6, &c, sizeof(c));
+}
+
 template <typename T>
-int adam_pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles, AdamArgs a) {
+int adam_pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles, AdamArgs a, const float* coef_dev) {
     if (njobs == 0 || total_tiles == 0) return HLMC_OK;
-    adam_pack_kernel<T><<<total_tiles, 256, 0, s>>>(jobs_dev, njobs, adam_coef(a));
+    adam_pack_kernel<T><<<total_tiles, 256, 0, s>>>(jobs_dev, njobs, adam_coef(a),
+                                                    reinterpret_cast<const AdamCoef*>(coef_dev));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1080,7 +1091,7 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
     template int reparam_fwd<T>(hipStream_t, const float*, const float*, const float*, int, int, T*, int);           \
     template int reparam_bwd<T>(hipStream_t, const T*, int, const float*, const float*, int, int, float*, float*);   \
     template int pack<T>(hipStream_t, const AdamJob*, int, int);                                                     \
-    template int adam_pack<T>(hipStream_t, const AdamJob*, int, int, AdamArgs);
+    template int adam_pack<T>(hipStream_t, const AdamJob*, int, int, AdamArgs, const float*);
 
 INST(float)
 INST(bf16)

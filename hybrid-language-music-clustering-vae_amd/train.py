@@ -56,6 +56,11 @@ class Trainer:
             L.check(L.lib().hlmc_net_set_bucket_sync(self.net.h, 1), "hlmc_net_set_bucket_sync")
             self._comm = torch.cuda.Stream(device=dev)
         self._mv = (L.vp_array([t.data_ptr() for t in mv]), L.vp_array([t.data_ptr() for t in vv]))
+        # graph replay (GraphedStep): Adam reads its step-dependent coefficients from _coef_dev, refreshed from a
+        # pinned host ring before every launch
+        self._graph = False
+        self._coef_dev = torch.zeros(6, dtype=torch.float32, device=dev)
+        self._coef_ring = torch.zeros(1024, 6, dtype=torch.float32).pin_memory() if dev.type == "cuda" else None
         # weights change only through hlmc_net_adam_step (which refreshes the packed GEMM layouts)
         L.check(L.lib().hlmc_net_set_trust_packs(self.net.h, 1))
         self._cache = {}
@@ -109,11 +114,25 @@ class Trainer:
                 self._allreduce_overlapped()
             else:
                 self.allreduce_grads()
+        if self._graph:  # coefficients staged by prepare_step_coefficients()
+            L.check(lib.hlmc_net_adam_step_dev(self.net.h, s, *self._mv, self._coef_dev.data_ptr()),
+                    "hlmc_net_adam_step_dev")
+            return c["sums"]
         self.step_count += 1
         b1, b2 = self.betas
         L.check(lib.hlmc_net_adam_step(self.net.h, s, *self._mv, float(self.lr), float(b1), float(b2), float(self.eps),
                                        float(self.wd), self.step_count), "hlmc_net_adam_step")
         return c["sums"]
+
+    def prepare_step_coefficients(self):
+        """Advance the step counter and stage that step's Adam coefficients (host -> pinned ring -> device,
+        stream-ordered) for the next graph-mode step."""
+        self.step_count += 1
+        slot = self._coef_ring[self.step_count % self._coef_ring.shape[0]]
+        b1, b2 = self.betas
+        L.check(L.lib().hlmc_adam_coef(float(self.lr), float(b1), float(b2), float(self.eps), float(self.wd),
+                                       self.step_count, slot.data_ptr()), "hlmc_adam_coef")
+        self._coef_dev.copy_(slot, non_blocking=True)
 
     def release(self):
         """Hand the model back to the nn.Module path (forward re-packs weights every call again)."""
@@ -187,3 +206,46 @@ def _allreduce_sum(buf, grad_dtype, group, async_op=False):
 class _Done:
     def wait(self):
         return True
+
+
+class GraphedStep:
+    """A whole train step captured once into a HIP graph and replayed (hipGraphLaunch): `body()` issues the
+    step's device work on static tensors — e.g. the mel stage followed by ``trainer.step(...)`` — and returns
+    its outputs.  The engine's weight-gradient stream joins the capture through its fork/join events; torch's
+    RNG (the reparameterisation noise) is graph-safe; Adam's step-dependent coefficients are staged before
+    every replay.  `warmup` eager steps (real optimisation steps) run first so every buffer, packed weight
+    and job list exists before capture.  Single-process only: the data-parallel path keeps the eager
+    bucketed all-reduce."""
+
+    def __init__(self, trainer, body, warmup=2, before_capture=None):
+        if trainer.distributed:
+            raise L.HLMCError("GraphedStep is single-process; data parallel training uses Trainer.step")
+        self.trainer = trainer
+        trainer._graph = True
+        try:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(max(1, warmup)):
+                    trainer.prepare_step_coefficients()
+                    body()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            if before_capture is not None:
+                before_capture()
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = body()
+        except Exception:
+            trainer._graph = False
+            raise
+
+    def __call__(self):
+        self.trainer.prepare_step_coefficients()
+        self.graph.replay()
+        return self.out
+
+    def release(self):
+        """Back to eager Trainer.step."""
+        self.trainer._graph = False
+        self.graph.reset()

@@ -120,6 +120,12 @@ int hlmc_net_backward(hlmc_net* net, void* stream, int64_t batch, const float* d
  * refreshing the packed GEMM weight layouts in the same pass. */
 int hlmc_net_adam_step(hlmc_net* net, void* stream, float* const* exp_avg, float* const* exp_avg_sq, float lr,
                        float beta1, float beta2, float eps, float weight_decay, int step);
+/* The same step with its step-dependent coefficients read from device memory (coef_dev: 6 floats written by
+ * hlmc_adam_coef on the host and copied before each launch) — the form a captured HIP graph replays. */
+int hlmc_net_adam_step_dev(hlmc_net* net, void* stream, float* const* exp_avg, float* const* exp_avg_sq,
+                           const float* coef_dev);
+/* torch.optim.Adam step coefficients for `step` (host): {b1, b2, eps, wd, lr/(1-b1^step), sqrt(1-b2^step)}. */
+int hlmc_adam_coef(float lr, float beta1, float beta2, float eps, float weight_decay, int step, float* out6);
 /* trust != 0: forward re-packs weights only when they changed through hlmc_net_adam_step (a caller that
  * writes parameters any other way must pass 0, the default, so forward always re-packs). */
 int hlmc_net_set_trust_packs(hlmc_net* net, int trust);

@@ -87,3 +87,37 @@ def test_trainer_dp_overlapped_allreduce_world1(cuda, kind):
     finally:
         if own:
             dist.destroy_process_group()
+
+
+def test_graphed_step_equals_eager(cuda):
+    """GraphedStep (whole step captured into a HIP graph, Adam coefficients staged per replay) updates the
+    parameters exactly like eager Trainer.step on the same batches."""
+    def make():
+        torch.manual_seed(42)
+        return hlmc_amd.HybridVAE(128, 384, (128, 128), compute_dtype="bf16").cuda()
+    a, b = make(), make()
+    ta = hlmc_amd.Trainer(a, lr=1e-3)
+    tb = hlmc_amd.Trainer(b, lr=1e-3)
+    g = torch.Generator().manual_seed(3)
+    batches = [(torch.randn(8, 1, 128, 128, generator=g), torch.randn(8, 384, generator=g) / 384 ** 0.5,
+                torch.randn(8, 128, generator=g)) for _ in range(4)]
+    audio, text, eps = (t.clone().cuda() for t in batches[0])
+
+    def body():
+        return tb.step(audio, text, eps=eps)
+
+    gs = hlmc_amd.GraphedStep(tb, body, warmup=1)   # the warmup is batch 0's real step
+    for i, (x, t, e) in enumerate(batches):
+        sa = ta.step(x.cuda(), t.cuda(), eps=e.cuda())
+        if i > 0:
+            audio.copy_(x)
+            text.copy_(t)
+            eps.copy_(e)
+            sb = gs()
+            torch.cuda.synchronize()
+            assert torch.equal(sa, sb), i
+    torch.cuda.synchronize()
+    assert ta.step_count == tb.step_count == 4
+    for (n, p), q in zip(a.named_parameters(), b.parameters()):
+        assert torch.equal(p, q), n
+    gs.release()

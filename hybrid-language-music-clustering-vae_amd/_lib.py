@@ -54,6 +54,8 @@ _SIGS = {
     "hlmc_net_set_trust_packs": (c_int, [c_vp, c_int]),
     "hlmc_net_adam_step_dev": (c_int, [c_vp, c_vp, P_vp, P_vp, c_vp]),
     "hlmc_adam_coef": (c_int, [c_f32, c_f32, c_f32, c_f32, c_f32, c_int, c_vp]),
+    "hlmc_net_set_overlap_adam": (c_int, [c_vp, c_int]),
+    "hlmc_net_settle": (c_int, [c_vp, c_vp]),
     "hlmc_net_grad_buckets": (c_int, [c_vp, C.POINTER(c_int), c_int]),
     "hlmc_net_set_bucket_sync": (c_int, [c_vp, c_int]),
     "hlmc_net_bucket_wait": (c_int, [c_vp, c_int, c_vp]),

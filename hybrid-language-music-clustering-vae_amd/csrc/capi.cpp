@@ -256,6 +256,15 @@ int hlmc_net_set_trust_packs(hlmc_net* h, int trust) {
     if (!trust) h->impl->packs_valid = false;
     return HLMC_OK;
 }
+int hlmc_net_settle(hlmc_net* h, void* stream) {
+    HLMC_CHECK_ARG(h, "net is NULL");
+    return h->impl->settle(S(stream));
+}
+int hlmc_net_set_overlap_adam(hlmc_net* h, int enable) {
+    HLMC_CHECK_ARG(h, "net is NULL");
+    h->impl->overlap_adam = enable != 0;
+    return HLMC_OK;
+}
 int hlmc_net_grad_buckets(const hlmc_net* h, int* starts, int cap) {
     HLMC_CHECK_ARG(h && starts && cap > 0, "NULL argument");
     const auto& b = h->impl->bucket_starts;

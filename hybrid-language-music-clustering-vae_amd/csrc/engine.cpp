@@ -109,8 +109,18 @@ class NetT : public NetBase {
             HLMC_HIP(hipMemcpyAsync(state + ajobs_off, ajobs.data(), ajobs.size() * sizeof(ops::AdamJob),
                                     hipMemcpyHostToDevice, s));
         }
-        HLMC_TRY(ops::adam_pack<T>(s, reinterpret_cast<const ops::AdamJob*>(state + ajobs_off), (int)np, adam_tiles, a,
-                                   coef_dev));
+        const auto* jd = reinterpret_cast<const ops::AdamJob*>(state + ajobs_off);
+        if (join_pending) {
+            // every gradient but the late ones is final once the side stream passed prelate_ev
+            const int tsplit = ajobs[this->late_params].tile0;
+            HLMC_HIP(hipStreamWaitEvent(s, prelate_ev, 0));
+            HLMC_TRY(ops::adam_pack<T>(s, jd, (int)np, adam_tiles, a, coef_dev, tsplit));
+            HLMC_TRY(join(s));
+            join_pending = false;
+            HLMC_TRY(ops::adam_pack<T>(s, jd, (int)np, tsplit, a, coef_dev, 0));
+        } else {
+            HLMC_TRY(ops::adam_pack<T>(s, jd, (int)np, adam_tiles, a, coef_dev));
+        }
         packs_valid = true;
         return HLMC_OK;
     }
@@ -164,10 +174,35 @@ class NetT : public NetBase {
     std::vector<hipEvent_t> evs;
     int ev_next = 0;
     bool use_side = true;
+    hipEvent_t prelate_ev = nullptr;  // side stream passed every weight gradient except the late ones
+    bool join_pending = false;         // backward left the side stream running (NetBase::overlap_adam)
     ~NetT() override {
         if (s2) (void)hipStreamDestroy(s2);
         for (auto e : evs) (void)hipEventDestroy(e);
         for (auto e : this->bucket_ev) (void)hipEventDestroy(e);
+        if (prelate_ev) (void)hipEventDestroy(prelate_ev);
+    }
+    bool tail_overlap() const { return use_side && this->overlap_adam && !this->bucket_sync && this->late_params > 0; }
+    // called in backward once every non-late weight gradient has been issued
+    int prelate(hipStream_t s) {
+        if (!tail_overlap()) return HLMC_OK;
+        HLMC_TRY(fork(s));
+        HLMC_HIP(hipEventRecord(prelate_ev, s2));
+        return HLMC_OK;
+    }
+    // end of backward: join the weight-gradient stream, or leave it to adam_step (tail overlap)
+    // a pending tail (backward without the adam_step that joins it) is joined before anything else runs
+    int settle(hipStream_t s) override {
+        if (!join_pending) return HLMC_OK;
+        join_pending = false;
+        return join(s);
+    }
+    int finish_backward(hipStream_t s) {
+        if (tail_overlap()) {
+            join_pending = true;
+            return HLMC_OK;
+        }
+        return join(s);
     }
     int side_init() {
         static const bool env_off = [] {
@@ -179,6 +214,7 @@ class NetT : public NetBase {
             HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
             evs.resize(32);
             for (auto& e : evs) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HLMC_HIP(hipEventCreateWithFlags(&prelate_ev, hipEventDisableTiming));
         }
         if (this->bucket_sync && this->bucket_ev.size() != this->bucket_starts.size()) {
             for (auto e : this->bucket_ev) (void)hipEventDestroy(e);
@@ -200,7 +236,7 @@ class NetT : public NetBase {
         return HLMC_OK;
     }
     int join(hipStream_t s) {
-        if (!use_side) return HLMC_OK;
+        if (!use_side || !s2) return HLMC_OK;
         hipEvent_t e = next_ev();
         HLMC_HIP(hipEventRecord(e, s2));
         HLMC_HIP(hipStreamWaitEvent(s, e, 0));
@@ -408,6 +444,7 @@ class NetT : public NetBase {
                 HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch, nullptr, &fuse));
             }
             if (l == 3 && bucket_hi >= 0) HLMC_TRY(mark(s, bucket_hi));
+            if (l == 2) HLMC_TRY(prelate(s));  // layers 0-1 (late_params) remain
         }
         return HLMC_OK;
     }
@@ -601,6 +638,7 @@ class HybridNet : public NetT<T> {
         this->finalize_state();
         // backward finishes: audio + text decoder | audio_fc .. audio_decoder_fc | encoder layers 3-5 | layers 0-2
         this->bucket_starts = {this->dec.w[0], afc_w, this->enc.w[3], 0};
+        this->late_params = this->enc.w[2];  // encoder layers 0-1: the last weight gradients of backward
     }
 
     void plan(Arena& A, int64_t B) override {
@@ -690,6 +728,7 @@ class HybridNet : public NetT<T> {
         HLMC_CHECK_ARG(B >= 2 || !a.train, "BatchNorm in train mode needs batch >= 2");
         this->ws_bytes(B);
         this->set_ws(a.ws);
+        HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
         HLMC_TRY(encode(s, a, B));
         if (a.encode_only) return HLMC_OK;
@@ -716,6 +755,7 @@ class HybridNet : public NetT<T> {
         HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
+        HLMC_TRY(this->settle(s));
         T* gA = AT(gA_);
         // ---- text decoder
         if (text) {
@@ -763,7 +803,7 @@ class HybridNet : public NetT<T> {
         HLMC_TRY(this->mark(s, 1));
         HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(gflat_), ldF, B, H / 64, W / 64, 512, gA));
         HLMC_TRY(this->enc_bwd(s, B, gA, 2));
-        HLMC_TRY(this->join(s));
+        HLMC_TRY(this->finish_backward(s));
         return this->mark(s, 3);
     }
 };
@@ -819,6 +859,7 @@ class CvaeNet : public NetT<T> {
         this->finalize_state();
         // backward finishes: text + audio decoder | text_encoder .. decoder_fc | encoder layers 3-5 | layers 0-2
         this->bucket_starts = {td_w[0], te_w, this->enc.w[3], 0};
+        this->late_params = this->enc.w[2];
     }
 
     void plan(Arena& A, int64_t B) override {
@@ -882,6 +923,7 @@ class CvaeNet : public NetT<T> {
         HLMC_CHECK_ARG(B >= 2 || !a.train, "BatchNorm in train mode needs batch >= 2");
         this->ws_bytes(B);
         this->set_ws(a.ws);
+        HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
         HLMC_TRY(encode(s, a, B));
         if (a.encode_only) return HLMC_OK;
@@ -904,6 +946,7 @@ class CvaeNet : public NetT<T> {
         HLMC_CHECK_ARG(a.d_recon_text, "d_recon_text required");
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
+        HLMC_TRY(this->settle(s));
         T* gA = AT(gA_);
         // text decoder
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon_text, TD, AT(grt_), ldT, B, TD));
@@ -935,7 +978,7 @@ class CvaeNet : public NetT<T> {
         // audio encoder
         HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(gX_), ldX, B, H / 64, W / 64, 512, gA));
         HLMC_TRY(this->enc_bwd(s, B, gA, 2));
-        HLMC_TRY(this->join(s));
+        HLMC_TRY(this->finish_backward(s));
         return this->mark(s, 3);
     }
 };
@@ -1078,6 +1121,7 @@ class SimpleNet : public NetT<T> {
         HLMC_CHECK_ARG(B >= 2 || !a.train, "BatchNorm in train mode needs batch >= 2");
         this->ws_bytes(B);
         this->set_ws(a.ws);
+        HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
         HLMC_TRY(encode(s, a, B));
         if (a.encode_only) return HLMC_OK;
@@ -1103,6 +1147,7 @@ class SimpleNet : public NetT<T> {
         HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
+        HLMC_TRY(this->settle(s));
         T* g1 = AT(gx1_);
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon, D, AT(grec_), ldD, B, D));
         const Blk& last = decb.back();

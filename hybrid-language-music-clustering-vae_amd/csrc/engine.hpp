@@ -91,6 +91,14 @@ class NetBase {
     std::vector<int> bucket_starts{0};
     std::vector<hipEvent_t> bucket_ev;
     bool bucket_sync = false;
+
+    // Tail overlap (single process): the gradients of params [0, late_params) are the last the weight-gradient
+    // stream writes.  With overlap_adam set (and no bucket sync), backward() leaves that stream running and
+    // adam_step() updates every other parameter first, joins, then updates the late ones — the first part of
+    // Adam runs under the tail of the backward pass.
+    int late_params = 0;
+    bool overlap_adam = false;
+    virtual int settle(hipStream_t s) = 0;  // make every gradient of the last backward final on s
 };
 
 // factory: kind 0 hybrid, 1 cvae, 2 simple; cfg per hlmc.h

@@ -663,10 +663,11 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, AdamCoef c) {
 // Unpacked tensors (BatchNorm affine, biases) are 4096-element chunks of the same launch.
 template <typename T>
 // cdev (nullable): coefficients read from device memory (graph replays: the host refreshes them per step)
+// tile_base: first tile of this launch (a launch may cover a contiguous tile range of the job list)
 __global__ __launch_bounds__(256) void adam_pack_kernel(const ops::AdamJob* __restrict__ jobs, int njobs, AdamCoef cv,
-                                                        const AdamCoef* __restrict__ cdev) {
+                                                        const AdamCoef* __restrict__ cdev, int tile_base) {
     const AdamCoef c = cdev ? *cdev : cv;
-    const int bid = blockIdx.x;
+    const int bid = blockIdx.x + tile_base;
     int lo = 0, hi = njobs - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -1053,10 +1054,11 @@ void adam_coef_host(const AdamArgs& a, float* out6) {
 }
 
 template <typename T>
-int adam_pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles, AdamArgs a, const float* coef_dev) {
-    if (njobs == 0 || total_tiles == 0) return HLMC_OK;
-    adam_pack_kernel<T><<<total_tiles, 256, 0, s>>>(jobs_dev, njobs, adam_coef(a),
-                                                    reinterpret_cast<const AdamCoef*>(coef_dev));
+int adam_pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles, AdamArgs a, const float* coef_dev,
+              int tile_begin) {
+    if (njobs == 0 || total_tiles <= tile_begin) return HLMC_OK;
+    adam_pack_kernel<T><<<total_tiles - tile_begin, 256, 0, s>>>(jobs_dev, njobs, adam_coef(a),
+                                                                 reinterpret_cast<const AdamCoef*>(coef_dev), tile_begin);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1091,7 +1093,7 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
     template int reparam_fwd<T>(hipStream_t, const float*, const float*, const float*, int, int, T*, int);           \
     template int reparam_bwd<T>(hipStream_t, const T*, int, const float*, const float*, int, int, float*, float*);   \
     template int pack<T>(hipStream_t, const AdamJob*, int, int);                                                     \
-    template int adam_pack<T>(hipStream_t, const AdamJob*, int, int, AdamArgs, const float*);
+    template int adam_pack<T>(hipStream_t, const AdamJob*, int, int, AdamArgs, const float*, int);
 
 INST(float)
 INST(bf16)

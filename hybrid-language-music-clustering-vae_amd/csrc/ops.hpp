@@ -155,7 +155,8 @@ struct AdamJob {
 int adam_job_tiles(AdamJob& j);  // sets nt1, returns the job's block count
 template <typename T>
 int adam_pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles, AdamArgs a,
-              const float* coef_dev = nullptr);  // coef_dev: 6 device floats (adam_coef_host) used instead of a
+              const float* coef_dev = nullptr,  // coef_dev: 6 device floats (adam_coef_host) used instead of a
+              int tile_begin = 0);              // launch tiles [tile_begin, total_tiles) only
 // torch.optim.Adam step coefficients {beta1, beta2, eps, weight_decay, lr / (1 - beta1^t), sqrt(1 - beta2^t)}
 void adam_coef_host(const AdamArgs& a, float* out6);
 template <typename T>

@@ -163,6 +163,8 @@ class _NetFn(torch.autograd.Function):
         d_rt = g(d_rt, "recon_text") if ctx.has_text else None
         L.check(L.lib().hlmc_net_backward(net.h, L.stream(), ctx.B, L.ptr(d_recon), L.ptr(d_rt), L.ptr(d_mu),
                                           L.ptr(d_lv), ctx.ws.data_ptr()), "hlmc_net_backward")
+        # autograd reads every gradient right away: no Adam-overlapped tail on this path
+        L.check(L.lib().hlmc_net_settle(net.h, L.stream()), "hlmc_net_settle")
         ctx.ws = None
         return (None, None, None, None, None, None, None, *owner._grad_views)
 

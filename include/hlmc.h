@@ -130,6 +130,15 @@ int hlmc_adam_coef(float lr, float beta1, float beta2, float eps, float weight_d
  * writes parameters any other way must pass 0, the default, so forward always re-packs). */
 int hlmc_net_set_trust_packs(hlmc_net* net, int trust);
 
+/* enable != 0 (single process): hlmc_net_backward returns with the last weight gradients (encoder layers
+ * 0-1) still in flight on the engine's weight-gradient stream, and the next hlmc_net_adam_step(_dev) updates
+ * every other parameter first, then waits for them (Adam overlaps the tail of the backward pass).  Those
+ * gradients are final only after that Adam step (or the next forward / backward, which wait for them).
+ * Ignored while bucket sync is enabled. */
+int hlmc_net_set_overlap_adam(hlmc_net* net, int enable);
+/* Make every gradient of the last hlmc_net_backward final on `stream` (joins a pending tail; no-op otherwise). */
+int hlmc_net_settle(hlmc_net* net, void* stream);
+
 /* Data-parallel gradient buckets (the reference trains on one device; its DDP counterpart is the gradient
  * all-reduce of SURVEY.md §8e).  Bucket k = parameters [starts[k], starts[k-1]) in registration order
  * (starts[-1] = num_params), listed in the order hlmc_net_backward finishes them; the last start is 0.

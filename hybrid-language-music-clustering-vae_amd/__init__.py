@@ -7,6 +7,8 @@ Drop-in surface (reference names):
   melspectrogram, power_to_db, mfcc, extract_mel_spectrogram, mean_std_pool, StandardScaler
                                                (librosa / sklearn calls of src/1_preprocessing*.py)
   KMeans                                       (sklearn KMeans calls of the three model scripts)
+  metrics.silhouette_score / davies_bouldin_score / calinski_harabasz_score / adjusted_rand_score /
+  normalized_mutual_info_score / calculate_purity   (the sklearn.metrics evaluation calls)
   Adam                                         (torch.optim.Adam of the train loops)
   Trainer                                      (fused train step + RCCL data parallel)
 All compute runs in libhlmc.so (hand-written HIP for gfx950); see include/hlmc.h.
@@ -15,6 +17,7 @@ from . import _lib
 from .cluster import KMeans
 from .features import (StandardScaler, extract_mel_spectrogram, mean_std_pool, mel_filterbank, melspectrogram, mfcc,
                        power_to_db)
+from . import metrics
 from .losses import cvae_loss_function, loss_function, vae_loss
 from .models import VAE, ConditionalVAE, HybridVAE
 from .optim import Adam
@@ -22,4 +25,4 @@ from .train import GraphedStep, Trainer
 
 __all__ = ["HybridVAE", "ConditionalVAE", "VAE", "loss_function", "cvae_loss_function", "vae_loss", "melspectrogram",
            "power_to_db", "mfcc", "extract_mel_spectrogram", "mean_std_pool", "mel_filterbank", "StandardScaler",
-           "KMeans", "Adam", "Trainer", "GraphedStep"]
+           "KMeans", "Adam", "Trainer", "GraphedStep", "metrics"]

@@ -75,6 +75,10 @@ _SIGS = {
     "hlmc_km_sums": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp]),
     "hlmc_km_rowdist": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),
     "hlmc_km_inertia": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "hlmc_silhouette_workspace": (c_i64, [c_i64, c_int]),
+    "hlmc_silhouette": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_i64]),
+    "hlmc_cluster_scores_workspace": (c_i64, [c_int, c_int]),
+    "hlmc_cluster_scores": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_i64]),
     "hlmc_op_conv_s2": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64]),
     "hlmc_op_subpixel": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64]),
     "hlmc_op_wgrad_s2": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_i64]),

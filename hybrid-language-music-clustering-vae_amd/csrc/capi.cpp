@@ -331,6 +331,18 @@ int hlmc_km_rowdist(void* stream, const float* X, int64_t n, int d, const float*
     return km::rowdist(S(stream), X, n, d, C, labels, out);
 }
 
+// ------------------------------------------------------------------------------------ metrics
+int64_t hlmc_silhouette_workspace(int64_t n, int k) { return (int64_t)metrics::silhouette_workspace(n, k); }
+int hlmc_silhouette(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, double* samples,
+                    double* score, void* ws, int64_t ws_bytes) {
+    return metrics::silhouette(S(stream), X, n, d, labels, k, samples, score, ws, (size_t)ws_bytes);
+}
+int64_t hlmc_cluster_scores_workspace(int k, int d) { return (int64_t)metrics::cluster_scores_workspace(k, d); }
+int hlmc_cluster_scores(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, double* out2,
+                        void* ws, int64_t ws_bytes) {
+    return metrics::cluster_scores(S(stream), X, n, d, labels, k, out2, ws, (size_t)ws_bytes);
+}
+
 
 // ------------------------------------------------------------------------------------ op-level entries
 // Individual GEMM-family kernels (the building blocks of hlmc_net_*), exposed for testing and reuse.

@@ -52,4 +52,15 @@ int inertia(hipStream_t s, const float* X, int64_t n, int d, const float* C, con
 int rowdist(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out);
 }  // namespace km
 
+// cluster-quality metrics (metrics.hip): silhouette (sklearn silhouette_score / silhouette_samples),
+// Davies-Bouldin + Calinski-Harabasz.  Labels are 0..k-1 int32.
+namespace metrics {
+size_t silhouette_workspace(int64_t n, int k);
+int silhouette(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, double* samples,
+               double* score, void* ws, size_t ws_bytes);
+size_t cluster_scores_workspace(int k, int d);
+int cluster_scores(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, double* out2,
+                   void* ws, size_t ws_bytes);
+}  // namespace metrics
+
 }  // namespace hlmc

@@ -204,6 +204,20 @@ int hlmc_km_rowdist(void* stream, const float* X, int64_t n, int d, const float*
 int hlmc_km_inertia(void* stream, const float* X, int64_t n, int d, const float* centers, const int32_t* labels,
                     float* out, float* tmp);
 
+/* ============================================================== cluster-quality metrics
+ * sklearn.metrics.silhouette_score / silhouette_samples (metric "euclidean"), replacing the calls at
+ * src/Convolutional_VAE.py:320,337,361,399, src/Conditional_VAE.py:298, src/Simple_VAE.py:247,256,262.
+ * X [n][d] f32 (d <= 128), labels int32 in [0, k), 2 <= k <= 64.  samples (nullable) [n] f64, score: device
+ * f64 scalar.  Deterministic (fixed-order f64 reductions). */
+int64_t hlmc_silhouette_workspace(int64_t n, int k);
+int hlmc_silhouette(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, double* samples,
+                    double* score, void* ws, int64_t ws_bytes);
+/* out2 (device f64[2]) = { davies_bouldin_score, calinski_harabasz_score } (src/Convolutional_VAE.py:400,
+ * src/Simple_VAE.py:257,263); every label in [0, k) must occur. */
+int64_t hlmc_cluster_scores_workspace(int k, int d);
+int hlmc_cluster_scores(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, double* out2,
+                        void* ws, int64_t ws_bytes);
+
 
 /* ============================================================== op-level entry points
  * The kernels hlmc_net_* is built from, on NHWC activations (dtype HLMC_F32 / HLMC_BF16 for x, y, packed

@@ -115,3 +115,25 @@ def blobs(n, d, k, seed):
     c = rng.normal(0, 3.0, (k, d))
     lab = rng.integers(0, k, n)
     return (c[lab] + rng.normal(0, 1.0, (n, d))).astype(np.float32)
+
+
+def blob_labels(n, d, k, seed):
+    """The blob membership of blobs(n, d, k, seed) (same generator sequence): ground-truth labels."""
+    rng = np.random.default_rng(seed)
+    rng.normal(0, 3.0, (k, d))
+    return rng.integers(0, k, n)
+
+
+# cluster-quality metric cases: the KMEANS_CASES entries whose sklearn labels are scored
+METRICS_CASES = [KMEANS_CASES[0], KMEANS_CASES[1], KMEANS_CASES[3], KMEANS_CASES[5]]
+
+
+def kmeans_fixture_name(case):
+    n, d, centers, k, n_init = case
+    return f"kmeans_n{n}_d{d}_k{k}_i{n_init}.npz"
+
+
+def metrics_fixture_name(case):
+    n, d, centers, k, n_init = case
+    return f"metrics_n{n}_d{d}_k{k}.npz"
+

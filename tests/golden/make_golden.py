@@ -13,8 +13,9 @@ What it does (nothing here ships or runs on the GPU box):
     outputs, losses, gradient summaries and 1- / 3-step Adam states.
   * Checks that oracle/models_oracle.py (the restatement used on the GPU box) reproduces every
     recorded value bit-for-bit, and fails otherwise.
-  * Records sklearn 1.7.2 KMeans(random_state=42, n_init=10) labels on seeded blob data, and the
-    oracle's mel / MFCC / pooling outputs on seeded synthetic PCM.
+  * Records sklearn 1.7.2 KMeans(random_state=42, n_init=10) labels on seeded blob data, the sklearn.metrics
+    scores of those labels (silhouette incl. per-sample, Davies-Bouldin, Calinski-Harabasz, ARI, NMI) and the
+    reference's own calculate_purity, and the oracle's mel / MFCC / pooling outputs on seeded synthetic PCM.
 Fixtures are data (inputs + expected outputs); no reference source is stored.
 """
 from __future__ import annotations
@@ -190,6 +191,32 @@ def make_kmeans():
         print("kmeans", n, d, k, n_init, km.n_iter_, flush=True)
 
 
+def make_metrics():
+    """sklearn.metrics scores of the K-Means fixture labels (and the blob ground truth), plus the reference's own
+    calculate_purity (src/Conditional_VAE.py:279-287, AST-loaded) — §8f rows 1 and 4."""
+    from sklearn import metrics as skm
+    src = open(os.path.join(REF, "Conditional_VAE.py")).read()
+    tree = ast.parse(src)
+    keep = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == "calculate_purity"]
+    ns = {"np": np, "confusion_matrix": skm.confusion_matrix}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), "Conditional_VAE.py", "exec"), ns)
+    purity = ns["calculate_purity"]
+    for case in fixtures.METRICS_CASES:
+        n, d, centers, k, n_init = case
+        X = fixtures.blobs(n, d, centers, seed=n + d + k)
+        y_true = fixtures.blob_labels(n, d, centers, seed=n + d + k)
+        y_pred = np.load(os.path.join(HERE, fixtures.kmeans_fixture_name(case)))["labels"].astype(np.int64)
+        np.savez_compressed(os.path.join(HERE, fixtures.metrics_fixture_name(case)),
+                            silhouette=np.float64(skm.silhouette_score(X, y_pred)),
+                            silhouette_samples=skm.silhouette_samples(X, y_pred).astype(np.float64),
+                            davies_bouldin=np.float64(skm.davies_bouldin_score(X, y_pred)),
+                            calinski_harabasz=np.float64(skm.calinski_harabasz_score(X, y_pred)),
+                            ari=np.float64(skm.adjusted_rand_score(y_true, y_pred)),
+                            nmi=np.float64(skm.normalized_mutual_info_score(y_true, y_pred)),
+                            purity=np.float64(purity(y_true, y_pred)))
+        print("metrics", n, d, k, flush=True)
+
+
 def make_features():
     from sklearn.preprocessing import StandardScaler
     y = mel_oracle.synthetic_pcm(2, 65024, seed=7)
@@ -208,10 +235,12 @@ def make_features():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    what = sys.argv[1:] or ["models", "kmeans", "features"]
+    what = sys.argv[1:] or ["models", "kmeans", "metrics", "features"]
     if "features" in what:
         make_features()
     if "kmeans" in what:
         make_kmeans()
+    if "metrics" in what:
+        make_metrics()
     if "models" in what:
         make_models()

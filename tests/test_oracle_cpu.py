@@ -1,4 +1,6 @@
 """CPU checks of the oracle itself against the reference's pins and the committed golden fixtures."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -7,6 +9,8 @@ from oracle import kmeans_oracle as KO
 from oracle import mel_oracle as MO
 from oracle import models_oracle as OM
 from tests.golden import fixtures as FX
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def test_librosa_documented_filterbank_value():
@@ -88,3 +92,25 @@ def test_native_shapes_match_reference_at_128x1024():
     torch.manual_seed(42)
     m = OM.HybridVAE()  # reference default (128 x 1024)
     assert m.audio_fc.weight.shape == (1024, 16384) and sum(p.numel() for p in m.parameters()) == 43272065
+
+
+# ---------------------------------------------------------------- cluster-quality metrics (§8f rows 1, 4)
+@pytest.mark.parametrize("case", FX.METRICS_CASES)
+def test_metrics_oracle_matches_sklearn_fixtures(case):
+    """The numpy restatement (the GPU tests' checker) reproduces sklearn's recorded scores; the host label
+    metrics of hlmc_amd.metrics (ARI / NMI / purity) reproduce sklearn and the reference's calculate_purity."""
+    from oracle import metrics_oracle as MO
+    import hlmc_amd
+    n, d, centers, k, n_init = case
+    fx = np.load(os.path.join(GOLDEN, FX.metrics_fixture_name(case)))
+    X = FX.blobs(n, d, centers, seed=n + d + k)
+    y_true = FX.blob_labels(n, d, centers, seed=n + d + k)
+    y_pred = np.load(os.path.join(GOLDEN, FX.kmeans_fixture_name(case)))["labels"].astype(np.int64)
+    np.testing.assert_allclose(MO.silhouette_samples(X, y_pred), fx["silhouette_samples"], rtol=1e-5, atol=1e-6)
+    assert abs(MO.silhouette_score(X, y_pred) - float(fx["silhouette"])) <= 1e-6 * abs(float(fx["silhouette"])) + 1e-7
+    assert abs(MO.davies_bouldin_score(X, y_pred) - float(fx["davies_bouldin"])) <= 1e-6 * float(fx["davies_bouldin"])  # sklearn: float32 centroids
+    assert abs(MO.calinski_harabasz_score(X, y_pred) - float(fx["calinski_harabasz"])) <= 1e-6 * float(fx["calinski_harabasz"])
+    M = hlmc_amd.metrics
+    assert abs(M.adjusted_rand_score(y_true, y_pred) - float(fx["ari"])) <= 1e-12
+    assert abs(M.normalized_mutual_info_score(y_true, y_pred) - float(fx["nmi"])) <= 1e-12
+    assert M.calculate_purity(y_true, y_pred) == float(fx["purity"])

@@ -125,6 +125,19 @@ __device__ __forceinline__ float lrelu(float x) { return x > 0.f ? x : 0.01f * x
 
 inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Division by a runtime constant via a precomputed magic number (n < 2^31): q = (umulhi(n, mul) + n) >> sh
+struct FastDiv {
+    uint32_t d, mul, sh;
+    FastDiv() = default;
+    explicit FastDiv(uint32_t div) : d(div) {
+        sh = 0;
+        while ((1u << sh) < div) ++sh;
+        mul = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << sh) - div)) / div + 1);
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, mul) + n) >> sh; }
+};
+
+
 // wave-level sums (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

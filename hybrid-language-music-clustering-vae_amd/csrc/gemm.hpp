@@ -21,18 +21,6 @@ constexpr int kKCH = 8;
 template <typename T>
 constexpr int gemm_bk() { return kKCH * Vec16<T>::N; }
 
-// Division by a runtime constant via a precomputed magic number (n < 2^31): q = (umulhi(n, mul) + n) >> sh
-struct FastDiv {
-    uint32_t d, mul, sh;
-    FastDiv() = default;
-    explicit FastDiv(uint32_t div) : d(div) {
-        sh = 0;
-        while ((1u << sh) < div) ++sh;
-        mul = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << sh) - div)) / div + 1);
-    }
-    __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(n, mul) + n) >> sh; }
-};
-
 // XCD-aware block order (cdna_hip_programming.md T1): the dispatcher deals linear block ids round-robin over
 // the 8 XCDs (ids b and b+8 share an L2), so map them to logical ids that run consecutively on one XCD; blocks
 // that share operand rows (the N-tiles / phases of one M-tile, the tiles of one K-split) then share an L2.

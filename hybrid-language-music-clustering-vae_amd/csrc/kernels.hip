@@ -332,59 +332,61 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
 // ---------------------------------------------------------------- edge convs (one channel side)
 // y[b,oh,ow,co] = bias[co] + sum_{kh,kw} x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + kh*3+kw]
 // One thread per output pixel; the 9*CO weights are read at wave-uniform addresses (scalar loads).
+// y[b, oh, ow, co] = bias[co] + sum_taps x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + tap]  (1 input channel, CO = 32)
+// Four threads per output pixel, each computing 8 channels (one 16-byte store): a wave's store instruction
+// writes 1 KB contiguous; the 9 input taps are re-read by the 4 threads from L1.
 template <typename T, int CO>
 __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
-                                                         T* __restrict__ y) {
+                                                         T* __restrict__ y, FastDiv dWo, FastDiv dHo) {
+    constexpr int V = Vec16<T>::N, G = CO / V;  // threads per pixel
+    __shared__ float wsh[CO * 9], bsh[CO];       // per-lane channel groups: LDS broadcast reads, not global
+    for (int i = threadIdx.x; i < CO * 9; i += blockDim.x) wsh[i] = w[i];
+    for (int i = threadIdx.x; i < CO; i += blockDim.x) bsh[i] = bias ? bias[i] : 0.f;
+    __syncthreads();
     const int Ho = Hi / 2, Wo = Wi / 2;
-    const int64_t npix = (int64_t)B * Ho * Wo;
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
-        int ow = (int)(p % Wo);
-        int64_t t = p / Wo;
-        int oh = (int)(t % Ho);
-        int b = (int)(t / Ho);
+    const int nthr = B * Ho * Wo * G;  // < 2^31 (checked by the launcher)
+    for (int t0 = blockIdx.x * blockDim.x + threadIdx.x; t0 < nthr; t0 += gridDim.x * blockDim.x) {
+        const int p = t0 / G, c0 = (t0 - p * G) * V;
+        const int t = (int)dWo.div((uint32_t)p), ow = p - t * Wo;
+        const int b = (int)dHo.div((uint32_t)t), oh = t - b * Ho;
         float in[9];
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
-                int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
-                in[kh * 3 + kw] = ((unsigned)ih < (unsigned)Hi && (unsigned)iw < (unsigned)Wi)
-                                      ? x[((int64_t)b * Hi + ih) * Wi + iw] : 0.f;
+                const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
+                in[kh * 3 + kw] = (ih >= 0 && iw >= 0) ? x[((int64_t)b * Hi + ih) * Wi + iw] : 0.f;  // ih, iw < Hi, Wi
             }
-        constexpr int V = Vec16<T>::N;
+        float o[V];
 #pragma unroll
-        for (int c0 = 0; c0 < CO; c0 += V) {
-            float o[V];
+        for (int v = 0; v < V; ++v) {
+            float s = bsh[c0 + v];
 #pragma unroll
-            for (int v = 0; v < V; ++v) {
-                float s = bias ? bias[c0 + v] : 0.f;
-#pragma unroll
-                for (int k = 0; k < 9; ++k) s = fmaf(in[k], w[(c0 + v) * 9 + k], s);
-                o[v] = s;
-            }
-            store16_f32(y + p * CO + c0, o);
+            for (int k = 0; k < 9; ++k) s = fmaf(in[k], wsh[(c0 + v) * 9 + k], s);
+            o[v] = s;
         }
+        store16_f32(y + (int64_t)p * CO + c0, o);
     }
 }
 
-// y[b, oh, ow] = bias + sum_ci sum_taps x[b, ih, iw, ci] * w[ci*9 + kh*3 + kw]  (transposed, 1 output channel)
+// y[b, oh, ow] = bias + sum_ci sum_taps x[b, ih, iw, ci] * w[ci*9 + kh*3 + kw]  (transposed, 1 output channel).
+// (Measured: one thread per output pixel beats one thread per low-res pixel computing the 2 x 2 block, whose
+// long per-accumulator FMA chains leave it latency-bound: 47 vs 61 us at B = 256.)
 template <typename T, int CI>
 __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
-                                                       float* __restrict__ y) {
+                                                       float* __restrict__ y, FastDiv dWo, FastDiv dHo) {
     __shared__ float ws[CI * 9];
     for (int i = threadIdx.x; i < CI * 9; i += blockDim.x) ws[i] = w[i];
     __syncthreads();
     const float b0 = bias ? bias[0] : 0.f;
     const int Ho = 2 * Hi, Wo = 2 * Wi;
-    const int64_t npix = (int64_t)B * Ho * Wo;
+    const int npix = B * Ho * Wo;  // < 2^31 (checked by the launcher)
     constexpr int V = Vec16<T>::N;
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
-        int ow = (int)(p % Wo);
-        int64_t t = p / Wo;
-        int oh = (int)(t % Ho);
-        int b = (int)(t / Ho);
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += gridDim.x * blockDim.x) {
+        const int t = (int)dWo.div((uint32_t)p), ow = p - t * Wo;
+        const int b = (int)dHo.div((uint32_t)t), oh = t - b * Ho;
         int py = oh & 1, px = ow & 1, r = oh >> 1, c = ow >> 1;
         float s = b0;
         for (int ty = 0; ty < (py ? 2 : 1); ++ty) {
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, 
 template <typename T, int M>
 __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, int B, int Hl, int Wl,
                                                        const float* __restrict__ Xh, int rows_per_blk,
-                                                       float* __restrict__ part) {
+                                                       float* __restrict__ part, FastDiv dWl, FastDiv dHl) {
     static_assert(M == 32, "one 8 x 4 channel tiling");
     constexpr int RC = 256;
     // one LDS block: [RC][M+1] rows + [RC][9] taps during accumulation, [32][M*9] partials afterwards
@@ -448,19 +450,17 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, 
 #pragma unroll
             for (int q = 0; q < V; ++q) Ls[rr][cg * V + q] = v[q];
         }
-        for (int i = threadIdx.x; i < RC * 9; i += blockDim.x) {
-            const int rr = i / 9, tap = i % 9;
-            const int64_t k = kb + rr;
-            float v = 0.f;
-            if (k < k1) {
-                const int c = (int)(k % Wl);
-                const int64_t t = k / Wl;
-                const int r = (int)(t % Hl);
-                const int b = (int)(t / Hl);
+        for (int rr = threadIdx.x; rr < RC; rr += blockDim.x) {  // one (b, r, c) decode per row, 9 taps
+            const int k = (int)(kb + rr);
+            const bool ok = k < k1;
+            const int t = (int)dWl.div((uint32_t)k), c = k - t * Wl;
+            const int b = (int)dHl.div((uint32_t)t), r = t - b * Hl;
+            const float* xr = Xh + ((int64_t)b * Hh + 2 * r - 1) * Wh + 2 * c - 1;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
                 const int ih = 2 * r - 1 + tap / 3, iw = 2 * c - 1 + tap % 3;
-                if ((unsigned)ih < (unsigned)Hh && (unsigned)iw < (unsigned)Wh) v = Xh[((int64_t)b * Hh + ih) * Wh + iw];
+                Hs[rr][tap] = (ok && ih >= 0 && iw >= 0) ? xr[(tap / 3) * Wh + tap % 3] : 0.f;
             }
-            Hs[rr][tap] = v;
         }
         __syncthreads();
         for (int rr = rg; rr < RC; rr += 32) {
@@ -852,8 +852,10 @@ int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float*
 template <typename T>
 int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y) {
     HLMC_CHECK_ARG(Co == 32 && Hi % 2 == 0 && Wi % 2 == 0, "conv_c1_s2: only Co == 32, even H/W");
-    int64_t npix = (int64_t)B * (Hi / 2) * (Wi / 2);
-    conv_c1_s2_kernel<T, 32><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y);
+    int64_t nthr = (int64_t)B * (Hi / 2) * (Wi / 2) * (32 / Vec16<T>::N);
+    HLMC_CHECK_ARG(nthr < (int64_t)1 << 31, "conv_c1_s2: too many pixels");
+    conv_c1_s2_kernel<T, 32><<<grid_for(nthr, kThreads, 16384), kThreads, 0, s>>>(
+        x, B, Hi, Wi, w, bias, y, FastDiv((uint32_t)(Wi / 2)), FastDiv((uint32_t)(Hi / 2)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -862,7 +864,9 @@ template <typename T>
 int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y) {
     HLMC_CHECK_ARG(Ci == 32, "convT_c1: only Ci == 32");
     int64_t npix = (int64_t)B * 4 * Hi * Wi;
-    convT_c1_kernel<T, 32><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y);
+    HLMC_CHECK_ARG(npix < (int64_t)1 << 31, "convT_c1: too many pixels");
+    convT_c1_kernel<T, 32><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, FastDiv((uint32_t)(2 * Wi)),
+                                                               FastDiv((uint32_t)(2 * Hi)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -879,7 +883,9 @@ int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const floa
     int nblk = wgrad_c1_blocks(K);
     HLMC_CHECK_ARG(ws.bytes >= wgrad_c1_ws(B, Hl, Wl, M), "wgrad_c1 workspace");
     int rpb = (int)((K + nblk - 1) / nblk);
-    wgrad_c1_kernel<T, 32><<<nblk, kThreads, 0, s>>>(L, B, Hl, Wl, Xh, rpb, ws.p);
+    HLMC_CHECK_ARG(K < (int64_t)1 << 31, "wgrad_c1: too many rows");
+    wgrad_c1_kernel<T, 32><<<nblk, kThreads, 0, s>>>(L, B, Hl, Wl, Xh, rpb, ws.p, FastDiv((uint32_t)Wl),
+                                                     FastDiv((uint32_t)Hl));
     HLMC_LAUNCHED();
     sum_partials_f32_kernel<<<M * 9, 256, 0, s>>>(ws.p, nblk, M * 9, dW);
     HLMC_LAUNCHED();

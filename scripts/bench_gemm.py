@@ -92,3 +92,20 @@ for l in range(5):
 tot = sum(r[1] for r in rows)
 ideal = sum(r[2] for r in rows)
 print(f"TOTAL {tot:.1f} us  ideal {ideal:.1f} us")
+
+# single-channel edge convolutions (VALU / HBM kernels): ideal = bytes / 6 TB/s
+audio = torch.randn(B, 128, 128, device=dev)
+w9 = torch.randn(32, 9, device=dev) * 0.1
+bias = torch.zeros(32, device=dev)
+y0 = torch.empty(B, 64, 64, 32, device=dev, dtype=bf)
+us = timeit(lambda: lib.hlmc_op_conv_c1_s2(L.stream(), L.HLMC_BF16, audio.data_ptr(), B, 128, 128, w9.data_ptr(),
+                                           bias.data_ptr(), 32, y0.data_ptr()))
+report("enc1 fwd conv_c1_s2 1->32", us, 2.0 * y0.numel() * 9, 4.0 * audio.numel() + 2.0 * y0.numel())
+rec = torch.empty(B, 128, 128, device=dev)
+us = timeit(lambda: lib.hlmc_op_convT_c1(L.stream(), L.HLMC_BF16, y0.data_ptr(), B, 64, 64, 32, w9.data_ptr(),
+                                         bias[:1].data_ptr(), rec.data_ptr()))
+report("dec5 fwd convT_c1 32->1", us, 2.0 * y0.numel() * 9, 2.0 * y0.numel() + 4.0 * rec.numel())
+dw = torch.empty(32, 9, device=dev)
+us = timeit(lambda: lib.hlmc_op_wgrad_c1(L.stream(), L.HLMC_BF16, y0.data_ptr(), B, 64, 64, 32, audio.data_ptr(),
+                                         dw.data_ptr(), ws.data_ptr(), WS))
+report("enc1 wgrad wgrad_c1 32x9", us, 2.0 * y0.numel() * 9, 2.0 * y0.numel() + 4.0 * audio.numel())

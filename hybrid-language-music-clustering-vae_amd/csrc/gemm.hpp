@@ -449,7 +449,11 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    uint4 ra[AR], rb[BR];
+    struct Regs {
+        uint4 a[AR], b[BR];
+    };
+    Regs r0;  // staging set: one K-step of global loads in flight (measured: a second set, two steps in
+              // flight, was 1.2-1.6x slower on every short-K layer — lower occupancy)
     typename AL::Row arow[AR];
     typename BL::Row brow[BR];
 #pragma unroll
@@ -457,89 +461,92 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
 #pragma unroll
     for (int i = 0; i < BR; ++i) brow[i] = bl.prep(n0 + ((tid + i * 256) / KCH));
     const int kc = (tid % KCH) * V;  // this thread's chunk column (256 % KCH == 0: the same for every i)
-    auto gload = [&](int k0) {
+    auto gload = [&](Regs& rg, int k0) {
         const typename AL::Ctx ax = al.ctx(k0 + kc);
         const typename BL::Ctx bx = bl.ctx(k0 + kc);
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (ACH % 256 == 0 || c < ACH) ra[i] = al.load(arow[i], ax);
+            if (ACH % 256 == 0 || c < ACH) rg.a[i] = al.load(arow[i], ax);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (BCH % 256 == 0 || c < BCH) rb[i] = bl.load(brow[i], bx);
+            if (BCH % 256 == 0 || c < BCH) rg.b[i] = bl.load(brow[i], bx);
         }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](const Regs& rg, int buf) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
             if (ACH % 256 == 0 || c < ACH)
-                *reinterpret_cast<uint4*>(&As[buf][(c / KCH) * BK + nt_lds_chunk<KCH>(c / KCH, c % KCH) * V]) = ra[i];
+                *reinterpret_cast<uint4*>(&As[buf][(c / KCH) * BK + nt_lds_chunk<KCH>(c / KCH, c % KCH) * V]) = rg.a[i];
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
             if (BCH % 256 == 0 || c < BCH)
-                *reinterpret_cast<uint4*>(&Bs[buf][(c / KCH) * BK + nt_lds_chunk<KCH>(c / KCH, c % KCH) * V]) = rb[i];
+                *reinterpret_cast<uint4*>(&Bs[buf][(c / KCH) * BK + nt_lds_chunk<KCH>(c / KCH, c % KCH) * V]) = rg.b[i];
         }
     };
 
+    auto mma_step = [&](int cur) {
+        const T* A = As[cur];
+        const T* B = Bs[cur];
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int s = 0; s < BK / 32; ++s) {
+                bf16x8_t af[TM], bfr[TN];
+                const int c = s * 4 + (lane >> 4);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = wm0 + i * 16 + (lane & 15);
+                    af[i] = *reinterpret_cast<const bf16x8_t*>(&A[row * BK + nt_lds_chunk<KCH>(row, c) * 8]);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int row = wn0 + j * 16 + (lane & 15);
+                    bfr[j] = *reinterpret_cast<const bf16x8_t*>(&B[row * BK + nt_lds_chunk<KCH>(row, c) * 8]);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < BK / 4; ++s) {
+                float af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = wm0 + i * 16 + (lane & 15);
+                    af[i] = A[row * BK + nt_lds_chunk<KCH>(row, s) * 4 + (lane >> 4)];
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int row = wn0 + j * 16 + (lane & 15);
+                    bfr[j] = B[row * BK + nt_lds_chunk<KCH>(row, s) * 4 + (lane >> 4)];
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
     if (kb < ke) {
-        gload(kb);
-        lstore(0);
+        gload(r0, kb);
+        lstore(r0, 0);
         __syncthreads();
         int it = 0;
         for (int k0 = kb; k0 < ke; k0 += BK, ++it) {
             const int cur = it & 1;
             const bool more = k0 + BK < ke;
-            if (more) gload(k0 + BK);
-            const T* A = As[cur];
-            const T* B = Bs[cur];
-            if constexpr (sizeof(T) == 2) {
-#pragma unroll
-                for (int s = 0; s < BK / 32; ++s) {
-                    bf16x8_t af[TM], bfr[TN];
-                    const int c = s * 4 + (lane >> 4);
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) {
-                        const int row = wm0 + i * 16 + (lane & 15);
-                        af[i] = *reinterpret_cast<const bf16x8_t*>(&A[row * BK + nt_lds_chunk<KCH>(row, c) * 8]);
-                    }
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const int row = wn0 + j * 16 + (lane & 15);
-                        bfr[j] = *reinterpret_cast<const bf16x8_t*>(&B[row * BK + nt_lds_chunk<KCH>(row, c) * 8]);
-                    }
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-                }
-            } else {
-#pragma unroll
-                for (int s = 0; s < BK / 4; ++s) {
-                    float af[TM], bfr[TN];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) {
-                        const int row = wm0 + i * 16 + (lane & 15);
-                        af[i] = A[row * BK + nt_lds_chunk<KCH>(row, s) * 4 + (lane >> 4)];
-                    }
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const int row = wn0 + j * 16 + (lane & 15);
-                        bfr[j] = B[row * BK + nt_lds_chunk<KCH>(row, s) * 4 + (lane >> 4)];
-                    }
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-                }
-            }
-            if (more) lstore(cur ^ 1);
+            if (more) gload(r0, k0 + BK);
+            mma_step(cur);
+            if (more) lstore(r0, cur ^ 1);
             __syncthreads();
         }
     }

@@ -221,24 +221,36 @@ size_t tn_ws(int M, int N, int K, int BK) {
     return (size_t)pl.S * M * N * sizeof(float);
 }
 
-// Conv weight gradients have N = 9 C: C = 32 gives N = 288, which 128-wide tiles cover with 25 % zero columns;
-// 96-wide tiles cover it exactly (measured: 83 -> 72 us for the 64 x 288 x 262144 layers).
+// Weight-gradient tile choice.  Weight gradients reduce over K = B * pixels (16 k - 262 k) into a small
+// M x N output; the grid is filled by split-K.  Conv weight gradients have N = 9 C: C = 32 gives N = 288,
+// which 128-wide tiles cover with 25 % zero columns; 96-wide tiles cover it exactly (measured: 83 -> 72 us for
+// the 64 x 288 x 262144 layers).  (Measured and rejected: 64 x 64 tiles everywhere, which cut the split-K slab
+// bytes 3-4x but were 10-35 % slower per layer — the kernel is bound by per-block load latency, not slabs.)
 inline bool tn_n96(int N) { return N % 128 != 0 && N % 96 == 0; }
+// 0: 128x128, 1: 64x128, 2: 64x96, 3: 32x128
+inline int tn_tile(int M, int N) {
+    if (M >= 128) return 0;
+    if (M > 32) return tn_n96(N) ? 2 : 1;
+    return 3;
+}
 template <typename T, class LL, class HL, class EP>
 int dispatch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws) {
-    if (M >= 128) return launch_tn<T, 128, 128, 64, 64>(s, ll, hl, ep, M, N, K, ws);  // 128x96: slower at N = 576
-    if (M > 32) {
-        if (tn_n96(N)) return launch_tn<T, 64, 96, 32, 48>(s, ll, hl, ep, M, N, K, ws);
-        return launch_tn<T, 64, 128, 32, 64>(s, ll, hl, ep, M, N, K, ws);
+    switch (tn_tile(M, N)) {
+        case 0: return launch_tn<T, 128, 128, 64, 64>(s, ll, hl, ep, M, N, K, ws);
+        case 1: return launch_tn<T, 64, 128, 32, 64>(s, ll, hl, ep, M, N, K, ws);
+        case 2: return launch_tn<T, 64, 96, 32, 48>(s, ll, hl, ep, M, N, K, ws);
+        default: return launch_tn<T, 32, 128, 32, 32>(s, ll, hl, ep, M, N, K, ws);
     }
-    return launch_tn<T, 32, 128, 32, 32>(s, ll, hl, ep, M, N, K, ws);
 }
 template <typename T>
 size_t dispatch_tn_ws(int M, int N, int K) {
     constexpr int BK = gemm_bk<T>();
-    if (M >= 128) return tn_ws<128, 128>(M, N, K, BK);
-    if (M > 32) return tn_n96(N) ? tn_ws<64, 96>(M, N, K, BK) : tn_ws<64, 128>(M, N, K, BK);
-    return tn_ws<32, 128>(M, N, K, BK);
+    switch (tn_tile(M, N)) {
+        case 0: return tn_ws<128, 128>(M, N, K, BK);
+        case 1: return tn_ws<64, 128>(M, N, K, BK);
+        case 2: return tn_ws<64, 96>(M, N, K, BK);
+        default: return tn_ws<32, 128>(M, N, K, BK);
+    }
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }

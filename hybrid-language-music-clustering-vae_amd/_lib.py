@@ -33,6 +33,8 @@ _SIGS = {
     "hlmc_mel_db": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_f32, c_vp, c_vp]),
     "hlmc_power_to_db": (c_int, [c_vp, c_vp, c_i64, c_i64, c_int, c_f32, c_f32, c_f32, c_vp, c_vp]),
     "hlmc_mfcc": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
+    "hlmc_spectral_shape": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_vp]),
+    "hlmc_zcr_rms": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "hlmc_row_mean_std": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "hlmc_colstats_workspace": (c_i64, [c_i64, c_i64]),
     "hlmc_colstats_sum": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),

@@ -142,6 +142,15 @@ int hlmc_mfcc(const hlmc_mel_plan* cp, void* stream, const float* pcm, int64_t B
     }
     return feat::mfcc(p->impl, S(stream), pcm, B, n, n_mfcc, p->d_dct, 1e-10f, 80.f, out, ws);
 }
+int hlmc_spectral_shape(const hlmc_mel_plan* p, void* stream, const float* pcm, int64_t B, int64_t n,
+                        double roll_percent, double* out) {
+    HLMC_CHECK_ARG(p, "null plan");
+    return feat::spectral_shape(p->impl, S(stream), pcm, B, n, roll_percent, out);
+}
+int hlmc_zcr_rms(const hlmc_mel_plan* p, void* stream, const float* pcm, int64_t B, int64_t n, double* zcr, float* rms) {
+    HLMC_CHECK_ARG(p, "null plan");
+    return feat::zcr_rms(p->impl, S(stream), pcm, B, n, zcr, rms);
+}
 int hlmc_row_mean_std(void* stream, const float* x, int64_t rows, int64_t cols, float* mean, float* sd) {
     return feat::row_mean_std(S(stream), x, rows, cols, mean, sd);
 }

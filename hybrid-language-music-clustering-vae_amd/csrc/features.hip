@@ -107,13 +107,135 @@ __device__ __forceinline__ void dft16(float2 (&a)[16]) {
 }
 __device__ __forceinline__ constexpr int slot16(int r) { return 4 * (r & 3) + (r >> 2); }
 
+// librosa.feature.spectral_centroid / spectral_bandwidth / spectral_rolloff of one frame from its power bins
+// pw[0..1024] (wave-private LDS).  S_k = sqrt(pw_k) (power = 1), f_k = k sr / n_fft; librosa normalises
+// S / sum(S) in float32 (left unnormalised when the sum is below float32 tiny) and sums freq * S_norm in
+// float64.  Lane l owns bins 16 l .. 16 l + 15 (contiguous, for the rolloff prefix sum); lane 63 also owns
+// the Nyquist bin 1024.  out[0], out[T], out[2T] <- centroid, bandwidth, rolloff (Hz).
+__device__ __forceinline__ void spectral_shape(const float* pw, int ln, double bin_hz, double roll, double* out, int T) {
+    const float4* pw4 = reinterpret_cast<const float4*>(pw);
+    float m[17];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float4 v = pw4[4 * ln + c];
+        m[4 * c] = sqrtf(v.x); m[4 * c + 1] = sqrtf(v.y); m[4 * c + 2] = sqrtf(v.z); m[4 * c + 3] = sqrtf(v.w);
+    }
+    m[16] = ln == 63 ? sqrtf(pw[kFFT]) : 0.f;
+    double sl = 0.0;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) sl += (double)m[j];
+    const double total = wave_sum(sl);
+    const float tot32 = (float)total;
+    const float div = tot32 < 1.17549435e-38f ? 1.f : tot32;
+    const int k0 = 16 * ln;
+    auto fk = [&](int j) { return (double)(j < 16 ? k0 + j : kFFT) * bin_hz; };
+    double cl = 0.0;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) cl += (double)(m[j] / div) * fk(j);
+    const double centroid = wave_sum(cl);
+    double bl = 0.0;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        const double d = fk(j) - centroid;
+        bl += (double)(m[j] / div) * (d * d);
+    }
+    const double bandwidth = sqrt(wave_sum(bl));
+    // rolloff: first bin whose cumulative magnitude reaches roll * total (wave exclusive scan of lane sums)
+    double inc = sl;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double t = __shfl_up(inc, o, 64);
+        if (ln >= o) inc += t;
+    }
+    const double thr = roll * total;
+    double cum = inc - sl;
+    int first = 1 << 30;
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        cum += (double)m[j];
+        const int k = j < 16 ? k0 + j : kFFT;
+        if (cum >= thr && (j < 16 || ln == 63)) first = min(first, k);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) first = min(first, __shfl_xor(first, o, 64));
+    if (ln == 0) {
+        out[0] = centroid;
+        out[T] = bandwidth;
+        out[2 * T] = (double)first * bin_hz;
+    }
+}
+
+// librosa.feature.zero_crossing_rate(frame_length, hop, center=True: edge padding, threshold 1e-10,
+// zero_pos=True) and librosa.feature.rms(frame_length, hop, center=True: zero padding), one wavefront per frame.
+// Lane l holds samples 4 (l + 64 r) + c (r < 8 for frame_length 2048): coalesced float4 loads.
+constexpr int kZrFrame = 2048;
+__global__ __launch_bounds__(256) void zcr_rms_kernel(const float* __restrict__ pcm, int64_t n, int T, int hop,
+                                                      double* __restrict__ zcr, float* __restrict__ rms) {
+    constexpr int R = kZrFrame / 256;  // float4 groups per lane
+    const int b = blockIdx.y;
+    const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const float* x = pcm + (int64_t)b * n;
+    for (int t = blockIdx.x * 16 + wave; t < min(T, (int)blockIdx.x * 16 + 16); t += 4) {
+        const int64_t start = (int64_t)t * hop - kZrFrame / 2;
+        const bool interior = start >= 0 && start + kZrFrame <= n && ((reinterpret_cast<uintptr_t>(x + start) & 15) == 0);
+        float4 e[R];  // edge-padded samples
+        double sq = 0.0;
+        if (interior) {
+            const float4* xs = reinterpret_cast<const float4*>(x + start);
+#pragma unroll
+            for (int r = 0; r < R; ++r) e[r] = xs[ln + 64 * r];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                sq += (double)(e[r].x * e[r].x) + (double)(e[r].y * e[r].y) + (double)(e[r].z * e[r].z) + (double)(e[r].w * e[r].w);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                float v[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int64_t i = start + 4 * (ln + 64 * r) + c;
+                    const float xv = x[min(max(i, (int64_t)0), n - 1)];
+                    v[c] = xv;
+                    const float z = (i >= 0 && i < n) ? xv : 0.f;
+                    sq += (double)(z * z);
+                }
+                e[r] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+        // signbit after |y| <= 1e-10 -> +0
+        auto neg = [](float v) -> int { return (fabsf(v) <= 1e-10f) ? 0 : (int)(__float_as_uint(v) >> 31); };
+        int cnt = 0;
+        int up_prev = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int s0 = neg(e[r].x), s1 = neg(e[r].y), s2 = neg(e[r].z), s3 = neg(e[r].w);
+            cnt += (s0 != s1) + (s1 != s2) + (s2 != s3);
+            const int up = __shfl(s3, (ln + 63) & 63, 64);  // last sign of the previous float4 group
+            if (ln > 0) cnt += (up != s0);
+            else if (r > 0) cnt += (up_prev != s0);     // lane 63 of group r - 1
+            up_prev = up;
+        }
+        double c = (double)cnt;
+        c = wave_sum(c);
+        sq = wave_sum(sq);
+        if (ln == 0) {
+            zcr[(int64_t)b * T + t] = c / (double)kZrFrame;
+            rms[(int64_t)b * T + t] = sqrtf((float)(sq / (double)kZrFrame));
+        }
+    }
+}
+
+// kMode 0: banded mel (stored [b][m][t]) + per-clip max/min.  kMode 1: spectral shape of |X| (power 1):
+// centroid, bandwidth (p = 2) and rolloff per frame, stored f64 [b][3][t] (sout); the mel tables are unused.
+template <int kMode>
 __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__ pcm, int64_t n_samples, int T,
                                                        int hop, const float* __restrict__ window,
                                                        const float2* __restrict__ rtw, const float2* __restrict__ tw23,
                                                        const int* __restrict__ band,
                                                        const int* __restrict__ woff, const float* __restrict__ wts,
                                                        int n_mels, int nnz, float* __restrict__ out,
-                                                       unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min) {
+                                                       unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min,
+                                                       double bin_hz, double roll, double* __restrict__ sout) {
     __shared__ float2 stw[kFFT + 1];
     __shared__ float2 stw23[kTw2 + kTw3];
     __shared__ __align__(16) float2 zb[kWaves][kZ];
@@ -128,8 +250,10 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
     const float* x = pcm + (int64_t)b * n_samples;
     for (int i = threadIdx.x; i <= kFFT; i += 256) stw[i] = rtw[i];
     for (int i = threadIdx.x; i < kTw2 + kTw3; i += 256) stw23[i] = tw23[i];
-    for (int i = threadIdx.x; i < nnz / 4; i += 256) sw4[i] = reinterpret_cast<const float4*>(wts)[i];
-    for (int l = threadIdx.x; l < kMelLanes; l += 256) sbl[l] = reinterpret_cast<const int4*>(band)[l];
+    if constexpr (kMode == 0) {
+        for (int i = threadIdx.x; i < nnz / 4; i += 256) sw4[i] = reinterpret_cast<const float4*>(wts)[i];
+        for (int l = threadIdx.x; l < kMelLanes; l += 256) sbl[l] = reinterpret_cast<const int4*>(band)[l];
+    }
     __syncthreads();
     float2* z = zb[wave];
     float* pw = reinterpret_cast<float*>(z);  // power bins overwrite the spectrum after the split
@@ -235,7 +359,9 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
         wave_lds_fence();
         // ---- banded mel: lane l owns the band pair (l, n_mels-1-l) (narrow + wide filter); each band is a
         // fixed-order fma chain over 8-bin steps of b128 LDS reads (power bins and chunk-transposed weights)
-        {
+        if constexpr (kMode == 1) {
+            spectral_shape(pw, ln, bin_hz, roll, sout + (int64_t)b * 3 * T + t0 + fl, T);
+        } else {
             const float4* pw4 = reinterpret_cast<const float4*>(pw);
             const int4 bl = sbl[ln];
             float acc0 = 0.f, acc1 = 0.f;
@@ -270,6 +396,7 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
         }
         wave_lds_fence();
     }
+    if constexpr (kMode == 1) return;
     __syncthreads();
     // write [n_mels][frames] rows: out[b][m][t0 + f]
     for (int i = threadIdx.x; i < n_mels * kFpb; i += 256) {
@@ -517,8 +644,8 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
                     (double)B * ((double)n * 4 + (double)p->n_mels * T * 4));
     }
     HLMC_PROBE_BEGIN(s);
-    stft_mel_kernel<<<grid, 256, dyn, s>>>(
-        pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff, p->d_w, p->n_mels, p->nnz, out, cmax, cmin);
+    stft_mel_kernel<0><<<grid, 256, dyn, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
+                                              p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0, nullptr);
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     return HLMC_OK;
@@ -587,6 +714,29 @@ int power_to_db(hipStream_t s, const float* S, int64_t B, int64_t per, int ref_m
     HLMC_LAUNCHED();
     power_to_db_kernel<<<gridn(B * per), 256, 0, s>>>(S, (int)B, 1, (int)per, (int)per, cmax, cmin, ref_max, ref_value,
                                                       amin, top_db, out);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+int spectral_shape(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, double roll_percent,
+                   double* out) {
+    HLMC_CHECK_ARG(pcm && out && B > 0 && n > 0 && B <= 65535, "bad spectral_shape arguments");
+    HLMC_CHECK_ARG(roll_percent > 0.0 && roll_percent < 1.0, "0 < roll_percent < 1");
+    const int T = (int)frames(p, n);
+    dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
+    stft_mel_kernel<1><<<grid, 256, 0, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
+                                            p->d_w, 0, 0, nullptr, nullptr, nullptr, (double)p->sr / p->n_fft,
+                                            roll_percent, out);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+int zcr_rms(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, double* zcr, float* rms) {
+    HLMC_CHECK_ARG(pcm && zcr && rms && B > 0 && n > 0 && B <= 65535, "bad zcr_rms arguments");
+    HLMC_CHECK_ARG(p->n_fft == kZrFrame, "frame_length = 2048 only");
+    const int T = (int)frames(p, n);
+    dim3 grid((T + 15) / 16, (unsigned)B);
+    zcr_rms_kernel<<<grid, 256, 0, s>>>(pcm, n, T, p->hop, zcr, rms);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -34,6 +34,9 @@ int mfcc(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64
          float amin, float top_db, float* out, void* ws);
 int power_to_db(hipStream_t s, const float* S, int64_t B, int64_t per, int ref_max, float ref_value, float amin,
                 float top_db, float* out, void* ws);
+int spectral_shape(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, double roll_percent,
+                   double* out);
+int zcr_rms(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, double* zcr, float* rms);
 int row_mean_std(hipStream_t s, const float* x, int64_t rows, int64_t cols, float* mean, float* sd);
 int64_t colstats_workspace(int64_t n, int64_t cols);
 int colstats(hipStream_t s, const float* x, int64_t n, int64_t cols, const double* mean, double* o0, double* o1, void* ws);

@@ -5,6 +5,9 @@ Replaces (reference call sites):
     src/1_preprocessing.py:48-58, src/1_preprocessing_advanced.py:97-114 (``extract_mel_spectrogram``)
   * ``librosa.feature.mfcc(n_mfcc=40)`` — src/1_preprocessing.py:61-70
   * mean/std pooling — src/1_preprocessing.py:115-121, src/1_preprocessing_advanced.py:144-146
+  * ``librosa.feature.spectral_centroid / spectral_bandwidth / spectral_rolloff / zero_crossing_rate /
+    rms`` and their mean/std pooling — src/1_preprocessing.py:73-91,123-125,
+    src/1_preprocessing_advanced.py:133-137,149-151 (``extract_spectral_features``)
   * ``StandardScaler`` — src/1_preprocessing.py:305-311, src/1_preprocessing_advanced.py:376-391
     (per-pixel z-score over [N, 128*T]; the fit can be distributed across ranks)
 Inputs may be numpy arrays (results come back as numpy, like librosa) or CUDA tensors (results stay
@@ -118,6 +121,80 @@ def mfcc(y, sr=22050, n_mfcc=20, n_fft=2048, hop_length=512, n_mels=128):
     ws = torch.empty(int(L.lib().hlmc_mel_workspace(p, B, n)), dtype=torch.uint8, device=x.device)
     L.check(L.lib().hlmc_mfcc(p, L.stream(), x.data_ptr(), B, n, n_mfcc, out.data_ptr(), ws.data_ptr()), "hlmc_mfcc")
     return _ret(out, was_np, sq)
+
+
+def _spectral_shape(y, sr, n_fft, hop_length, roll_percent):
+    x, was_np, sq = _to_dev(y)
+    p = _plan(sr, n_fft, hop_length, 128)
+    B, n = x.shape
+    T = int(L.lib().hlmc_mel_frames(p, n))
+    out = torch.empty(B, 3, T, dtype=torch.float64, device=x.device)
+    L.check(L.lib().hlmc_spectral_shape(p, L.stream(), x.data_ptr(), B, n, float(roll_percent), out.data_ptr()),
+            "hlmc_spectral_shape")
+    return out, was_np, sq
+
+
+def _zcr_rms(y, frame_length, hop_length):
+    x, was_np, sq = _to_dev(y)
+    p = _plan(22050, frame_length, hop_length, 128)
+    B, n = x.shape
+    T = int(L.lib().hlmc_mel_frames(p, n))
+    zcr = torch.empty(B, 1, T, dtype=torch.float64, device=x.device)
+    rms_ = torch.empty(B, 1, T, dtype=torch.float32, device=x.device)
+    L.check(L.lib().hlmc_zcr_rms(p, L.stream(), x.data_ptr(), B, n, zcr.data_ptr(), rms_.data_ptr()), "hlmc_zcr_rms")
+    return zcr, rms_, was_np, sq
+
+
+def spectral_centroid(y, sr=22050, n_fft=2048, hop_length=512):
+    """librosa.feature.spectral_centroid(y, sr, hop_length) -> float64 [..., 1, T] (Hz)."""
+    out, was_np, sq = _spectral_shape(y, sr, n_fft, hop_length, 0.85)
+    return _ret(out[:, 0:1], was_np, sq)
+
+
+def spectral_bandwidth(y, sr=22050, n_fft=2048, hop_length=512):
+    """librosa.feature.spectral_bandwidth(y, sr, hop_length) (p=2, norm=True) -> float64 [..., 1, T] (Hz)."""
+    out, was_np, sq = _spectral_shape(y, sr, n_fft, hop_length, 0.85)
+    return _ret(out[:, 1:2], was_np, sq)
+
+
+def spectral_rolloff(y, sr=22050, n_fft=2048, hop_length=512, roll_percent=0.85):
+    """librosa.feature.spectral_rolloff(y, sr, hop_length, roll_percent) -> float64 [..., 1, T] (Hz)."""
+    out, was_np, sq = _spectral_shape(y, sr, n_fft, hop_length, roll_percent)
+    return _ret(out[:, 2:3], was_np, sq)
+
+
+def zero_crossing_rate(y, frame_length=2048, hop_length=512):
+    """librosa.feature.zero_crossing_rate(y, frame_length, hop_length) -> float64 [..., 1, T]."""
+    zcr, _, was_np, sq = _zcr_rms(y, frame_length, hop_length)
+    return _ret(zcr, was_np, sq)
+
+
+def rms(y=None, frame_length=2048, hop_length=512):
+    """librosa.feature.rms(y=y, frame_length, hop_length) -> float32 [..., 1, T]."""
+    _, r, was_np, sq = _zcr_rms(y, frame_length, hop_length)
+    return _ret(r, was_np, sq)
+
+
+SPECTRAL_FEATURES = ("spectral_centroid", "spectral_bandwidth", "spectral_rolloff", "zcr", "rms")
+
+
+def extract_spectral_features(audio, sr=22050, hop_length=512):
+    """src/1_preprocessing.py:73-91: dict of the five frame features, two kernel launches for the batch
+    (one STFT pass for centroid/bandwidth/rolloff, one time-domain pass for zcr/rms)."""
+    shape, was_np, sq = _spectral_shape(audio, sr, 2048, hop_length, 0.85)
+    zcr, r, _, _ = _zcr_rms(audio, 2048, hop_length)
+    feats = (shape[:, 0:1], shape[:, 1:2], shape[:, 2:3], zcr, r)
+    return {k: _ret(v, was_np, sq) for k, v in zip(SPECTRAL_FEATURES, feats)}
+
+
+def spectral_stats(audio, sr=22050, hop_length=512):
+    """The 10 pooled values src/1_preprocessing.py:123-125 appends (per feature: np.mean, np.std over frames),
+    float64 [..., 10] in the reference's order."""
+    shape, was_np, sq = _spectral_shape(audio, sr, 2048, hop_length, 0.85)
+    zcr, r, _, _ = _zcr_rms(audio, 2048, hop_length)
+    feats = torch.cat([shape, zcr, r.to(torch.float64)], dim=1)          # [B, 5, T]
+    stats = torch.stack([feats.mean(-1), feats.std(-1, unbiased=False)], dim=-1).reshape(feats.shape[0], 10)
+    return _ret(stats, was_np, sq)
 
 
 def mean_std_pool(feat):

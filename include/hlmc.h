@@ -61,6 +61,16 @@ int hlmc_power_to_db(void* stream, const float* S, int64_t batch, int64_t per_cl
  * out [batch][n_mfcc][T] */
 int hlmc_mfcc(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
               int n_mfcc, float* out, void* ws);
+/* Handcrafted spectral features of src/1_preprocessing.py:73-91 and src/1_preprocessing_advanced.py:133-137,
+ * same framing as the plan (center=True, periodic Hann, n_fft, hop; T = hlmc_mel_frames):
+ * librosa.feature.spectral_centroid / spectral_bandwidth (p=2, norm=True) / spectral_rolloff(roll_percent)
+ * on |STFT| (power 1).  out [batch][3][T] f64, rows centroid, bandwidth, rolloff (Hz). */
+int hlmc_spectral_shape(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
+                        double roll_percent, double* out);
+/* librosa.feature.zero_crossing_rate(frame_length=n_fft, hop) (edge padding, threshold 1e-10) -> zcr [batch][T]
+ * f64 and librosa.feature.rms(frame_length=n_fft, hop) (zero padding) -> rms [batch][T] f32.  n_fft = 2048. */
+int hlmc_zcr_rms(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
+                 double* zcr, float* rms);
 /* mean and std (ddof=0) of each row of x [rows][cols] (the mean/std pooling of the feature vectors) */
 int hlmc_row_mean_std(void* stream, const float* x, int64_t rows, int64_t cols, float* mean, float* std);
 /* StandardScaler fit, two passes with float64 accumulators (sklearn _incremental_mean_and_var):

@@ -114,3 +114,30 @@ def test_metrics_oracle_matches_sklearn_fixtures(case):
     assert abs(M.adjusted_rand_score(y_true, y_pred) - float(fx["ari"])) <= 1e-12
     assert abs(M.normalized_mutual_info_score(y_true, y_pred) - float(fx["nmi"])) <= 1e-12
     assert M.calculate_purity(y_true, y_pred) == float(fx["purity"])
+
+
+def test_spectral_oracle_properties():
+    """Pins the restatement of librosa's frame features (parity against librosa itself is unpinned):
+    a bin-centred tone has its centroid and rolloff at the tone, zcr = 2 f / sr, rms = A / sqrt(2);
+    silence gives zeros (the unnormalised branch of librosa.util.normalize)."""
+    from oracle import spectral_oracle as SO
+    sr, n = 22050, 22050 * 2
+    f = 100 * sr / 2048.0                      # bin 100
+    t = np.arange(n) / sr
+    y = (0.5 * np.sin(2 * np.pi * f * t)).astype(np.float32)
+    inner = slice(4, -4)
+    c = SO.spectral_centroid(y)[0, inner]
+    assert np.all(np.abs(c - f) < 2e-3)
+    # Hann main lobe: |X| = (1/2, 1, 1/2) at bins 99..101 -> cumsum crosses 0.85 * 2 at bin 101
+    assert np.all(SO.spectral_rolloff(y)[0, inner] == 101 * sr / 2048.0)
+    bw = SO.spectral_bandwidth(y)[0, inner]
+    # S_norm = (1/4, 1/2, 1/4) -> bandwidth = sqrt(1/2) df; the float32 quantisation floor of y spread over
+    # 1025 bins adds a few percent (deviations up to 10 kHz weigh it)
+    df = sr / 2048.0
+    assert np.all((bw > np.sqrt(0.5) * df) & (bw < 1.06 * np.sqrt(0.5) * df))
+    np.testing.assert_allclose(SO.zero_crossing_rate(y)[0, inner], 2 * f / sr, atol=1.5 / 2048)
+    np.testing.assert_allclose(SO.rms(y)[0, inner], 0.5 / np.sqrt(2), rtol=2e-3)
+    z = np.zeros(n, np.float32)
+    assert not SO.spectral_stats(z).any()
+    stats = SO.spectral_stats(y)
+    assert stats.shape == (10,) and np.isfinite(stats).all()

@@ -87,9 +87,9 @@ template <typename T> struct Vec16;
 template <> struct Vec16<float> { static constexpr int N = 4; };
 template <> struct Vec16<bf16> { static constexpr int N = 8; };
 
+// 16 raw bytes -> f32 values (4 floats or 8 bf16)
 template <typename T>
-__device__ __forceinline__ void load16_f32(const T* p, float* out) {
-    uint4 v = *reinterpret_cast<const uint4*>(p);
+__device__ __forceinline__ void cvt16_f32(uint4 v, float* out) {
     if constexpr (sizeof(T) == 4) {
         out[0] = __uint_as_float(v.x); out[1] = __uint_as_float(v.y);
         out[2] = __uint_as_float(v.z); out[3] = __uint_as_float(v.w);
@@ -102,6 +102,12 @@ __device__ __forceinline__ void load16_f32(const T* p, float* out) {
         }
     }
 }
+template <typename T>
+__device__ __forceinline__ void load16_f32(const T* p, float* out) {
+    cvt16_f32<T>(*reinterpret_cast<const uint4*>(p), out);
+}
+template <typename T>
+__device__ __forceinline__ uint4 load16_raw(const T* p) { return *reinterpret_cast<const uint4*>(p); }
 
 template <typename T>
 __device__ __forceinline__ void store16_f32(T* p, const float* in) {

@@ -304,6 +304,12 @@ class NetT : public NetBase {
     struct BnBufs {
         size_t mean = 0, inv = 0;
     };
+    // the part of the main scratch after n f64 partials that start at its base (fold space for their reduction)
+    Ws after_parts(const double* part, size_t n) const {
+        const size_t off = (n * sizeof(double) + 255) & ~(size_t)255;
+        if (reinterpret_cast<const void*>(part) != scratch.p || off >= scratch.bytes) return Ws{nullptr, 0};
+        return Ws{reinterpret_cast<float*>(reinterpret_cast<char*>(scratch.p) + off), scratch.bytes - off};
+    }
     BnBufs bn_plan(Arena& A, int C) { return BnBufs{A.take(C * 4), A.take(C * 4)}; }
     // st: statistics already emitted by the producing GEMM's epilogue (nparts > 0), else a separate pass
     int bn_fwd(hipStream_t s, bool train, const T* y, int64_t R, int C, int bn, const BnBufs& bb, int g, int beta, int act,
@@ -312,7 +318,7 @@ class NetT : public NetBase {
         float* inv = AF(bb.inv);
         if (train && st && st->nparts > 0)
             HLMC_TRY(ops::bn_stats_from_parts(s, st->part, st->nparts, R, C, mean, inv, RM[bn], RV[bn], NBT[bn],
-                                              kBnMomentum, kBnEps));
+                                              kBnMomentum, kBnEps, after_parts(st->part, (size_t)st->nparts * 2 * C)));
         else if (train)
             HLMC_TRY(ops::bn_stats<T>(s, y, R, C, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps, scratch));
         else
@@ -329,8 +335,8 @@ class NetT : public NetBase {
                                     G[g], G[beta], bias >= 0 ? G[bias] : nullptr, scratch, fused, bp));
         if (bp) {
             float* gb = G[bias];
-            const int np = ops::bn_bias_parts(R);
-            HLMC_TRY(side(s, [&](hipStream_t q, Ws) { return ops::colsum_finalize(q, bp, np, C, gb); }));
+            const int np = ops::bn_bias_parts(R, C);
+            HLMC_TRY(side(s, [&](hipStream_t q, Ws w2) { return ops::colsum_finalize(q, bp, np, C, gb, w2); }));
         }
         return HLMC_OK;
     }
@@ -387,7 +393,7 @@ class NetT : public NetBase {
             enc.y[l] = A.take(n * sizeof(T));
             enc.a[l] = A.take(n * sizeof(T));
             enc.dy[l] = A.take(n * sizeof(T));
-            enc.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * h * w) * co * sizeof(double));
+            enc.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * h * w, co) * co * sizeof(double));
             // the sub-pixel data-gradient GEMM writing this layer's output grad (4 phases over the low grid)
             need_bnb(ops::col_stats_bytes(B * (h / 2) * (w / 2), 4, co));
             enc.bb[l] = bn_plan(A, co);
@@ -484,7 +490,7 @@ class NetT : public NetBase {
                 dec.y[l] = A.take(n * sizeof(T));
                 dec.a[l] = A.take(n * sizeof(T));
                 dec.dy[l] = A.take(n * sizeof(T));
-                dec.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * 4 * h * w) * co * sizeof(double));
+                dec.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * 4 * h * w, co) * co * sizeof(double));
                 // the stride-2 conv data-gradient GEMM writing this layer's output grad (output grid 2h x 2w)
                 need_bnb(ops::col_stats_bytes(B * 4 * h * w, 1, co));
                 dec.bb[l] = bn_plan(A, co);

@@ -274,7 +274,10 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
                 (double)sizeof(T) * ((double)B * Hi * Wi * Ci + (double)Co * K + (double)M * Co));
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st, bf);
 }
-size_t col_stats_bytes(int64_t M, int phases, int C) { return (size_t)phases * cdiv((int)M, 64) * 2 * C * sizeof(double); }
+// partial rows (phases x 64-row tiles, the smallest BM) | fold scratch for their reduction
+size_t col_stats_bytes(int64_t M, int phases, int C) {
+    return (((size_t)phases * cdiv((int)M, 64) * 2 * C * sizeof(double) + 255) & ~(size_t)255) + fold_ws(2 * C);
+}
 
 template <typename T>
 size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {

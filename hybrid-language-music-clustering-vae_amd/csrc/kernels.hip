@@ -17,8 +17,17 @@ inline int grid_for(int64_t n, int per_block = kThreads, int cap = 8192) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(cap, (n + per_block - 1) / per_block));
 }
 
-// Row-chunking shared by every [R][C] column reduction: nblk blocks, each a contiguous row range.
-inline int col_blocks(int64_t R) { return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (R + 63) / 64)); }
+// Row-chunking shared by the [R][C] BatchNorm column reductions: each block streams one contiguous range of
+// 8192 / C rows (16 KB of bf16, every thread's rows in flight at once) and emits one partial row.  (Measured:
+// the former 1024-block cap left the wide-channel layers with 16-64 blocks, latency-bound at 5-20% of HBM.)
+// <= 1024 blocks (about 4 per CU); each range is a multiple of 8192 / C rows (one 4-row-per-thread step for bf16)
+// and the backward kernels prefetch the next step's rows into registers while reducing the current one.
+inline int64_t bn_rows_per_blk(int64_t R, int C) {
+    const int64_t step = std::max(1, 8192 / C);
+    const int64_t want = std::max<int64_t>(1, (R + 1023) / 1024);
+    return (want + step - 1) / step * step;
+}
+inline int bn_blocks(int64_t R, int C) { return (int)((R + bn_rows_per_blk(R, C) - 1) / bn_rows_per_blk(R, C)); }
 
 __device__ __forceinline__ float act_fwd(float z, int act) {
     if (act == 0) return z > 0.f ? z : 0.01f * z;
@@ -31,6 +40,34 @@ __device__ __forceinline__ float act_grad(float z, int act) {
     return 1.f;
 }
 
+
+// Column sums of per-thread V-channel accumulators across a 256-thread block whose thread t covers row
+// rr = t / tpr, channel group cg = t % tpr (tpr = C / V, a power of two dividing 256).  Fixed order:
+// xor-shuffle tree inside each wavefront over the lanes sharing cg, then the (<= 4) wave / row slots in LDS.
+// out[c] for c < C.  lds: >= 256 * V doubles.
+template <int V>
+__device__ __forceinline__ void block_colsum(double (&a)[V], int tpr, int C, double* lds, double* out) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int slot, cg, nslot;
+    bool valid;
+    if (tpr < 64) {
+        for (int o = tpr; o < 64; o <<= 1)
+#pragma unroll
+            for (int v = 0; v < V; ++v) a[v] += __shfl_xor(a[v], o, 64);
+        slot = w; cg = lane; valid = lane < tpr; nslot = 4;
+    } else {
+        slot = tid / tpr; cg = tid % tpr; valid = true; nslot = 256 / tpr;
+    }
+    if (valid)
+#pragma unroll
+        for (int v = 0; v < V; ++v) lds[slot * C + cg * V + v] = a[v];
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        double x = 0.0;
+        for (int k = 0; k < nslot; ++k) x += lds[k * C + c];
+        out[c] = x;
+    }
+}
 
 // Deterministic block reduction of per-block partials: part[k * stride + col] for k < nblk.
 // Thread t sums k = t, t+256, ... in order; the 256 thread sums are combined by a fixed tree.
@@ -55,7 +92,7 @@ __device__ __forceinline__ double block_sum_partials(const double* __restrict__ 
 // a block pass covers rpp = 256 / (C/V) consecutive rows (one contiguous 4 KB span); each thread keeps its
 // V channels' parameters in registers and has kU rows in flight.
 constexpr int kU = 4;   // rows in flight, forward streaming kernels
-constexpr int kUb = 2;  // backward (two operands per row)
+constexpr int kUb = 4;  // backward (two operands per row)
 
 template <typename T>
 __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ y, int64_t R, int C, int64_t rows_per_blk,
@@ -71,37 +108,85 @@ __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ 
     for (int v = 0; v < V; ++v) a[v] = b[v] = 0.0;
     const T* yp = y + cg * V;
     for (int64_t r = r0 + rr; r < r1; r += kU * rpp) {
-        float x[kU][V];
+        // every row load issued before any use: clamped (always in-bounds) rows, skipped below
+        uint4 raw[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u)
-            if (r + u * rpp < r1) load16_f32(yp + (r + u * rpp) * C, x[u]);
+        for (int u = 0; u < kU; ++u) raw[u] = load16_raw(yp + min(r + u * rpp, r1 - 1) * C);
 #pragma unroll
-        for (int u = 0; u < kU; ++u)
-            if (r + u * rpp < r1)
+        for (int u = 0; u < kU; ++u) {
+            if (r + u * rpp >= r1) break;
+            float x[V];
+            cvt16_f32<T>(raw[u], x);
 #pragma unroll
-                for (int v = 0; v < V; ++v) { a[v] += x[u][v]; b[v] += (double)x[u][v] * x[u][v]; }
+            for (int v = 0; v < V; ++v) { a[v] += x[v]; b[v] += (double)x[v] * x[v]; }
+        }
     }
-    // rpp * C == 256 * V <= 2048
-#pragma unroll
-    for (int v = 0; v < V; ++v) { s1[rr * C + cg * V + v] = a[v]; s2[rr * C + cg * V + v] = b[v]; }
-    __syncthreads();
-    for (int c = tid; c < C; c += kThreads) {
-        double x = 0.0, q = 0.0;
-        for (int k = 0; k < rpp; ++k) { x += s1[k * C + c]; q += s2[k * C + c]; }
-        part[(int64_t)blockIdx.x * 2 * C + c] = x;
-        part[(int64_t)blockIdx.x * 2 * C + C + c] = q;
-    }
+    block_colsum<V>(a, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C);
+    block_colsum<V>(b, tpr, C, s2, part + (int64_t)blockIdx.x * 2 * C + C);
 }
 
-// one block per channel: reduce the block partials of sum / sum of squares, then mean / invstd / running
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const double* __restrict__ part, int nblk, int C, int64_t R,
-                                                          float* mean, float* invstd, float* rmean, float* rvar,
-                                                          int64_t* nbt, float momentum, float eps) {
-    __shared__ double sh[256];
-    const int c = blockIdx.x;
-    const double s = block_sum_partials(part, nblk, 2 * C, c, sh);
-    const double q = block_sum_partials(part, nblk, 2 * C, C + c, sh);
-    if (threadIdx.x != 0) return;
+// ---------------------------------------------------------------- partial-row reductions
+// Partials are [rows][ncols] f64 tables (one row per producing block / GEMM tile).  Large tables are first
+// folded to <= kFoldRows rows by parts_fold_kernel (grid: 64-column slabs x row chunks, lanes = columns so
+// every wave reads 512 contiguous bytes); the finalizers then reduce <= a few hundred rows with 16 waves per
+// 64 columns.  Both passes use fixed partitions and fixed combine orders (deterministic).
+constexpr int kFoldRows = 64;      // max rows a fold leaves (one load round per wave in the finalizers)
+constexpr int kFoldMin = 64;       // fold tables with more rows than this
+__global__ __launch_bounds__(256) void parts_fold_kernel(const double* __restrict__ part, int nrows, int ncols, int rp,
+                                                         double* __restrict__ out) {
+    __shared__ double red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    const int r0 = blockIdx.y * rp, r1 = min(nrows, r0 + rp);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (c < ncols) {
+        const double* p = part + c;
+        int r = r0 + w;
+        for (; r + 12 < r1; r += 16) {
+            a0 += p[(int64_t)r * ncols];
+            a1 += p[(int64_t)(r + 4) * ncols];
+            a2 += p[(int64_t)(r + 8) * ncols];
+            a3 += p[(int64_t)(r + 12) * ncols];
+        }
+        for (; r < r1; r += 4) a0 += p[(int64_t)r * ncols];
+    }
+    red[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (w == 0 && c < ncols) out[(int64_t)blockIdx.y * ncols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+// sum over rows of column col of a [nrows][stride] table: 16 waves x 4 accumulators, LDS combine (1024 threads)
+__device__ __forceinline__ double fold_column(const double* __restrict__ p, int nrows, int64_t stride, int col, bool ok,
+                                              double (*sh)[64]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (ok) {
+        int r = w;
+        for (; r + 48 < nrows; r += 64) {
+            a0 += p[(int64_t)r * stride + col];
+            a1 += p[(int64_t)(r + 16) * stride + col];
+            a2 += p[(int64_t)(r + 32) * stride + col];
+            a3 += p[(int64_t)(r + 48) * stride + col];
+        }
+        for (; r < nrows; r += 16) a0 += p[(int64_t)r * stride + col];
+    }
+    sh[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    double x = 0.0;
+    for (int k = 0; k < 16; ++k) x += sh[k][lane];
+    __syncthreads();
+    return x;
+}
+
+// mean / invstd / running statistics from [nblk][2C] partials (sum | sum of squares); grid ceil(C / 64) x 1024
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const double* __restrict__ part, int nblk, int C, int64_t R,
+                                                           float* mean, float* invstd, float* rmean, float* rvar,
+                                                           int64_t* nbt, float momentum, float eps) {
+    __shared__ double sh[16][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool ok = c < C;
+    const double s = fold_column(part, nblk, 2 * C, c, ok, sh);
+    const double q = fold_column(part, nblk, 2 * C, C + c, ok, sh);
+    if (threadIdx.x >= 64 || !ok) return;
     if (c == 0 && nbt) nbt[0] += 1;
     const double m = s / (double)R;
     double var = q / (double)R - m * m;
@@ -131,7 +216,7 @@ struct BnChan {  // one thread's V channels of BatchNorm parameters
 };
 
 // a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale]; grid-stride over row passes
-template <typename T>
+template <typename T, bool kMask>
 __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ y, int64_t R, int C,
                                                      const float* __restrict__ mean, const float* __restrict__ invstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -148,20 +233,20 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ y, in
     BnChan::load(beta, c0, be);
     const int64_t step = (int64_t)gridDim.x * rpp;
     for (int64_t r = (int64_t)blockIdx.x * rpp + rr; r < R; r += kU * step) {
-        float x[kU][V];
+        uint4 raw[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u)
-            if (r + u * step < R) load16_f32(y + (r + u * step) * C + c0, x[u]);
+        for (int u = 0; u < kU; ++u) raw[u] = load16_raw(y + min(r + u * step, R - 1) * C + c0);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int64_t ru = r + u * step;
             if (ru >= R) break;
-            float o[V];
+            float x[V], o[V];
+            cvt16_f32<T>(raw[u], x);
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                float z = (x[u][v] - mu[v]) * is[v] * ga[v] + be[v];
+                float z = (x[v] - mu[v]) * is[v] * ga[v] + be[v];
                 float t = act_fwd(z, act);
-                if (mask) t = mask[ru * C + c0 + v] ? t * mscale : 0.f;
+                if constexpr (kMask) t = mask[ru * C + c0 + v] ? t * mscale : 0.f;
                 o[v] = t;
             }
             store16_f32(a + ru * lda + c0, o);
@@ -170,7 +255,7 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ y, in
 }
 
 // backward partial sums: part[blk][0..C) = sum dz, [C..2C) = sum dz*xhat
-template <typename T>
+template <typename T, bool kMask>
 __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
                                                              int64_t R, int C, const float* __restrict__ mean,
                                                              const float* __restrict__ invstd,
@@ -192,48 +277,52 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
     double a[V], b[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) a[v] = b[v] = 0.0;
-    for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
-        float x[kUb][V], g[kUb][V];
+    uint4 nx[kUb], ng[kUb];  // next step's rows (clamped, always in-bounds)
+    auto fetch = [&](int64_t rb) {
 #pragma unroll
-        for (int u = 0; u < kUb; ++u)
-            if (r + u * rpp < r1) {
-                load16_f32(y + (r + u * rpp) * C + c0, x[u]);
-                load16_f32(da + (r + u * rpp) * lda + c0, g[u]);
-            }
+        for (int u = 0; u < kUb; ++u) {
+            const int64_t rc = min(rb + u * rpp, r1 - 1);
+            nx[u] = load16_raw(y + rc * C + c0);
+            ng[u] = load16_raw(da + rc * lda + c0);
+        }
+    };
+    if (r0 + rr < r1) fetch(r0 + rr);
+    for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
+        uint4 rx[kUb], rg[kUb];
+#pragma unroll
+        for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
+        if (r + kUb * rpp < r1) fetch(r + kUb * rpp);
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t ru = r + u * rpp;
             if (ru >= r1) break;
+            float x[1][V], g[1][V];
+            cvt16_f32<T>(rx[u], x[0]);
+            cvt16_f32<T>(rg[u], g[0]);
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                float xh = (x[u][v] - mu[v]) * is[v];
+                float xh = (x[0][v] - mu[v]) * is[v];
                 float z = xh * ga[v] + be[v];
-                float dz = g[u][v] * act_grad(z, act);
-                if (mask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
+                float dz = g[0][v] * act_grad(z, act);
+                if constexpr (kMask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
                 a[v] += dz;
                 b[v] += (double)dz * xh;
             }
         }
     }
-#pragma unroll
-    for (int v = 0; v < V; ++v) { s1[rr * C + c0 + v] = a[v]; s2[rr * C + c0 + v] = b[v]; }
-    __syncthreads();
-    for (int c = tid; c < C; c += kThreads) {
-        double x = 0.0, q = 0.0;
-        for (int k = 0; k < rpp; ++k) { x += s1[k * C + c]; q += s2[k * C + c]; }
-        part[(int64_t)blockIdx.x * 2 * C + c] = x;
-        part[(int64_t)blockIdx.x * 2 * C + C + c] = q;
-    }
+    block_colsum<V>(a, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C);
+    block_colsum<V>(b, tpr, C, s2, part + (int64_t)blockIdx.x * 2 * C + C);
 }
 
-// reduce backward partials (one block per channel): sum dz (-> dbeta), sum dz*xhat (-> dgamma)
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nblk, int C,
-                                                              float* dgamma, float* dbeta, float* sums_f) {
-    __shared__ double sh[256];
-    const int c = blockIdx.x;
-    const double s = block_sum_partials(part, nblk, 2 * C, c, sh);
-    const double q = block_sum_partials(part, nblk, 2 * C, C + c, sh);
-    if (threadIdx.x != 0) return;
+// backward partials [nblk][2C]: sum dz (-> dbeta), sum dz*xhat (-> dgamma); grid ceil(C / 64) x 1024
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nblk, int C,
+                                                               float* dgamma, float* dbeta, float* sums_f) {
+    __shared__ double sh[16][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool ok = c < C;
+    const double s = fold_column(part, nblk, 2 * C, c, ok, sh);
+    const double q = fold_column(part, nblk, 2 * C, C + c, ok, sh);
+    if (threadIdx.x >= 64 || !ok) return;
     dbeta[c] = (float)s;
     dgamma[c] = (float)q;
     sums_f[c] = (float)s;
@@ -241,7 +330,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
 }
 
 // dy = gamma*invstd*(dz - sum_dz/R - xhat*sum_dzxh/R); also column partial sums of dy (bias grad)
-template <typename T>
+template <typename T, bool kMask>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
                                                            int64_t R, int C, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -267,25 +356,35 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     double a[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) a[v] = 0.0;
-    for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
-        float x[kUb][V], g[kUb][V];
+    uint4 nx[kUb], ng[kUb];  // next step's rows (clamped, always in-bounds)
+    auto fetch = [&](int64_t rb) {
 #pragma unroll
-        for (int u = 0; u < kUb; ++u)
-            if (r + u * rpp < r1) {
-                load16_f32(y + (r + u * rpp) * C + c0, x[u]);
-                load16_f32(da + (r + u * rpp) * lda + c0, g[u]);
-            }
+        for (int u = 0; u < kUb; ++u) {
+            const int64_t rc = min(rb + u * rpp, r1 - 1);
+            nx[u] = load16_raw(y + rc * C + c0);
+            ng[u] = load16_raw(da + rc * lda + c0);
+        }
+    };
+    if (r0 + rr < r1) fetch(r0 + rr);
+    for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
+        uint4 rx[kUb], rg[kUb];
+#pragma unroll
+        for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
+        if (r + kUb * rpp < r1) fetch(r + kUb * rpp);
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t ru = r + u * rpp;
             if (ru >= r1) break;
+            float x[1][V], g[1][V];
+            cvt16_f32<T>(rx[u], x[0]);
+            cvt16_f32<T>(rg[u], g[0]);
             float o[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                float xh = (x[u][v] - mu[v]) * is[v];
+                float xh = (x[0][v] - mu[v]) * is[v];
                 float z = xh * ga[v] + be[v];
-                float dz = g[u][v] * act_grad(z, act);
-                if (mask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
+                float dz = g[0][v] * act_grad(z, act);
+                if constexpr (kMask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
                 o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
             }
             store16_f32(dy + ru * C + c0, o);
@@ -294,23 +393,35 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
             for (int v = 0; v < V; ++v) a[v] += to_f32<T>(from_f32<T>(o[v]));
         }
     }
-#pragma unroll
-    for (int v = 0; v < V; ++v) s1[rr * C + c0 + v] = a[v];
-    __syncthreads();
-    for (int c = tid; c < C; c += kThreads) {
-        double x = 0.0;
-        for (int k = 0; k < rpp; ++k) x += s1[k * C + c];
-        part[(int64_t)blockIdx.x * C + c] = x;
-    }
+    block_colsum<V>(a, tpr, C, s1, part + (int64_t)blockIdx.x * C);
 }
 
-__global__ __launch_bounds__(256) void colsum_finalize_kernel(const double* __restrict__ part, int nblk, int C,
-                                                              float* out) {
-    __shared__ double sh[256];
-    const int c = blockIdx.x;
-    const double s = block_sum_partials(part, nblk, C, c, sh);
-    if (threadIdx.x == 0) out[c] = (float)s;
+// out[c] = sum_k part[k][c] over [nblk][C] partials; grid ceil(C / 64) x 1024
+__global__ __launch_bounds__(1024) void colsum_finalize_kernel(const double* __restrict__ part, int nblk, int C,
+                                                               float* out) {
+    __shared__ double sh[16][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const bool ok = c < C;
+    const double s = fold_column(part, nblk, C, c, ok, sh);
+    if (threadIdx.x < 64 && ok) out[c] = (float)s;
 }
+
+// Fold a [nrows][ncols] partial table into scratch when it is large; returns the table the finalizers read.
+size_t fold_bytes(int ncols) { return (size_t)kFoldRows * ncols * sizeof(double); }
+struct Folded {
+    const double* p;
+    int rows;
+};
+Folded fold_parts(hipStream_t s, const double* part, int nrows, int ncols, Ws ws) {
+    if (nrows <= kFoldMin || !ws.p || ws.bytes < fold_bytes(ncols)) return Folded{part, nrows};
+    int G = std::min(kFoldRows, cdiv(nrows, 64));  // >= 64 rows per fold block: one 4-load round per wave
+    const int rp = cdiv(nrows, G);
+    G = cdiv(nrows, rp);
+    double* out = reinterpret_cast<double*>(ws.p);
+    parts_fold_kernel<<<dim3(cdiv(ncols, 64), G), 256, 0, s>>>(part, nrows, ncols, rp, out);
+    return Folded{out, G};
+}
+inline unsigned fin_grid(int C) { return (unsigned)cdiv(C, 64); }
 
 // generic column sum for arbitrary ld/cols (bias grads): block = (row chunk, 64-column slab);
 // 4 waves split the chunk's rows, lanes own columns; fixed-order combine in LDS.
@@ -760,7 +871,15 @@ __global__ __launch_bounds__(256) void pack_kernel(const ops::AdamJob* __restric
 // ============================================================================ launchers
 namespace ops {
 
-size_t bn_ws(int64_t R, int C) { return (size_t)col_blocks(R) * 2 * C * sizeof(double) + 2 * C * sizeof(float); }
+size_t fold_ws(int ncols) { return fold_bytes(ncols); }
+// [nblk][2C] f64 partials | sums 2C f32 | fold scratch
+static size_t bn_fold_off(int64_t R, int C) {
+    return ((size_t)bn_blocks(R, C) * 2 * C * sizeof(double) + 2 * C * sizeof(float) + 255) & ~(size_t)255;
+}
+size_t bn_ws(int64_t R, int C) { return bn_fold_off(R, C) + fold_ws(2 * C); }
+static Ws ws_from(Ws ws, size_t off) {
+    return off < ws.bytes ? Ws{reinterpret_cast<float*>(reinterpret_cast<char*>(ws.p) + off), ws.bytes - off} : Ws{nullptr, 0};
+}
 
 template <typename T>
 static int check_bn_shape(int C) {
@@ -773,21 +892,22 @@ template <typename T>
 int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean, float* run_var,
              int64_t* nbt, float momentum, float eps, Ws ws) {
     HLMC_TRY(check_bn_shape<T>(C));
-    const int nblk = col_blocks(R);
+    const int nblk = bn_blocks(R, C);
     HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
-    const int64_t rpb = (R + nblk - 1) / nblk;
     double* part = reinterpret_cast<double*>(ws.p);
-    col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, rpb, part);
+    col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), part);
     HLMC_LAUNCHED();
-    bn_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
+    const Folded f = fold_parts(s, part, nblk, 2 * C, ws_from(ws, bn_fold_off(R, C)));
+    bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
 
 int bn_stats_from_parts(hipStream_t s, const double* part, int nparts, int64_t R, int C, float* mean, float* invstd,
-                        float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps) {
+                        float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, Ws fold) {
     HLMC_CHECK_ARG(part && nparts > 0 && R > 0, "bn_stats_from_parts arguments");
-    bn_finalize_kernel<<<C, 256, 0, s>>>(part, nparts, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
+    const Folded f = fold_parts(s, part, nparts, 2 * C, fold);
+    bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -804,7 +924,11 @@ int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const
     HLMC_TRY(check_bn_shape<T>(C));
     HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act: output row stride must be a multiple of 16 bytes");
     const int rpp = kThreads / (C / Vec16<T>::N);
-    bn_act_kernel<T><<<grid_for(R, rpp * kU), kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
+    const unsigned g = grid_for(R, rpp * kU);
+    if (mask)
+        bn_act_kernel<T, true><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
+    else
+        bn_act_kernel<T, false><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -815,36 +939,42 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
                float* dbeta, float* dbias, Ws ws, const BnBwdFuse* fused, double* bias_part) {
     HLMC_TRY(check_bn_shape<T>(C));
     HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act_bwd: grad row stride must be a multiple of 16 bytes");
-    const int nblk = col_blocks(R);
+    const int nblk = bn_blocks(R, C);
     HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
-    const int64_t rpb = (R + nblk - 1) / nblk;
+    const int64_t rpb = bn_rows_per_blk(R, C);
     double* part = reinterpret_cast<double*>(ws.p);
     float* sums = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
+    const Ws fw = ws_from(ws, bn_fold_off(R, C));
     if (fused && fused->nparts > 0) {  // moments came with the producing GEMM's epilogue
         HLMC_CHECK_ARG(lda == C && !mask && act == 0, "bn_act_bwd: fused moments need a dense lrelu layer");
-        bn_bwd_finalize_kernel<<<C, 256, 0, s>>>(fused->part, fused->nparts, C, dgamma, dbeta, sums);
+        const Folded f = fold_parts(s, fused->part, fused->nparts, 2 * C, fw);
+        bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums);
         HLMC_LAUNCHED();
     } else {
-        bn_bwd_moments_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale,
-                                                           rpb, part);
+        auto k = mask ? bn_bwd_moments_kernel<T, true> : bn_bwd_moments_kernel<T, false>;
+        k<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb, part);
         HLMC_LAUNCHED();
-        bn_bwd_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, dgamma, dbeta, sums);
+        const Folded f = fold_parts(s, part, nblk, 2 * C, fw);
+        bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums);
         HLMC_LAUNCHED();
     }
     double* bpart = bias_part ? bias_part : part;
-    bn_bwd_apply_kernel<T><<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
+    auto ka = mask ? bn_bwd_apply_kernel<T, true> : bn_bwd_apply_kernel<T, false>;
+    ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
                                                      dy, rpb, bpart);
     HLMC_LAUNCHED();
     if (dbias && !bias_part) {
-        colsum_finalize_kernel<<<C, 256, 0, s>>>(part, nblk, C, dbias);
+        const Folded f = fold_parts(s, part, nblk, C, fw);
+        colsum_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dbias);
         HLMC_LAUNCHED();
     }
     return HLMC_OK;
 }
-int bn_bias_parts(int64_t R) { return col_blocks(R); }
-int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out) {
+int bn_bias_parts(int64_t R, int C) { return bn_blocks(R, C); }
+int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out, Ws fold) {
     HLMC_CHECK_ARG(part && out && nparts > 0 && C > 0, "colsum_finalize: bad arguments");
-    colsum_finalize_kernel<<<C, 256, 0, s>>>(part, nparts, C, out);
+    const Folded f = fold_parts(s, part, nparts, C, fold);
+    colsum_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, out);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -935,7 +1065,7 @@ int relu_bwd(hipStream_t s, T* dy, int lddy, const T* y, int ldy, int rows, int 
     return HLMC_OK;
 }
 static int colsum_blocks(int rows) { return std::max(1, std::min(1024, rows / 256)); }
-size_t colsum_ws(int rows, int cols) { return (size_t)colsum_blocks(rows) * cols * sizeof(double); }
+size_t colsum_ws(int rows, int cols) { return (size_t)colsum_blocks(rows) * cols * sizeof(double); }  // <= 1024 rows: no fold
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_narrow_kernel(const T* __restrict__ x, int ld, int rows, int cols,
                                                             int rows_per_blk, double* __restrict__ part) {
@@ -964,7 +1094,7 @@ int colsum(hipStream_t s, const T* dy, int ld, int rows, int cols, float* db, Ws
         double* part = reinterpret_cast<double*>(ws.p);
         colsum_narrow_kernel<T><<<nblk, 256, 0, s>>>(dy, ld, rows, cols, rpb, part);
         HLMC_LAUNCHED();
-        colsum_finalize_kernel<<<cols, 256, 0, s>>>(part, nblk, cols, db);
+        colsum_finalize_kernel<<<fin_grid(cols), 1024, 0, s>>>(part, nblk, cols, db);
         HLMC_LAUNCHED();
         return HLMC_OK;
     }
@@ -974,7 +1104,7 @@ int colsum(hipStream_t s, const T* dy, int ld, int rows, int cols, float* db, Ws
     dim3 grid(nblk, cdiv(cols, 64));
     colsum_partial_kernel<T><<<grid, 256, 0, s>>>(dy, ld, rows, cols, rpb, part);
     HLMC_LAUNCHED();
-    colsum_finalize_kernel<<<cols, 256, 0, s>>>(part, nblk, cols, db);
+    colsum_finalize_kernel<<<fin_grid(cols), 1024, 0, s>>>(part, nblk, cols, db);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -82,8 +82,10 @@ int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* in
              int64_t* nbt, float momentum, float eps, Ws ws);
 size_t bn_ws(int64_t R, int C);
 // Train-mode statistics from nparts fused partial rows ([nparts][2C] f64, ColStats) over R rows.
+// fold: scratch (>= fold_ws(2C) bytes, not overlapping part) for folding large partial tables; may be empty.
 int bn_stats_from_parts(hipStream_t s, const double* part, int nparts, int64_t R, int C, float* mean, float* invstd,
-                        float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps);
+                        float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, Ws fold);
+size_t fold_ws(int ncols);  // scratch bytes to fold a [rows][ncols] f64 partial table
 // Eval-mode statistics from running buffers.
 int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, int C, float eps, float* mean, float* invstd);
 // a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale];  act: 0 lrelu(0.01), 1 relu, 2 none
@@ -98,9 +100,9 @@ template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
                float* dbeta, float* dbias, Ws ws, const BnBwdFuse* fused = nullptr, double* bias_part = nullptr);
-int bn_bias_parts(int64_t R);  // partial rows of bn_act_bwd's bias column sums
-// out[c] = sum_k part[k * C + c], k < nparts (fixed order, f64)
-int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out);
+int bn_bias_parts(int64_t R, int C);  // partial rows of bn_act_bwd's bias column sums
+// out[c] = sum_k part[k * C + c], k < nparts (fixed order, f64); fold: scratch >= fold_ws(C) bytes (may be empty)
+int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out, Ws fold);
 
 // ---------------------------------------------------------------- misc elementwise (kernels.hip)
 template <typename T> int cast_from_f32(hipStream_t s, const float* x, T* y, int64_t n);

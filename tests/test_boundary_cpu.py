@@ -24,6 +24,12 @@ def test_library_exports_every_header_symbol():
     assert lib.hlmc_version() == 1
 
 
+def test_library_resolves_every_symbol_at_load():
+    """RTLD_NOW binding: an internal function declared but never defined fails here, not in a GPU call."""
+    import os
+    C.CDLL(L.LIB_PATH, mode=os.RTLD_NOW | os.RTLD_LOCAL)
+
+
 def test_bad_arguments_return_einval_with_message():
     lib = L.lib()
     h = C.c_void_p()

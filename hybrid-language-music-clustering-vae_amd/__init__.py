@@ -15,10 +15,11 @@ All compute runs in libhlmc.so (hand-written HIP for gfx950); see include/hlmc.h
 """
 from . import _lib
 from .cluster import KMeans
-from .features import (SPECTRAL_FEATURES, StandardScaler, extract_mel_spectrogram, extract_spectral_features,
+from .features import (SPECTRAL_FEATURES, StandardScaler, chroma_stft, extract_mel_spectrogram, extract_spectral_features,
                        mean_std_pool, mel_filterbank, melspectrogram, mfcc, power_to_db, rms, spectral_bandwidth,
                        spectral_centroid, spectral_rolloff, spectral_stats, zero_crossing_rate)
 from . import metrics
+from . import preprocess
 from .losses import cvae_loss_function, loss_function, vae_loss
 from .models import VAE, ConditionalVAE, HybridVAE
 from .optim import Adam

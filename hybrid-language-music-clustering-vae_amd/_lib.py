@@ -35,6 +35,8 @@ _SIGS = {
     "hlmc_mfcc": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "hlmc_spectral_shape": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_vp]),
     "hlmc_zcr_rms": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "hlmc_chroma_workspace": (c_i64, [c_vp, c_i64, c_i64]),
+    "hlmc_chroma_stft": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
     "hlmc_row_mean_std": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "hlmc_colstats_workspace": (c_i64, [c_i64, c_i64]),
     "hlmc_colstats_sum": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),

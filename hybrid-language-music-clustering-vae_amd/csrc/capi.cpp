@@ -147,6 +147,14 @@ int hlmc_spectral_shape(const hlmc_mel_plan* p, void* stream, const float* pcm, 
     HLMC_CHECK_ARG(p, "null plan");
     return feat::spectral_shape(p->impl, S(stream), pcm, B, n, roll_percent, out);
 }
+int64_t hlmc_chroma_workspace(const hlmc_mel_plan* p, int64_t B, int64_t n) {
+    return p ? feat::chroma_workspace(p->impl, B, n) : -1;
+}
+int hlmc_chroma_stft(const hlmc_mel_plan* p, void* stream, const float* pcm, int64_t B, int64_t n, float* out,
+                     double* tuning, void* ws) {
+    HLMC_CHECK_ARG(p, "null plan");
+    return feat::chroma_stft(p->impl, S(stream), pcm, B, n, out, tuning, ws);
+}
 int hlmc_zcr_rms(const hlmc_mel_plan* p, void* stream, const float* pcm, int64_t B, int64_t n, double* zcr, float* rms) {
     HLMC_CHECK_ARG(p, "null plan");
     return feat::zcr_rms(p->impl, S(stream), pcm, B, n, zcr, rms);

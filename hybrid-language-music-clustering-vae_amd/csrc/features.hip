@@ -225,6 +225,69 @@ __global__ __launch_bounds__(256) void zcr_rms_kernel(const float* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------- chroma_stft (librosa.feature.chroma_stft)
+// Pass A (stft_mel_kernel<2>): per frame, the power bins S (stored [b][t][kSRow] for pass C) and
+// librosa.piptrack(S=S, fmin=150, fmax=4000, threshold=0.1): ref = 0.1 * max_k S_k; peaks are bins of the
+// frequency mask where x = S * (S > ref) is a local maximum (x_k > x_{k-1}, x_k >= x_{k+1}); parabolic
+// interpolation a = S_{k+1} + S_{k-1} - 2 S_k, b = (S_{k+1} - S_{k-1}) / 2, shift = |b| >= |a| ? 0 : -b / a
+// (f64, stored f32), pitch = f32((k + shift) sr / n_fft), mag = S_k + 0.5 avg shift with avg = np.gradient(S).
+// Peaks are compacted per frame (bin order) into cand[b][t][kMaxPk].
+constexpr int kSRow = 1028;   // power row stride (floats, 16-byte aligned)
+constexpr int kMaxPk = 192;   // >= peaks per frame (<= half of the masked bins)
+struct PipArgs {
+    float* S;
+    float2* cand;   // (pitch, mag)
+    int* cnt;       // peaks per frame
+    int kmin, kmax; // frequency mask [kmin, kmax)
+    double sr;
+    int n_fft;
+};
+
+__device__ __forceinline__ void piptrack_frame(const float* pw, int ln, const PipArgs& pa, int64_t row) {
+    const float4* pw4 = reinterpret_cast<const float4*>(pw);
+    float4* dst = reinterpret_cast<float4*>(pa.S + row * kSRow);
+    for (int i = ln; i < 256; i += 64) dst[i] = pw4[i];
+    if (ln == 0) dst[256] = make_float4(pw[kFFT], 0.f, 0.f, 0.f);
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) m = fmaxf(m, pw[16 * ln + j]);
+    if (ln == 63) m = fmaxf(m, pw[kFFT]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    const float ref = 0.1f * m;
+    auto thr = [&](float v) { return v > ref ? v : 0.f; };
+    auto is_peak = [&](int k) {
+        if (k < pa.kmin || k >= pa.kmax) return false;
+        const float x = thr(pw[k]);
+        return x > thr(pw[k - 1]) && x >= thr(pw[k + 1]);
+    };
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) n += is_peak(16 * ln + j) ? 1 : 0;
+    int inc = n;  // inclusive scan of the per-lane counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(inc, o, 64);
+        if (ln >= o) inc += t;
+    }
+    int slot = inc - n;
+    float2* out = pa.cand + row * kMaxPk;
+    for (int j = 0; j < 16; ++j) {
+        const int k = 16 * ln + j;
+        if (!is_peak(k) || slot >= kMaxPk) continue;
+        const float s0 = pw[k], sl = pw[k - 1], sr = pw[k + 1];
+        // librosa >= 0.10 numba stencil: f32 sums promoted to f64 by the integer constants
+        const double a = (double)(sr + sl) - 2.0 * (double)s0;
+        const double bb = (double)(sr - sl) / 2.0;
+        const float shift = fabs(bb) >= fabs(a) ? 0.f : (float)(-bb / a);
+        const float pitch = (float)(((double)k + (double)shift) * pa.sr / (double)pa.n_fft);
+        const float avg = (sr - sl) / 2.f;  // np.gradient (float32)
+        const float mag = s0 + (0.5f * avg) * shift;
+        out[slot++] = make_float2(pitch, mag);
+    }
+    if (ln == 63) pa.cnt[row] = min(inc, kMaxPk);
+}
+
 // kMode 0: banded mel (stored [b][m][t]) + per-clip max/min.  kMode 1: spectral shape of |X| (power 1):
 // centroid, bandwidth (p = 2) and rolloff per frame, stored f64 [b][3][t] (sout); the mel tables are unused.
 template <int kMode>
@@ -235,7 +298,8 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
                                                        const int* __restrict__ woff, const float* __restrict__ wts,
                                                        int n_mels, int nnz, float* __restrict__ out,
                                                        unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min,
-                                                       double bin_hz, double roll, double* __restrict__ sout) {
+                                                       double bin_hz, double roll, double* __restrict__ sout,
+                                                       PipArgs pa) {
     __shared__ float2 stw[kFFT + 1];
     __shared__ float2 stw23[kTw2 + kTw3];
     __shared__ __align__(16) float2 zb[kWaves][kZ];
@@ -361,6 +425,8 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
         // fixed-order fma chain over 8-bin steps of b128 LDS reads (power bins and chunk-transposed weights)
         if constexpr (kMode == 1) {
             spectral_shape(pw, ln, bin_hz, roll, sout + (int64_t)b * 3 * T + t0 + fl, T);
+        } else if constexpr (kMode == 2) {
+            piptrack_frame(pw, ln, pa, (int64_t)b * T + t0 + fl);
         } else {
             const float4* pw4 = reinterpret_cast<const float4*>(pw);
             const int4 bl = sbl[ln];
@@ -396,7 +462,7 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
         }
         wave_lds_fence();
     }
-    if constexpr (kMode == 1) return;
+    if constexpr (kMode != 0) return;
     __syncthreads();
     // write [n_mels][frames] rows: out[b][m][t0 + f]
     for (int i = threadIdx.x; i < n_mels * kFpb; i += 256) {
@@ -523,6 +589,143 @@ __global__ void zscore_kernel(const float* __restrict__ x, int64_t n, int64_t co
     }
 }
 
+// Pass B: librosa.estimate_tuning per clip (one 1024-thread block per clip).
+// threshold = np.median(mag over all peaks) (exact: 4-pass radix select on the non-negative float bits, the
+// two middle elements averaged in float32); residual = mod(12 * log2(pitch / 27.5), 1) in float32, folded
+// to [-0.5, 0.5); np.histogram over the 100 host-built linspace edges (99 bins, last bin closed); tuning =
+// the first edge of the first fullest bin (bin 50 = 0.0 when no peak passes).
+__device__ unsigned radix_select(const float2* __restrict__ cand, const int* __restrict__ cnt, int T, unsigned k,
+                                 unsigned* hist, unsigned* shared) {
+    unsigned prefix = 0, mask = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+        for (int t = threadIdx.x >> 6; t < T; t += blockDim.x >> 6) {
+            const int n = cnt[t];
+            for (int j = threadIdx.x & 63; j < n; j += 64) {
+                const unsigned u = __float_as_uint(cand[(int64_t)t * kMaxPk + j].y);
+                if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1u);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned acc = 0, d = 0;
+            for (; d < 256; ++d) {
+                if (acc + hist[d] > k) break;
+                acc += hist[d];
+            }
+            shared[0] = d;
+            shared[1] = k - acc;
+        }
+        __syncthreads();
+        prefix |= shared[0] << shift;
+        mask |= 255u << shift;
+        k = shared[1];
+        __syncthreads();
+    }
+    return prefix;
+}
+
+__global__ __launch_bounds__(1024) void tuning_kernel(const float2* __restrict__ cand_all, const int* __restrict__ cnt_all,
+                                                      int T, const double* __restrict__ edges, int* __restrict__ tidx,
+                                                      double* __restrict__ tval) {
+    __shared__ unsigned hist[256], sh[4];
+    __shared__ unsigned counts[100];
+    __shared__ int red[1024];
+    const int b = blockIdx.x;
+    const float2* cand = cand_all + (int64_t)b * T * kMaxPk;
+    const int* cnt = cnt_all + (int64_t)b * T;
+    int n = 0;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) n += cnt[t];
+    red[threadIdx.x] = n;
+    __syncthreads();
+    for (int w = 512; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    const unsigned total = (unsigned)red[0];
+    __syncthreads();
+    float thr = 0.f;
+    if (total > 0) {
+        const unsigned k1 = (total - 1) / 2, k2 = total / 2;
+        const float v1 = __uint_as_float(radix_select(cand, cnt, T, k1, hist, sh));
+        const float v2 = k2 == k1 ? v1 : __uint_as_float(radix_select(cand, cnt, T, k2, hist, sh));
+        thr = (v1 + v2) / 2.f;
+    }
+    for (int i = threadIdx.x; i < 100; i += blockDim.x) counts[i] = 0;
+    __syncthreads();
+    for (int t = threadIdx.x >> 6; t < T; t += blockDim.x >> 6) {
+        const int nn = cnt[t];
+        for (int j = threadIdx.x & 63; j < nn; j += 64) {
+            const float2 pm = cand[(int64_t)t * kMaxPk + j];
+            if (!(pm.y >= thr) || !(pm.x > 0.f)) continue;
+            const float o = log2f(pm.x / 27.5f);
+            float r = fmodf(12.f * o, 1.f);
+            if (r < 0.f) r += 1.f;
+            if (r >= 0.5f) r -= 1.f;
+            const double x = (double)r;
+            if (x < edges[0] || x > edges[99]) continue;
+            int lo = 0, hi = 99;  // largest i with edges[i] <= x (x == edges[99] joins the last bin)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (edges[mid] <= x) lo = mid; else hi = mid;
+            }
+            atomicAdd(&counts[lo], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int best = 50;
+        unsigned bc = 0;
+        for (int i = 0; i < 99; ++i)
+            if (counts[i] > bc) { bc = counts[i]; best = i; }
+        tidx[b] = best;
+        if (tval) tval[b] = edges[best];
+    }
+}
+
+// Pass C: chroma[c][t] = sum_k fb[tuning][c][k] S[t][k] (float32), then librosa.util.normalize(norm=inf)
+// over the 12 chroma (columns below float32 tiny stay unnormalised).  Grid (ceil(T/16), B); the clip's
+// filterbank [12][kSRow] is LDS-resident; one wavefront per frame, lane l owns bins 16 l .. 16 l + 15.
+__global__ __launch_bounds__(256) void chroma_kernel(const float* __restrict__ S, int T, const float* __restrict__ fbs,
+                                                     const int* __restrict__ tidx, float* __restrict__ out) {
+    __shared__ __align__(16) float fb[12 * kSRow];
+    const int b = blockIdx.y;
+    const float* src = fbs + (int64_t)tidx[b] * 12 * kSRow;
+    for (int i = threadIdx.x; i < 12 * kSRow / 4; i += 256)
+        reinterpret_cast<float4*>(fb)[i] = reinterpret_cast<const float4*>(src)[i];
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    for (int t = blockIdx.x * 16 + wave; t < min(T, (int)blockIdx.x * 16 + 16); t += 4) {
+        const float* row = S + ((int64_t)b * T + t) * kSRow;
+        float p[17];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float4 v = reinterpret_cast<const float4*>(row)[4 * ln + c];
+            p[4 * c] = v.x; p[4 * c + 1] = v.y; p[4 * c + 2] = v.z; p[4 * c + 3] = v.w;
+        }
+        p[16] = ln == 63 ? row[kFFT] : 0.f;
+        float raw[12];
+#pragma unroll
+        for (int c = 0; c < 12; ++c) {
+            const float* w = fb + c * kSRow + 16 * ln;
+            float acc = 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc = fmaf(w[j], p[j], acc);
+            if (ln == 63) acc = fmaf(fb[c * kSRow + kFFT], p[16], acc);
+            raw[c] = wave_sum(acc);
+        }
+        if (ln == 0) {
+            float mx = 0.f;
+#pragma unroll
+            for (int c = 0; c < 12; ++c) mx = fmaxf(mx, fabsf(raw[c]));
+            const float d = mx < 1.17549435e-38f ? 1.f : mx;
+#pragma unroll
+            for (int c = 0; c < 12; ++c) out[((int64_t)b * 12 + c) * T + t] = raw[c] / d;
+        }
+    }
+}
+
 inline int gridn(int64_t n, int cap = 8192) { return (int)std::max<int64_t>(1, std::min<int64_t>(cap, (n + 255) / 256)); }
 
 template <typename U>
@@ -617,6 +820,7 @@ void plan_destroy(MelPlanImpl* p) {
     if (!p) return;
     (void)hipFree(p->d_window); (void)hipFree(p->d_tw); (void)hipFree(p->d_rtw);
     (void)hipFree(p->d_band); (void)hipFree(p->d_woff); (void)hipFree(p->d_w);
+    (void)hipFree(p->d_chroma_fb); (void)hipFree(p->d_tune_edges);
     delete p;
 }
 
@@ -645,7 +849,7 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
     }
     HLMC_PROBE_BEGIN(s);
     stft_mel_kernel<0><<<grid, 256, dyn, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
-                                              p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0, nullptr);
+                                              p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0, nullptr, PipArgs{});
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     return HLMC_OK;
@@ -726,7 +930,110 @@ int spectral_shape(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_
     dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
     stft_mel_kernel<1><<<grid, 256, 0, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
                                             p->d_w, 0, 0, nullptr, nullptr, nullptr, (double)p->sr / p->n_fft,
-                                            roll_percent, out);
+                                            roll_percent, out, PipArgs{});
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+// librosa.filters.chroma(sr, n_fft, n_chroma=12, tuning, ctroct=5, octwidth=2, norm=2, base_c=True) in double,
+// stored float32 [12][kSRow] (bins 0..n_fft/2), for every tuning edge of estimate_tuning's histogram.
+static std::vector<float> chroma_filterbank(int sr, int n_fft, double tuning) {
+    const int nc = 12, nb = n_fft / 2 + 1;
+    std::vector<double> frq(n_fft), bw(n_fft);
+    const double a440 = 440.0 * std::pow(2.0, tuning / nc);
+    const double step = (double)sr / n_fft;
+    for (int k = 1; k < n_fft; ++k) frq[k] = nc * std::log2(((double)k * step) / (a440 / 16));
+    frq[0] = frq[1] - 1.5 * nc;
+    for (int k = 0; k + 1 < n_fft; ++k) bw[k] = std::max(frq[k + 1] - frq[k], 1.0);
+    bw[n_fft - 1] = 1.0;
+    std::vector<double> w((size_t)nc * n_fft);
+    const double half = std::round(nc / 2.0);
+    for (int c = 0; c < nc; ++c)
+        for (int k = 0; k < n_fft; ++k) {
+            double d = frq[k] - c + half + 10.0 * nc;
+            d = d - std::floor(d / nc) * nc;  // np.remainder (Python modulo)
+            d -= half;
+            const double z = 2.0 * d / bw[k];
+            w[(size_t)c * n_fft + k] = std::exp(-0.5 * z * z);
+        }
+    for (int k = 0; k < n_fft; ++k) {
+        double ss = 0.0;
+        for (int c = 0; c < nc; ++c) ss += w[(size_t)c * n_fft + k] * w[(size_t)c * n_fft + k];
+        const double len = std::sqrt(ss);
+        const double oct = (frq[k] / nc - 5.0) / 2.0;
+        const double sc = std::exp(-0.5 * oct * oct);
+        for (int c = 0; c < nc; ++c) {
+            double v = w[(size_t)c * n_fft + k];
+            if (len >= 2.2250738585072014e-308) v /= len;
+            w[(size_t)c * n_fft + k] = v * sc;
+        }
+    }
+    std::vector<float> out((size_t)nc * kSRow, 0.f);
+    for (int c = 0; c < nc; ++c)  // np.roll(wts, -3, axis=0): row c <- row (c + 3) % 12
+        for (int k = 0; k < nb; ++k) out[(size_t)c * kSRow + k] = (float)w[(size_t)((c + 3) % nc) * n_fft + k];
+    return out;
+}
+
+int chroma_tables(MelPlanImpl* p) {
+    if (p->d_chroma_fb) return HLMC_OK;
+    // np.linspace(-0.5, 0.5, 100, endpoint=False) edges
+    std::vector<double> edges(100);
+    const double stp = 1.0 / 100;
+    for (int i = 0; i < 100; ++i) edges[i] = (double)i * stp + -0.5;
+    std::vector<float> all;
+    all.reserve((size_t)99 * 12 * kSRow);
+    for (int i = 0; i < 99; ++i) {
+        const std::vector<float> f = chroma_filterbank(p->sr, p->n_fft, edges[i]);
+        all.insert(all.end(), f.begin(), f.end());
+    }
+    int st = HLMC_OK;
+    if ((st = upload(edges, &p->d_tune_edges)) || (st = upload(all, &p->d_chroma_fb))) return st;
+    // piptrack frequency mask on np.fft.rfftfreq(n_fft, 1 / sr): 150 <= f < min(4000, sr / 2)
+    const double val = 1.0 / (p->n_fft * (1.0 / p->sr));
+    const double fmax = std::min(4000.0, p->sr / 2.0);
+    p->pip_kmin = -1;
+    p->pip_kmax = 0;
+    for (int k = 0; k <= p->n_fft / 2; ++k) {
+        const double f = (double)k * val;
+        if (f >= 150.0 && f < fmax) {
+            if (p->pip_kmin < 0) p->pip_kmin = k;
+            p->pip_kmax = k + 1;
+        }
+    }
+    return HLMC_OK;
+}
+
+int64_t chroma_workspace(const MelPlanImpl* p, int64_t B, int64_t n) {
+    const int64_t T = frames(p, n);
+    auto al = [](int64_t x) { return (x + 255) & ~int64_t(255); };
+    return al(B * T * kSRow * 4) + al(B * T * kMaxPk * 8) + al(B * T * 4) + al(B * 4);
+}
+
+int chroma_stft(MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, float* out, double* tuning,
+                void* ws) {
+    HLMC_CHECK_ARG(pcm && out && ws && B > 0 && n > 0 && B <= 65535, "bad chroma_stft arguments");
+    HLMC_TRY(chroma_tables(p));
+    HLMC_CHECK_ARG(p->pip_kmin >= 1 && p->pip_kmax <= p->n_fft / 2 && (p->pip_kmax - p->pip_kmin + 1) / 2 <= kMaxPk,
+                   "piptrack frequency mask out of range");
+    const int T = (int)frames(p, n);
+    auto al = [](int64_t x) { return (x + 255) & ~int64_t(255); };
+    char* w = reinterpret_cast<char*>(ws);
+    PipArgs pa;
+    pa.S = reinterpret_cast<float*>(w);
+    pa.cand = reinterpret_cast<float2*>(w + al(B * T * kSRow * 4));
+    pa.cnt = reinterpret_cast<int*>(w + al(B * T * kSRow * 4) + al(B * T * kMaxPk * 8));
+    int* tidx = reinterpret_cast<int*>(w + al(B * T * kSRow * 4) + al(B * T * kMaxPk * 8) + al(B * T * 4));
+    pa.kmin = p->pip_kmin;
+    pa.kmax = p->pip_kmax;
+    pa.sr = p->sr;
+    pa.n_fft = p->n_fft;
+    dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
+    stft_mel_kernel<2><<<grid, 256, 0, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
+                                            p->d_w, 0, 0, nullptr, nullptr, nullptr, 0.0, 0.0, nullptr, pa);
+    HLMC_LAUNCHED();
+    tuning_kernel<<<(unsigned)B, 1024, 0, s>>>(pa.cand, pa.cnt, T, p->d_tune_edges, tidx, tuning);
+    HLMC_LAUNCHED();
+    chroma_kernel<<<dim3((T + 15) / 16, (unsigned)B), 256, 0, s>>>(pa.S, T, p->d_chroma_fb, tidx, out);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

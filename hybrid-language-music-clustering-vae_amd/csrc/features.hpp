@@ -20,6 +20,10 @@ struct MelPlanImpl {
     float* d_w = nullptr;            // packed weights
     int max_band = 0;
     int nnz = 0;
+    // chroma_stft tables (built on first use): 99 filterbanks [12][1028] f32 (one per tuning edge), edges
+    float* d_chroma_fb = nullptr;
+    double* d_tune_edges = nullptr;
+    int pip_kmin = -1, pip_kmax = 0;
 };
 
 namespace feat {
@@ -37,6 +41,9 @@ int power_to_db(hipStream_t s, const float* S, int64_t B, int64_t per, int ref_m
 int spectral_shape(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, double roll_percent,
                    double* out);
 int zcr_rms(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, double* zcr, float* rms);
+int64_t chroma_workspace(const MelPlanImpl* p, int64_t B, int64_t n);
+int chroma_stft(MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, float* out, double* tuning,
+                void* ws);
 int row_mean_std(hipStream_t s, const float* x, int64_t rows, int64_t cols, float* mean, float* sd);
 int64_t colstats_workspace(int64_t n, int64_t cols);
 int colstats(hipStream_t s, const float* x, int64_t n, int64_t cols, const double* mean, double* o0, double* o1, void* ws);

@@ -175,6 +175,24 @@ def rms(y=None, frame_length=2048, hop_length=512):
     return _ret(r, was_np, sq)
 
 
+def chroma_stft(y, sr=22050, n_fft=2048, hop_length=512, return_tuning=False):
+    """librosa.feature.chroma_stft(y, sr, n_fft, hop_length) (src/1_preprocessing.py:94-102,
+    src/1_preprocessing_advanced.py:139-141): power STFT -> estimate_tuning -> chroma filterbank -> norm=inf.
+    float32 [..., 12, T]; with return_tuning also the per-clip tuning estimate (float64 [...])."""
+    x, was_np, sq = _to_dev(y)
+    p = _plan(sr, n_fft, hop_length, 128)
+    B, n = x.shape
+    T = int(L.lib().hlmc_mel_frames(p, n))
+    out = torch.empty(B, 12, T, dtype=torch.float32, device=x.device)
+    tun = torch.empty(B, dtype=torch.float64, device=x.device)
+    ws = torch.empty(int(L.lib().hlmc_chroma_workspace(p, B, n)), dtype=torch.uint8, device=x.device)
+    L.check(L.lib().hlmc_chroma_stft(p, L.stream(), x.data_ptr(), B, n, out.data_ptr(), tun.data_ptr(),
+                                     ws.data_ptr()), "hlmc_chroma_stft")
+    del ws
+    c = _ret(out, was_np, sq)
+    return (c, _ret(tun, was_np, sq)) if return_tuning else c
+
+
 SPECTRAL_FEATURES = ("spectral_centroid", "spectral_bandwidth", "spectral_rolloff", "zcr", "rms")
 
 

@@ -71,6 +71,13 @@ int hlmc_spectral_shape(const hlmc_mel_plan* plan, void* stream, const float* pc
  * f64 and librosa.feature.rms(frame_length=n_fft, hop) (zero padding) -> rms [batch][T] f32.  n_fft = 2048. */
 int hlmc_zcr_rms(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
                  double* zcr, float* rms);
+/* librosa.feature.chroma_stft(y, sr, n_fft, hop) of src/1_preprocessing.py:94-102 and
+ * src/1_preprocessing_advanced.py:139-141: power |STFT|^2 -> estimate_tuning (piptrack fmin 150, fmax 4000,
+ * threshold 0.1; median-magnitude peaks; 0.01-semitone histogram) -> filters.chroma(tuning) -> norm=inf.
+ * out [batch][12][T] f32; tuning [batch] f64 (nullable); ws: hlmc_chroma_workspace bytes. */
+int64_t hlmc_chroma_workspace(const hlmc_mel_plan* plan, int64_t batch, int64_t n_samples);
+int hlmc_chroma_stft(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
+                     float* out, double* tuning, void* ws);
 /* mean and std (ddof=0) of each row of x [rows][cols] (the mean/std pooling of the feature vectors) */
 int hlmc_row_mean_std(void* stream, const float* x, int64_t rows, int64_t cols, float* mean, float* std);
 /* StandardScaler fit, two passes with float64 accumulators (sklearn _incremental_mean_and_var):

@@ -47,6 +47,21 @@ def main():
     print(json.dumps({"kernel": "zcr_rms_kernel", "clips": B, "ms": round(ms_zr, 3),
                       "clips_per_s": round(B / ms_zr * 1e3, 1), "pcm_GBps": round(pcm / ms_zr / 1e6, 1),
                       "hbm_frac": round(pcm / ms_zr / 1e6 / 8000.0, 3)}))
+    ws = torch.empty(int(L.lib().hlmc_chroma_workspace(p, B, n)), dtype=torch.uint8, device="cuda")
+    ch = torch.empty(B, 12, T, device="cuda")
+    ms_ch = timed(lambda: L.check(L.lib().hlmc_chroma_stft(p, L.stream(), y.data_ptr(), B, n, ch.data_ptr(), None,
+                                                           ws.data_ptr())), reps=5)
+    print(json.dumps({"kernel": "chroma_stft (piptrack STFT + tuning + chroma passes)", "clips": B,
+                      "ms": round(ms_ch, 3), "clips_per_s": round(B / ms_ch * 1e3, 1)}))
+    del ws
+    from hlmc_amd import preprocess as P
+
+    def advanced():
+        P.handcrafted_features(y, kind="advanced")
+        hlmc_amd.extract_mel_spectrogram(y, fixed_time_steps=1024)
+    ms_adv = timed(advanced, reps=3)
+    print(json.dumps({"path": "processed_data2 per-clip work (mel-dB 128x1024 + 290-d vector)", "clips": B,
+                      "ms": round(ms_adv, 3), "clips_per_s": round(B / ms_adv * 1e3, 1)}))
     ms_all = timed(lambda: hlmc_amd.spectral_stats(y), reps=5)
     from oracle import spectral_oracle as SO
     yh = y[:2].cpu().numpy()
@@ -54,6 +69,16 @@ def main():
     for c in yh:
         SO.spectral_stats(c)
     cpu = (time.perf_counter() - t0) / 2
+    from oracle import mel_oracle as MO
+    t0 = time.perf_counter()
+    c = yh[0]
+    mel = MO.extract_mel_spectrogram(c)
+    SO.spectral_stats(c)
+    SO.chroma_stft(c)
+    MO.extract_mel_spectrogram(c, fixed_time_steps=1024)
+    cpu_adv = time.perf_counter() - t0
+    print(json.dumps({"path": "processed_data2 per-clip work, numpy restatement", "cpu_clips_per_s": round(1 / cpu_adv, 2),
+                      "cpu_cores": 1, "gpu_speedup": round(B / ms_adv * 1e3 * cpu_adv, 1)}))
     print(json.dumps({"path": "spectral_stats (10 pooled values per clip)", "clips": B, "ms": round(ms_all, 3),
                       "clips_per_s": round(B / ms_all * 1e3, 1),
                       "cpu_oracle_clips_per_s": round(1.0 / cpu, 2), "cpu_cores": 1}))

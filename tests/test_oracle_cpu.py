@@ -141,3 +141,25 @@ def test_spectral_oracle_properties():
     assert not SO.spectral_stats(z).any()
     stats = SO.spectral_stats(y)
     assert stats.shape == (10,) and np.isfinite(stats).all()
+
+
+def test_chroma_oracle_properties():
+    """Pins the chroma_stft restatement (parity vs librosa unpinned): the filterbank is 12 x 1025 float32 with
+    unit-L2 columns before the octave weighting (so every column's norm is that weight); an A tone lands on
+    chroma 9 (base_c=True); the tuning estimate follows a detuned tone to within the 0.01-semitone histogram's
+    piptrack error; silence gives tuning 0 and all-zero chroma."""
+    from oracle import spectral_oracle as SO
+    fb = SO.chroma_filterbank()
+    assert fb.shape == (12, 1025) and fb.dtype == np.float32
+    freqs = np.linspace(0, 22050, 2048, endpoint=False)[1:1025]
+    octw = np.exp(-0.5 * (((np.log2(freqs / 27.5) - 5.0) / 2) ** 2))
+    np.testing.assert_allclose(np.linalg.norm(fb[:, 1:].astype(np.float64), axis=0), octw, rtol=1e-5)
+    t = np.arange(22050 * 3) / 22050
+    for det in (0.0, 0.23, -0.31):
+        f = 440 * 2 ** (det / 12)
+        y = (0.3 * np.sin(2 * np.pi * f * t) + 0.2 * np.sin(2 * np.pi * 1.5 * f * t)).astype(np.float32)
+        ch, tun = SO.chroma_stft(y)
+        assert abs(tun - det) <= 0.06, (det, tun)
+        assert np.argmax(ch[:, 8:-8].mean(1)) == 9
+    ch, tun = SO.chroma_stft(np.zeros(8192, np.float32))
+    assert tun == 0.0 and not ch.any()

@@ -91,3 +91,41 @@ def test_spectral_stats_and_device_io(cuda):
 def test_spectral_rejects_bad_arguments(cuda):
     with pytest.raises(Exception):
         hlmc_amd.spectral_rolloff(np.zeros(4096, np.float32), roll_percent=1.5)
+
+
+def _tones(n, dets, seed=0):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / 22050
+    out = []
+    for d in dets:
+        f = 440 * 2 ** (d / 12)
+        y = 0.3 * np.sin(2 * np.pi * f * t) + 0.2 * np.sin(2 * np.pi * f * 1.5 * t) + rng.normal(0, 0.01, n)
+        out.append(y)
+    return np.asarray(out, dtype=np.float32)
+
+
+@pytest.mark.parametrize("kind", ["tones", "synthetic"])
+def test_chroma_stft_vs_oracle(cuda, kind):
+    """Tuning estimates must agree exactly (they select the filterbank); chroma then rtol 1e-4 (float32 sums
+    in a different order than numpy's BLAS einsum)."""
+    y = _tones(22050 * 3, [0.0, 0.23, -0.31]) if kind == "tones" else MO.synthetic_pcm(3, 22050 * 4 + 5, seed=5)
+    got, tun = hlmc_amd.chroma_stft(y, return_tuning=True)
+    assert got.shape == (3, 12, MO.n_frames(y.shape[1])) and got.dtype == np.float32
+    for b in range(3):
+        ref, rt = SO.chroma_stft(y[b])
+        assert tun[b] == rt, (b, tun[b], rt)
+        np.testing.assert_allclose(got[b], ref, rtol=1e-4, atol=1e-6)
+
+
+def test_chroma_edge_cases(cuda):
+    z = np.zeros((2, 4096), np.float32)                      # silence: no peaks -> tuning 0, chroma 0
+    c, tun = hlmc_amd.chroma_stft(z, return_tuning=True)
+    assert not c.any() and not tun.any()
+    y = _tones(1500, [0.1])[0]                               # shorter than one frame, 1-D input
+    c, tun = hlmc_amd.chroma_stft(y, return_tuning=True)
+    ref, rt = SO.chroma_stft(y)
+    assert c.shape == ref.shape and float(tun) == rt
+    np.testing.assert_allclose(c, ref, rtol=1e-4, atol=1e-6)
+    # an A tone: the A chroma (index 9, base_c=True) dominates
+    a = _tones(22050 * 2, [0.0])
+    assert np.argmax(hlmc_amd.chroma_stft(a)[0][:, 8:-8].mean(1)) == 9

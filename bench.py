@@ -201,12 +201,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 and world == 1:
         raise SystemExit("--gpus N>1: launch with python -m torch.distributed.run --nproc-per-node N bench.py ...")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one rank per GPU; HLMC_DIST_BACKEND=gloo (with ranks sharing a device) rehearses the N > 1 control flow
+    # (barriers, max-over-ranks timing, bucketed all-reduce) on a one-GPU box
+    backend = os.environ.get("HLMC_DIST_BACKEND", "nccl")
+    local_dev = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
+    torch.cuda.set_device(local_dev)
+    device = torch.device("cuda", local_dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     B = args.batch
     audio_only = args.workload == "audio"
@@ -303,7 +310,7 @@ def main():
                                        "Convolutional_VAE hybrid, text_dim 384 (BASELINE config[2])") +
                                       ": PCM[256,65024] -> HIP mel-dB 128x128 -> z-score -> VAE fwd+bwd+Adam",
                           "per_gpu_batch": B, "global_batch": B * world, "mel": "128x128", "params": sum(
-                              p.numel() for p in model.parameters()), "parallelism": f"dp{world}",
+                              p.numel() for p in model.parameters()), "parallelism": f"dp{world}", **({"backend": backend} if world > 1 else {}),
                           "final_loss": round(loss, 3),
                           "execution": ("HIP graph replay of the whole step" if graphed else
                                         "eager launches; mel stage of step k+1 on its own stream during step k"

@@ -327,18 +327,39 @@ class NetT : public NetBase {
     }
     // fused: moments emitted by the GEMM that wrote da (nullable); bias_part: per-layer buffer of the conv bias
     // column partials, reduced on the weight-gradient stream (nullable: reduced here)
+    // defer_bias: leave the bias reduction to the next side_bias() call (one fork for it and the layer's weight
+    // gradient: every fork puts an event marker on the main stream, measured as a ~10 us bubble)
     int bn_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const BnBufs& bb, int g, int beta,
                int act, const uint8_t* mask, float mscale, T* dy, int bias, const ops::BnBwdFuse* fused = nullptr,
-               double* bias_part = nullptr) {
+               double* bias_part = nullptr, bool defer_bias = false) {
         double* bp = (bias >= 0 && use_side) ? bias_part : nullptr;
         HLMC_TRY(ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask, mscale, dy,
                                     G[g], G[beta], bias >= 0 ? G[bias] : nullptr, scratch, fused, bp));
         if (bp) {
             float* gb = G[bias];
             const int np = ops::bn_bias_parts(R, C);
-            HLMC_TRY(side(s, [&](hipStream_t q, Ws w2) { return ops::colsum_finalize(q, bp, np, C, gb, w2); }));
+            if (defer_bias)
+                pend_bias = PendingBias{bp, np, C, gb};
+            else
+                HLMC_TRY(side(s, [&](hipStream_t q, Ws w2) { return ops::colsum_finalize(q, bp, np, C, gb, w2); }));
         }
         return HLMC_OK;
+    }
+    struct PendingBias {
+        double* bp = nullptr;
+        int np = 0, C = 0;
+        float* gb = nullptr;
+    };
+    PendingBias pend_bias;
+    // f on the weight-gradient stream, after the bias reduction a preceding bn_bwd(defer_bias) left pending
+    template <class F>
+    int side_bias(hipStream_t s, F&& f) {
+        const PendingBias pb = pend_bias;
+        pend_bias = PendingBias{};
+        return side(s, [&](hipStream_t q, Ws sc) {
+            if (pb.bp) HLMC_TRY(ops::colsum_finalize(q, pb.bp, pb.np, pb.C, pb.gb, sc));
+            return f(q, sc);
+        });
     }
     // fused BN-backward moments request for the GEMM that writes the grad of a BN layer's output
     // Off by default: measured on MI355X (scripts/gpu_ab_env.sh, 3 alternating rounds) the epilogue's extra
@@ -438,13 +459,13 @@ class NetT : public NetBase {
             const int64_t R = (int64_t)B * ho * wo;
             T* dy = AT(enc.dy[l]);
             HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
-                            &fuse, reinterpret_cast<double*>(ws + enc.bpart[l])));
+                            &fuse, reinterpret_cast<double*>(ws + enc.bpart[l]), true));
             float* gw = G[enc.w[l]];
             if (l == 0) {
-                HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
+                HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
             } else {
                 const T* xin = AT(enc.a[l - 1]);
-                HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
+                HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
                 // grad of layer l-1's activation, with layer l-1's BN-backward moments from the epilogue
                 fuse = bn_fuse(AT(enc.y[l - 1]), enc.bb[l - 1], enc.g[l - 1], enc.beta[l - 1]);
                 HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch, nullptr, &fuse));
@@ -552,10 +573,10 @@ class NetT : public NetBase {
             const int64_t R = (int64_t)B * 4 * hl * wl;
             T* dy = AT(dec.dy[l]);
             HLMC_TRY(bn_bwd(s, gA, co, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f, dy, dec.b[l],
-                            &fuse, reinterpret_cast<double*>(ws + dec.bpart[l])));
+                            &fuse, reinterpret_cast<double*>(ws + dec.bpart[l]), true));
             const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
             float* gw = G[dec.w[l]];
-            HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
+            HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
             if (l > 0) {
                 fuse = bn_fuse(AT(dec.y[l - 1]), dec.bb[l - 1], dec.g[l - 1], dec.beta[l - 1]);
                 HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch, nullptr, &fuse));

@@ -249,6 +249,17 @@ class NetT : public NetBase {
         HLMC_TRY(fork(s));
         return f(s2, scratch2);
     }
+    // weight gradients of the dense layers: on the second stream (HLMC_DENSE_SIDE=1, default) or inline on s
+    // (their GEMMs are 5-20 us, about the main-stream bubble a fork's event marker costs)
+    template <class F>
+    int dense_side(hipStream_t s, F&& f) {
+        static const bool on = [] {
+            const char* e = std::getenv("HLMC_DENSE_SIDE");
+            return !(e && e[0] == '0');
+        }();
+        if (on) return side(s, std::forward<F>(f));
+        return f(s, scratch);
+    }
     // bucket k of the data-parallel all-reduce is final once both streams pass this point
     int mark(hipStream_t s, int k) {
         if (!this->bucket_sync) return HLMC_OK;
@@ -281,7 +292,7 @@ class NetT : public NetBase {
         const int N = (int)params[w].shape[0], K = (int)params[w].shape[1];
         float* gw = G[w];
         float* gb = b >= 0 ? G[b] : nullptr;
-        HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) {
+        HLMC_TRY(dense_side(s, [&](hipStream_t q, Ws sc) {
             HLMC_TRY(ops::linear_wgrad<T>(q, dy, lddy, x, ldx, B, N, K, gw, sc));
             if (gb) HLMC_TRY(ops::colsum<T>(q, dy, lddy, B, N, gb, sc));
             return (int)HLMC_OK;
@@ -294,7 +305,7 @@ class NetT : public NetBase {
     int head_wgrad(hipStream_t s, const T* dyT, const float* dyF, int L, const T* x, int ldx, int B, int K, int w, int b) {
         float* gw = G[w];
         float* gb = G[b];
-        return side(s, [&](hipStream_t q, Ws sc) {
+        return dense_side(s, [&](hipStream_t q, Ws sc) {
             HLMC_TRY(ops::linear_wgrad<T>(q, dyT, L, x, ldx, B, L, K, gw, sc));
             HLMC_TRY(ops::colsum<float>(q, dyF, L, B, L, gb, sc));
             return (int)HLMC_OK;

@@ -29,8 +29,12 @@ inline Plan plan_nt(int tiles, int Kmax, int BK) {
 }
 inline Plan plan_tn(int tiles, int K, int BK) {
     // weight gradients: long K (= batch x pixels), tiny M x N: split K until the grid fills the chip
-    // (>= 8 k-tiles per split); the slab reduction keeps 4 loads in flight
-    int S = cdiv(kTargetBlocks, tiles);
+    // (>= 4 k-tiles per split); the slab reduction keeps 4 loads in flight.  HLMC_TN_BLOCKS: target grid
+    static const int target = [] {
+        const char* e = std::getenv("HLMC_TN_BLOCKS");
+        return e ? std::max(64, std::atoi(e)) : kTargetBlocks;
+    }();
+    int S = cdiv(target, tiles);
     S = std::max(1, std::min(S, K / (4 * BK)));
     int ksl = cdiv(cdiv(K, S), BK) * BK;
     S = cdiv(K, ksl);

@@ -8,7 +8,11 @@
 namespace hlmc {
 namespace {
 
-constexpr int kTargetBlocks = 512;  // 256 CUs x 2
+// split-K grid targets (A/B on the bench step, scripts in DESIGN.md §8): NT (forward / data-gradient convs,
+// linears) 256 = one block per CU: 94.7k vs 93.3k at 512, 92.1k at 128; TN (weight gradients) 512: 93.2k vs
+// 92.8k at 1024, 90.7k at 2048
+constexpr int kNtTargetBlocks = 256;
+constexpr int kTnTargetBlocks = 512;
 constexpr int kXcdRemapDefault = probe::kWgradS2 | probe::kLinearWgrad;  // measured: helps the TN (wgrad) family, hurts sub-pixel
 
 // Split-K plan shared by the launcher and the workspace query (must agree).
@@ -18,9 +22,13 @@ struct Plan {
 // BK = the largest K-step (split ranges are multiples of it); the minimum work per split is counted in
 // steps of the short (BK/2) K-step the kernel uses for short ranges
 inline Plan plan_nt(int tiles, int Kmax, int BK) {
+    static const int target = [] {  // HLMC_NT_BLOCKS: target grid of the split-K plan (measurement aid)
+        const char* e = std::getenv("HLMC_NT_BLOCKS");
+        return e ? std::max(64, std::atoi(e)) : kNtTargetBlocks;
+    }();
     int S = 1;
-    if (tiles < kTargetBlocks / 2) {
-        S = cdiv(kTargetBlocks, tiles);
+    if (tiles < target / 2) {
+        S = cdiv(target, tiles);
         S = std::min(S, std::max(1, Kmax / (2 * BK)));
     }
     int ksl = cdiv(cdiv(Kmax, S), BK) * BK;
@@ -32,7 +40,7 @@ inline Plan plan_tn(int tiles, int K, int BK) {
     // (>= 4 k-tiles per split); the slab reduction keeps 4 loads in flight.  HLMC_TN_BLOCKS: target grid
     static const int target = [] {
         const char* e = std::getenv("HLMC_TN_BLOCKS");
-        return e ? std::max(64, std::atoi(e)) : kTargetBlocks;
+        return e ? std::max(64, std::atoi(e)) : kTnTargetBlocks;
     }();
     int S = cdiv(target, tiles);
     S = std::max(1, std::min(S, K / (4 * BK)));

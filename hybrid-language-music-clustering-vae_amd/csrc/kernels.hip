@@ -547,33 +547,48 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, 
 #pragma unroll
         for (int j = 0; j < 9; ++j) acc[i][j] = 0.f;
     constexpr int V = Vec16<T>::N;
-    for (int64_t kb = k0; kb < k1; kb += RC) {
-        for (int i = threadIdx.x; i < RC * (M / V); i += blockDim.x) {
-            const int rr = i / (M / V), cg = i % (M / V);
-            const int64_t k = kb + rr;
+    constexpr int LPT = RC * (M / V) / 256;  // 16-byte L chunks per thread per row chunk
+    static_assert(RC == 256 && LPT * 256 == RC * (M / V), "one H row and LPT L chunks per thread");
+    // the next row chunk's operands are prefetched into registers while the current one is reduced from LDS
+    uint4 nl[LPT];
+    float nh[9];
+    auto fetch = [&](int64_t kb) {
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) {
+            const int i = threadIdx.x + u * 256, rr = i / (M / V), cg = i % (M / V);
+            const int64_t k = min(kb + rr, k1 - 1);  // clamped (zeroed when stored)
+            nl[u] = load16_raw(L + k * M + cg * V);
+        }
+        const int64_t kr = kb + threadIdx.x;
+        const int k = (int)min(kr, k1 - 1);
+        const int t = (int)dWl.div((uint32_t)k), c = k - t * Wl;
+        const int b = (int)dHl.div((uint32_t)t), r = t - b * Hl;
+        const float* xr = Xh + ((int64_t)b * Hh + 2 * r - 1) * Wh + 2 * c - 1;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int ih = 2 * r - 1 + tap / 3, iw = 2 * c - 1 + tap % 3;
+            nh[tap] = (ih >= 0 && iw >= 0) ? xr[(tap / 3) * Wh + tap % 3] : 0.f;
+        }
+    };
+    auto stage = [&](int64_t kb) {
+#pragma unroll
+        for (int u = 0; u < LPT; ++u) {
+            const int i = threadIdx.x + u * 256, rr = i / (M / V), cg = i % (M / V);
             float v[V];
-            if (k < k1) {
-                load16_f32(L + k * M + cg * V, v);
-            } else {
+            cvt16_f32<T>(nl[u], v);
+            const bool ok = kb + rr < k1;
 #pragma unroll
-                for (int q = 0; q < V; ++q) v[q] = 0.f;
-            }
-#pragma unroll
-            for (int q = 0; q < V; ++q) Ls[rr][cg * V + q] = v[q];
+            for (int q = 0; q < V; ++q) Ls[rr][cg * V + q] = ok ? v[q] : 0.f;
         }
-        for (int rr = threadIdx.x; rr < RC; rr += blockDim.x) {  // one (b, r, c) decode per row, 9 taps
-            const int k = (int)(kb + rr);
-            const bool ok = k < k1;
-            const int t = (int)dWl.div((uint32_t)k), c = k - t * Wl;
-            const int b = (int)dHl.div((uint32_t)t), r = t - b * Hl;
-            const float* xr = Xh + ((int64_t)b * Hh + 2 * r - 1) * Wh + 2 * c - 1;
+        const bool ok = kb + threadIdx.x < k1;
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                const int ih = 2 * r - 1 + tap / 3, iw = 2 * c - 1 + tap % 3;
-                Hs[rr][tap] = (ok && ih >= 0 && iw >= 0) ? xr[(tap / 3) * Wh + tap % 3] : 0.f;
-            }
-        }
+        for (int tap = 0; tap < 9; ++tap) Hs[threadIdx.x][tap] = ok ? nh[tap] : 0.f;
+    };
+    if (k0 < k1) fetch(k0);
+    for (int64_t kb = k0; kb < k1; kb += RC) {
+        stage(kb);
         __syncthreads();
+        if (kb + RC < k1) fetch(kb + RC);
         for (int rr = rg; rr < RC; rr += 32) {
             float l[4], h[9];
 #pragma unroll

@@ -756,8 +756,6 @@ class HybridNet : public NetT<T> {
         HLMC_TRY(this->template lin_fwd<T>(s, AT(fuse_), ldFU, B, fus_w, fus_b, AT(h_), 512, 1));
         HLMC_TRY(this->template lin_fwd<float>(s, AT(h_), 512, B, mu_w, mu_b, AF(mu_), L, 0));
         HLMC_TRY(this->template lin_fwd<float>(s, AT(h_), 512, B, lv_w, lv_b, AF(lv_), L, 0));
-        if (a.mu) HLMC_HIP(hipMemcpyAsync(a.mu, AF(mu_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
-        if (a.logvar) HLMC_HIP(hipMemcpyAsync(a.logvar, AF(lv_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
         return HLMC_OK;
     }
 
@@ -769,9 +767,14 @@ class HybridNet : public NetT<T> {
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
         HLMC_TRY(encode(s, a, B));
+        {  // latent outputs (and the eps the backward keeps) in one launch
+            const int64_t nl = (int64_t)B * L;
+            const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
+                                        {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
+            HLMC_TRY(ops::copy_segments(s, cs, 3));
+        }
         if (a.encode_only) return HLMC_OK;
         HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
-        HLMC_HIP(hipMemcpyAsync(AF(eps_), a.eps, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
         HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), L));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(z_), L, B, di_w, di_b, AT(d1_), 512, 1));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(d1_), 512, B, ds_w, ds_b, AT(s_), ldSP, 1));
@@ -816,8 +819,10 @@ class HybridNet : public NetT<T> {
         HLMC_TRY(ops::relu_bwd<T>(s, AT(gd1_), 512, AT(d1_), 512, B, 512));
         HLMC_TRY(this->lin_bwd(s, AT(gd1_), 512, AT(z_), L, B, di_w, di_b, AT(gz_), L));
         // ---- reparameterisation + heads
-        HLMC_HIP(hipMemcpyAsync(AF(gdmu_), a.d_mu, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
-        HLMC_HIP(hipMemcpyAsync(AF(gdlv_), a.d_logvar, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        {
+            const ops::CopySeg cs[2] = {{AF(gdmu_), a.d_mu, (int64_t)B * L}, {AF(gdlv_), a.d_logvar, (int64_t)B * L}};
+            HLMC_TRY(ops::copy_segments(s, cs, 2));
+        }
         HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), L, AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
@@ -951,8 +956,6 @@ class CvaeNet : public NetT<T> {
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in2, C, AT(X_) + F + 256, ldX, B, C));
         HLMC_TRY(this->template lin_fwd<float>(s, AT(X_), ldX, B, mu_w, mu_b, AF(mu_), L, 0));
         HLMC_TRY(this->template lin_fwd<float>(s, AT(X_), ldX, B, lv_w, lv_b, AF(lv_), L, 0));
-        if (a.mu) HLMC_HIP(hipMemcpyAsync(a.mu, AF(mu_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
-        if (a.logvar) HLMC_HIP(hipMemcpyAsync(a.logvar, AF(lv_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
         return HLMC_OK;
     }
 
@@ -964,9 +967,14 @@ class CvaeNet : public NetT<T> {
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
         HLMC_TRY(encode(s, a, B));
+        {  // latent outputs (and the eps the backward keeps) in one launch
+            const int64_t nl = (int64_t)B * L;
+            const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
+                                        {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
+            HLMC_TRY(ops::copy_segments(s, cs, 3));
+        }
         if (a.encode_only) return HLMC_OK;
         HLMC_CHECK_ARG(a.eps && a.recon && a.recon_text, "eps / recon / recon_text required");
-        HLMC_HIP(hipMemcpyAsync(AF(eps_), a.eps, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
         HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(Z_), ldZ));
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in2, C, AT(Z_) + L, ldZ, B, C));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(S_), ldS, 0));
@@ -999,8 +1007,10 @@ class CvaeNet : public NetT<T> {
         // decoder_fc (no activation)
         HLMC_TRY(this->lin_bwd(s, AT(gS_), ldS, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(gZ_), ldZ));
         // reparameterisation
-        HLMC_HIP(hipMemcpyAsync(AF(gdmu_), a.d_mu, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
-        HLMC_HIP(hipMemcpyAsync(AF(gdlv_), a.d_logvar, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        {
+            const ops::CopySeg cs[2] = {{AF(gdmu_), a.d_mu, (int64_t)B * L}, {AF(gdlv_), a.d_logvar, (int64_t)B * L}};
+            HLMC_TRY(ops::copy_segments(s, cs, 2));
+        }
         HLMC_TRY(ops::reparam_bwd<T>(s, AT(gZ_), ldZ, AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
@@ -1149,8 +1159,6 @@ class SimpleNet : public NetT<T> {
         }
         HLMC_TRY(this->template lin_fwd<float>(s, x, ldx, B, mu_w, mu_b, AF(mu_), L, 0));
         HLMC_TRY(this->template lin_fwd<float>(s, x, ldx, B, lv_w, lv_b, AF(lv_), L, 0));
-        if (a.mu) HLMC_HIP(hipMemcpyAsync(a.mu, AF(mu_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
-        if (a.logvar) HLMC_HIP(hipMemcpyAsync(a.logvar, AF(lv_), (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
         return HLMC_OK;
     }
 
@@ -1162,9 +1170,14 @@ class SimpleNet : public NetT<T> {
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
         HLMC_TRY(encode(s, a, B));
+        {  // latent outputs (and the eps the backward keeps) in one launch
+            const int64_t nl = (int64_t)B * L;
+            const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
+                                        {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
+            HLMC_TRY(ops::copy_segments(s, cs, 3));
+        }
         if (a.encode_only) return HLMC_OK;
         HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
-        HLMC_HIP(hipMemcpyAsync(AF(eps_), a.eps, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
         HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), pad8(L)));
         if (a.z) HLMC_TRY(ops::reparam_fwd<float>(s, AF(mu_), AF(lv_), AF(eps_), B, L, a.z, L));
         const T* x = AT(z_);
@@ -1200,8 +1213,10 @@ class SimpleNet : public NetT<T> {
             const int ldg = i == 0 ? pad8(L) : b.din;
             HLMC_TRY(this->lin_bwd(s, dy, b.dout, xin, ldx, B, b.w, -1, gin, ldg));
         }
-        HLMC_HIP(hipMemcpyAsync(AF(gdmu_), a.d_mu, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
-        HLMC_HIP(hipMemcpyAsync(AF(gdlv_), a.d_logvar, (size_t)B * L * 4, hipMemcpyDeviceToDevice, s));
+        {
+            const ops::CopySeg cs[2] = {{AF(gdmu_), a.d_mu, (int64_t)B * L}, {AF(gdlv_), a.d_logvar, (int64_t)B * L}};
+            HLMC_TRY(ops::copy_segments(s, cs, 2));
+        }
         HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), pad8(L), AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
         HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));

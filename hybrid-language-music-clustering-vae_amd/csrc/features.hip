@@ -726,6 +726,15 @@ __global__ __launch_bounds__(256) void chroma_kernel(const float* __restrict__ S
     }
 }
 
+// per-clip max / min accumulators: 0 and a large positive float bit pattern, in one launch (two memsets
+// were two blit launches, each with its stream bubble)
+__global__ void init_minmax_kernel(unsigned* cmax, unsigned* cmin, int64_t B) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B; i += (int64_t)gridDim.x * blockDim.x) {
+        cmax[i] = 0u;
+        cmin[i] = 0x7f7f7f7fu;
+    }
+}
+
 inline int gridn(int64_t n, int cap = 8192) { return (int)std::max<int64_t>(1, std::min<int64_t>(cap, (n + 255) / 256)); }
 
 template <typename U>
@@ -836,8 +845,8 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
     HLMC_CHECK_ARG(pcm && out && B > 0 && n > 0, "bad melspectrogram arguments");
     HLMC_CHECK_ARG(B <= 65535, "batch <= 65535");
     const int T = (int)frames(p, n);
-    HLMC_HIP(hipMemsetAsync(cmax, 0, B * sizeof(unsigned), s));
-    HLMC_HIP(hipMemsetAsync(cmin, 0x7f, B * sizeof(unsigned), s));  // 0x7f7f7f7f = large positive float
+    init_minmax_kernel<<<(unsigned)((B + 255) / 256), 256, 0, s>>>(cmax, cmin, B);  // 0x7f7f7f7f: large positive float
+    HLMC_LAUNCHED();
     HLMC_CHECK_ARG(p->nnz <= kMaxW, "filterbank too large for the LDS-resident mel stage");
     HLMC_CHECK_ARG(p->n_mels <= 2 * kMelLanes, "n_mels <= 128");
     dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
@@ -911,8 +920,8 @@ int power_to_db(hipStream_t s, const float* S, int64_t B, int64_t per, int ref_m
     HLMC_CHECK_ARG(S && out && ws && B > 0 && B <= 65535, "bad power_to_db arguments");
     unsigned* cmax = reinterpret_cast<unsigned*>(ws);
     unsigned* cmin = cmax + B;
-    HLMC_HIP(hipMemsetAsync(cmax, 0, B * sizeof(unsigned), s));
-    HLMC_HIP(hipMemsetAsync(cmin, 0x7f, B * sizeof(unsigned), s));
+    init_minmax_kernel<<<(unsigned)((B + 255) / 256), 256, 0, s>>>(cmax, cmin, B);
+    HLMC_LAUNCHED();
     dim3 g(std::min<int64_t>(64, (per + 255) / 256), (unsigned)B);
     clip_max_kernel<<<g, 256, 0, s>>>(S, per, cmax, cmin);
     HLMC_LAUNCHED();

@@ -1123,6 +1123,33 @@ int colsum(hipStream_t s, const T* dy, int ld, int rows, int cols, float* db, Ws
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
+struct CopySegs4 {
+    CopySeg seg[4];
+    int64_t start[5];
+};
+__global__ __launch_bounds__(256) void copy_segments_kernel(CopySegs4 c) {
+    const int64_t total = c.start[4];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int k = 0;
+        while (k < 3 && i >= c.start[k + 1]) ++k;
+        const int64_t j = i - c.start[k];
+        c.seg[k].dst[j] = c.seg[k].src[j];
+    }
+}
+int copy_segments(hipStream_t s, const CopySeg* segs, int nseg) {
+    HLMC_CHECK_ARG(nseg >= 0 && nseg <= 4, "copy_segments: at most 4 segments");
+    CopySegs4 c{};
+    int k = 0;
+    for (int i = 0; i < nseg; ++i)
+        if (segs[i].dst && segs[i].src && segs[i].n > 0) c.seg[k++] = segs[i];
+    if (k == 0) return HLMC_OK;
+    c.start[0] = 0;
+    for (int i = 0; i < 4; ++i) c.start[i + 1] = c.start[i] + (i < k ? c.seg[i].n : 0);
+    copy_segments_kernel<<<grid_for(c.start[4]), kThreads, 0, s>>>(c);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
 template <typename T>
 int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz) {
     reparam_fwd_kernel<T><<<grid_for((int64_t)n_rows * L), kThreads, 0, s>>>(mu, lv, eps, n_rows, L, z, ldz);

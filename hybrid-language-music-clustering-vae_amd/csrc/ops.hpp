@@ -105,6 +105,14 @@ int bn_bias_parts(int64_t R, int C);  // partial rows of bn_act_bwd's bias colum
 int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out, Ws fold);
 
 // ---------------------------------------------------------------- misc elementwise (kernels.hip)
+// Up to 4 float copies in one launch (segments with null dst or src are skipped): the small per-step copies
+// (latent outputs, eps, latent gradients) each cost a launch plus a stream bubble on their own.
+struct CopySeg {
+    float* dst;
+    const float* src;
+    int64_t n;
+};
+int copy_segments(hipStream_t s, const CopySeg* segs, int nseg);
 template <typename T> int cast_from_f32(hipStream_t s, const float* x, T* y, int64_t n);
 template <typename T> int cast_to_f32(hipStream_t s, const T* x, float* y, int64_t n);
 // rows x cols submatrix copy with leading dims (T -> T)

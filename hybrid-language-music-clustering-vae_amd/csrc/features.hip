@@ -231,14 +231,14 @@ __global__ __launch_bounds__(256) void zcr_rms_kernel(const float* __restrict__ 
 // frequency mask where x = S * (S > ref) is a local maximum (x_k > x_{k-1}, x_k >= x_{k+1}); parabolic
 // interpolation a = S_{k+1} + S_{k-1} - 2 S_k, b = (S_{k+1} - S_{k-1}) / 2, shift = |b| >= |a| ? 0 : -b / a
 // (f64, stored f32), pitch = f32((k + shift) sr / n_fft), mag = S_k + 0.5 avg shift with avg = np.gradient(S).
-// Peaks are compacted per frame (bin order) into cand[b][t][kMaxPk].
+// Peaks are compacted per frame (bin order) into cand[b][t][maxpk].
 constexpr int kSRow = 1028;   // power row stride (floats, 16-byte aligned)
-constexpr int kMaxPk = 192;   // >= peaks per frame (<= half of the masked bins)
 struct PipArgs {
     float* S;
     float2* cand;   // (pitch, mag)
     int* cnt;       // peaks per frame
     int kmin, kmax; // frequency mask [kmin, kmax)
+    int maxpk;      // slots per frame: >= peaks per frame (at most every other masked bin)
     double sr;
     int n_fft;
 };
@@ -271,10 +271,10 @@ __device__ __forceinline__ void piptrack_frame(const float* pw, int ln, const Pi
         if (ln >= o) inc += t;
     }
     int slot = inc - n;
-    float2* out = pa.cand + row * kMaxPk;
+    float2* out = pa.cand + row * pa.maxpk;
     for (int j = 0; j < 16; ++j) {
         const int k = 16 * ln + j;
-        if (!is_peak(k) || slot >= kMaxPk) continue;
+        if (!is_peak(k) || slot >= pa.maxpk) continue;
         const float s0 = pw[k], sl = pw[k - 1], sr = pw[k + 1];
         // librosa >= 0.10 numba stencil: f32 sums promoted to f64 by the integer constants
         const double a = (double)(sr + sl) - 2.0 * (double)s0;
@@ -285,7 +285,7 @@ __device__ __forceinline__ void piptrack_frame(const float* pw, int ln, const Pi
         const float mag = s0 + (0.5f * avg) * shift;
         out[slot++] = make_float2(pitch, mag);
     }
-    if (ln == 63) pa.cnt[row] = min(inc, kMaxPk);
+    if (ln == 63) pa.cnt[row] = min(inc, pa.maxpk);
 }
 
 // kMode 0: banded mel (stored [b][m][t]) + per-clip max/min.  kMode 1: spectral shape of |X| (power 1):
@@ -594,8 +594,8 @@ __global__ void zscore_kernel(const float* __restrict__ x, int64_t n, int64_t co
 // two middle elements averaged in float32); residual = mod(12 * log2(pitch / 27.5), 1) in float32, folded
 // to [-0.5, 0.5); np.histogram over the 100 host-built linspace edges (99 bins, last bin closed); tuning =
 // the first edge of the first fullest bin (bin 50 = 0.0 when no peak passes).
-__device__ unsigned radix_select(const float2* __restrict__ cand, const int* __restrict__ cnt, int T, unsigned k,
-                                 unsigned* hist, unsigned* shared) {
+__device__ unsigned radix_select(const float2* __restrict__ cand, const int* __restrict__ cnt, int T, int maxpk,
+                                 unsigned k, unsigned* hist, unsigned* shared) {
     unsigned prefix = 0, mask = 0;
     for (int shift = 24; shift >= 0; shift -= 8) {
         for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
@@ -603,7 +603,7 @@ __device__ unsigned radix_select(const float2* __restrict__ cand, const int* __r
         for (int t = threadIdx.x >> 6; t < T; t += blockDim.x >> 6) {
             const int n = cnt[t];
             for (int j = threadIdx.x & 63; j < n; j += 64) {
-                const unsigned u = __float_as_uint(cand[(int64_t)t * kMaxPk + j].y);
+                const unsigned u = __float_as_uint(cand[(int64_t)t * maxpk + j].y);
                 if ((u & mask) == prefix) atomicAdd(&hist[(u >> shift) & 255], 1u);
             }
         }
@@ -627,13 +627,13 @@ __device__ unsigned radix_select(const float2* __restrict__ cand, const int* __r
 }
 
 __global__ __launch_bounds__(1024) void tuning_kernel(const float2* __restrict__ cand_all, const int* __restrict__ cnt_all,
-                                                      int T, const double* __restrict__ edges, int* __restrict__ tidx,
+                                                      int T, int maxpk, const double* __restrict__ edges, int* __restrict__ tidx,
                                                       double* __restrict__ tval) {
     __shared__ unsigned hist[256], sh[4];
     __shared__ unsigned counts[100];
     __shared__ int red[1024];
     const int b = blockIdx.x;
-    const float2* cand = cand_all + (int64_t)b * T * kMaxPk;
+    const float2* cand = cand_all + (int64_t)b * T * maxpk;
     const int* cnt = cnt_all + (int64_t)b * T;
     int n = 0;
     for (int t = threadIdx.x; t < T; t += blockDim.x) n += cnt[t];
@@ -648,8 +648,8 @@ __global__ __launch_bounds__(1024) void tuning_kernel(const float2* __restrict__
     float thr = 0.f;
     if (total > 0) {
         const unsigned k1 = (total - 1) / 2, k2 = total / 2;
-        const float v1 = __uint_as_float(radix_select(cand, cnt, T, k1, hist, sh));
-        const float v2 = k2 == k1 ? v1 : __uint_as_float(radix_select(cand, cnt, T, k2, hist, sh));
+        const float v1 = __uint_as_float(radix_select(cand, cnt, T, maxpk, k1, hist, sh));
+        const float v2 = k2 == k1 ? v1 : __uint_as_float(radix_select(cand, cnt, T, maxpk, k2, hist, sh));
         thr = (v1 + v2) / 2.f;
     }
     for (int i = threadIdx.x; i < 100; i += blockDim.x) counts[i] = 0;
@@ -657,7 +657,7 @@ __global__ __launch_bounds__(1024) void tuning_kernel(const float2* __restrict__
     for (int t = threadIdx.x >> 6; t < T; t += blockDim.x >> 6) {
         const int nn = cnt[t];
         for (int j = threadIdx.x & 63; j < nn; j += 64) {
-            const float2 pm = cand[(int64_t)t * kMaxPk + j];
+            const float2 pm = cand[(int64_t)t * maxpk + j];
             if (!(pm.y >= thr) || !(pm.x > 0.f)) continue;
             const float o = log2f(pm.x / 27.5f);
             float r = fmodf(12.f * o, 1.f);
@@ -983,6 +983,26 @@ static std::vector<float> chroma_filterbank(int sr, int n_fft, double tuning) {
     return out;
 }
 
+// piptrack frequency mask on np.fft.rfftfreq(n_fft, 1 / sr): 150 <= f < min(4000, sr / 2) -> [kmin, kmax)
+static void pip_range(int sr, int n_fft, int* kmin, int* kmax) {
+    const double val = 1.0 / (n_fft * (1.0 / sr));
+    const double fmax = std::min(4000.0, sr / 2.0);
+    *kmin = -1;
+    *kmax = 0;
+    for (int k = 0; k <= n_fft / 2; ++k) {
+        const double f = (double)k * val;
+        if (f >= 150.0 && f < fmax) {
+            if (*kmin < 0) *kmin = k;
+            *kmax = k + 1;
+        }
+    }
+}
+static int pip_slots(int sr, int n_fft) {
+    int kmin, kmax;
+    pip_range(sr, n_fft, &kmin, &kmax);
+    return std::max(8, ((kmax - kmin + 2) / 2 + 7) / 8 * 8);
+}
+
 int chroma_tables(MelPlanImpl* p) {
     if (p->d_chroma_fb) return HLMC_OK;
     // np.linspace(-0.5, 0.5, 100, endpoint=False) edges
@@ -997,32 +1017,23 @@ int chroma_tables(MelPlanImpl* p) {
     }
     int st = HLMC_OK;
     if ((st = upload(edges, &p->d_tune_edges)) || (st = upload(all, &p->d_chroma_fb))) return st;
-    // piptrack frequency mask on np.fft.rfftfreq(n_fft, 1 / sr): 150 <= f < min(4000, sr / 2)
-    const double val = 1.0 / (p->n_fft * (1.0 / p->sr));
-    const double fmax = std::min(4000.0, p->sr / 2.0);
-    p->pip_kmin = -1;
-    p->pip_kmax = 0;
-    for (int k = 0; k <= p->n_fft / 2; ++k) {
-        const double f = (double)k * val;
-        if (f >= 150.0 && f < fmax) {
-            if (p->pip_kmin < 0) p->pip_kmin = k;
-            p->pip_kmax = k + 1;
-        }
-    }
+    pip_range(p->sr, p->n_fft, &p->pip_kmin, &p->pip_kmax);
     return HLMC_OK;
 }
 
 int64_t chroma_workspace(const MelPlanImpl* p, int64_t B, int64_t n) {
     const int64_t T = frames(p, n);
     auto al = [](int64_t x) { return (x + 255) & ~int64_t(255); };
-    return al(B * T * kSRow * 4) + al(B * T * kMaxPk * 8) + al(B * T * 4) + al(B * 4);
+    const int64_t mp = pip_slots(p->sr, p->n_fft);
+    return al(B * T * kSRow * 4) + al(B * T * mp * 8) + al(B * T * 4) + al(B * 4);
 }
 
 int chroma_stft(MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, float* out, double* tuning,
                 void* ws) {
     HLMC_CHECK_ARG(pcm && out && ws && B > 0 && n > 0 && B <= 65535, "bad chroma_stft arguments");
     HLMC_TRY(chroma_tables(p));
-    HLMC_CHECK_ARG(p->pip_kmin >= 1 && p->pip_kmax <= p->n_fft / 2 && (p->pip_kmax - p->pip_kmin + 1) / 2 <= kMaxPk,
+    const int mp = pip_slots(p->sr, p->n_fft);
+    HLMC_CHECK_ARG(p->pip_kmin >= 1 && p->pip_kmax <= p->n_fft / 2 && (p->pip_kmax - p->pip_kmin + 1) / 2 < mp,
                    "piptrack frequency mask out of range");
     const int T = (int)frames(p, n);
     auto al = [](int64_t x) { return (x + 255) & ~int64_t(255); };
@@ -1030,8 +1041,9 @@ int chroma_stft(MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int6
     PipArgs pa;
     pa.S = reinterpret_cast<float*>(w);
     pa.cand = reinterpret_cast<float2*>(w + al(B * T * kSRow * 4));
-    pa.cnt = reinterpret_cast<int*>(w + al(B * T * kSRow * 4) + al(B * T * kMaxPk * 8));
-    int* tidx = reinterpret_cast<int*>(w + al(B * T * kSRow * 4) + al(B * T * kMaxPk * 8) + al(B * T * 4));
+    pa.cnt = reinterpret_cast<int*>(w + al(B * T * kSRow * 4) + al(B * T * (int64_t)mp * 8));
+    int* tidx = reinterpret_cast<int*>(w + al(B * T * kSRow * 4) + al(B * T * (int64_t)mp * 8) + al(B * T * 4));
+    pa.maxpk = mp;
     pa.kmin = p->pip_kmin;
     pa.kmax = p->pip_kmax;
     pa.sr = p->sr;
@@ -1040,7 +1052,7 @@ int chroma_stft(MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int6
     stft_mel_kernel<2><<<grid, 256, 0, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
                                             p->d_w, 0, 0, nullptr, nullptr, nullptr, 0.0, 0.0, nullptr, pa);
     HLMC_LAUNCHED();
-    tuning_kernel<<<(unsigned)B, 1024, 0, s>>>(pa.cand, pa.cnt, T, p->d_tune_edges, tidx, tuning);
+    tuning_kernel<<<(unsigned)B, 1024, 0, s>>>(pa.cand, pa.cnt, T, mp, p->d_tune_edges, tidx, tuning);
     HLMC_LAUNCHED();
     chroma_kernel<<<dim3((T + 15) / 16, (unsigned)B), 256, 0, s>>>(pa.S, T, p->d_chroma_fb, tidx, out);
     HLMC_LAUNCHED();

@@ -129,3 +129,20 @@ def test_chroma_edge_cases(cuda):
     # an A tone: the A chroma (index 9, base_c=True) dominates
     a = _tones(22050 * 2, [0.0])
     assert np.argmax(hlmc_amd.chroma_stft(a)[0][:, 8:-8].mean(1)) == 9
+
+
+def test_other_rate_and_hop(cuda):
+    """sr = 16 kHz, hop = 256: the bin frequencies, the piptrack mask and the chroma filterbank follow sr."""
+    sr, hop = 16000, 256
+    y = MO.synthetic_pcm(2, sr * 2, seed=21)
+    c = hlmc_amd.spectral_centroid(y, sr=sr, hop_length=hop)
+    assert c.shape == (2, 1, 1 + y.shape[1] // hop)
+    for b in range(2):
+        np.testing.assert_allclose(c[b, 0], SO.spectral_centroid(y[b], sr, 2048, hop)[0], rtol=1e-5, atol=0.05)
+        np.testing.assert_array_equal(hlmc_amd.zero_crossing_rate(y[b:b + 1], hop_length=hop)[0, 0],
+                                      SO.zero_crossing_rate(y[b], 2048, hop)[0])
+    ch, tun = hlmc_amd.chroma_stft(y, sr=sr, hop_length=hop, return_tuning=True)
+    for b in range(2):
+        ref, rt = SO.chroma_stft(y[b], sr, 2048, hop)
+        assert tun[b] == rt
+        np.testing.assert_allclose(ch[b], ref, rtol=1e-4, atol=1e-6)

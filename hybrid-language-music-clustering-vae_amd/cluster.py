@@ -11,6 +11,13 @@ searchsorted), potentials as float32 BLAS dot products, the best-of-n_init rule 
 centre shifts and the strict / tolerance convergence tests.  Device kernels (libhlmc) compute the
 numpy-order column mean/variance, the float64-upcast candidate distances, the float32 E-step
 (||c||^2 - 2 x.c, first minimum), per-cluster sums in sklearn's single-thread row order, and inertia.
+
+Multi-GPU (``process_group=``): the n_init restarts are independent objects, so they shard across ranks
+with no collective on the data path.  Every rank holds the same (small, [N, D] f32) latents and runs ALL
+k-means++ seedings -- sklearn draws every restart's seeds from one RandomState stream, and a seeding costs
+k distance rows against a Lloyd run's up-to-300 E/M passes -- but runs Lloyd only for restarts
+``i % world == rank``.  One ``all_gather_object`` of (restart, labels, inertia, centres, n_iter) at the end
+feeds sklearn's sequential best-of rule in restart order, so the result is bit-identical for any world size.
 """
 from __future__ import annotations
 
@@ -18,6 +25,7 @@ import ctypes as C
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import _lib as L
 
@@ -52,16 +60,26 @@ def _euclid_f32(a, b):
 
 class KMeans:
     def __init__(self, n_clusters=8, *, init="k-means++", n_init="auto", max_iter=300, tol=1e-4, verbose=0,
-                 random_state=None, copy_x=True, algorithm="lloyd", device=None):
+                 random_state=None, copy_x=True, algorithm="lloyd", device=None, process_group=None):
         if init != "k-means++" or algorithm not in ("lloyd", "auto"):
             raise ValueError("only init='k-means++', algorithm='lloyd' are implemented (the reference's defaults)")
         self.n_clusters, self.init, self.n_init, self.max_iter, self.tol = n_clusters, init, n_init, max_iter, tol
         self.verbose, self.random_state, self.copy_x, self.algorithm = verbose, random_state, copy_x, algorithm
         self.device = device
+        self.process_group = process_group
 
     # ------------------------------------------------------------------ device helpers
     def _dev(self):
         return torch.device(self.device) if self.device is not None else torch.device("cuda", torch.cuda.current_device())
+
+    def _center(self, Xd):
+        n, d = Xd.shape
+        mean = torch.empty(d, dtype=torch.float32, device=Xd.device)
+        var = torch.empty(d, dtype=torch.float32, device=Xd.device)
+        Xc = torch.empty_like(Xd)
+        L.check(L.lib().hlmc_km_center(L.stream(), Xd.data_ptr(), n, d, mean.data_ptr(), var.data_ptr(),
+                                       Xc.data_ptr()), "hlmc_km_center")
+        return mean, var, Xc
 
     def _sqdist(self, Xc, cand):
         n, d = Xc.shape
@@ -151,6 +169,16 @@ class KMeans:
                                         inertia.data_ptr(), tmp.data_ptr()))
         return labels, float(inertia.item()), centers, it + 1
 
+    @staticmethod
+    def _select_best(runs, k):
+        """sklearn's best-of-n_init rule applied in restart order (sklearn/cluster/_kmeans.py, KMeans.fit):
+        a later restart wins only with strictly lower inertia AND a different partition."""
+        best = None
+        for r in runs:
+            if best is None or (r[2] < best[2] and not _is_same_clustering(r[1], best[1], k)):
+                best = r
+        return best
+
     # ------------------------------------------------------------------ sklearn API
     def fit(self, X, y=None, sample_weight=None):
         if sample_weight is not None:
@@ -161,27 +189,32 @@ class KMeans:
         n, d = Xd.shape
         if n < self.n_clusters:
             raise ValueError(f"n_samples={n} should be >= n_clusters={self.n_clusters}")
-        mean = torch.empty(d, dtype=torch.float32, device=dev)
-        var = torch.empty(d, dtype=torch.float32, device=dev)
-        Xc = torch.empty_like(Xd)
-        L.check(L.lib().hlmc_km_center(L.stream(), Xd.data_ptr(), n, d, mean.data_ptr(), var.data_ptr(),
-                                       Xc.data_ptr()), "hlmc_km_center")
+        mean, var, Xc = self._center(Xd)
         tol = np.mean(var.cpu().numpy()) * self.tol if self.tol else 0.0
         rs = self.random_state if isinstance(self.random_state, np.random.RandomState) \
             else np.random.RandomState(self.random_state)
         n_init = 1 if self.n_init == "auto" else int(self.n_init)
         w = np.ones(n, dtype=np.float32)
-        best = None
-        for _ in range(n_init):
-            c0, _ = self._kmeans_plusplus(Xc, rs, w)
+        world, rank = 1, 0
+        if self.process_group is not None:
+            world = dist.get_world_size(self.process_group)
+            rank = dist.get_rank(self.process_group)
+        runs = []
+        for i in range(n_init):
+            c0, _ = self._kmeans_plusplus(Xc, rs, w)      # every rank: keeps the one RandomState stream
+            if i % world != rank:
+                continue
             labels, inertia, centers, n_iter = self._lloyd(Xc, c0, tol)
-            lab = labels.cpu().numpy()
-            if best is None or (inertia < best[1] and not _is_same_clustering(lab, best[0], self.n_clusters)):
-                best = (lab, inertia, centers, n_iter)
-        self.labels_ = best[0].astype(np.int32)
-        self.inertia_ = best[1]
-        self.cluster_centers_ = (best[2] + mean).cpu().numpy()
-        self.n_iter_ = best[3]
+            runs.append((i, labels.cpu().numpy(), inertia, centers.cpu().numpy(), n_iter))
+        if world > 1:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, runs, group=self.process_group)
+            runs = sorted((r for part in gathered for r in part), key=lambda r: r[0])
+        best = self._select_best(runs, self.n_clusters)
+        self.labels_ = best[1].astype(np.int32)
+        self.inertia_ = best[2]
+        self.cluster_centers_ = best[3] + mean.cpu().numpy()
+        self.n_iter_ = best[4]
         self.n_features_in_ = d
         return self
 

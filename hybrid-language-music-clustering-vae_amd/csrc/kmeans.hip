@@ -120,22 +120,64 @@ __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict_
     }
 }
 
-// sums[j][c] = sum_{i: l_i == j} X[i][c] in row order (float32); weight[j] = count
-__global__ void km_sums_kernel(const float* __restrict__ X, int64_t n, int d, const int32_t* __restrict__ labels, int k,
-                               float* __restrict__ sums, float* __restrict__ weight) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= k * (d + 1)) return;
-    const int j = t / (d + 1), c = t % (d + 1);
+// sums[j][c] = sum_{i: l_i == j} X[i][c] in row order (float32); weight[j] = count.
+// One wave per (64-column slab, cluster j).  The wave walks the labels in super-tiles of 1024 rows (16 per
+// lane, the next super-tile prefetched into registers), compacts the rows of cluster j in row order with
+// ballots into LDS, then gathers those rows' columns in groups of 64 (independent loads, all in flight)
+// and adds them into one float32 accumulator per column in row order -- sklearn's single-thread order.
+constexpr int kLabQ = 16;
+constexpr int kSumGrp = 64;
+__global__ __launch_bounds__(64) void km_sums_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                     const int32_t* __restrict__ labels, int k,
+                                                     float* __restrict__ sums, float* __restrict__ weight) {
+    __shared__ int64_t list[64 * kLabQ];
+    const int j = blockIdx.y;
+    const int lane = threadIdx.x;
+    const int c = blockIdx.x * 64 + lane;
+    const int cc = c < d ? c : d - 1;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     float s = 0.f;
-    if (c < d) {
-        for (int64_t i = 0; i < n; ++i)
-            if (labels[i] == j) s += X[i * d + c];
-        sums[j * d + c] = s;
-    } else {
-        for (int64_t i = 0; i < n; ++i)
-            if (labels[i] == j) s += 1.f;
-        weight[j] = s;
+    int64_t count = 0;
+    int lab[kLabQ], nxt[kLabQ];
+#pragma unroll
+    for (int q = 0; q < kLabQ; ++q) {
+        const int64_t row = (int64_t)q * 64 + lane;
+        lab[q] = row < n ? labels[row] : -1;
     }
+    for (int64_t base = 0; base < n; base += 64 * kLabQ) {
+        const int64_t nb = base + 64 * kLabQ;
+#pragma unroll
+        for (int q = 0; q < kLabQ; ++q) {
+            const int64_t row = nb + (int64_t)q * 64 + lane;
+            nxt[q] = row < n ? labels[row] : -1;
+        }
+        int m = 0;
+#pragma unroll
+        for (int q = 0; q < kLabQ; ++q) {
+            const bool hit = lab[q] == j;
+            const uint64_t mask = __ballot(hit);
+            if (hit) list[m + __popcll(mask & lt)] = base + (int64_t)q * 64 + lane;
+            m += __popcll(mask);
+        }
+        __syncthreads();
+        count += m;
+        for (int g = 0; g < m; g += kSumGrp) {
+            float v[kSumGrp];
+#pragma unroll
+            for (int t = 0; t < kSumGrp; ++t) {
+                const int idx = g + t < m ? g + t : m - 1;
+                v[t] = X[list[idx] * d + cc];
+            }
+#pragma unroll
+            for (int t = 0; t < kSumGrp; ++t)
+                if (g + t < m) s += v[t];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kLabQ; ++q) lab[q] = nxt[q];
+    }
+    if (c < d) sums[(int64_t)j * d + c] = s;
+    if (blockIdx.x == 0 && lane == 0) weight[j] = (float)count;
 }
 
 // _euclidean_dense_dense(squared=True): float32 sum of 4-element groups, then the tail
@@ -158,11 +200,37 @@ __global__ void km_rowdist_kernel(const float* __restrict__ X, int64_t n, int d,
         out[i] = r;
     }
 }
-__global__ void km_seqsum_kernel(const float* __restrict__ v, int64_t n, float* out) {
-    if (threadIdx.x || blockIdx.x) return;
+// float32 sum of v[0..n) in index order: one wave stages 1024 values per round in LDS (coalesced loads,
+// the next round prefetched in registers); lane 0 adds them sequentially from LDS.
+__global__ __launch_bounds__(64) void km_seqsum_kernel(const float* __restrict__ v, int64_t n, float* out) {
+    __shared__ float buf[64 * kLabQ];
+    const int lane = threadIdx.x;
+    float cur[kLabQ], nxt[kLabQ];
+#pragma unroll
+    for (int q = 0; q < kLabQ; ++q) {
+        const int64_t i = (int64_t)q * 64 + lane;
+        cur[q] = i < n ? v[i] : 0.f;
+    }
     float s = 0.f;
-    for (int64_t i = 0; i < n; ++i) s += v[i];
-    out[0] = s;
+    for (int64_t base = 0; base < n; base += 64 * kLabQ) {
+        const int64_t nb = base + 64 * kLabQ;
+#pragma unroll
+        for (int q = 0; q < kLabQ; ++q) {
+            const int64_t i = nb + (int64_t)q * 64 + lane;
+            nxt[q] = i < n ? v[i] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < kLabQ; ++q) buf[q * 64 + lane] = cur[q];
+        __syncthreads();
+        if (lane == 0) {
+            const int m = (int)((n - base) < 64 * kLabQ ? (n - base) : 64 * kLabQ);
+            for (int t = 0; t < m; ++t) s += buf[t];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kLabQ; ++q) cur[q] = nxt[q];
+    }
+    if (lane == 0) out[0] = s;
 }
 
 }  // namespace
@@ -204,8 +272,8 @@ int assign(hipStream_t s, const float* X, int64_t n, int d, const float* C, int 
 
 int sums(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w) {
     HLMC_CHECK_ARG(X && labels && sm && w && k > 0, "bad km_sums arguments");
-    const int t = k * (d + 1);
-    km_sums_kernel<<<(t + 63) / 64, 64, 0, s>>>(X, n, d, labels, k, sm, w);
+    HLMC_CHECK_ARG(n > 0 && d > 0 && k <= 65535, "bad km_sums sizes");
+    km_sums_kernel<<<dim3((unsigned)((d + 63) / 64), (unsigned)k), 64, 0, s>>>(X, n, d, labels, k, sm, w);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -38,3 +38,65 @@ def test_kmeans_empty_cluster_relocation(cuda):
         ref = SK(n_clusters=12, random_state=42, n_init=3).fit(X)
     ours = hlmc_amd.KMeans(n_clusters=12, random_state=42, n_init=3).fit(X)
     np.testing.assert_array_equal(ours.labels_, ref.labels_)
+
+
+def _sharded_worker(rank, port, outdir, case):
+    import os
+    import sys
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    import hlmc_amd
+    torch.cuda.set_device(0)
+    n, d, centers, k, n_init = case
+    X = FX.blobs(n, d, centers, seed=n + d + k)
+    km = hlmc_amd.KMeans(n_clusters=k, random_state=42, n_init=n_init, process_group=dist.group.WORLD).fit(X)
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), labels=km.labels_, centers=km.cluster_centers_,
+             inertia=km.inertia_, n_iter=km.n_iter_)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_kmeans_restarts_sharded_two_ranks(cuda):
+    """n_init restarts sharded over 2 ranks (gloo, both on cuda:0): each rank's result equals the
+    single-process fit and the sklearn golden labels bit-for-bit."""
+    import os
+    import tempfile
+    import torch.multiprocessing as mp
+    case = [c for c in FX.KMEANS_CASES if c[0] == 1336 and c[1] == 128 and c[3] == 10 and c[4] == 10][0]
+    n, d, centers, k, n_init = case
+    fx = np.load(f"tests/golden/kmeans_n{n}_d{d}_k{k}_i{n_init}.npz")
+    with tempfile.TemporaryDirectory() as outdir:
+        mp.spawn(_sharded_worker, args=(29800 + os.getpid() % 100, outdir, case), nprocs=2, join=True)
+        res = [dict(np.load(os.path.join(outdir, f"rank{r}.npz"))) for r in range(2)]
+    single = hlmc_amd.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(FX.blobs(n, d, centers, seed=n + d + k))
+    for r in res:
+        np.testing.assert_array_equal(r["labels"], fx["labels"])
+        np.testing.assert_array_equal(r["labels"], single.labels_)
+        np.testing.assert_array_equal(r["centers"], single.cluster_centers_)
+        assert float(r["inertia"]) == single.inertia_ and int(r["n_iter"]) == single.n_iter_
+
+
+@pytest.mark.parametrize("n,d,k", [(20000, 80, 7), (3000, 130, 3), (1025, 64, 1)])
+def test_km_sums_row_order_bitexact(cuda, n, d, k):
+    """hlmc_km_sums = sklearn's single-thread float32 centre sums: per cluster and column a strictly
+    sequential row-order add (np.add.accumulate), counts exact; ragged column slabs and super-tiles."""
+    import torch
+    from hlmc_amd import _lib as L
+    rng = np.random.default_rng(n + d + k)
+    X = rng.normal(0, 2.0, (n, d)).astype(np.float32)
+    lab = rng.integers(0, k, n).astype(np.int32)
+    lab[: n // 3] = 0                                     # one heavy cluster
+    Xd, ld = torch.as_tensor(X, device="cuda"), torch.as_tensor(lab, device="cuda")
+    sums = torch.empty(k, d, device="cuda")
+    w = torch.empty(k, device="cuda")
+    L.check(L.lib().hlmc_km_sums(L.stream(), Xd.data_ptr(), n, d, ld.data_ptr(), k, sums.data_ptr(), w.data_ptr()))
+    got = sums.cpu().numpy()
+    for j in range(k):
+        rows = X[lab == j]
+        ref = np.add.accumulate(rows, axis=0)[-1] if len(rows) else np.zeros(d, np.float32)
+        np.testing.assert_array_equal(got[j], ref)
+        assert float(w[j]) == float((lab == j).sum())

@@ -127,55 +127,62 @@ __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict_
 // and adds them into one float32 accumulator per column in row order -- sklearn's single-thread order.
 constexpr int kLabQ = 16;
 constexpr int kSumGrp = 64;
-__global__ __launch_bounds__(64) void km_sums_kernel(const float* __restrict__ X, int64_t n, int d,
+template <bool kFull>
+__device__ __forceinline__ float km_gather_add(const float* __restrict__ Xc, int d, const int* list, int g, int m,
+                                               int lane, float s) {
+    // one LDS read per 64 list entries; each row index is broadcast with readlane (no LDS round trip)
+    const int mine = list[kFull ? g + lane : min(g + lane, m - 1)];
+    float v[kSumGrp];
+#pragma unroll
+    for (int t = 0; t < kSumGrp; ++t) v[t] = Xc[(int64_t)__builtin_amdgcn_readlane(mine, t) * d];
+#pragma unroll
+    for (int t = 0; t < kSumGrp; ++t)
+        if (kFull || g + t < m) s += v[t];
+    return s;
+}
+
+__global__ __launch_bounds__(64) void km_sums_kernel(const float* __restrict__ X, int n, int d,
                                                      const int32_t* __restrict__ labels, int k,
                                                      float* __restrict__ sums, float* __restrict__ weight) {
-    __shared__ int64_t list[64 * kLabQ];
+    __shared__ int list[64 * kLabQ + kSumGrp];     // carried partial group + one super-tile of hits
     const int j = blockIdx.y;
     const int lane = threadIdx.x;
     const int c = blockIdx.x * 64 + lane;
-    const int cc = c < d ? c : d - 1;
+    const float* __restrict__ Xc = X + (c < d ? c : d - 1);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     float s = 0.f;
-    int64_t count = 0;
+    int count = 0, p = 0;
     int lab[kLabQ], nxt[kLabQ];
+    // rows past n read the last label (clamped, unconditional loads) and are masked out below
 #pragma unroll
-    for (int q = 0; q < kLabQ; ++q) {
-        const int64_t row = (int64_t)q * 64 + lane;
-        lab[q] = row < n ? labels[row] : -1;
-    }
-    for (int64_t base = 0; base < n; base += 64 * kLabQ) {
-        const int64_t nb = base + 64 * kLabQ;
+    for (int q = 0; q < kLabQ; ++q) lab[q] = labels[min(q * 64 + lane, n - 1)];
+    for (int base = 0; base < n; base += 64 * kLabQ) {
+        const int nb = base + 64 * kLabQ;
 #pragma unroll
-        for (int q = 0; q < kLabQ; ++q) {
-            const int64_t row = nb + (int64_t)q * 64 + lane;
-            nxt[q] = row < n ? labels[row] : -1;
-        }
-        int m = 0;
+        for (int q = 0; q < kLabQ; ++q) nxt[q] = labels[min(nb + q * 64 + lane, n - 1)];
+        int tot = p;
 #pragma unroll
         for (int q = 0; q < kLabQ; ++q) {
-            const bool hit = lab[q] == j;
+            const int row = base + q * 64 + lane;
+            const bool hit = lab[q] == j && row < n;
             const uint64_t mask = __ballot(hit);
-            if (hit) list[m + __popcll(mask & lt)] = base + (int64_t)q * 64 + lane;
-            m += __popcll(mask);
+            if (hit) list[tot + __popcll(mask & lt)] = row;
+            tot += __popcll(mask);
         }
         __syncthreads();
-        count += m;
-        for (int g = 0; g < m; g += kSumGrp) {
-            float v[kSumGrp];
-#pragma unroll
-            for (int t = 0; t < kSumGrp; ++t) {
-                const int idx = g + t < m ? g + t : m - 1;
-                v[t] = X[list[idx] * d + cc];
-            }
-#pragma unroll
-            for (int t = 0; t < kSumGrp; ++t)
-                if (g + t < m) s += v[t];
-        }
+        count += tot - p;
+        int g = 0;
+        for (; g + kSumGrp <= tot; g += kSumGrp) s = km_gather_add<true>(Xc, d, list, g, tot, lane, s);
+        // carry the partial group (< 64 rows, row order kept) to the front of the list
+        p = tot - g;
+        const int carry = lane < p ? list[g + lane] : 0;
+        __syncthreads();
+        if (lane < p) list[lane] = carry;
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < kLabQ; ++q) lab[q] = nxt[q];
     }
+    if (p > 0) s = km_gather_add<false>(Xc, d, list, 0, p, lane, s);
     if (c < d) sums[(int64_t)j * d + c] = s;
     if (blockIdx.x == 0 && lane == 0) weight[j] = (float)count;
 }
@@ -272,8 +279,8 @@ int assign(hipStream_t s, const float* X, int64_t n, int d, const float* C, int 
 
 int sums(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w) {
     HLMC_CHECK_ARG(X && labels && sm && w && k > 0, "bad km_sums arguments");
-    HLMC_CHECK_ARG(n > 0 && d > 0 && k <= 65535, "bad km_sums sizes");
-    km_sums_kernel<<<dim3((unsigned)((d + 63) / 64), (unsigned)k), 64, 0, s>>>(X, n, d, labels, k, sm, w);
+    HLMC_CHECK_ARG(n > 0 && n < (int64_t)1 << 30 && d > 0 && k <= 65535, "bad km_sums sizes");
+    km_sums_kernel<<<dim3((unsigned)((d + 63) / 64), (unsigned)k), 64, 0, s>>>(X, (int)n, d, labels, k, sm, w);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -13,21 +13,37 @@ namespace {
 
 // X.mean(axis=0) in numpy: sequential float32 row accumulation, then / n; Xc = X - mean.
 // np.var(X, axis=0): sequential float32 sum of (x - mean)^2, then / n (sklearn's tolerance input).
-__global__ void km_colmean_kernel(const float* __restrict__ X, int64_t n, int d, float* __restrict__ mean,
-                                  float* __restrict__ var) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= d) return;
+// One wave per 64 columns; rows are read in groups of 64 (coalesced 256-B row segments, all loads of a
+// group in flight) and added in row order into one accumulator per column.
+constexpr int kColGrp = 64;
+__global__ __launch_bounds__(64) void km_colmean_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                        float* __restrict__ mean, float* __restrict__ var) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const float* __restrict__ Xc = X + (c < d ? c : d - 1);
     float s = 0.f;
-    for (int64_t i = 0; i < n; ++i) s += X[i * d + c];
+    for (int64_t g = 0; g < n; g += kColGrp) {
+        float v[kColGrp];
+#pragma unroll
+        for (int t = 0; t < kColGrp; ++t) v[t] = Xc[(g + t < n ? g + t : n - 1) * d];
+#pragma unroll
+        for (int t = 0; t < kColGrp; ++t)
+            if (g + t < n) s += v[t];
+    }
     const float m = s / (float)n;
-    mean[c] = m;
+    if (c < d) mean[c] = m;
     if (var) {
         float q = 0.f;
-        for (int64_t i = 0; i < n; ++i) {
-            const float e = X[i * d + c] - m;
-            q += e * e;
+        for (int64_t g = 0; g < n; g += kColGrp) {
+            float v[kColGrp];
+#pragma unroll
+            for (int t = 0; t < kColGrp; ++t) v[t] = Xc[(g + t < n ? g + t : n - 1) * d];
+#pragma unroll
+            for (int t = 0; t < kColGrp; ++t) {
+                const float e = v[t] - m;
+                if (g + t < n) q += e * e;
+            }
         }
-        var[c] = q / (float)n;
+        if (c < d) var[c] = q / (float)n;
     }
 }
 __global__ void km_sub_kernel(const float* __restrict__ X, int64_t n, int d, const float* __restrict__ mean,

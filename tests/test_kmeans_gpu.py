@@ -100,3 +100,17 @@ def test_km_sums_row_order_bitexact(cuda, n, d, k):
         ref = np.add.accumulate(rows, axis=0)[-1] if len(rows) else np.zeros(d, np.float32)
         np.testing.assert_array_equal(got[j], ref)
         assert float(w[j]) == float((lab == j).sum())
+
+
+@pytest.mark.parametrize("n,d", [(20000, 80), (1337, 128), (70, 3)])
+def test_km_center_numpy_order_bitexact(cuda, n, d):
+    """hlmc_km_center = numpy's X.mean(axis=0) / np.var(X, axis=0) (row-sequential float32) bit for bit."""
+    import torch
+    from hlmc_amd import _lib as L
+    X = np.random.default_rng(n * d).normal(0.5, 2.0, (n, d)).astype(np.float32)
+    Xd = torch.as_tensor(X, device="cuda")
+    mean, var, Xc = torch.empty(d, device="cuda"), torch.empty(d, device="cuda"), torch.empty_like(Xd)
+    L.check(L.lib().hlmc_km_center(L.stream(), Xd.data_ptr(), n, d, mean.data_ptr(), var.data_ptr(), Xc.data_ptr()))
+    np.testing.assert_array_equal(mean.cpu().numpy(), X.mean(axis=0))
+    np.testing.assert_array_equal(var.cpu().numpy(), np.var(X, axis=0))
+    np.testing.assert_array_equal(Xc.cpu().numpy(), X - X.mean(axis=0))

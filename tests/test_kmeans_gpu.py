@@ -80,7 +80,7 @@ def test_kmeans_restarts_sharded_two_ranks(cuda):
         assert float(r["inertia"]) == single.inertia_ and int(r["n_iter"]) == single.n_iter_
 
 
-@pytest.mark.parametrize("n,d,k", [(20000, 80, 7), (3000, 130, 3), (1025, 64, 1)])
+@pytest.mark.parametrize("n,d,k", [(20000, 80, 7), (3000, 130, 3), (1025, 64, 1), (5000, 16, 100)])
 def test_km_sums_row_order_bitexact(cuda, n, d, k):
     """hlmc_km_sums = sklearn's single-thread float32 centre sums: per cluster and column a strictly
     sequential row-order add (np.add.accumulate), counts exact; ragged column slabs and super-tiles."""

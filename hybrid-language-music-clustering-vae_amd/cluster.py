@@ -116,9 +116,11 @@ class KMeans:
         dev = Xc.device
         labels = torch.full((n,), -1, dtype=torch.int32, device=dev)
         labels_new = torch.empty_like(labels)
-        changed = torch.zeros(1, dtype=torch.int32, device=dev)
-        sums = torch.empty(k, d, dtype=torch.float32, device=dev)
-        wts = torch.empty(k, dtype=torch.float32, device=dev)
+        # one device buffer [sums k*d | weights k | changed (int32 bits)]: one copy back per iteration
+        pack = torch.empty(k * d + k + 1, dtype=torch.float32, device=dev)
+        sums, wts = pack[:k * d], pack[k * d:k * d + k]
+        changed = pack[k * d + k:].view(torch.int32)
+        old_c = centers.cpu().numpy()
         strict = False
         it = 0
         for it in range(self.max_iter):
@@ -127,9 +129,10 @@ class KMeans:
                                            labels_new.data_ptr(), labels.data_ptr(), changed.data_ptr()))
             L.check(L.lib().hlmc_km_sums(L.stream(), Xc.data_ptr(), n, d, labels_new.data_ptr(), k, sums.data_ptr(),
                                          wts.data_ptr()))
-            new = sums.cpu().numpy()
-            wic = wts.cpu().numpy()
-            old_c = centers.cpu().numpy()
+            pack_h = pack.cpu().numpy()
+            new = pack_h[:k * d].reshape(k, d)
+            wic = pack_h[k * d:k * d + k]
+            n_changed = int(pack_h[k * d + k:].view(np.int32)[0])
             empty = np.where(wic == 0)[0]
             if empty.size:
                 dist = torch.empty(n, dtype=torch.float32, device=dev)
@@ -154,8 +157,9 @@ class KMeans:
                     new[j] = new[amax]
             shift = np.sqrt(_euclid_f32(new, old_c)).astype(np.float32)
             centers = torch.from_numpy(new).to(dev)
+            old_c = new
             labels, labels_new = labels_new, labels
-            if int(changed.item()) == 0 and it > 0:
+            if n_changed == 0 and it > 0:
                 strict = True
                 break
             if (shift ** 2).sum() <= tol:

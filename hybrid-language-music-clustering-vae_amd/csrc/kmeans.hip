@@ -96,21 +96,27 @@ __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict_
                                                         const int32_t* __restrict__ old,
                                                         int32_t* __restrict__ n_changed) {
     extern __shared__ float smem[];
-    float* Cs = smem;                    // [k][d]
-    float* cn = Cs + k * d;              // [k] ||c||^2 (float32, einsum order)
+    const int ldc = d + 1;               // padded: the 4 centres a wave reads per c sit in distinct banks
+    float* Cs = smem;                    // [k][d + 1]
+    float* cn = Cs + k * ldc;            // [k] ||c||^2 (float32, einsum order)
     float* Xs = cn + k;                  // [kRows][d + 1]
     const int ld = d + 1;
-    for (int i = threadIdx.x; i < k * d; i += blockDim.x) Cs[i] = C[i];
+    for (int i = threadIdx.x; i < k * d; i += blockDim.x) Cs[(i / d) * ldc + i % d] = C[i];
     __syncthreads();
     for (int j = threadIdx.x; j < k; j += blockDim.x) {
         float s = 0.f;
-        for (int c = 0; c < d; ++c) s = fmaf(Cs[j * d + c], Cs[j * d + c], s);
+        for (int c = 0; c < d; ++c) s = fmaf(Cs[j * ldc + c], Cs[j * ldc + c], s);
         cn[j] = s;
     }
     const int64_t r0 = (int64_t)blockIdx.x * kRows;
-    for (int i = threadIdx.x; i < kRows * d; i += blockDim.x) {
-        const int rr = i / d, c = i % d;
-        Xs[rr * ld + c] = (r0 + rr < n) ? X[(r0 + rr) * d + c] : 0.f;
+    {
+        // row-wise staging (no per-element division by d): wave w copies rows w, w + 4, ... lane-strided
+        const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+        for (int rr = w; rr < kRows; rr += 4) {
+            const bool ok = r0 + rr < n;
+            const float* src = X + (ok ? r0 + rr : 0) * d;
+            for (int c = l; c < d; c += 64) Xs[rr * ld + c] = ok ? src[c] : 0.f;
+        }
     }
     __syncthreads();
     const int rr = threadIdx.x >> 2, part = threadIdx.x & 3;
@@ -119,7 +125,7 @@ __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict_
     int bj = 0x7fffffff;
     for (int j = part; j < k; j += 4) {
         double dot = 0.0;
-        for (int c = 0; c < d; ++c) dot += (double)Xs[rr * ld + c] * (double)Cs[j * d + c];
+        for (int c = 0; c < d; ++c) dot += (double)Xs[rr * ld + c] * (double)Cs[j * ldc + c];
         const float dist = cn[j] + (-2.0f * (float)dot);
         if (dist < best || (dist == best && j < bj)) { best = dist; bj = j; }
     }
@@ -286,7 +292,7 @@ int sqdist_rows(hipStream_t s, const float* X, int64_t n, int d, const int64_t* 
 int assign(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, int32_t* labels, const int32_t* old,
            int32_t* n_changed) {
     HLMC_CHECK_ARG(X && C && labels && n > 0 && d > 0 && k > 0, "bad km_assign arguments");
-    const size_t sh = ((size_t)k * d + k + (size_t)kRows * (d + 1)) * sizeof(float);
+    const size_t sh = ((size_t)k * (d + 1) + k + (size_t)kRows * (d + 1)) * sizeof(float);
     HLMC_CHECK_ARG(sh <= 160 * 1024, "k * d too large for LDS");
     km_assign_kernel<<<(unsigned)((n + kRows - 1) / kRows), 256, sh, s>>>(X, n, d, C, k, labels, old, n_changed);
     HLMC_LAUNCHED();

@@ -125,7 +125,8 @@ __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict_
     int bj = 0x7fffffff;
     for (int j = part; j < k; j += 4) {
         double dot = 0.0;
-        for (int c = 0; c < d; ++c) dot += (double)Xs[rr * ld + c] * (double)Cs[j * ldc + c];
+        // f32 x f32 products are exact in f64, so fma == the separately rounded add of the product
+        for (int c = 0; c < d; ++c) dot = fma((double)Xs[rr * ld + c], (double)Cs[j * ldc + c], dot);
         const float dist = cn[j] + (-2.0f * (float)dot);
         if (dist < best || (dist == best && j < bj)) { best = dist; bj = j; }
     }

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void km_sqdist_kernel(const float* __restrict_
     __syncthreads();
     for (int t = threadIdx.x; t < cand.n; t += blockDim.x) {
         double s = 0.0;
-        for (int k = 0; k < d; ++k) s += A[t * d + k] * A[t * d + k];
+        for (int k = 0; k < d; ++k) s = fma(A[t * d + k], A[t * d + k], s);
         An[t] = s;
     }
     __syncthreads();
@@ -78,8 +78,8 @@ __global__ __launch_bounds__(256) void km_sqdist_kernel(const float* __restrict_
         for (int t = 0; t < cand.n; ++t) dot[t] = 0.0;
         for (int k = 0; k < d; ++k) {
             const double v = xr[k];
-            xx += v * v;
-            for (int t = 0; t < cand.n; ++t) dot[t] += A[t * d + k] * v;
+            xx = fma(v, v, xx);   // products of f32 values are exact in f64: fma == mul + add
+            for (int t = 0; t < cand.n; ++t) dot[t] = fma(A[t * d + k], v, dot[t]);
         }
         for (int t = 0; t < cand.n; ++t) {
             const double dd = -2.0 * dot[t] + An[t] + xx;

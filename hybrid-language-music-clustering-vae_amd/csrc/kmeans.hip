@@ -13,37 +13,51 @@ namespace {
 
 // X.mean(axis=0) in numpy: sequential float32 row accumulation, then / n; Xc = X - mean.
 // np.var(X, axis=0): sequential float32 sum of (x - mean)^2, then / n (sklearn's tolerance input).
-// One wave per 64 columns; rows are read in groups of 64 (coalesced 256-B row segments, all loads of a
-// group in flight) and added in row order into one accumulator per column.
-constexpr int kColGrp = 64;
-__global__ __launch_bounds__(64) void km_colmean_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                        float* __restrict__ mean, float* __restrict__ var) {
-    const int c = blockIdx.x * 64 + threadIdx.x;
+// One block (4 waves) per 64 columns: all 4 waves load a 256-row group (64 rows each, all loads in flight,
+// the next group prefetched in registers) into LDS; wave 0 adds the group in row order, one float32
+// accumulator per column.
+constexpr int kCmRows = 256;
+__global__ __launch_bounds__(256) void km_colmean_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                         float* __restrict__ mean, float* __restrict__ var) {
+    __shared__ float tile[kCmRows][64];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int c = blockIdx.x * 64 + l;
     const float* __restrict__ Xc = X + (c < d ? c : d - 1);
-    float s = 0.f;
-    for (int64_t g = 0; g < n; g += kColGrp) {
-        float v[kColGrp];
+    float m = 0.f;
+    for (int pass = 0; pass < (var ? 2 : 1); ++pass) {
+        float acc = 0.f;
+        float v[64];
 #pragma unroll
-        for (int t = 0; t < kColGrp; ++t) v[t] = Xc[(g + t < n ? g + t : n - 1) * d];
+        for (int t = 0; t < 64; ++t) v[t] = Xc[min((int64_t)(w * 64 + t), n - 1) * d];
+        for (int64_t g = 0; g < n; g += kCmRows) {
+            __syncthreads();
 #pragma unroll
-        for (int t = 0; t < kColGrp; ++t)
-            if (g + t < n) s += v[t];
-    }
-    const float m = s / (float)n;
-    if (c < d) mean[c] = m;
-    if (var) {
-        float q = 0.f;
-        for (int64_t g = 0; g < n; g += kColGrp) {
-            float v[kColGrp];
+            for (int t = 0; t < 64; ++t) tile[w * 64 + t][l] = v[t];
+            __syncthreads();
+            if (g + kCmRows < n) {
 #pragma unroll
-            for (int t = 0; t < kColGrp; ++t) v[t] = Xc[(g + t < n ? g + t : n - 1) * d];
-#pragma unroll
-            for (int t = 0; t < kColGrp; ++t) {
-                const float e = v[t] - m;
-                if (g + t < n) q += e * e;
+                for (int t = 0; t < 64; ++t) v[t] = Xc[min(g + kCmRows + w * 64 + t, n - 1) * d];
+            }
+            if (w == 0) {
+                const int rows = (int)min((int64_t)kCmRows, n - g);
+                if (pass == 0) {
+#pragma unroll 8
+                    for (int r = 0; r < rows; ++r) acc += tile[r][l];
+                } else {
+#pragma unroll 8
+                    for (int r = 0; r < rows; ++r) {
+                        const float e = tile[r][l] - m;
+                        acc += e * e;
+                    }
+                }
             }
         }
-        if (c < d) var[c] = q / (float)n;
+        if (pass == 0) {
+            m = acc / (float)n;
+            if (w == 0 && c < d) mean[c] = m;
+        } else if (w == 0 && c < d) {
+            var[c] = acc / (float)n;
+        }
     }
 }
 __global__ void km_sub_kernel(const float* __restrict__ X, int64_t n, int d, const float* __restrict__ mean,
@@ -269,7 +283,7 @@ namespace km {
 
 int center(hipStream_t s, const float* X, int64_t n, int d, float* mean, float* var, float* Xc) {
     HLMC_CHECK_ARG(X && mean && Xc && n > 0 && d > 0, "bad km_center arguments");
-    km_colmean_kernel<<<(d + 63) / 64, 64, 0, s>>>(X, n, d, mean, var);
+    km_colmean_kernel<<<(d + 63) / 64, 256, 0, s>>>(X, n, d, mean, var);
     HLMC_LAUNCHED();
     km_sub_kernel<<<(unsigned)std::min<int64_t>(8192, (n * d + 255) / 256), 256, 0, s>>>(X, n, d, mean, Xc);
     HLMC_LAUNCHED();

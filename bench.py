@@ -146,13 +146,29 @@ def pmc_traffic(kind):
         return None, None
 
 
+def host_cpu_share():
+    """Host cores the CPU baseline may use: every core in this process's affinity mask, unless a cgroup CPU
+    quota (cgroup v2 cpu.max) grants fewer, in which case the quota's CPU count.  Returns (cores, quota)."""
+    cores = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = round(int(q) / int(period), 2)
+            cores = max(1, min(cores, int(quota)))
+    except (OSError, ValueError):
+        pass
+    return cores, quota
+
+
 def cpu_baseline(batch=256, steps=5):
     """Oracle (torch-CPU restatement of the reference model + numpy restatement of librosa) on host cores."""
     from multiprocessing import Pool
 
     from oracle import mel_oracle, models_oracle
 
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores, quota = host_cpu_share()
     torch.set_num_threads(cores)
     pcm = mel_oracle.synthetic_pcm(batch, N_SAMPLES, seed=0)
     torch.manual_seed(42)
@@ -173,9 +189,10 @@ def cpu_baseline(batch=256, steps=5):
             one_step()
         dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 2), "unit": "clips/s", "cores": cores, "kind": "port",
-            "sample": f"audio-only HybridVAE 128x128 torch-CPU restatement fwd+bwd+Adam + numpy librosa-mel "
-                      f"restatement ({cores}-process pool), bs={batch}, {steps} timed steps after 1 warmup "
-                      f"({dt:.1f} s)"}
+            "affinity_cores": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota,
+            "sample": f"audio-only HybridVAE 128x128 torch-CPU restatement fwd+bwd+Adam ({cores} torch threads) + "
+                      f"numpy librosa-mel restatement ({cores}-process pool), bs={batch}, {steps} timed steps after "
+                      f"1 warmup ({dt:.1f} s)"}
 
 
 PROBE_STEPS = int(os.environ.get("HLMC_PROBE_STEPS", "3"))  # timed steps whose dominant-kernel launches are timed

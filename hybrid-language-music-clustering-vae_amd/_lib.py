@@ -53,6 +53,7 @@ _SIGS = {
     "hlmc_net_forward": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                  c_vp, c_vp]),
     "hlmc_net_encode": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "hlmc_net_decode": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hlmc_net_backward": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hlmc_net_adam_step": (c_int, [c_vp, c_vp, P_vp, P_vp, c_f32, c_f32, c_f32, c_f32, c_f32, c_int]),
     "hlmc_net_set_trust_packs": (c_int, [c_vp, c_int]),

@@ -10,7 +10,9 @@ searchsorted), potentials as float32 BLAS dot products, the best-of-n_init rule 
 ``_is_same_clustering``, empty-cluster relocation, centre averaging (float32 ``*= 1/w``),
 centre shifts and the strict / tolerance convergence tests.  Device kernels (libhlmc) compute the
 numpy-order column mean/variance, the float64-upcast candidate distances, the float32 E-step
-(||c||^2 - 2 x.c, first minimum), per-cluster sums in sklearn's single-thread row order, and inertia.
+(||c||^2 - 2 x.c, first minimum) in the exact rounding order of sklearn's einsum row norms and its OpenBLAS
+sgemm call (oracle/kmeans_oracle.py estep_dist), per-cluster sums in sklearn's single-thread row order, and
+inertia.
 
 Multi-GPU (``process_group=``): the n_init restarts are independent objects, so they shard across ranks
 with no collective on the data path.  Every rank holds the same (small, [N, D] f32) latents and runs ALL
@@ -135,14 +137,15 @@ class KMeans:
             n_changed = int(pack_h[k * d + k:].view(np.int32)[0])
             empty = np.where(wic == 0)[0]
             if empty.size:
-                dist = torch.empty(n, dtype=torch.float32, device=dev)
-                L.check(L.lib().hlmc_km_rowdist(L.stream(), Xc.data_ptr(), n, d, centers.data_ptr(),
-                                                labels_new.data_ptr(), dist.data_ptr()))
-                dist = dist.cpu().numpy()
+                # _relocate_empty_clusters_dense (sklearn/cluster/_k_means_common.pyx) ranks rows by the numpy
+                # expression ((X - C[labels])**2).sum(axis=1) (pairwise row sums): evaluated here on host copies
+                # exactly as written, so near-tied farthest points resolve as in sklearn (empty clusters are rare)
+                lab_h = labels_new.cpu().numpy()
+                Xh = Xc.cpu().numpy()
+                dist = ((Xh - old_c[lab_h]) ** 2).sum(axis=1)
                 if dist.max() > 0:
                     far = np.argpartition(dist, -empty.size)[:-empty.size - 1:-1]
-                    lab_h = labels_new.cpu().numpy()
-                    rows = Xc[torch.as_tensor(far, device=dev)].cpu().numpy()
+                    rows = Xh[far]
                     for e, f, xr in zip(empty, far, rows):
                         old = lab_h[f]
                         new[old] -= xr

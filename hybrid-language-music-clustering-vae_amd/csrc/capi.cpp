@@ -243,6 +243,14 @@ int hlmc_net_encode(hlmc_net* h, void* stream, int64_t batch, int train, const f
     ForwardArgs a{batch, train, in0, in1, in2, nullptr, nullptr, nullptr, nullptr, mu, logvar, nullptr, ws, true};
     return h->impl->forward(S(stream), a);
 }
+int hlmc_net_decode(hlmc_net* h, void* stream, int64_t batch, int train, const float* z, const float* cond,
+                    const uint8_t* dropout, float* recon, float* recon_text, void* ws) {
+    HLMC_CHECK_ARG(h && ws && batch > 0 && z && recon, "bad arguments");
+    HLMC_CHECK_ARG(!h->impl->P.empty(), "net is not bound");
+    ForwardArgs a{batch, train, z, nullptr, cond, nullptr, dropout, recon, recon_text, nullptr, nullptr, nullptr, ws,
+                  false, true};
+    return h->impl->forward(S(stream), a);
+}
 int hlmc_net_backward(hlmc_net* h, void* stream, int64_t batch, const float* d_recon, const float* d_recon_text,
                       const float* d_mu, const float* d_logvar, void* ws) {
     HLMC_CHECK_ARG(h && ws && d_recon && d_mu && d_logvar, "bad arguments");

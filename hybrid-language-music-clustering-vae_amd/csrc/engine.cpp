@@ -766,16 +766,22 @@ class HybridNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        HLMC_TRY(encode(s, a, B));
-        {  // latent outputs (and the eps the backward keeps) in one launch
-            const int64_t nl = (int64_t)B * L;
-            const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
-                                        {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
-            HLMC_TRY(ops::copy_segments(s, cs, 3));
+        this->last_full_forward = !a.encode_only && !a.decode_only;
+        if (a.decode_only) {  // decode(z), src/Convolutional_VAE.py:167-179
+            HLMC_CHECK_ARG(a.in0 && a.recon, "z and recon required");
+            HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in0, L, AT(z_), L, B, L));
+        } else {
+            HLMC_TRY(encode(s, a, B));
+            {  // latent outputs (and the eps the backward keeps) in one launch
+                const int64_t nl = (int64_t)B * L;
+                const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
+                                            {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
+                HLMC_TRY(ops::copy_segments(s, cs, 3));
+            }
+            if (a.encode_only) return HLMC_OK;
+            HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
+            HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), L));
         }
-        if (a.encode_only) return HLMC_OK;
-        HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
-        HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), L));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(z_), L, B, di_w, di_b, AT(d1_), 512, 1));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(d1_), 512, B, ds_w, ds_b, AT(s_), ldSP, 1));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(s_), ldSP, B, adf_w, adf_b, AT(ah_), ldF, 1));
@@ -794,6 +800,7 @@ class HybridNet : public NetT<T> {
     int backward(hipStream_t s, const BackwardArgs& a) override {
         const int B = (int)a.B;
         HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
+        HLMC_CHECK_ARG(this->last_full_forward, "backward needs a full hlmc_net_forward (not encode / decode)");
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
         HLMC_TRY(this->settle(s));
@@ -966,16 +973,22 @@ class CvaeNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        HLMC_TRY(encode(s, a, B));
-        {  // latent outputs (and the eps the backward keeps) in one launch
-            const int64_t nl = (int64_t)B * L;
-            const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
-                                        {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
-            HLMC_TRY(ops::copy_segments(s, cs, 3));
+        this->last_full_forward = !a.encode_only && !a.decode_only;
+        if (a.decode_only) {  // decode(z, condition), src/Conditional_VAE.py:206-225
+            HLMC_CHECK_ARG(a.in0 && a.in2 && a.recon && a.recon_text, "z / condition / recon / recon_text required");
+            HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in0, L, AT(Z_), ldZ, B, L));
+        } else {
+            HLMC_TRY(encode(s, a, B));
+            {  // latent outputs (and the eps the backward keeps) in one launch
+                const int64_t nl = (int64_t)B * L;
+                const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
+                                            {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
+                HLMC_TRY(ops::copy_segments(s, cs, 3));
+            }
+            if (a.encode_only) return HLMC_OK;
+            HLMC_CHECK_ARG(a.eps && a.recon && a.recon_text, "eps / recon / recon_text required");
+            HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(Z_), ldZ));
         }
-        if (a.encode_only) return HLMC_OK;
-        HLMC_CHECK_ARG(a.eps && a.recon && a.recon_text, "eps / recon / recon_text required");
-        HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(Z_), ldZ));
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in2, C, AT(Z_) + L, ldZ, B, C));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(S_), ldS, 0));
         HLMC_TRY(ops::flat_to_nhwc<T>(s, AT(S_), ldS, B, H / 64, W / 64, 512, AT(u_)));
@@ -989,6 +1002,7 @@ class CvaeNet : public NetT<T> {
     int backward(hipStream_t s, const BackwardArgs& a) override {
         const int B = (int)a.B;
         HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
+        HLMC_CHECK_ARG(this->last_full_forward, "backward needs a full hlmc_net_forward (not encode / decode)");
         HLMC_CHECK_ARG(a.d_recon_text, "d_recon_text required");
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
@@ -1169,17 +1183,28 @@ class SimpleNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        HLMC_TRY(encode(s, a, B));
-        {  // latent outputs (and the eps the backward keeps) in one launch
-            const int64_t nl = (int64_t)B * L;
-            const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
-                                        {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
-            HLMC_TRY(ops::copy_segments(s, cs, 3));
+        this->last_full_forward = !a.encode_only && !a.decode_only;
+        if (a.decode_only) {  // decode(z), src/Simple_VAE.py:95-96 (decoder blocks' dropout from the same mask layout)
+            HLMC_CHECK_ARG(a.in0 && a.recon, "z and recon required");
+            dropout = nullptr;
+            if (a.train && a.dropout) {
+                HLMC_HIP(hipMemcpyAsync(AU8(mask_), a.dropout, (size_t)mask_total, hipMemcpyDeviceToDevice, s));
+                dropout = AU8(mask_);
+            }
+            HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in0, L, AT(z_), pad8(L), B, L));
+        } else {
+            HLMC_TRY(encode(s, a, B));
+            {  // latent outputs (and the eps the backward keeps) in one launch
+                const int64_t nl = (int64_t)B * L;
+                const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
+                                            {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
+                HLMC_TRY(ops::copy_segments(s, cs, 3));
+            }
+            if (a.encode_only) return HLMC_OK;
+            HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
+            HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), pad8(L)));
+            if (a.z) HLMC_TRY(ops::reparam_fwd<float>(s, AF(mu_), AF(lv_), AF(eps_), B, L, a.z, L));
         }
-        if (a.encode_only) return HLMC_OK;
-        HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
-        HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), pad8(L)));
-        if (a.z) HLMC_TRY(ops::reparam_fwd<float>(s, AF(mu_), AF(lv_), AF(eps_), B, L, a.z, L));
         const T* x = AT(z_);
         int ldx = pad8(L);
         for (auto& b : decb) {
@@ -1196,6 +1221,7 @@ class SimpleNet : public NetT<T> {
     int backward(hipStream_t s, const BackwardArgs& a) override {
         const int B = (int)a.B;
         HLMC_CHECK_ARG(B == this->planned_B, "backward batch differs from the last forward");
+        HLMC_CHECK_ARG(this->last_full_forward, "backward needs a full hlmc_net_forward (not encode / decode)");
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
         HLMC_TRY(this->settle(s));

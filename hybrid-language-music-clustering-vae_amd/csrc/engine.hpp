@@ -43,6 +43,7 @@ struct ForwardArgs {
     float* z;
     void* ws;
     bool encode_only;
+    bool decode_only = false;  // in0 = z [B][latent] (cvae: in2 = condition); eps, mu, logvar unused
 };
 
 struct BackwardArgs {
@@ -98,6 +99,7 @@ class NetBase {
     // Adam runs under the tail of the backward pass.
     int late_params = 0;
     bool overlap_adam = false;
+    bool last_full_forward = false;  // the workspace holds a full forward (backward's precondition)
     virtual int settle(hipStream_t s) = 0;  // make every gradient of the last backward final on s
 };
 

@@ -67,7 +67,28 @@ __global__ void km_sub_kernel(const float* __restrict__ X, int64_t n, int d, con
         Xc[i] = X[i] - mean[i % d];
 }
 
-// float32(max(0, ||a||^2 - 2 a.x + ||x||^2)) in float64 for up to 16 candidate rows a = X[cand[t]]
+// np.einsum("ij,ij->i") of one float64 row (sklearn row_norms on the upcast chunks): numpy's baseline-SSE2
+// loop, 2 lanes, 8-element blocks added as 3, 2, 1, 0 with a separate multiply and add, then l0 + l1.
+template <typename Ld>
+__device__ __forceinline__ double einsum_sq_f64(Ld ld, int d) {
+    double a0 = 0.0, a1 = 0.0;
+    int i = 0;
+    for (; d - i >= 8; i += 8)
+        for (int t = 3; t >= 0; --t) {
+            const double u = ld(i + 2 * t), v = ld(i + 2 * t + 1);
+            a0 = u * u + a0;
+            a1 = v * v + a1;
+        }
+    for (; i < d; i += 2) {
+        const double u = ld(i), v = i + 1 < d ? ld(i + 1) : 0.0;
+        a0 = u * u + a0;
+        a1 = v * v + a1;
+    }
+    return a0 + a1;
+}
+
+// float32(max(0, (-2 a.x + ||a||^2) + ||x||^2)) in float64 for up to 16 candidate rows a = X[cand[t]]
+// (sklearn _euclidean_distances_upcast: d = -2 * dot; d += XX; d += YY; float32; max 0)
 struct Cand {
     int64_t idx[16];
     int n;
@@ -79,20 +100,16 @@ __global__ __launch_bounds__(256) void km_sqdist_kernel(const float* __restrict_
     double* An = sh + cand.n * d;
     for (int i = threadIdx.x; i < cand.n * d; i += blockDim.x) A[i] = (double)X[cand.idx[i / d] * d + (i % d)];
     __syncthreads();
-    for (int t = threadIdx.x; t < cand.n; t += blockDim.x) {
-        double s = 0.0;
-        for (int k = 0; k < d; ++k) s = fma(A[t * d + k], A[t * d + k], s);
-        An[t] = s;
-    }
+    for (int t = threadIdx.x; t < cand.n; t += blockDim.x)
+        An[t] = einsum_sq_f64([&](int c) { return A[t * d + c]; }, d);
     __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float* xr = X + i * d;
-        double xx = 0.0;
+        const double xx = einsum_sq_f64([&](int c) { return (double)xr[c]; }, d);
         double dot[16];
         for (int t = 0; t < cand.n; ++t) dot[t] = 0.0;
         for (int k = 0; k < d; ++k) {
             const double v = xr[k];
-            xx = fma(v, v, xx);   // products of f32 values are exact in f64: fma == mul + add
             for (int t = 0; t < cand.n; ++t) dot[t] = fma(A[t * d + k], v, dot[t]);
         }
         for (int t = 0; t < cand.n; ++t) {
@@ -102,8 +119,34 @@ __global__ __launch_bounds__(256) void km_sqdist_kernel(const float* __restrict_
     }
 }
 
-// E-step: 4 threads per row (each a quarter of the centres), rows staged in LDS.
+// E-step, bit-exact to sklearn's lloyd_iter_chunked_dense (oracle/kmeans_oracle.py estep_dist):
+//   ||c||^2: np.einsum row norms (4 lanes, 16-element blocks added as 3, 2, 1, 0, separate mul and add,
+//            (l0 + l1) + (l2 + l3));
+//   x.c:     OpenBLAS sgemm per 256-row chunk, column-major TN (M = k, N = chunk rows, K = d).  Small-matrix
+//            kernel (M*N <= 1200, K >= 32, M*N*K <= 1e6): 16 lanes of fma over k = l (mod 16), reduced by an
+//            adjacent-pair tree, or halves-first when the element lies in both remainders of 4; else one
+//            sequential fma chain over k;
+//   dist = ||c||^2 + (-2 * dot), first minimum.
+// 4 threads per row (cluster j = part, part + 4, ...), 64 rows staged in LDS.  A block never straddles a
+// 256-row chunk, so the small-kernel decision is block-uniform.
 constexpr int kRows = 64;
+constexpr int kChunk = 256;
+
+__device__ __forceinline__ float km_tree_adjacent(float* a) {
+#pragma unroll
+    for (int w = 16; w > 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w / 2; ++i) a[i] = a[2 * i] + a[2 * i + 1];
+    return a[0];
+}
+__device__ __forceinline__ float km_tree_halves(float* a) {
+#pragma unroll
+    for (int w = 16; w > 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w / 2; ++i) a[i] = a[i] + a[i + w / 2];
+    return a[0];
+}
+
 __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict__ X, int64_t n, int d,
                                                         const float* __restrict__ C, int k,
                                                         int32_t* __restrict__ labels,
@@ -112,15 +155,29 @@ __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict_
     extern __shared__ float smem[];
     const int ldc = d + 1;               // padded: the 4 centres a wave reads per c sit in distinct banks
     float* Cs = smem;                    // [k][d + 1]
-    float* cn = Cs + k * ldc;            // [k] ||c||^2 (float32, einsum order)
+    float* cn = Cs + k * ldc;            // [k] ||c||^2 (einsum order)
     float* Xs = cn + k;                  // [kRows][d + 1]
     const int ld = d + 1;
     for (int i = threadIdx.x; i < k * d; i += blockDim.x) Cs[(i / d) * ldc + i % d] = C[i];
     __syncthreads();
     for (int j = threadIdx.x; j < k; j += blockDim.x) {
-        float s = 0.f;
-        for (int c = 0; c < d; ++c) s = fmaf(Cs[j * ldc + c], Cs[j * ldc + c], s);
-        cn[j] = s;
+        const float* cj = Cs + j * ldc;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        int i = 0;
+        for (; d - i >= 16; i += 16)
+            for (int t = 3; t >= 0; --t)
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    const float v = cj[i + 4 * t + l];
+                    acc[l] = v * v + acc[l];
+                }
+        for (; i < d; i += 4)
+#pragma unroll
+            for (int l = 0; l < 4; ++l) {
+                const float v = i + l < d ? cj[i + l] : 0.f;
+                acc[l] = v * v + acc[l];
+            }
+        cn[j] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
     }
     const int64_t r0 = (int64_t)blockIdx.x * kRows;
     {
@@ -135,14 +192,47 @@ __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict_
     __syncthreads();
     const int rr = threadIdx.x >> 2, part = threadIdx.x & 3;
     const int64_t row = r0 + rr;
+    const int64_t cs = r0 / kChunk * kChunk;                      // this chunk's first row
+    const int N = (int)min((int64_t)kChunk, n - cs);              // rows in the chunk (the last one is short)
+    const bool small = (int64_t)k * N <= 1200 && d >= 32 && (double)k * N * d <= 1e6;
+    const int jl = (int)(row - cs);
+    const bool row_rem = jl >= 4 * (N / 4);
+    const int k4 = 4 * (k / 4);
+    const float* xr = Xs + rr * ld;
     float best = INFINITY;
     int bj = 0x7fffffff;
-    for (int j = part; j < k; j += 4) {
-        double dot = 0.0;
-        // f32 x f32 products are exact in f64, so fma == the separately rounded add of the product
-        for (int c = 0; c < d; ++c) dot = fma((double)Xs[rr * ld + c], (double)Cs[j * ldc + c], dot);
-        const float dist = cn[j] + (-2.0f * (float)dot);
+    auto consider = [&](int j, float dot) {
+        const float dist = cn[j] + (-2.0f * dot);
         if (dist < best || (dist == best && j < bj)) { best = dist; bj = j; }
+    };
+    if (!small) {
+        // regular kernel: sequential fma chains, up to 4 clusters interleaved per thread
+        for (int j0 = part; j0 < k; j0 += 16) {
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            const float* cp[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cp[q] = Cs + min(j0 + 4 * q, k - 1) * ldc;
+            for (int c = 0; c < d; ++c) {
+                const float x = xr[c];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] = fmaf(x, cp[q][c], acc[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (j0 + 4 * q < k) consider(j0 + 4 * q, acc[q]);
+        }
+    } else {
+        for (int j = part; j < k; j += 4) {
+            const float* cj = Cs + j * ldc;
+            float a[16];
+#pragma unroll
+            for (int l = 0; l < 16; ++l) a[l] = 0.f;
+            for (int b = 0; b < d; b += 16)
+#pragma unroll
+                for (int l = 0; l < 16; ++l)
+                    if (b + l < d) a[l] = fmaf(xr[b + l], cj[b + l], a[l]);
+            consider(j, (row_rem && j >= k4) ? km_tree_halves(a) : km_tree_adjacent(a));
+        }
     }
     // combine the 4 partials (first minimum = smallest index among equal distances)
 #pragma unroll

@@ -206,6 +206,30 @@ class _NativeModule(nn.Module):
     def _params(self):
         return list(self.parameters())
 
+    def _flatten_bn_buffers(self):
+        """Re-point every BatchNorm's running_mean / running_var at views of ONE flat fp32 tensor (values kept;
+        state_dict keys and shapes unchanged), so the data-parallel Trainer broadcasts them in one collective.
+        Returns the flat tensor."""
+        bns = [m for m in self.modules() if isinstance(m, nn.modules.batchnorm._BatchNorm)]
+        if not bns:
+            return torch.zeros(0, device=next(self.parameters()).device)
+        first = bns[0].running_mean
+        flat = getattr(self, "_bn_flat", None)
+        if flat is not None and first.data_ptr() == flat.data_ptr() and first.device == flat.device:
+            return flat
+        n = sum(2 * b.running_mean.numel() for b in bns)
+        flat = torch.empty(n, dtype=torch.float32, device=first.device)
+        off = 0
+        for b in bns:
+            for name in ("running_mean", "running_var"):
+                t = getattr(b, name)
+                v = flat[off:off + t.numel()]
+                v.copy_(t)
+                setattr(b, name, v)
+                off += t.numel()
+        self._bn_flat = flat
+        return flat
+
     def _run(self, audio, text=None, cond=None, eps=None, dropout=None):
         L.require_cuda(audio, text, cond, eps, dropout)
         train = self.training
@@ -221,6 +245,24 @@ class _NativeModule(nn.Module):
         L.check(L.lib().hlmc_net_encode(net.h, L.stream(), B, int(self.training), L.ptr(in0), L.ptr(in1), L.ptr(in2),
                                         L.ptr(mu), L.ptr(lv), ws.data_ptr()), "hlmc_net_encode")
         return mu, lv
+
+    def _decode_native(self, z, cond=None, dropout=None):
+        """Decoder-only native call (hlmc_net_decode): inference entry, no autograd graph is recorded."""
+        net = self._native_net()
+        L.require_cuda(z, cond, dropout)
+        z = z.detach().float().contiguous()
+        B = z.shape[0]
+        if z.dim() != 2 or z.shape[1] != self.latent_dim:
+            raise ValueError(f"z must be [batch, {self.latent_dim}], got {tuple(z.shape)}")
+        if self.training and B < 2:
+            raise ValueError("BatchNorm in train mode needs batch >= 2 (call .eval() to decode one latent)")
+        out = self._alloc_outputs(B, z.device)
+        ws = net.new_workspace(B, z.device)
+        c = None if cond is None else cond.detach().float().contiguous()
+        L.check(L.lib().hlmc_net_decode(net.h, L.stream(), B, int(self.training), L.ptr(z), L.ptr(c), L.ptr(dropout),
+                                        L.ptr(out["recon"]), L.ptr(out.get("recon_text")), ws.data_ptr()),
+                "hlmc_net_decode")
+        return out
 
     @staticmethod
     def reparameterize(mu, logvar, eps=None):
@@ -275,6 +317,12 @@ class HybridVAE(_NativeModule):
         """(mu, logvar) of the encoder (latent extraction, src/Convolutional_VAE.py:286-303)."""
         return self._encode_native(audio.contiguous(), None if self.audio_only else text.contiguous())
 
+    def decode(self, z):
+        """(recon_audio [B,1,H,W], recon_text [B,text_dim] or None when audio_only) — src/Convolutional_VAE.py:167-179.
+        Inference entry: computed by the native decoder without recording an autograd graph."""
+        out = self._decode_native(z)
+        return out["recon"], out.get("recon_text")
+
     def forward(self, audio, text=None, eps=None):
         B = audio.shape[0]
         if eps is None:
@@ -315,6 +363,14 @@ class ConditionalVAE(_NativeModule):
 
     def encode(self, audio, text, condition):
         return self._encode_native(audio.contiguous(), text.contiguous(), condition.float().contiguous())
+
+    def decode(self, z, condition):
+        """(recon_audio, recon_text) from z and the one-hot condition — src/Conditional_VAE.py:206-225.
+        Inference entry: computed by the native decoder without recording an autograd graph."""
+        if condition.shape != (z.shape[0], self.num_classes):
+            raise ValueError(f"condition must be [batch, {self.num_classes}], got {tuple(condition.shape)}")
+        out = self._decode_native(z, condition)
+        return out["recon"], out["recon_text"]
 
     def forward(self, audio, text, condition, eps=None):
         B = audio.shape[0]
@@ -367,8 +423,13 @@ class VAE(_NativeModule):
     def encode(self, x):
         return self._encode_native(x.float().contiguous())
 
-    def decode(self, z):  # pragma: no cover - decode-only entry not exposed by the engine yet
-        raise NotImplementedError("VAE.decode: use forward(); a decode-only native entry is not built yet")
+    def decode(self, z, dropout_mask=None):
+        """self.decoder(z) — src/Simple_VAE.py:95-96.  In train mode the decoder's Dropout(0.2) layers apply
+        `dropout_mask` (the forward's keep-mask layout, make_dropout_mask; drawn when None).  Inference entry:
+        no autograd graph is recorded."""
+        if self.training and dropout_mask is None:
+            dropout_mask = self.make_dropout_mask(z.shape[0], z.device)
+        return self._decode_native(z, None, dropout_mask if self.training else None)["recon"]
 
     def forward(self, x, eps=None, dropout_mask=None):
         B = x.shape[0]

@@ -8,10 +8,18 @@ per-batch ``loss.item()`` is replaced by device-side loss sums that the caller m
 Data parallel: one process per GPU; the flat fp32 gradient buffer is all-reduced with SUM over
 ``torch.distributed`` (backend "nccl" = RCCL over xGMI on MI355X), i.e. gradients of the loss summed
 over the global batch — the reference's sum-reduced losses make SUM the matching reduction.
-BatchNorm statistics stay per rank (DDP semantics).  The buffer is reduced in the engine's gradient
+BatchNorm batch statistics stay per rank (DDP semantics).  The buffer is reduced in the engine's gradient
 buckets (hlmc_net_grad_buckets: contiguous parameter ranges in the order backward finishes them); on a
 GPU each bucket's all-reduce is issued on a communication stream that waits on the bucket's event, so
 RCCL overlaps the rest of the backward pass, and Adam waits for all of them.
+
+BatchNorm running statistics follow DDP's ``broadcast_buffers=True``: DDP broadcasts rank 0's buffers at the
+start of every forward, so step k's forward on rank r updates rank 0's step-(k-1) statistics with rank r's
+batch, and any later forward (train or eval) sees rank 0's.  Here the running means / variances live in one
+flat fp32 tensor per model and rank 0's copy is broadcast right after each forward, on the communication
+stream under the backward pass: every forward after step k starts from rank 0's post-step-k statistics, the
+same values DDP's pre-forward broadcast hands it, and all ranks hold identical buffers between steps (so
+eval-mode ``encode`` — the latents K-Means clusters — agrees across ranks).
 """
 from __future__ import annotations
 
@@ -25,8 +33,14 @@ from .models import ConditionalVAE, HybridVAE, VAE
 
 class Trainer:
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, beta=None, text_weight=None,
-                 process_group=None, distributed=False, grad_dtype=torch.float32):
+                 process_group=None, distributed=False, grad_dtype=torch.float32, broadcast_buffers=True):
         self.model = model
+        self.distributed = distributed or process_group is not None
+        self.process_group = process_group
+        self.broadcast_buffers = bool(broadcast_buffers) and self.distributed
+        # BatchNorm running stats as views of one flat tensor: one broadcast per step (before the native net
+        # binds their addresses)
+        self.bn_flat = model._flatten_bn_buffers() if self.broadcast_buffers else None
         self.kind = "simple" if isinstance(model, VAE) else ("cvae" if isinstance(model, ConditionalVAE) else "hybrid")
         self.net = model._native_net()
         dev = next(model.parameters()).device
@@ -49,12 +63,12 @@ class Trainer:
         if text_weight is None:
             text_weight = {"hybrid": 350.0, "cvae": 200.0, "simple": 0.0}[self.kind]
         self.beta, self.text_weight = float(beta), float(text_weight)
-        self.distributed = distributed or process_group is not None
-        self.process_group = process_group
         self.grad_dtype = grad_dtype
         self.buckets = self._bucket_ranges()
         self._comm = None
+        self._fwd_done = None
         if self.distributed and dev.type == "cuda":
+            self._fwd_done = torch.cuda.Event()
             L.check(L.lib().hlmc_net_set_bucket_sync(self.net.h, 1), "hlmc_net_set_bucket_sync")
             self._comm = torch.cuda.Stream(device=dev)
         else:  # single process, HLMC_OVERLAP_ADAM=1: Adam starts under the tail of the backward pass (measured
@@ -106,6 +120,9 @@ class Trainer:
                                      L.ptr(dropout), L.ptr(out["recon"]), L.ptr(out.get("recon_text")),
                                      L.ptr(out["mu"]), L.ptr(out["logvar"]), L.ptr(out.get("z")), c["ws"].data_ptr()),
                 "hlmc_net_forward")
+        bcast = None
+        if self.broadcast_buffers:
+            bcast = self._broadcast_buffers_after_forward()
         na, nt, nl = c["n"]
         rt, t = out.get("recon_text"), (in1 if nt else None)
         L.check(lib.hlmc_loss_sums(s, L.ptr(out["recon"]), L.ptr(in0), na, L.ptr(rt), L.ptr(t), nt, L.ptr(out["mu"]),
@@ -117,7 +134,7 @@ class Trainer:
                                       L.ptr(d["logvar"]), c["ws"].data_ptr()), "hlmc_net_backward")
         if self.distributed:
             if self._comm is not None:
-                self._allreduce_overlapped()
+                self._allreduce_overlapped(bcast)
             else:
                 self.allreduce_grads()
         if self._graph:  # coefficients staged by prepare_step_coefficients()
@@ -157,18 +174,39 @@ class Trainer:
             L.check(nb, "hlmc_net_grad_buckets")
         return bucket_ranges(list(starts)[:nb], offs)
 
-    def _allreduce_overlapped(self):
-        """Per-bucket SUM all-reduces on the comm stream, each gated on its bucket's backward event;
-        the current stream (Adam) waits for all of them."""
+    def _broadcast_buffers_after_forward(self):
+        """Rank 0's BatchNorm running statistics to every rank (DDP broadcast_buffers), issued right after the
+        forward that updated them: on the comm stream (under the backward pass) on a GPU, else synchronously."""
         import torch.distributed as dist
+        src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
+        if self._comm is None:
+            dist.broadcast(self.bn_flat, src=src, group=self.process_group)
+            return None
+        self._fwd_done.record()
+        self._comm.wait_event(self._fwd_done)
+        with torch.cuda.stream(self._comm):
+            return dist.broadcast(self.bn_flat, src=src, group=self.process_group, async_op=True)
+
+    def sync_buffers(self):
+        """Broadcast rank 0's BatchNorm running statistics now (what DDP does before an eval-mode forward)."""
+        if self.broadcast_buffers:
+            import torch.distributed as dist
+            src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
+            dist.broadcast(self.bn_flat, src=src, group=self.process_group)
+
+    def _allreduce_overlapped(self, bcast=None):
+        """Per-bucket SUM all-reduces on the comm stream, each gated on its bucket's backward event; the
+        current stream (Adam, then the next step's forward and backward) waits for all of them — and for the
+        comm stream itself, which also runs the bf16 wire copies and the buffer broadcast."""
         lib = L.lib()
-        works = []
+        works = [] if bcast is None else [bcast]
         with torch.cuda.stream(self._comm):
             for k, (lo, hi) in enumerate(self.buckets):
                 L.check(lib.hlmc_net_bucket_wait(self.net.h, k, self._comm.cuda_stream), "hlmc_net_bucket_wait")
                 works.append(_allreduce_sum(self.gflat[lo:hi], self.grad_dtype, self.process_group, async_op=True))
         for w in works:
             w.wait()
+        torch.cuda.current_stream().wait_stream(self._comm)
 
     def allreduce_grads(self):
         """SUM all-reduce of the flat gradient buffer, bucket by bucket (RCCL under 'nccl', gloo on CPU)."""
@@ -200,7 +238,8 @@ def bucket_ranges(starts, offsets):
 
 
 def _allreduce_sum(buf, grad_dtype, group, async_op=False):
-    """SUM all-reduce of a contiguous fp32 gradient slice (optionally on a bf16 wire copy, synchronous)."""
+    """SUM all-reduce of a contiguous fp32 gradient slice (optionally on a bf16 wire copy: converted, reduced and
+    copied back on the current stream, which the caller must make its consumers wait for)."""
     import torch.distributed as dist
     if grad_dtype == torch.float32:
         return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group, async_op=async_op)

@@ -128,6 +128,14 @@ int hlmc_net_forward(hlmc_net* net, void* stream, int64_t batch, int train, cons
 /* encoder only (latent extraction, src/Convolutional_VAE.py:286-303): mu, logvar */
 int hlmc_net_encode(hlmc_net* net, void* stream, int64_t batch, int train, const float* in0, const float* in1,
                     const float* in2, float* mu, float* logvar, void* ws);
+/* decoder only: HybridVAE.decode(z) (src/Convolutional_VAE.py:167-179), ConditionalVAE.decode(z, condition)
+ * (src/Conditional_VAE.py:206-225), VAE.decode(z) (src/Simple_VAE.py:95-96).  z [B][latent]; cond [B][C]
+ * (cvae, else NULL); dropout: the forward's keep-mask layout (Simple, train; only the decoder blocks' part is
+ * read; NULL = none).  train != 0: decoder BatchNorms use batch statistics and update running stats.
+ * recon [B][...], recon_text [B][text_dim] (hybrid with text, cvae; else NULL).  Inference only: a later
+ * hlmc_net_backward needs a full hlmc_net_forward. */
+int hlmc_net_decode(hlmc_net* net, void* stream, int64_t batch, int train, const float* z, const float* cond,
+                    const uint8_t* dropout, float* recon, float* recon_text, void* ws);
 /* Backward of the last hlmc_net_forward (same ws): writes (overwrites) all parameter gradients.
  * d_recon_text may be NULL when the model has no text branch. */
 int hlmc_net_backward(hlmc_net* net, void* stream, int64_t batch, const float* d_recon, const float* d_recon_text,

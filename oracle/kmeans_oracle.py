@@ -4,18 +4,34 @@ Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
 
 Reference call sites (the algorithms themselves live in scikit-learn, a third-party dependency the
 reference leaves unpinned, >=1.2 for ``OneHotEncoder(sparse_output=)``; restated here from the
-installed scikit-learn 1.7.2):
+installed scikit-learn 1.7.2 with the OpenBLAS 0.3.28 (SkylakeX kernels) that scipy bundles):
   * ``KMeans(n_clusters=k, random_state=42, n_init=10).fit_predict`` —
     src/Convolutional_VAE.py:317-319, 379-380; src/Conditional_VAE.py:293-295; src/Simple_VAE.py:244-261
   * ``KMeans(k, random_state=42)`` (n_init='auto' -> 1 for k-means++) — src/Conditional_VAE.py:528
   * ``StandardScaler().fit_transform`` — src/1_preprocessing.py:310-311; src/1_preprocessing_advanced.py:376-391
-sklearn semantics restated (sklearn/cluster/_kmeans.py, _k_means_lloyd.pyx, _k_means_common.pyx):
+sklearn semantics restated (sklearn/cluster/_kmeans.py, _k_means_lloyd.pyx, _k_means_common.pyx), single
+thread (threadpoolctl limits=1, as the fixtures are generated):
   X (float32) is mean-centred; tol = mean(var(X, axis=0)) * 1e-4; per init one shared RandomState
   stream: k-means++ (first centre ``choice(N, p=w/sum w)``, then per centre ``uniform(size=2+int(ln k))
   * pot`` -> searchsorted(float64 cumsum) -> candidates; distances in float64 rounded to float32);
   Lloyd: dist = ||c||^2 - 2 x.c (float32), first-minimum argmin, empty clusters relocated to the
   farthest points, centres = sum / w, stop on identical labels or sum(shift^2) <= tol, max_iter 300;
   if not strictly converged a final E-step; keep the best inertia unless it is the same clustering.
+
+The Lloyd E-step is restated at the bit level (``estep_dist``), because labels are decided by float32
+rounding wherever two centres are nearly equidistant (overlapping clusters, real latents):
+  * ||c||^2 = ``np.einsum("ij,ij->i", C, C)`` (sklearn row_norms): numpy's baseline-SSE loop, 4 lanes, each
+    16-element block added as blocks 3, 2, 1, 0 with a separate multiply and add, zero-filled tail
+    vectors, then (l0 + l1) + (l2 + l3);
+  * x.c: ``_update_chunk_dense`` calls sgemm per 256-row chunk as column-major TN with M = k, N = rows,
+    K = d, alpha = -2, beta = 1 on a buffer holding ||c||^2.  OpenBLAS takes its small-matrix TN kernel
+    when M*N <= 1200, K >= 32 and M*N*K <= 1e6: 16 float32 lanes (lane l sums k = l, l+16, ... with fma),
+    reduced by an adjacent-pair tree, except elements in both the M and the N remainder of 4 (a single
+    ``_mm512_reduce_add_ps``: halves first).  Otherwise its regular kernel: one sequential fma chain over
+    k.  Then dist = ||c||^2 + (-2 * dot) with one rounding.
+  ``estep_dist_blas`` makes the very sgemm call sklearn makes (scipy's BLAS); tests pin the restatement to
+  it on near-tie data.  M-step sums: sequential float32 per cluster in row order (one thread's
+  ``centers_new_chunk``), counts exact.
 Pinned against sklearn's own output in tests/golden/kmeans_*.npz (labels bit-identical).
 """
 from __future__ import annotations
@@ -23,15 +39,137 @@ from __future__ import annotations
 import numpy as np
 
 CHUNK = 256
+f32 = np.float32
+
+
+# ----------------------------------------------------------------------------- E-step arithmetic
+def row_norms_sq_f32(C: np.ndarray) -> np.ndarray:
+    """np.einsum('ij,ij->i', C, C) for float32 C (numpy baseline-SSE sum_of_products, outstride 0)."""
+    C = np.asarray(C, f32)
+    k, d = C.shape
+    acc = np.zeros((k, 4), f32)
+    i = 0
+    while d - i >= 16:
+        for t in (3, 2, 1, 0):
+            a = C[:, i + 4 * t:i + 4 * t + 4]
+            acc = (a * a).astype(f32) + acc
+        i += 16
+    while i < d:
+        a = np.zeros((k, 4), f32)
+        m = min(4, d - i)
+        a[:, :m] = C[:, i:i + m]
+        acc = (a * a).astype(f32) + acc
+        i += 4
+    return ((acc[:, 0] + acc[:, 1]).astype(f32) + (acc[:, 2] + acc[:, 3]).astype(f32)).astype(f32)
+
+
+def _fma(a, b, c):
+    """float32 fused multiply-add (the f32 x f32 product is exact in float64)."""
+    return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(f32)
+
+
+def _tree_adjacent(v):
+    while v.shape[-1] > 1:
+        v = (v[..., 0::2] + v[..., 1::2]).astype(f32)
+    return v[..., 0]
+
+
+def _tree_halves(v):
+    while v.shape[-1] > 1:
+        h = v.shape[-1] // 2
+        v = (v[..., :h] + v[..., h:]).astype(f32)
+    return v[..., 0]
+
+
+def sgemm_small_path(k: int, rows: int, d: int) -> bool:
+    """OpenBLAS (SkylakeX) small-matrix permit for sklearn's TN sgemm call (M = k, N = rows, K = d)."""
+    return k * rows <= 1200 and d >= 32 and float(k) * rows * d <= 1e6
+
+
+def estep_dist(Xc: np.ndarray, C: np.ndarray, cn: np.ndarray) -> np.ndarray:
+    """float32 ||c||^2 - 2 x.c of one sklearn chunk (rows of Xc), bit-exact restatement of the sgemm call."""
+    N, d = Xc.shape
+    k = C.shape[0]
+    if sgemm_small_path(k, N, d):
+        dp = (d + 15) // 16 * 16
+        Xp = np.zeros((N, dp), f32)
+        Xp[:, :d] = Xc
+        Cp = np.zeros((k, dp), f32)
+        Cp[:, :d] = C
+        acc = np.zeros((N, k, 16), f32)
+        for b in range(0, dp, 16):
+            acc = _fma(Xp[:, None, b:b + 16], Cp[None, :, b:b + 16], acc)
+        s = _tree_adjacent(acc.copy())
+        n4, k4 = 4 * (N // 4), 4 * (k // 4)
+        if n4 < N and k4 < k:
+            s[n4:, k4:] = _tree_halves(acc[n4:, k4:].copy())
+    else:
+        s = np.zeros((N, k), f32)
+        for t in range(d):
+            s = _fma(Xc[:, None, t], C[None, :, t], s)
+    return (cn[None, :] + (f32(-2.0) * s).astype(f32)).astype(f32)
+
+
+def estep_dist_blas(Xc: np.ndarray, C: np.ndarray, cn: np.ndarray) -> np.ndarray:
+    """The chunk's distances through the very BLAS call sklearn makes (scipy's sgemm, column-major TN)."""
+    from scipy.linalg import blas
+    pd = np.asfortranarray(np.tile(cn, (Xc.shape[0], 1)).T)
+    return blas.sgemm(-2.0, np.asfortranarray(C.T), np.asfortranarray(Xc.T), beta=1.0, c=pd,
+                      trans_a=1, trans_b=0).T
+
+
+def assign_labels(X: np.ndarray, centers: np.ndarray, dist_fn=estep_dist) -> np.ndarray:
+    """lloyd_iter_chunked_dense(update_centers=False): 256-row chunks, first-minimum argmin."""
+    X = np.asarray(X, f32)
+    C = np.asarray(centers, f32)
+    cn = row_norms_sq_f32(C)
+    out = [np.argmin(dist_fn(X[s:s + CHUNK], C, cn), axis=1) for s in range(0, X.shape[0], CHUNK)]
+    return np.concatenate(out).astype(np.int32)
+
+
+def cluster_sums_f32(X: np.ndarray, labels: np.ndarray, k: int):
+    """Per-cluster float32 sums added in row order (one accumulator per column) and exact counts."""
+    order = np.argsort(labels, kind="stable")
+    Xs = np.asarray(X, f32)[order]
+    ls = labels[order]
+    sums = np.zeros((k, X.shape[1]), f32)
+    counts = np.bincount(labels, minlength=k).astype(f32)
+    start = 0
+    for j in range(k):
+        m = int(counts[j])
+        if m:
+            sums[j] = np.add.accumulate(Xs[start:start + m], axis=0)[-1]
+        start += m
+    assert start == len(ls)
+    return sums, counts
+
+
+def euclidean_dense_dense_sq(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """sklearn _euclidean_dense_dense(squared=True): float32, 4-element groups summed left to right, tail."""
+    a = np.asarray(a, f32)
+    b = np.asarray(b, f32)
+    d = a.shape[-1]
+    q = d // 4
+    r = np.zeros(np.broadcast(a[..., 0], b[..., 0]).shape, f32)
+    for g in range(q):
+        e = [(a[..., 4 * g + t] - b[..., 4 * g + t]).astype(f32) for t in range(4)]
+        s = (e[0] * e[0]).astype(f32) + (e[1] * e[1]).astype(f32)
+        s = (s + (e[2] * e[2]).astype(f32)).astype(f32)
+        s = (s + (e[3] * e[3]).astype(f32)).astype(f32)
+        r = (r + s).astype(f32)
+    for c in range(4 * q, d):
+        e = (a[..., c] - b[..., c]).astype(f32)
+        r = (r + (e * e).astype(f32)).astype(f32)
+    return r
 
 
 def _sqdist_upcast(A: np.ndarray, X: np.ndarray) -> np.ndarray:
-    """sklearn _euclidean_distances_upcast: float64 ||a||^2 - 2 a.x + ||x||^2, clipped at 0, float32."""
+    """sklearn _euclidean_distances_upcast: float64 (-2 a.x + ||a||^2) + ||x||^2, clipped at 0, float32."""
     A64 = A.astype(np.float64)
     X64 = X.astype(np.float64)
     d = -2.0 * (A64 @ X64.T)
-    d += (A64 * A64).sum(1)[:, None]
-    d += (X64 * X64).sum(1)[None, :]
+    d += np.einsum("ij,ij->i", A64, A64)[:, None]
+    d += np.einsum("ij,ij->i", X64, X64)[None, :]
     return np.maximum(d.astype(np.float32), np.float32(0))
 
 
@@ -59,26 +197,15 @@ def kmeans_plusplus(X: np.ndarray, k: int, rs: np.random.RandomState, w: np.ndar
     return centers, idx
 
 
-def assign_labels(X: np.ndarray, centers: np.ndarray) -> np.ndarray:
-    """E-step in float32: ||c||^2 - 2 x.c, first-minimum argmin."""
-    cn = np.einsum("ij,ij->i", centers, centers)
-    d = cn[None, :] + np.float32(-2.0) * (X @ centers.T)
-    return np.argmin(d, axis=1).astype(np.int32)
-
-
 def _lloyd_iter(X, w, centers, labels, update=True):
     k, D = centers.shape
     labels[:] = assign_labels(X, centers)
     if not update:
         return None, None, None
-    new = np.zeros((k, D), np.float64)
-    wic = np.zeros(k, np.float64)
-    np.add.at(new, labels, X.astype(np.float64) * w[:, None])
-    np.add.at(wic, labels, w.astype(np.float64))
-    new = new.astype(np.float32)
-    wic = wic.astype(np.float32)
+    new, wic = cluster_sums_f32(X, labels, k)
     empty = np.where(wic == 0)[0]
     if empty.size:
+        # _relocate_empty_clusters_dense: numpy expression (pairwise row sums)
         dist = ((X - centers[labels]) ** 2).sum(axis=1)
         if dist.max() > 0:
             far = np.argpartition(dist, -empty.size)[:-empty.size - 1:-1]
@@ -91,11 +218,17 @@ def _lloyd_iter(X, w, centers, labels, update=True):
     amax = int(np.argmax(wic))
     for j in range(k):
         if wic[j] > 0:
-            new[j] *= np.float32(1.0) / wic[j]
+            new[j] *= np.float32(1.0 / float(wic[j]))
         else:
             new[j] = new[amax]
-    shift = np.sqrt(((new - centers) ** 2).sum(1))
+    shift = np.sqrt(euclidean_dense_dense_sq(new, centers))
     return new, wic, shift
+
+
+def inertia_f32(X, centers, labels) -> float:
+    """_inertia_dense, one thread: float32 sequential sum of _euclidean_dense_dense over rows."""
+    r = euclidean_dense_dense_sq(X, centers[labels])
+    return float(np.add.accumulate(r)[-1])
 
 
 def kmeans_single_lloyd(X, w, centers, max_iter=300, tol=0.0):
@@ -113,8 +246,7 @@ def kmeans_single_lloyd(X, w, centers, max_iter=300, tol=0.0):
         labels_old[:] = labels
     if not strict:
         _lloyd_iter(X, w, centers, labels, update=False)
-    inertia = float(((X - centers[labels]).astype(np.float32) ** 2).sum(1) @ w)
-    return labels, inertia, centers, i + 1
+    return labels, inertia_f32(X, centers, labels), centers, i + 1
 
 
 def is_same_clustering(a, b, k):

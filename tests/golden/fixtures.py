@@ -30,6 +30,23 @@ KMEANS_CASES = [
     (1336, 64, 10, 10, 1),
 ]
 
+# Overlapping-cluster cases (labels decided by float32 rounding at near-ties): (N, D, true clusters, centre std,
+# k, n_init).  Points are N(0, 1) around centres ~ N(0, spread^2): spread 1 = "blob spread = centre spread";
+# spread 0.15 = heavy overlap (every point nearly equidistant from several centres).
+KMEANS_OVERLAP_CASES = [
+    (1336, 128, 10, 1.0, 10, 10),
+    (1336, 128, 10, 0.15, 10, 10),
+    (4096, 64, 10, 0.15, 14, 10),
+    (1336, 64, 6, 0.15, 2, 10),
+    (1000, 128, 8, 0.15, 3, 10),
+    (999, 128, 8, 0.15, 5, 1),
+]
+# config[4] clustering scale: N = 100 000 latents-like rows (D = 128), k = 10, n_init = 10 (labels stored int16)
+KMEANS_BIG_CASE = (100000, 128, 10, 0.3, 10, 10)
+# eval-mode latents of the oracle HybridVAE (128x128, text 768) on 1336 synthetic clips; k = 2..14 sweep
+# (src/Convolutional_VAE.py:311-327); the latents themselves are stored in the fixture
+LATENT_N, LATENT_KS = 1336, list(range(2, 15))
+
 N_SAMPLES = 16
 
 
@@ -115,6 +132,24 @@ def blobs(n, d, k, seed):
     c = rng.normal(0, 3.0, (k, d))
     lab = rng.integers(0, k, n)
     return (c[lab] + rng.normal(0, 1.0, (n, d))).astype(np.float32)
+
+
+def overlap_blobs(n, d, k, spread, seed):
+    """Overlapping clusters: N(0, 1) points around k centres drawn from N(0, spread^2), float32."""
+    rng = np.random.default_rng(seed)
+    c = rng.normal(0, spread, (k, d))
+    lab = rng.integers(0, k, n)
+    return (c[lab] + rng.normal(0, 1.0, (n, d))).astype(np.float32)
+
+
+def overlap_fixture_name(case):
+    n, d, true_k, spread, k, n_init = case
+    return f"kmeans_overlap_n{n}_d{d}_s{int(round(spread * 100))}_k{k}_i{n_init}.npz"
+
+
+def overlap_seed(case):
+    n, d, true_k, spread, k, n_init = case
+    return 7 * n + 3 * d + 11 * true_k + int(round(spread * 100))
 
 
 def blob_labels(n, d, k, seed):

@@ -191,6 +191,67 @@ def make_kmeans():
         print("kmeans", n, d, k, n_init, km.n_iter_, flush=True)
 
 
+def _sk_kmeans(X, k, n_init):
+    from sklearn.cluster import KMeans
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(1):   # one OpenMP thread: sklearn's row-order centre sums are deterministic
+        return KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
+
+
+def make_kmeans_overlap():
+    """Overlapping clusters (near-tie E-steps) and the config[4]-scale case (N = 100 000)."""
+    for case in fixtures.KMEANS_OVERLAP_CASES + [fixtures.KMEANS_BIG_CASE]:
+        n, d, true_k, spread, k, n_init = case
+        X = fixtures.overlap_blobs(n, d, true_k, spread, fixtures.overlap_seed(case))
+        km = _sk_kmeans(X, k, n_init)
+        np.savez_compressed(os.path.join(HERE, fixtures.overlap_fixture_name(case)),
+                            labels=km.labels_.astype(np.int16), centers=km.cluster_centers_.astype(np.float32),
+                            inertia=np.float64(km.inertia_), n_iter=np.int32(km.n_iter_))
+        print("kmeans overlap", case, km.n_iter_, flush=True)
+
+
+def latent_dataset():
+    """Eval-mode mu of the oracle HybridVAE (128x128, text 768) on LATENT_N synthetic clips: oracle mel-dB ->
+    per-pixel z-score -> 5 train-mode Adam steps (so BatchNorm running statistics are real) -> eval encode."""
+    import torch
+    n = fixtures.LATENT_N
+    pcm = mel_oracle.synthetic_pcm(n, 65024, seed=2024)
+    mel = np.stack([mel_oracle.extract_mel_spectrogram(c) for c in pcm]).astype(np.float32)
+    z = ((mel - mel.mean(0)) / (mel.std(0) + 1e-8)).astype(np.float32)
+    g = torch.Generator().manual_seed(5)
+    text = torch.randn(n, 768, generator=g) / 768 ** 0.5
+    audio = torch.from_numpy(z)[:, None]
+    torch.manual_seed(42)
+    model = models_oracle.HybridVAE(128, 768, (128, 128))
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    model.train()
+    for step in range(5):
+        idx = torch.arange(step * 32, step * 32 + 32)
+        eps = torch.randn(32, 128, generator=g)
+        out = model(audio[idx], text[idx], eps=eps)
+        loss = models_oracle.loss_function(out[0], audio[idx], out[1], text[idx], out[2], out[3])[0]
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    model.eval()
+    with torch.no_grad():
+        mu = torch.cat([model.encode(audio[i:i + 128], text[i:i + 128])[0] for i in range(0, n, 128)])
+    return mu.numpy().astype(np.float32)
+
+
+def make_kmeans_latents():
+    X = latent_dataset()
+    out = {"X": X}
+    for k in fixtures.LATENT_KS:
+        km = _sk_kmeans(X, k, 10)
+        out[f"labels_k{k}"] = km.labels_.astype(np.int16)
+        out[f"centers_k{k}"] = km.cluster_centers_.astype(np.float32)
+        out[f"inertia_k{k}"] = np.float64(km.inertia_)
+        out[f"n_iter_k{k}"] = np.int32(km.n_iter_)
+        print("kmeans latents k", k, km.n_iter_, flush=True)
+    np.savez_compressed(os.path.join(HERE, "kmeans_latents_n1336_d128.npz"), **out)
+
+
 def make_metrics():
     """sklearn.metrics scores of the K-Means fixture labels (and the blob ground truth), plus the reference's own
     calculate_purity (src/Conditional_VAE.py:279-287, AST-loaded) — §8f rows 1 and 4."""
@@ -235,11 +296,15 @@ def make_features():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    what = sys.argv[1:] or ["models", "kmeans", "metrics", "features"]
+    what = sys.argv[1:] or ["models", "kmeans", "kmeans_overlap", "kmeans_latents", "metrics", "features"]
     if "features" in what:
         make_features()
     if "kmeans" in what:
         make_kmeans()
+    if "kmeans_overlap" in what:
+        make_kmeans_overlap()
+    if "kmeans_latents" in what:
+        make_kmeans_latents()
     if "metrics" in what:
         make_metrics()
     if "models" in what:

@@ -1,0 +1,146 @@
+"""Parity of the EXACT benchmarked configuration (bench.py, BASELINE config[1]): 256 clips of synthetic PCM
+(bench.synthetic_pcm, generated on the GPU as the bench does) -> bench.MelStage (HIP mel-dB 128x128 + the
+HIP StandardScaler z-score) -> audio-only HybridVAE 128x128 -> one fused Trainer.step (forward, ELBO sums,
+backward, Adam), the B = 256 GEMM plans (split-K factors, sub-pixel tiles, LDS-DMA variants) the bench
+times.  Compared with the oracle chain: oracle/mel_oracle.py (numpy librosa restatement) for the mel stage,
+oracle/models_oracle.py (pinned bit-exact to the AST-loaded reference classes) for the step, seed-42
+weights, eps from torch.Generator().manual_seed(1); reference step:
+src/Convolutional_VAE.py:224-240.
+
+Tolerances:
+  * mel-dB vs the oracle: atol 0.05 dB, <= 2e-3 dB above -60 dB (fp32 vs float64 STFT, as test_features_gpu);
+  * fp32 engine from the same z-scored input: mu / logvar / ELBO terms <= 1e-4 relative (north_star);
+    gradients by the f64-yardstick rule of test_models_gpu.compare_step; Adam exact vs torch.optim.Adam on
+    the same gradient; BatchNorm running statistics <= 1e-4;
+  * bf16 engine (the bench dtype): mu 3e-2, ELBO 2e-2, global gradient 0.15 relative L2 (test_models_gpu);
+  * the whole oracle chain (oracle mel -> oracle f64 scaler -> oracle model) vs the HIP chain: the inputs
+    differ by the mel tolerance, so ELBO / mu are compared at 1e-3 (fp32 engine).
+"""
+import numpy as np
+import pytest
+import torch
+
+import bench
+import hlmc_amd
+from oracle import kmeans_oracle as KO
+from oracle import mel_oracle as MO
+from oracle import models_oracle as OM
+from tests.test_models_gpu import _bias_feeds_bn, oracle64_with_kink_envelope, rel
+
+pytestmark = pytest.mark.gpu
+B = 256
+CASE = {"kind": "hybrid"}
+
+
+def _hip_chain(dtype):
+    dev = torch.device("cuda", 0)
+    pcm = bench.synthetic_pcm(B, bench.N_SAMPLES, seed=1000, device=dev)
+    calib = hlmc_amd.extract_mel_spectrogram(pcm, fixed_time_steps=bench.FRAMES)
+    scaler = hlmc_amd.StandardScaler().fit(calib.reshape(B, -1))
+    stage = bench.MelStage(B, dev, scaler)
+    x = stage(pcm)
+    torch.manual_seed(42)
+    model = hlmc_amd.HybridVAE(128, 384, (128, 128), audio_only=True, compute_dtype=dtype).to(dev)
+    trainer = hlmc_amd.Trainer(model, lr=1e-4)
+    eps = torch.randn(B, 128, generator=torch.Generator().manual_seed(1))
+    init = [p.detach().cpu().clone() for p in model.parameters()]
+    sums = trainer.step(x, None, eps=eps.to(dev))
+    out = trainer._cache[B]["out"]
+    torch.cuda.synchronize()
+    return dict(pcm=pcm.cpu().numpy(), mel=stage.mel.cpu().numpy(), x=x.detach().cpu().clone(), eps=eps,
+                loss=trainer.loss_tuple(sums), mu=out["mu"].cpu(), logvar=out["logvar"].cpu(),
+                grad=trainer.gflat.detach().cpu().clone(), init=init, model=model)
+
+
+def _oracle_model():
+    torch.manual_seed(42)
+    return OM.HybridVAE(128, 384, (128, 128), audio_only=True)
+
+
+def test_bench_mel_stage_matches_oracle(cuda):
+    h = _hip_chain("bf16")
+    ref = np.stack([MO.extract_mel_spectrogram(c, fixed_time_steps=bench.FRAMES) for c in h["pcm"]])
+    assert h["mel"].shape == ref.shape == (B, 128, 128)
+    err = np.abs(h["mel"] - ref)
+    print(f"mel-dB B={B}: max abs err {err.max():.2e} dB, above -60 dB {err[ref > -60].max():.2e} dB")
+    assert err.max() < 0.05 and err[ref > -60].max() < 2e-3
+    # z-score: the HIP StandardScaler (fitted on this batch) vs sklearn's float64 fit of the same mel
+    mean, var, scale = KO.standard_scaler_fit(h["mel"].reshape(B, -1))
+    z = KO.standard_scaler_transform(h["mel"].reshape(B, -1), mean, scale).reshape(B, 1, 128, 128)
+    np.testing.assert_allclose(h["x"].numpy(), z, rtol=1e-5, atol=1e-5)
+
+
+def test_bench_train_step_fp32_matches_oracle(cuda):
+    h = _hip_chain("fp32")
+    x, eps = h["x"], h["eps"]
+    ora = _oracle_model()
+    for p, q in zip(ora.parameters(), h["init"]):
+        assert torch.equal(p.detach(), q)
+    ora64, ora64f = oracle64_with_kink_envelope(CASE, ora, (x, None), eps, None)
+    out = ora(x, None, eps=eps)
+    lo = OM.loss_function(out[0], x, None, None, out[2], out[3])
+    lo[0].backward()
+    print(f"B={B} fp32: rel mu {rel(h['mu'], out[2].detach()):.2e}, rel logvar {rel(h['logvar'], out[3].detach()):.2e},"
+          f" ELBO {h['loss'][0]:.6e} vs {float(lo[0]):.6e}")
+    assert rel(h["mu"], out[2].detach()) < 1e-4 and rel(h["logvar"], out[3].detach()) < 1e-4
+    for a, b in zip(h["loss"], lo):
+        if b is not None and float(b) != 0.0:
+            assert abs(a - float(b)) <= 1e-4 * abs(float(b)), (a, float(b))
+    # gradients: f64 yardstick + kink envelope, BN-fed conv biases absolutely
+    off = 0
+    names = dict(ora.named_parameters())
+    o64, o64f = dict(ora64.named_parameters()), dict(ora64f.named_parameters())
+    worst = 0.0
+    for name, p in ora.named_parameters():
+        g = h["grad"][off:off + p.numel()].view_as(p)
+        off += p.numel()
+        if _bias_feeds_bn(ora, name):
+            scale = float(names[name[:-4] + "weight"].grad.abs().max())
+            assert float((g - p.grad).abs().max()) <= 1e-4 * scale + 1e-6, name
+            continue
+        g64 = o64[name].grad
+        e_ref, e_ours, e_kink = rel(p.grad, g64), rel(g, g64), rel(o64f[name].grad, g64)
+        worst = max(worst, e_ours)
+        assert e_ours <= max(1e-3, 8 * e_ref) + 1.5 * e_kink, f"grad {name}: {e_ours:.3e} vs {e_ref:.3e} / {e_kink:.3e}"
+    print(f"B={B} fp32: worst per-tensor gradient error vs float64 {worst:.2e}")
+    # Adam: exact torch.optim.Adam on the engine's own gradient
+    ps = [q.clone().requires_grad_(True) for q in h["init"]]
+    off = 0
+    for p in ps:
+        p.grad = h["grad"][off:off + p.numel()].view_as(p).clone()
+        off += p.numel()
+    torch.optim.Adam(ps, lr=1e-4).step()
+    for (name, pm), p in zip(h["model"].named_parameters(), ps):
+        torch.testing.assert_close(pm.detach().cpu(), p.detach(), rtol=1e-6, atol=1e-7, msg=name)
+    for (n, bo), (_, bm) in zip(ora.named_buffers(), h["model"].named_buffers()):
+        if bo.dtype.is_floating_point:
+            assert rel(bm, bo) < 1e-4, n
+        else:
+            assert torch.equal(bm.cpu(), bo), n
+
+
+def test_bench_train_step_bf16_tracks_oracle(cuda):
+    h = _hip_chain("bf16")
+    ora = _oracle_model()
+    out = ora(h["x"], None, eps=h["eps"])
+    lo = OM.loss_function(out[0], h["x"], None, None, out[2], out[3])
+    lo[0].backward()
+    go = torch.cat([p.grad.reshape(-1) for p in ora.parameters()])
+    e_mu, e_elbo, e_g = rel(h["mu"], out[2].detach()), abs(h["loss"][0] - float(lo[0])) / abs(float(lo[0])), rel(h["grad"], go)
+    print(f"B={B} bf16: rel mu {e_mu:.2e}, rel ELBO {e_elbo:.2e}, global grad rel L2 {e_g:.2e}")
+    assert e_mu < 3e-2 and e_elbo < 2e-2 and e_g < 0.15
+
+
+def test_bench_whole_oracle_chain(cuda):
+    """PCM -> oracle mel -> oracle (sklearn-f64) z-score -> oracle model vs the HIP chain end to end (fp32)."""
+    h = _hip_chain("fp32")
+    mel = np.stack([MO.extract_mel_spectrogram(c, fixed_time_steps=bench.FRAMES) for c in h["pcm"]])
+    mean, var, scale = KO.standard_scaler_fit(mel.reshape(B, -1))
+    x = torch.from_numpy(KO.standard_scaler_transform(mel.reshape(B, -1), mean, scale).reshape(B, 1, 128, 128))
+    print(f"input (z-score) max abs diff HIP vs oracle chain: {float((x - h['x']).abs().max()):.2e}")
+    ora = _oracle_model()
+    out = ora(x, None, eps=h["eps"])
+    lo = OM.loss_function(out[0], x, None, None, out[2], out[3])
+    e_mu, e_elbo = rel(h["mu"], out[2].detach()), abs(h["loss"][0] - float(lo[0])) / abs(float(lo[0]))
+    print(f"whole chain B={B}: rel mu {e_mu:.2e}, rel ELBO {e_elbo:.2e}")
+    assert e_mu < 1e-3 and e_elbo < 1e-3

@@ -4,6 +4,8 @@
   loss, the DP gradient of the global batch is the sum of the per-shard gradients (BatchNorm statistics per
   rank = DDP semantics, so each shard's gradient is that of the reference model run on the shard).  Checked
   bit-exact against the single-process sum of the oracle model's per-shard gradients.
+* Trainer's DDP broadcast_buffers: the model's BatchNorm running statistics are re-pointed at one flat tensor
+  (state_dict unchanged) and rank 0's values reach every rank through one broadcast.
 * StandardScaler(process_group): the two f64 passes are all-reduced and finalised with scaler_finalize; the
   result equals sklearn's StandardScaler on the concatenated shards.
 """
@@ -88,6 +90,19 @@ def _worker(rank, port, outdir):
     ns16 = types.SimpleNamespace(gflat=flat.clone(), grad_dtype=torch.bfloat16, process_group=None, buckets=buckets)
     hlmc_amd.Trainer.allreduce_grads(ns16)
 
+    # ---- BatchNorm running statistics: flat views + rank 0 broadcast (DDP broadcast_buffers)
+    torch.manual_seed(42)
+    model = hlmc_amd.HybridVAE(128, 768, (128, 128), audio_only=True)
+    keys = list(model.state_dict())
+    for i, b in enumerate(m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)):
+        b.running_mean.fill_(10.0 * rank + i)
+        b.running_var.fill_(1.0 + rank)
+    flat = model._flatten_bn_buffers()
+    assert list(model.state_dict()) == keys
+    trn = types.SimpleNamespace(bn_flat=flat, _comm=None, process_group=None)
+    hlmc_amd.Trainer._broadcast_buffers_after_forward(trn)
+    bn_state = {k: v.clone() for k, v in model.state_dict().items() if "running" in k}
+
     # ---- distributed StandardScaler statistics (numpy stands in for the f64 column-sum kernels)
     _, shard = _scaler_shard(rank)
     n = torch.tensor([float(shard.shape[0])], dtype=torch.float64)
@@ -100,7 +115,7 @@ def _worker(rank, port, outdir):
     dist.all_reduce(corr)
     dist.all_reduce(m2)
     mean, var, scale = scaler_finalize(float(n.item()), s, corr, m2)
-    torch.save({"g32": ns.gflat, "g16": ns16.gflat, "mean": mean, "var": var, "scale": scale},
+    torch.save({"g32": ns.gflat, "g16": ns16.gflat, "mean": mean, "var": var, "scale": scale, "bn": bn_state},
                os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
@@ -125,3 +140,8 @@ def test_dp_allreduce_and_distributed_scaler():
         np.testing.assert_allclose(r["var"].numpy(), sk.var_, rtol=1e-9, atol=1e-15)
         np.testing.assert_allclose(r["scale"].numpy(), sk.scale_, rtol=1e-9)
     assert res[0]["scale"][3] == 1.0
+    for k, v in res[1]["bn"].items():   # every rank holds rank 0's running statistics
+        assert torch.equal(v, res[0]["bn"][k]), k
+    means = [float(v.reshape(-1)[0]) for k, v in res[1]["bn"].items() if k.endswith("running_mean")]
+    assert means == [float(i) for i in range(len(means))]           # rank 0 filled 10 * 0 + i
+    assert all(float(v.max()) == float(v.min()) == 1.0 for k, v in res[1]["bn"].items() if k.endswith("running_var"))

@@ -1,5 +1,10 @@
 """K-Means on the GPU vs sklearn 1.7.2 KMeans(random_state=42) labels recorded in tests/golden
-(bit-identical labels required; centres within float32 rounding; ARI vs sklearn == 1)."""
+(bit-identical labels required; centres within float32 rounding; ARI vs sklearn == 1).
+
+Besides the well-separated blob cases, the fixtures hold overlapping clusters (near-tie E-steps, where the
+label is decided by float32 rounding), eval-mode VAE latents (k = 2..14, the reference's silhouette sweep)
+and the config[4] clustering scale (N = 100 000).  Each test reports the near-tie count of the final E-step
+(rows whose two smallest distances lie within 8 float32 ulps) and the ARI against sklearn's labels."""
 import glob
 
 import numpy as np
@@ -114,3 +119,85 @@ def test_km_center_numpy_order_bitexact(cuda, n, d):
     np.testing.assert_array_equal(mean.cpu().numpy(), X.mean(axis=0))
     np.testing.assert_array_equal(var.cpu().numpy(), np.var(X, axis=0))
     np.testing.assert_array_equal(Xc.cpu().numpy(), X - X.mean(axis=0))
+
+
+def _near_ties(X, centers, ulps=8):
+    """Rows whose two smallest E-step distances lie within `ulps` float32 ulps (oracle arithmetic)."""
+    from oracle import kmeans_oracle as KO
+    Xc = (X - X.mean(axis=0)).astype(np.float32)
+    C = (centers - X.mean(axis=0)).astype(np.float32)
+    cn = KO.row_norms_sq_f32(C)
+    cnt = 0
+    for s in range(0, Xc.shape[0], KO.CHUNK):
+        dd = np.sort(KO.estep_dist(Xc[s:s + KO.CHUNK], C, cn), axis=1)
+        if dd.shape[1] > 1:
+            cnt += int((dd[:, 1] - dd[:, 0] <= ulps * np.spacing(np.abs(dd[:, 1]))).sum())
+    return cnt
+
+
+def _check_against_fixture(km, labels, centers, inertia, n_iter, X, what):
+    from sklearn.metrics import adjusted_rand_score
+    ari = adjusted_rand_score(labels, km.labels_)
+    ties = _near_ties(X, centers) if X.shape[0] <= 5000 else -1
+    print(f"{what}: near-tie rows {ties}, ARI vs sklearn {ari:.6f}, n_iter {km.n_iter_}/{n_iter}")
+    np.testing.assert_array_equal(km.labels_, labels)
+    np.testing.assert_allclose(km.cluster_centers_, centers, rtol=1e-5, atol=1e-5)
+    assert km.n_iter_ == n_iter
+    assert km.inertia_ == inertia
+
+
+@pytest.mark.parametrize("case", FX.KMEANS_OVERLAP_CASES, ids=lambda c: f"n{c[0]}_d{c[1]}_s{c[3]}_k{c[4]}_i{c[5]}")
+def test_kmeans_overlapping_clusters_bitexact(cuda, case):
+    n, d, true_k, spread, k, n_init = case
+    X = FX.overlap_blobs(n, d, true_k, spread, FX.overlap_seed(case))
+    fx = np.load("tests/golden/" + FX.overlap_fixture_name(case))
+    km = hlmc_amd.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
+    _check_against_fixture(km, fx["labels"], fx["centers"], float(fx["inertia"]), int(fx["n_iter"]), X,
+                           FX.overlap_fixture_name(case))
+
+
+def test_kmeans_vae_latents_k_sweep(cuda):
+    """src/Convolutional_VAE.py:311-327: KMeans(k, random_state=42, n_init=10) for k = 2..14 on eval-mode
+    latents of the (oracle) HybridVAE, labels bit-identical to sklearn for every k."""
+    fx = np.load("tests/golden/kmeans_latents_n1336_d128.npz")
+    X = fx["X"]
+    for k in FX.LATENT_KS:
+        km = hlmc_amd.KMeans(n_clusters=k, random_state=42, n_init=10).fit(X)
+        _check_against_fixture(km, fx[f"labels_k{k}"], fx[f"centers_k{k}"], float(fx[f"inertia_k{k}"]),
+                               int(fx[f"n_iter_k{k}"]), X, f"latents k={k}")
+
+
+def test_kmeans_100k_config4_scale(cuda):
+    """BASELINE config[4]'s clustering scale: N = 100 000 latents-like rows, D = 128, k = 10, n_init = 10."""
+    case = FX.KMEANS_BIG_CASE
+    n, d, true_k, spread, k, n_init = case
+    X = FX.overlap_blobs(n, d, true_k, spread, FX.overlap_seed(case))
+    fx = np.load("tests/golden/" + FX.overlap_fixture_name(case))
+    km = hlmc_amd.KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(X)
+    _check_against_fixture(km, fx["labels"], fx["centers"], float(fx["inertia"]), int(fx["n_iter"]), X, "N=100k")
+
+
+@pytest.mark.parametrize("n,d,k", [(1336, 128, 2), (1336, 128, 10), (1000, 64, 5), (513, 100, 13), (257, 32, 16),
+                                   (300, 130, 3), (4096, 128, 14), (77, 40, 1)])
+def test_km_assign_matches_sklearn_estep(cuda, n, d, k):
+    """hlmc_km_assign on near-tie data (points on the bisector of two centres) equals the oracle's
+    restatement of sklearn's E-step (einsum norms + the OpenBLAS sgemm kernel sklearn's call takes) label
+    for label, including the short last chunk and the small-matrix kernel's remainder elements."""
+    import torch
+    from hlmc_amd import _lib as L
+    from oracle import kmeans_oracle as KO
+    rng = np.random.default_rng(n * 31 + d * 7 + k)
+    C = rng.standard_normal((k, d)).astype(np.float32)
+    t = rng.standard_normal((n, d)).astype(np.float32)
+    if k >= 2:
+        m, u = (C[0] + C[1]) / 2, C[1] - C[0]
+        u = u / np.linalg.norm(u)
+        t = t - np.outer(t @ u, u)
+        X = (m + 0.3 * t + np.outer(rng.standard_normal(n) * 1e-6, u)).astype(np.float32)
+    else:
+        X = t
+    ref = KO.assign_labels(X, C)
+    Xd, Cd = torch.as_tensor(X, device="cuda"), torch.as_tensor(C, device="cuda")
+    lab = torch.empty(n, dtype=torch.int32, device="cuda")
+    L.check(L.lib().hlmc_km_assign(L.stream(), Xd.data_ptr(), n, d, Cd.data_ptr(), k, lab.data_ptr(), None, None))
+    np.testing.assert_array_equal(lab.cpu().numpy(), ref)

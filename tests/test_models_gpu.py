@@ -269,3 +269,70 @@ def test_bf16_mode_tracks_fp32(cuda):
     gm = torch.cat([p.grad.reshape(-1).cpu() for p in ours.parameters()])
     go = torch.cat([p.grad.reshape(-1) for p in ora.parameters()])
     assert rel(gm, go) < 0.15
+
+
+@pytest.mark.parametrize("train", [True, False], ids=["train", "eval"])
+@pytest.mark.parametrize("name", ["hybrid_128x128_td768", "cvae_128x128", "simple_370", "hybrid_128x1024_td768"])
+def test_decode_matches_oracle(cuda, name, train):
+    """decode(z) / decode(z, condition) (src/Convolutional_VAE.py:167-179, src/Conditional_VAE.py:206-225,
+    src/Simple_VAE.py:95-96) vs the oracle's decode from identical weights; train mode also checks the
+    decoder BatchNorms' running-statistics update."""
+    case = FX.case_by_name(name)
+    ora, ours = build(case)
+    B, Ld = case["B"], case["ctor"]["latent_dim"]
+    g = torch.Generator().manual_seed(77)
+    z = torch.randn(B, Ld, generator=g)
+    ora.train(train)
+    ours.train(train)
+    if case["kind"] == "cvae":
+        cond = torch.nn.functional.one_hot(torch.randint(0, 10, (B,), generator=g), 10).float()
+        with torch.no_grad():
+            ro = ora.decode(z, cond)
+        rm = ours.decode(z.cuda(), cond.cuda())
+    elif case["kind"] == "simple":
+        masks, flat = simple_masks(case, B)
+        nh = len(case["ctor"]["hidden_dims"])
+        it = iter(masks[nh:])
+        hooks = [m.register_forward_hook(lambda mod, inp, out: inp[0] * next(it).to(inp[0].dtype) / 0.8)
+                 for m in ora.decoder.modules() if isinstance(m, torch.nn.Dropout)] if train else []
+        with torch.no_grad():
+            ro = (ora.decode(z),)
+        for h in hooks:
+            h.remove()
+        rm = (ours.decode(z.cuda(), dropout_mask=flat if train else None),)
+    else:
+        with torch.no_grad():
+            ro = ora.decode(z)
+        rm = ours.decode(z.cuda())
+    for a, b in zip(rm, ro):
+        assert not a.requires_grad
+        assert rel(a, b) < 1e-4, f"{name} decode: {rel(a, b)}"
+    for (n, bo), (_, bm) in zip(ora.named_buffers(), ours.named_buffers()):
+        if bo.dtype.is_floating_point:
+            assert rel(bm, bo) < 1e-4, f"buffer {n}: {rel(bm, bo)}"
+        else:
+            assert torch.equal(bm.cpu(), bo), n
+
+
+def test_decode_audio_only_and_backward_guard(cuda):
+    """Audio-only HybridVAE (config[1]) decode returns (recon, None); a backward without a full forward fails
+    loudly instead of reading a decode-only workspace."""
+    ctor = dict(latent_dim=128, text_dim=768, input_hw=(128, 128), audio_only=True)
+    torch.manual_seed(42)
+    ora = OM.HybridVAE(**ctor)
+    torch.manual_seed(42)
+    ours = hlmc_amd.HybridVAE(**ctor).cuda().eval()
+    ora.eval()
+    z = torch.randn(3, 128, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        ro = ora.decode(z)
+    ra, rt = ours.decode(z.cuda())
+    assert rt is None and rel(ra, ro[0]) < 1e-4
+    from hlmc_amd import _lib as L
+    net = ours._native_net()
+    ws = net.new_workspace(3, z.device if z.is_cuda else torch.device("cuda"))
+    d = torch.zeros(3, 1, 128, 128, device="cuda")
+    dm = torch.zeros(3, 128, device="cuda")
+    L.check(L.lib().hlmc_net_decode(net.h, L.stream(), 3, 0, L.ptr(z.cuda()), None, None, L.ptr(d), None, ws.data_ptr()))
+    with pytest.raises(L.HLMCError, match="full hlmc_net_forward"):
+        L.check(L.lib().hlmc_net_backward(net.h, L.stream(), 3, L.ptr(d), None, L.ptr(dm), L.ptr(dm), ws.data_ptr()))

@@ -55,6 +55,51 @@ def test_kmeans_oracle_matches_sklearn_fixture(case):
     assert km.n_iter_ == int(fx["n_iter"])
 
 
+@pytest.mark.parametrize("case", [c for c in FX.KMEANS_OVERLAP_CASES if c[0] * c[4] <= 14000],
+                         ids=lambda c: f"n{c[0]}_d{c[1]}_s{c[3]}_k{c[4]}_i{c[5]}")
+def test_kmeans_oracle_matches_sklearn_overlap_fixture(case):
+    """Overlapping clusters: labels decided by float32 rounding at near-ties; the oracle's bit-level E-step
+    restatement reproduces sklearn's labels, n_iter and inertia exactly."""
+    n, d, true_k, spread, k, n_init = case
+    X = FX.overlap_blobs(n, d, true_k, spread, FX.overlap_seed(case))
+    fx = np.load("tests/golden/" + FX.overlap_fixture_name(case))
+    km = KO.KMeans(k, random_state=42, n_init=n_init).fit(X)
+    np.testing.assert_array_equal(km.labels_, fx["labels"])
+    assert km.n_iter_ == int(fx["n_iter"]) and km.inertia_ == float(fx["inertia"])
+
+
+@pytest.mark.parametrize("k", [2, 7, 14])
+def test_kmeans_oracle_matches_sklearn_latent_fixture(k):
+    fx = np.load("tests/golden/kmeans_latents_n1336_d128.npz")
+    km = KO.KMeans(k, random_state=42, n_init=10).fit(fx["X"])
+    np.testing.assert_array_equal(km.labels_, fx[f"labels_k{k}"])
+    assert km.n_iter_ == int(fx[f"n_iter_k{k}"]) and km.inertia_ == float(fx[f"inertia_k{k}"])
+
+
+@pytest.mark.parametrize("n,d,k", [(1336, 128, 2), (1336, 128, 10), (1000, 64, 5), (513, 100, 13), (257, 32, 16),
+                                   (300, 130, 3), (77, 40, 1)])
+def test_estep_restatement_matches_blas(n, d, k):
+    """oracle estep_dist (the arithmetic hlmc_km_assign implements) == the sgemm call sklearn makes
+    (scipy's OpenBLAS, column-major TN per 256-row chunk), bit for bit, on near-tie data."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+    archs = {i.get("architecture") for i in threadpool_info() if i.get("internal_api") == "openblas"}
+    if archs != {"SkylakeX"}:
+        pytest.skip(f"the restatement is of the SkylakeX OpenBLAS kernels the fixtures were made with, not {archs}")
+    rng = np.random.default_rng(n * 31 + d * 7 + k)
+    C = rng.standard_normal((k, d)).astype(np.float32)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    if k >= 2:
+        m, u = (C[0] + C[1]) / 2, C[1] - C[0]
+        u = u / np.linalg.norm(u)
+        X = (m + 0.3 * (X - np.outer(X @ u, u)) + np.outer(rng.standard_normal(n) * 1e-6, u)).astype(np.float32)
+    cn = KO.row_norms_sq_f32(C)
+    np.testing.assert_array_equal(cn, np.einsum("ij,ij->i", C, C))
+    with threadpool_limits(1, "blas"):
+        for s in range(0, n, KO.CHUNK):
+            np.testing.assert_array_equal(KO.estep_dist(X[s:s + KO.CHUNK], C, cn),
+                                          KO.estep_dist_blas(X[s:s + KO.CHUNK], C, cn))
+
+
 def test_scaler_oracle_matches_fixture():
     fx = np.load("tests/golden/features.npz")
     rng = np.random.default_rng(11)

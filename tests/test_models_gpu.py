@@ -129,7 +129,7 @@ def oracle64_with_kink_envelope(case, ora, ins, eps, masks):
     hooks = []
     for i, m in enumerate(_act_modules(base)):
         hooks.append(m.register_forward_hook(lambda mod, inp, out, i=i: zs.__setitem__(i, inp[0].detach())))
-    run_oracle_step(case, base, [t.double() for t in ins], eps.double(), masks)
+    run_oracle_step(case, base, [None if t is None else t.double() for t in ins], eps.double(), masks)
     for h in hooks:
         h.remove()
     for i, m in enumerate(_act_modules(flip)):
@@ -147,7 +147,7 @@ def oracle64_with_kink_envelope(case, ora, ins, eps, masks):
             g[amb] = gout[0][amb] * other[amb]
             return (g,)
         m.register_full_backward_hook(bhook)
-    run_oracle_step(case, flip, [t.double() for t in ins], eps.double(), masks)
+    run_oracle_step(case, flip, [None if t is None else t.double() for t in ins], eps.double(), masks)
     return base, flip
 
 

@@ -609,6 +609,19 @@ __device__ __forceinline__ void wait_stage(int ahead) {  // ahead = stages still
     }
     wait_vmcnt<0>();
 }
+// the same for any ring depth: allow `ahead` (<= A) later stages of GPW instructions each to stay in flight
+template <int GPW, int A>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+    if constexpr (A <= 0) {
+        wait_vmcnt<0>();
+    } else {
+        if (ahead >= A) {
+            wait_vmcnt<A * GPW>();
+            return;
+        }
+        wait_ahead<GPW, A - 1>(ahead);
+    }
+}
 __device__ __forceinline__ void glds16(const void* g, void* l) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                      (__attribute__((address_space(3))) void*)l, 16, 0, 0);
@@ -794,6 +807,10 @@ struct KRowDense {
         int m;
     };
     __device__ Col prep(int m) const { return Col{m}; }
+    // LDS-DMA path (vec, Md % V == 0): the 16-byte chunk's address or g_zero16 outside the operand
+    __device__ const void* addr(int k, const Col& cl) const {
+        return (k < Kd && cl.m < Md) ? static_cast<const void*>(p + (int64_t)k * ld + cl.m) : &g_zero16;
+    }
     __device__ uint4 load(int k, const Col& cl) const {
         constexpr int V = Vec16<T>::N;
         const int m = cl.m;
@@ -824,6 +841,16 @@ struct KRowConvS2 {
         const int tap = n / C, ci = n - tap * C;
         const int kh = tap / 3, kw = tap - kh * 3;
         return Col{(kh * 2 * Wl + kw) * C + ci, kh, kw, true};
+    }
+    __device__ const void* addr(int k, const Col& cl) const {
+        if (k >= Kd || !cl.ok) return &g_zero16;
+        const uint32_t t = dW.div((uint32_t)k);
+        const int c = k - (int)t * Wl;
+        const uint32_t b = dH.div(t);
+        const int r = (int)t - (int)b * Hl;
+        if ((r == 0 && cl.kh == 0) || (c == 0 && cl.kw == 0)) return &g_zero16;
+        const int64_t pix = ((int64_t)b * 2 * Hl + 2 * r - 1) * (2 * Wl) + 2 * c - 1;
+        return x + pix * C + cl.off;
     }
     __device__ uint4 load(int k, const Col& cl) const {
         if (k >= Kd || !cl.ok) return make_uint4(0, 0, 0, 0);
@@ -972,6 +999,238 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
                 int n = n0 + wn0 + j * 16 + (lane & 15);
                 if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
             }
+}
+
+// ============================================================================ TN main loop, LDS-DMA pipeline
+// bf16 weight gradients.  NS-stage ring of 32-k-row stages filled by global_load_lds_dwordx4 (no register
+// staging): one 1 KB wave-instruction writes 512/BM k-rows of the L tile (or 512/BN of the H tile), lane l at
+// physical chunk l % CPR of its row, fetching logical chunk pc ^ tn_swz(row) (the XOR swizzle lives on the
+// SOURCE address, so the LDS image stays lane-linear).  The swizzle makes the ds_read_b64_tr_b16 fragment
+// reads conflict-free: each 32-lane half reads 8 k-rows x 32 bytes, and the XOR spreads those rows' chunk
+// pairs over all 64 banks (256-B rows: the row's low bits pick the pair; 128-B rows: two rows per bank sweep).
+// 4 waves split the BM x BN tile 2 x 2.  Per stage: counted vmcnt wait for this wave's DMA, raw barrier, issue
+// the stage NS-1 ahead into the slot everyone just finished, 16x16x32 MFMAs.  S > 1: the block writes its
+// K-split's partial tile to ws[(split * M + m) * N + n] (reduced in fixed split order); S == 1: the epilogue
+// stores the final value.
+// Two ds_read_b64_tr_b16 (k-rows lo and lo + 4 of a 16-lane group) forming one 16x16x32 bf16 fragment; no wait
+// (see lgkm_wait_tied).  lo / hi: LDS byte addresses.
+__device__ __forceinline__ bf16x8_t ds_read_tr16_pair(uint32_t lo, uint32_t hi) {
+    s16x4_t a, b;
+    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3" : "=v"(a), "=v"(b) : "v"(lo), "v"(hi));
+    return bf16x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+// s_waitcnt lgkmcnt(0) that every fragment depends on (the MFMAs cannot be scheduled above it)
+template <int TM, int TN>
+__device__ __forceinline__ void lgkm_wait_tied(bf16x8_t (&af)[TM], bf16x8_t (&bf)[TN]) {
+    static_assert(TM <= 4 && TN <= 4, "at most 8 tied fragments");
+    if constexpr (TM == 4 && TN == 4)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bf[0]),
+                     "+v"(bf[1]), "+v"(bf[2]), "+v"(bf[3]));
+    else if constexpr (TM == 4 && TN == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bf[0]),
+                     "+v"(bf[1]));
+    else if constexpr (TM == 2 && TN == 4)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bf[0]), "+v"(bf[1]), "+v"(bf[2]),
+                     "+v"(bf[3]));
+    else if constexpr (TM == 2 && TN == 2)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bf[0]), "+v"(bf[1]));
+    else
+        static_assert(TM == 0, "unsupported fragment counts");
+}
+
+template <int CPR>
+__device__ __forceinline__ int tn_swz(int row) {
+    if constexpr (CPR == 16) return 2 * ((row & 3) | (((row >> 3) & 1) << 2));
+    else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+}
+
+template <int BM, int BN, int NS, class LL, class HL, class EP>
+__global__ __launch_bounds__(256) void gemm_tn_dma_kernel(LL ll, HL hl, EP ep, float* ws, int M, int N, int K,
+                                                          int ksplit_len, int nsplit, int remap, int dbg) {
+    constexpr int BK = 32;
+    constexpr int ASZ = BK * BM * 2, BSZ = BK * BN * 2, STG = ASZ + BSZ;
+    constexpr int ACPR = BM / 8, BCPR = BN / 8;          // 16-byte chunks per k-row
+    constexpr int ARPI = 64 / ACPR, BRPI = 64 / BCPR;    // k-rows per 1 KB DMA instruction
+    constexpr int AI = ASZ / 1024, BI = BSZ / 1024, GI = AI + BI;
+    static_assert(GI % 4 == 0, "DMA instructions per stage must split over 4 waves");
+    constexpr int GPW = GI / 4;
+    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+    __shared__ __attribute__((aligned(1024))) char smem[NS * STG];  // the only LDS object (see vmcnt traps)
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave >> 1) * WM, wn0 = (wave & 1) * WN;
+    const int tiles_n = (N + BN - 1) / BN;
+    const int gx_ = (int)gridDim.x;
+    const int lg_ = remap ? xcd_logical_block((int)blockIdx.x + gx_ * (int)blockIdx.z, gx_ * (int)gridDim.z) : 0;
+    const int tile_ = remap ? lg_ % gx_ : (int)blockIdx.x, bz = remap ? lg_ / gx_ : (int)blockIdx.z;
+    const int m0 = (tile_ / tiles_n) * BM, n0 = (tile_ % tiles_n) * BN;
+    const int kb = bz * ksplit_len;
+    const int ke = min(K, kb + ksplit_len);
+    const int nsteps = kb < ke ? (ke - kb + BK - 1) / BK : 0;
+
+    f32x4_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // this wave's DMA instructions g = wave * GPW + u (A first, then H): k-row within the stage and operand column
+    int drow[GPW];
+    typename LL::Col acol[GPW];
+    typename HL::Col bcol[GPW];
+#pragma unroll
+    for (int u = 0; u < GPW; ++u) {
+        const int g = wave * GPW + u;
+        if (g < AI) {
+            const int row = g * ARPI + lane / ACPR, pc = lane % ACPR;
+            drow[u] = row;
+            acol[u] = ll.prep(m0 + 8 * (pc ^ tn_swz<ACPR>(row)));
+        } else {
+            const int row = (g - AI) * BRPI + lane / BCPR, pc = lane % BCPR;
+            drow[u] = row;
+            bcol[u] = hl.prep(n0 + 8 * (pc ^ tn_swz<BCPR>(row)));
+        }
+    }
+    auto issue = [&](int slot, int k0) {
+        char* sb = smem + slot * STG;
+#pragma unroll
+        for (int u = 0; u < GPW; ++u) {
+            const int g = wave * GPW + u;
+            if (g < AI) glds16(ll.addr(k0 + drow[u], acol[u]), sb + g * 1024);
+            else glds16(hl.addr(k0 + drow[u], bcol[u]), sb + ASZ + (g - AI) * 1024);
+        }
+    };
+
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+        if (p < nsteps) issue(p, kb + p * BK);
+    const int g4 = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+    const uint32_t lds_base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+    for (int t = 0; t < nsteps; ++t) {
+        wait_ahead<GPW, NS - 2>(min(NS - 2, nsteps - 1 - t));
+        __builtin_amdgcn_s_barrier();
+        if (t + NS - 1 < nsteps && !(dbg & 2)) issue((t + NS - 1) % NS, kb + (t + NS - 1) * BK);
+        if (dbg & 1) continue;
+        // Fragment reads as inline asm: hipcc cannot tie a ds_read_b64_tr_b16 builtin to the LDS-DMA slot it reads
+        // and drains the whole ring (vmcnt(0)) before it; the ring is ordered by the counted wait + barrier above,
+        // and the asm's own lgkmcnt wait (tied to the fragments) orders the MFMAs after the data.
+        const uint32_t sa = lds_base + (uint32_t)((t % NS) * STG);
+        const uint32_t sh = sa + ASZ;
+        bf16x8_t af[TM], bfr[TN];
+        const int rlo = 8 * g4 + q, rhi = rlo + 4;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int c = (wm0 + i * 16) / 8 + (pp >> 1);
+            const uint32_t lo = sa + rlo * (2 * BM) + ((c ^ tn_swz<ACPR>(rlo)) << 4) + 8 * (pp & 1);
+            const uint32_t hi = sa + rhi * (2 * BM) + ((c ^ tn_swz<ACPR>(rhi)) << 4) + 8 * (pp & 1);
+            af[i] = ds_read_tr16_pair(lo, hi);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int c = (wn0 + j * 16) / 8 + (pp >> 1);
+            const uint32_t lo = sh + rlo * (2 * BN) + ((c ^ tn_swz<BCPR>(rlo)) << 4) + 8 * (pp & 1);
+            const uint32_t hi = sh + rhi * (2 * BN) + ((c ^ tn_swz<BCPR>(rhi)) << 4) + 8 * (pp & 1);
+            bfr[j] = ds_read_tr16_pair(lo, hi);
+        }
+        lgkm_wait_tied<TM, TN>(af, bfr);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (nsplit == 1) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
+                if (m >= M) continue;
+                const typename EP::Row rw = ep.row(m);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = n0 + wn0 + j * 16 + (lane & 15);
+                    if (n < N) ep.store(rw, n, acc[i][j][r]);
+                }
+            }
+        return;
+    }
+    float* slab = ws + (int64_t)bz * M * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
+                const int n = n0 + wn0 + j * 16 + (lane & 15);
+                if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
+            }
+}
+
+// Split-K reduction parallel over the splits as well as the outputs: a block holds 256 / G outputs x G split
+// groups; thread (group g, output o) adds the slabs s = g, g + G, ... (loads issued 4 at a time) in order, then
+// the G group sums are added in group order.  Fixed order => deterministic; G = 1 is the plain split-order sum.
+// Deep split counts (the 16-262k-row weight gradients split 50-170 ways over 3-18 tiles) are latency chains
+// otherwise: one thread per output walking S slabs waits S / 4 memory round trips.
+template <int G, class EP>
+__global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(const float* __restrict__ ws, EP ep, int M, int N,
+                                                                    int S) {
+    constexpr int OPB = 256 / G;
+    __shared__ float part[G][OPB];
+    const int o = threadIdx.x % OPB, g = threadIdx.x / OPB;
+    const int64_t idx = (int64_t)blockIdx.x * OPB + o;
+    const int64_t total = (int64_t)M * N;
+    const int64_t st = total;
+    float acc = 0.f;
+    if (idx < total) {
+        const float* p = ws + idx;
+        int k = g;
+        for (; k + 3 * G < S; k += 4 * G) {
+            const float a0 = p[k * st], a1 = p[(k + G) * st], a2 = p[(k + 2 * G) * st], a3 = p[(k + 3 * G) * st];
+            acc += a0; acc += a1; acc += a2; acc += a3;
+        }
+        for (; k < S; k += G) acc += p[k * st];
+    }
+    if constexpr (G > 1) {
+        part[g][o] = acc;
+        __syncthreads();
+        if (g != 0) return;
+#pragma unroll
+        for (int j = 1; j < G; ++j) acc += part[j][o];
+    }
+    if (idx < total) {
+        const int m = (int)(idx / N), n = (int)(idx - (int64_t)m * N);
+        EP e = ep;
+        e.set_phase(0);
+        e.store(e.row(m), n, acc);
+    }
+}
+
+// Split-K reduction of a conv weight gradient straight into torch's dW[m][ci][tap] layout: one thread per
+// (m, ci) sums the S partial slabs of its 9 columns n = tap * C + ci in split order (loads coalesced along ci)
+// and writes its 9 contiguous outputs (stores coalesced along ci x tap).
+__global__ void splitk_reduce_wgrad_kernel(const float* __restrict__ ws, float* __restrict__ dW, int M, int C, int S) {
+    const int64_t total = (int64_t)M * C;
+    const int N = 9 * C;
+    const int64_t st = (int64_t)M * N;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int m = (int)(i / C), ci = (int)(i - (int64_t)m * C);
+        const float* p = ws + (int64_t)m * N + ci;
+        float s[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) s[t] = 0.f;
+        for (int k = 0; k < S; ++k) {
+            float v[9];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) v[t] = p[k * st + t * C];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) s[t] += v[t];
+        }
+        float* o = dW + (int64_t)m * N + ci * 9;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) o[t] = s[t];
+    }
 }
 
 }  // namespace hlmc

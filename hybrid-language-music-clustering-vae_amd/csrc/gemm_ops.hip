@@ -3,6 +3,7 @@
 #include "ops.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace hlmc {
@@ -205,6 +206,21 @@ struct StoreWgradConv {
     }
 };
 
+// S-way split-K reduction with the splits spread over G thread groups (splitk_reduce_grouped_kernel)
+template <class EP>
+void reduce_splits(hipStream_t s, const float* ws, const EP& ep, int M, int N, int S) {
+    const int64_t total = (int64_t)M * N;
+    auto go = [&](auto gtag) {
+        constexpr int G = decltype(gtag)::value;
+        const int64_t blocks = (total + 256 / G - 1) / (256 / G);
+        splitk_reduce_grouped_kernel<G, EP><<<(unsigned)blocks, 256, 0, s>>>(ws, ep, M, N, S);
+    };
+    if (S >= 32) go(std::integral_constant<int, 8>{});
+    else if (S >= 8) go(std::integral_constant<int, 4>{});
+    else if (S >= 4) go(std::integral_constant<int, 2>{});
+    else go(std::integral_constant<int, 1>{});
+}
+
 template <typename T, int BM, int BN, int WM, int WN, class LL, class HL, class EP>
 int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws) {
     constexpr int BK = gemm_bk<T>();
@@ -221,9 +237,7 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
         gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
-    int64_t total = (int64_t)M * N;
-    int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
-    splitk_reduce_kernel<EP><<<blocks, 256, 0, s>>>(ws.p, ep, M, N, pl.S, 1);
+    reduce_splits(s, ws.p, ep, M, N, pl.S);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -245,6 +259,93 @@ inline int tn_tile(int M, int N) {
     if (M > 32) return tn_n96(N) ? 2 : 1;
     return 3;
 }
+// ---- bf16 weight gradients on the LDS-DMA pipeline (gemm_tn_dma_kernel): OPT-IN (HLMC_TN_DMA=1), measured
+// slower than the register-staged kernel on every conv weight gradient of the step (scripts/bench_gemm.py,
+// 600-730 vs 478 us for the 10 layers; its compute phase alone ran at ~20 % of MFMA peak, the
+// fragment reads waiting on one lgkmcnt per 32-deep stage).  Kept as the measured alternative.
+// HLMC_TN_DMA_BLOCKS sets its grid target, HLMC_TN_DMA_NS its ring depth (4 / 8).
+constexpr int kTnDmaStages = 8;
+constexpr int kTnDmaTargetBlocks = 256;
+inline bool tn_dma_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HLMC_TN_DMA");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+inline bool tn_dma_linear() {  // HLMC_TN_DMA_LINEAR=0: linear weight gradients on the register-staged kernel
+    static const bool on = [] {
+        const char* e = std::getenv("HLMC_TN_DMA_LINEAR");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+inline Plan plan_tn_dma(int tiles, int K) {
+    static const int target = [] {
+        const char* e = std::getenv("HLMC_TN_DMA_BLOCKS");
+        return e ? std::max(16, std::atoi(e)) : kTnDmaTargetBlocks;
+    }();
+    constexpr int BK = 32;
+    int S = cdiv(target, tiles);
+    S = std::max(1, std::min(S, K / (8 * BK)));   // >= 8 stages per split
+    int ksl = cdiv(cdiv(K, S), BK) * BK;
+    S = cdiv(K, ksl);
+    return {S, ksl};
+}
+// tile: BM = 128 when M >= 128 else 64; BN = 64 when N is a multiple of 64 but not of 128 (N = 9 C: 288, 576)
+inline int tn_dma_tile(int M, int N) { return (M >= 128 ? 0 : 2) + ((N % 128 != 0 && N % 64 == 0) ? 1 : 0); }
+inline size_t tn_dma_ws(int M, int N, int K) {
+    const int bm = M >= 128 ? 128 : 64, bn = (N % 128 != 0 && N % 64 == 0) ? 64 : 128;
+    const Plan pl = plan_tn_dma(cdiv(M, bm) * cdiv(N, bn), K);
+    return pl.S > 1 ? (size_t)pl.S * M * N * sizeof(float) : 0;
+}
+struct ReduceWgradConv {  // S > 1 reduction of a conv weight gradient into torch's dW layout
+    float* dW;
+    int C;
+};
+template <int BM, int BN, class LL, class HL, class EP>
+int launch_tn_dma(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws,
+                  const ReduceWgradConv* rw) {
+    const int tiles = cdiv(M, BM) * cdiv(N, BN);
+    const Plan pl = plan_tn_dma(tiles, K);
+    if (pl.S > 1) {
+        const size_t need = (size_t)pl.S * M * N * sizeof(float);
+        HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "wgrad workspace too small");
+    }
+    dim3 grid(tiles, 1, pl.S);
+    const int rm = xcd_remap_for_site();
+    static const int dbg = [] {  // HLMC_TN_DMA_DBG: 1 skip fragment reads + MFMA, 2 skip the in-loop DMA (timing probes)
+        const char* e = std::getenv("HLMC_TN_DMA_DBG");
+        return e ? std::atoi(e) : 0;
+    }();
+    static const int stages = [] {  // HLMC_TN_DMA_NS = 4 or 8 (ring depth; measurement aid)
+        const char* e = std::getenv("HLMC_TN_DMA_NS");
+        return e ? std::atoi(e) : kTnDmaStages;
+    }();
+    HLMC_PROBE_BEGIN(s);
+    if (stages == 4)
+        gemm_tn_dma_kernel<BM, BN, 4, LL, HL, EP><<<grid, 256, 0, s>>>(ll, hl, ep, ws.p, M, N, K, pl.ksl, pl.S, rm, dbg);
+    else
+        gemm_tn_dma_kernel<BM, BN, 8, LL, HL, EP><<<grid, 256, 0, s>>>(ll, hl, ep, ws.p, M, N, K, pl.ksl, pl.S, rm, dbg);
+    HLMC_PROBE_END(s);
+    HLMC_LAUNCHED();
+    if (pl.S == 1) return HLMC_OK;
+    (void)rw;
+    reduce_splits(s, ws.p, ep, M, N, pl.S);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <class LL, class HL, class EP>
+int dispatch_tn_dma(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws,
+                    const ReduceWgradConv* rw) {
+    switch (tn_dma_tile(M, N)) {
+        case 0: return launch_tn_dma<128, 128>(s, ll, hl, ep, M, N, K, ws, rw);
+        case 1: return launch_tn_dma<128, 64>(s, ll, hl, ep, M, N, K, ws, rw);
+        case 2: return launch_tn_dma<64, 128>(s, ll, hl, ep, M, N, K, ws, rw);
+        default: return launch_tn_dma<64, 64>(s, ll, hl, ep, M, N, K, ws, rw);
+    }
+}
+
 template <typename T, class LL, class HL, class EP>
 int dispatch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws) {
     switch (tn_tile(M, N)) {
@@ -257,12 +358,15 @@ int dispatch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, 
 template <typename T>
 size_t dispatch_tn_ws(int M, int N, int K) {
     constexpr int BK = gemm_bk<T>();
+    size_t w = 0;
     switch (tn_tile(M, N)) {
-        case 0: return tn_ws<128, 128>(M, N, K, BK);
-        case 1: return tn_ws<64, 128>(M, N, K, BK);
-        case 2: return tn_ws<64, 96>(M, N, K, BK);
-        default: return tn_ws<32, 128>(M, N, K, BK);
+        case 0: w = tn_ws<128, 128>(M, N, K, BK); break;
+        case 1: w = tn_ws<64, 128>(M, N, K, BK); break;
+        case 2: w = tn_ws<64, 96>(M, N, K, BK); break;
+        default: w = tn_ws<32, 128>(M, N, K, BK); break;
     }
+    if constexpr (sizeof(T) == 2) w = std::max(w, tn_dma_ws(M, N, K));  // either path may run (alignment decides)
+    return w;
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -326,6 +430,12 @@ int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* X
     StoreWgradConv ep{dW, C};
     probe::site(probe::kWgradS2, 2.0 * M * N * K,
                 (double)sizeof(T) * ((double)K * M + 4.0 * K * C) + 4.0 * M * N);
+    if constexpr (sizeof(T) == 2) {
+        if (tn_dma_enabled() && ll.vec && aligned16(Xh)) {
+            const ReduceWgradConv rw{dW, C};
+            return dispatch_tn_dma(s, ll, hl, ep, M, N, K, ws, &rw);
+        }
+    }
     return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
 }
 template <typename T>
@@ -357,6 +467,10 @@ int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int 
     KRowDense<T> hl{x, ldx, Mb, K, (ldx % V == 0) && aligned16(x)};
     StoreRM<float> ep{dW, nullptr, K, 0, 0};
     probe::site(probe::kLinearWgrad, 2.0 * N * K * Mb, (double)sizeof(T) * ((double)Mb * N + (double)Mb * K) + 4.0 * N * K);
+    if constexpr (sizeof(T) == 2) {
+        if (tn_dma_enabled() && tn_dma_linear() && ll.vec && hl.vec && N % 8 == 0 && K % 8 == 0)
+            return dispatch_tn_dma(s, ll, hl, ep, N, K, Mb, ws, nullptr);
+    }
     return dispatch_tn<T>(s, ll, hl, ep, N, K, Mb, ws);
 }
 template <typename T>

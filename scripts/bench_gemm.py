@@ -75,6 +75,12 @@ def wgrad_case(tag, Bn, Hl, Wl, M, C):
     report(f"{tag} wgrad {Hl}x{M}x{C}", us, fl, by)
 
 
+ONLY = os.environ.get("HLMC_BENCH_ONLY", "")  # e.g. "wgrad": time only that family
+if ONLY:
+    _keep = {"conv": conv_case, "subpixel": subpixel_case, "wgrad": wgrad_case}
+    conv_case, subpixel_case, wgrad_case = [(f if ONLY == k else (lambda *a, **kw: None))
+                                            for k, f in (("conv", conv_case), ("subpixel", subpixel_case),
+                                                         ("wgrad", wgrad_case))]
 h = 128
 for l in range(1, 6):
     h //= 2  # input spatial of enc layer l: 128 / 2^l

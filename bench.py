@@ -6,8 +6,12 @@ HybridVAE without the text branch) forward + loss + backward + Adam, bf16 activa
 with fp32 accumulation and fp32 master weights; for N > 1 ranks the flat fp32 gradient is all-reduced
 (RCCL over xGMI) before Adam.  Weak scaling: 256 clips per GPU per step.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload audio|hybrid] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload audio|hybrid|cvae] [--dtype bf16|fp32]
+                    [--no-cpu-baseline] [--no-roofline] [--no-extras]
 N > 1 is launched by torch.distributed.run (one process per GPU); rank 0 prints ONE JSON line.
+Besides the headline (BASELINE config[1]), the default run times three more workloads on the same mel stage and
+reports them under "extras" (never as `value`): the headline in fp32 (the parity precision), the hybrid ConvVAE
+with 384-d lyrics (config[2]) and the genre-conditioned ConditionalVAE (config[3]), each bs=256 per GPU.
 """
 from __future__ import annotations
 
@@ -106,7 +110,63 @@ PROBE_KINDS = {
     8: ("linear", "gemm_nt DenseLoader (Linear fwd / dgrad)", "mfma"),
     16: ("linear_wgrad", "gemm_tn KRowDense (Linear weight gradient)", "mfma"),
     32: ("stft_mel", "stft_mel_kernel (STFT + mel)", "hbm"),
+    64: ("bn", "BatchNorm / reduction streaming family (bn_act, bn_bwd_moments, bn_bwd_apply, col_moments, "
+               "parts_fold, finalizers)", "hbm"),
 }
+
+
+WORKLOADS = {
+    "audio": "Convolutional_VAE audio-only (BASELINE config[1])",
+    "hybrid": "Convolutional_VAE hybrid, text_dim 384 (BASELINE config[2])",
+    "cvae": "Conditional_VAE genre-conditioned, latent 64, text_dim 768, 10 classes (BASELINE config[3])",
+}
+
+
+def build_workload(name, dtype, B, device, world, seed=42):
+    """Model (seed-42 init), fused Trainer and the synthetic side inputs (lyrics embeddings ~ N(0, 1/td), one-hot
+    genres) of one BASELINE workload at 128 x 128 mel."""
+    torch.manual_seed(seed)
+    g = torch.Generator(device=device).manual_seed(7)
+    text = cond = None
+    if name == "cvae":
+        model = hlmc_amd.ConditionalVAE(64, 768, 10, (128, 128), compute_dtype=dtype).to(device)
+        text = torch.randn(B, 768, device=device, generator=g) / 768 ** 0.5
+        cond = torch.nn.functional.one_hot(torch.randint(0, 10, (B,), device=device, generator=g), 10).float()
+    else:
+        model = hlmc_amd.HybridVAE(128, 384, (128, 128), audio_only=name == "audio", compute_dtype=dtype).to(device)
+        if name == "hybrid":
+            text = torch.randn(B, 384, device=device, generator=g) / 384 ** 0.5
+    trainer = hlmc_amd.Trainer(model, lr=1e-4, distributed=world > 1)
+    return model, trainer, text, cond
+
+
+def time_workload(name, dtype, B, device, world, mel, pcm, dist, steps=10, warmup=3):
+    """Whole-job clips/s of one extra workload (same mel stage, same timing protocol as the headline)."""
+    model, trainer, text, cond = build_workload(name, dtype, B, device, world)
+    for _ in range(warmup):
+        trainer.step(mel(pcm), text, cond)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sums = trainer.step(mel(pcm), text, cond)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    loss = trainer.loss_tuple(sums)[0]
+    out = {"workload": WORKLOADS[name], "dtype": dtype, "value": round(world * B * steps / el, 2), "unit": "clips/s",
+           "ms_per_step": round(1000 * el / steps, 4), "steps": steps, "warmup": warmup,
+           "params": sum(p.numel() for p in model.parameters()), "final_loss": round(loss, 3),
+           "finite": bool(np.isfinite(loss))}
+    del trainer, model
+    torch.cuda.empty_cache()
+    return out
 
 
 def probe_read(cap=4096):
@@ -135,15 +195,17 @@ def kind_roofline(kind, st):
 
 
 def pmc_traffic(kind):
-    """HBM bytes per launch of this kind from the committed rocprofv3 PMC summary (scripts/pmc_traffic.py:
-    2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes, per the gfx950 correction of MI355X_MICROARCH.md), or None."""
+    """HBM bytes per launch of this kind and its counter-based MFMA busy fraction from the committed rocprofv3
+    PMC summary (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes, per the gfx950 correction of
+    MI355X_MICROARCH.md; SQ_VALU_MFMA_BUSY_CYCLES over the dispatch's SIMD-cycles), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d["kinds"][PROBE_KINDS[kind][0]]["hbm_bytes_per_launch"], d.get("source")
+        e = d["kinds"][PROBE_KINDS[kind][0]]
+        return e.get("hbm_bytes_per_launch"), e.get("mfma_busy"), d.get("source")
     except (OSError, KeyError, ValueError):
-        return None, None
+        return None, None, None
 
 
 def host_cpu_share():
@@ -204,7 +266,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--workload", choices=["audio", "hybrid"], default="audio")
+    ap.add_argument("--workload", choices=["audio", "hybrid", "cvae"], default="audio")
+    ap.add_argument("--no-extras", action="store_true", help="skip the fp32 / hybrid / CVAE extra lines")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -238,20 +301,17 @@ def main():
     B = args.batch
     audio_only = args.workload == "audio"
     # ---- setup (untimed): model, optimizer state, scaler fit on a calibration batch
-    torch.manual_seed(42)
-    model = hlmc_amd.HybridVAE(128, 384, (128, 128), audio_only=audio_only, compute_dtype=args.dtype).to(device)
-    trainer = hlmc_amd.Trainer(model, lr=1e-4, distributed=world > 1)
     pcm = synthetic_pcm(B, N_SAMPLES, seed=1000 + rank, device=device)
-    text = (torch.randn(B, 384, device=device) / 384 ** 0.5) if not audio_only else None
     calib = hlmc_amd.extract_mel_spectrogram(pcm, fixed_time_steps=FRAMES)
     scaler = hlmc_amd.StandardScaler().fit(calib.reshape(B, -1))
     mel = MelStage(B, device, scaler)
-    prefetch = args.prefetch and not args.graph
+    model, trainer, text, cond = build_workload(args.workload, args.dtype, B, device, world)
+    prefetch = args.prefetch and not args.graph and args.workload != "cvae"
     pipe = MelPipeline(B, device, scaler) if prefetch else None
 
     def step():
         x = mel(pcm)
-        return trainer.step(x, text)
+        return trainer.step(x, text, cond)
 
     for _ in range(args.warmup):
         step()
@@ -269,7 +329,10 @@ def main():
                 r = kind_roofline(kind, st)
                 breakdown[r["op"]] = {"us_per_step": round(st["ms"] * 1e3, 1), "launches_per_step": st["launches"],
                                       "achieved": r["achieved"], "unit": r["unit"], "frac": r["frac"]}
-        dominant = max(PROBE_KINDS, key=lambda k: breakdown.get(PROBE_KINDS[k][0], {}).get("us_per_step", 0.0))
+        # the dominant single kernel (the BatchNorm family is 7 kernel types over ~96 launches per step: reported
+        # from this untimed calibration only — event pairs around all its launches would cost the timed steps ~2.5 %)
+        dominant = max((k for k in PROBE_KINDS if k != 64),
+                       key=lambda k: breakdown.get(PROBE_KINDS[k][0], {}).get("us_per_step", 0.0))
         # rehearse the timed probe once (untimed) so every event it records has been used before the clock starts
         L.check(L.lib().hlmc_probe_arm(dominant, 64 * min(args.steps, PROBE_STEPS)), "hlmc_probe_arm")
         for _ in range(min(args.steps, PROBE_STEPS)):
@@ -324,29 +387,40 @@ def main():
     loss = trainer.loss_tuple(sums)[0]
     if not np.isfinite(loss):
         raise SystemExit(f"non-finite loss {loss}")
+    params_of_headline = sum(p.numel() for p in model.parameters())
+    extras = {}
+    if not args.no_extras and args.workload == "audio" and args.dtype == "bf16" and args.batch == 256:
+        del trainer, model
+        torch.cuda.empty_cache()
+        for key, (wl, dt) in {"audio_fp32": ("audio", "fp32"), "hybrid_td384_bf16": ("hybrid", "bf16"),
+                              "cvae_bf16": ("cvae", "bf16")}.items():
+            extras[key] = time_workload(wl, dt, B, device, world, mel, pcm, dist)
 
     if rank == 0:
+        n_params = params_of_headline
         value = world * B * args.steps / elapsed
         ms = 1000 * elapsed / args.steps
-        flops_clip = 1.0668e9 if not audio_only else 1.0597e9   # fwd+bwd (FlopCounterMode)
+        # fwd+bwd FLOPs per clip (FlopCounterMode on the reference classes); CVAE not measured there
+        flops_clip = {"audio": 1.0597e9, "hybrid": 1.0668e9}.get(args.workload)
         rec = {"metric": "clips/sec mel+VAE train step, 128-mel x 128-frame, bs=256, 1/2/4/8 MI355X",
                "value": round(value, 2), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded sinusoid+noise PCM; random init)",
-               "config": {"workload": ("Convolutional_VAE audio-only (BASELINE config[1])" if audio_only else
-                                       "Convolutional_VAE hybrid, text_dim 384 (BASELINE config[2])") +
+               "config": {"workload": WORKLOADS[args.workload] +
                                       ": PCM[256,65024] -> HIP mel-dB 128x128 -> z-score -> VAE fwd+bwd+Adam",
-                          "per_gpu_batch": B, "global_batch": B * world, "mel": "128x128", "params": sum(
-                              p.numel() for p in model.parameters()), "parallelism": f"dp{world}", **({"backend": backend} if world > 1 else {}),
+                          "per_gpu_batch": B, "global_batch": B * world, "mel": "128x128", "params": n_params,
+                          "parallelism": f"dp{world}", **({"backend": backend} if world > 1 else {}),
                           "final_loss": round(loss, 3),
                           "execution": ("HIP graph replay of the whole step" if graphed else
                                         "eager launches; mel stage of step k+1 on its own stream during step k"
                                         if pipe is not None else "eager launches"),
-                          "step_mfma_frac": round(value / world * flops_clip / 1e12 / PEAK_BF16_TFLOPS, 4)}}
+                          "step_mfma_frac": (round(value / world * flops_clip / 1e12 / PEAK_BF16_TFLOPS, 4)
+                                             if flops_clip else None)}}
         if live is not None:
             roof = kind_roofline(dominant, live)
-            traffic, src = pmc_traffic(dominant)
+            traffic, mfma_busy, src = pmc_traffic(dominant)
             roof["traffic"] = traffic
+            roof["mfma_busy"] = mfma_busy
             roof["traffic_source"] = src
             roof["timing"] = (f"HIP events around each launch on its stream, inside the timed region "
                               + (f"(event nodes of the step graph; the {live['launches']} launches of the last "
@@ -357,6 +431,8 @@ def main():
                 roof["timing"] = probe_note
             roof["per_kind_untimed"] = breakdown  # concurrent streams: kernel times overlap
             rec["roofline"] = roof
+        if extras:
+            rec["extras"] = extras
         if not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline()
         print(json.dumps(rec), flush=True)

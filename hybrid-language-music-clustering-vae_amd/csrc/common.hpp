@@ -57,7 +57,7 @@ const char* get_error();
 // in the armed mask (hlmc_probe_arm) the launcher brackets its main kernel with a HIP event pair on the launch
 // stream.  Off (mask 0) it costs one branch per launch.
 namespace probe {
-enum : int { kConvS2 = 1, kSubpixel = 2, kWgradS2 = 4, kLinear = 8, kLinearWgrad = 16, kStftMel = 32 };
+enum : int { kConvS2 = 1, kSubpixel = 2, kWgradS2 = 4, kLinear = 8, kLinearWgrad = 16, kStftMel = 32, kBn = 64 };
 struct Site {
     int kind;
     double flops, bytes;

@@ -356,6 +356,7 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
     float bias[TN];
     int ncol[TN];
     float mu[TN], is[TN], ga[TN], be[TN];
+    float fs[TN], fq[TN];  // mode 2: this lane's <= 4 TM rows summed in f32, widened once below
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         ncol[j] = nb + j * 16 + (lane & 15);
@@ -363,6 +364,8 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
         bias[j] = ok ? ep.colbias(ncol[j]) : 0.f;
         cs[j] = 0.0;
         cq[j] = 0.0;
+        fs[j] = 0.f;
+        fq[j] = 0.f;
         if constexpr (EP::kStatMode == 2) {
             mu[j] = ok ? ep.mean[ncol[j]] : 0.f;
             is[j] = ok ? ep.invstd[ncol[j]] : 0.f;
@@ -390,10 +393,17 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
                     const float xh = (to_f32(ep.y[ro + ncol[j]]) - mu[j]) * is[j];
                     const float z = xh * ga[j] + be[j];
                     const float dz = v * (z > 0.f ? 1.f : 0.01f);
-                    cs[j] += dz;
-                    cq[j] += (double)dz * xh;
+                    fs[j] += dz;
+                    fq[j] = fmaf(dz, xh, fq[j]);
                 }
             }
+        }
+    }
+    if constexpr (EP::kStatMode == 2) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            cs[j] = fs[j];
+            cq[j] = fq[j];
         }
     }
 }

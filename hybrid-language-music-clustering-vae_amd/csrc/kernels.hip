@@ -292,6 +292,11 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
 #pragma unroll
         for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
         if (r + kUb * rpp < r1) fetch(r + kUb * rpp);
+        // the kUb rows of this step are added in f32, then once into the f64 accumulators (a per-element f64
+        // update made this pass FP64-bound: 1.6 TB/s against 4+ TB/s for the apply pass over the same operands)
+        float fa[V], fb[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) fa[v] = fb[v] = 0.f;
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t ru = r + u * rpp;
@@ -305,10 +310,12 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
                 float z = xh * ga[v] + be[v];
                 float dz = g[0][v] * act_grad(z, act);
                 if constexpr (kMask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
-                a[v] += dz;
-                b[v] += (double)dz * xh;
+                fa[v] += dz;
+                fb[v] = fmaf(dz, xh, fb[v]);
             }
         }
+#pragma unroll
+        for (int v = 0; v < V; ++v) { a[v] += fa[v]; b[v] += fb[v]; }
     }
     block_colsum<V>(a, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C);
     block_colsum<V>(b, tpr, C, s2, part + (int64_t)blockIdx.x * 2 * C + C);
@@ -371,6 +378,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
         for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
         if (r + kUb * rpp < r1) fetch(r + kUb * rpp);
+        float fa[V];  // this step's rows in f32, then once into the f64 accumulators
+#pragma unroll
+        for (int v = 0; v < V; ++v) fa[v] = 0.f;
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t ru = r + u * rpp;
@@ -390,8 +400,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
             store16_f32(dy + ru * C + c0, o);
             // the bias grad is the sum of the dy actually stored (rounded to T)
 #pragma unroll
-            for (int v = 0; v < V; ++v) a[v] += to_f32<T>(from_f32<T>(o[v]));
+            for (int v = 0; v < V; ++v) fa[v] += to_f32<T>(from_f32<T>(o[v]));
         }
+#pragma unroll
+        for (int v = 0; v < V; ++v) a[v] += fa[v];
     }
     block_colsum<V>(a, tpr, C, s1, part + (int64_t)blockIdx.x * C);
 }
@@ -406,6 +418,16 @@ __global__ __launch_bounds__(1024) void colsum_finalize_kernel(const double* __r
     if (threadIdx.x < 64 && ok) out[c] = (float)s;
 }
 
+// Live-probe site of one BatchNorm-family launch (kind kBn, HBM-bound): algorithmic bytes = tensor bytes it
+// must read + write (flops reported as 0)
+#define HLMC_BN_PROBED(s, bytes, launch)                  \
+    do {                                                  \
+        probe::site(probe::kBn, 0.0, (double)(bytes));    \
+        HLMC_PROBE_BEGIN(s);                              \
+        launch;                                           \
+        HLMC_PROBE_END(s);                                \
+    } while (0)
+
 // Fold a [nrows][ncols] partial table into scratch when it is large; returns the table the finalizers read.
 size_t fold_bytes(int ncols) { return (size_t)kFoldRows * ncols * sizeof(double); }
 struct Folded {
@@ -418,7 +440,8 @@ Folded fold_parts(hipStream_t s, const double* part, int nrows, int ncols, Ws ws
     const int rp = cdiv(nrows, G);
     G = cdiv(nrows, rp);
     double* out = reinterpret_cast<double*>(ws.p);
-    parts_fold_kernel<<<dim3(cdiv(ncols, 64), G), 256, 0, s>>>(part, nrows, ncols, rp, out);
+    HLMC_BN_PROBED(s, 8.0 * ((double)nrows + G) * ncols,
+                   (parts_fold_kernel<<<dim3(cdiv(ncols, 64), G), 256, 0, s>>>(part, nrows, ncols, rp, out)));
     return Folded{out, G};
 }
 inline unsigned fin_grid(int C) { return (unsigned)cdiv(C, 64); }
@@ -910,10 +933,13 @@ int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* in
     const int nblk = bn_blocks(R, C);
     HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
     double* part = reinterpret_cast<double*>(ws.p);
-    col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), part);
+    HLMC_BN_PROBED(s, (double)sizeof(T) * R * C + 16.0 * nblk * C,
+                   (col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), part)));
     HLMC_LAUNCHED();
     const Folded f = fold_parts(s, part, nblk, 2 * C, ws_from(ws, bn_fold_off(R, C)));
-    bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
+    HLMC_BN_PROBED(s, 16.0 * f.rows * C,
+                   (bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, R, mean, invstd, run_mean, run_var,
+                                                                    nbt, momentum, eps)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -922,7 +948,9 @@ int bn_stats_from_parts(hipStream_t s, const double* part, int nparts, int64_t R
                         float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, Ws fold) {
     HLMC_CHECK_ARG(part && nparts > 0 && R > 0, "bn_stats_from_parts arguments");
     const Folded f = fold_parts(s, part, nparts, 2 * C, fold);
-    bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
+    HLMC_BN_PROBED(s, 16.0 * f.rows * C,
+                   (bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, R, mean, invstd, run_mean, run_var,
+                                                                    nbt, momentum, eps)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -940,10 +968,13 @@ int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const
     HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act: output row stride must be a multiple of 16 bytes");
     const int rpp = kThreads / (C / Vec16<T>::N);
     const unsigned g = grid_for(R, rpp * kU);
+    const double by = 2.0 * sizeof(T) * R * C;
     if (mask)
-        bn_act_kernel<T, true><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
+        HLMC_BN_PROBED(s, by, (bn_act_kernel<T, true><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask,
+                                                                            mscale, a, lda)));
     else
-        bn_act_kernel<T, false><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
+        HLMC_BN_PROBED(s, by, (bn_act_kernel<T, false><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act,
+                                                                             mask, mscale, a, lda)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -963,24 +994,29 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
     if (fused && fused->nparts > 0) {  // moments came with the producing GEMM's epilogue
         HLMC_CHECK_ARG(lda == C && !mask && act == 0, "bn_act_bwd: fused moments need a dense lrelu layer");
         const Folded f = fold_parts(s, fused->part, fused->nparts, 2 * C, fw);
-        bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums);
+        HLMC_BN_PROBED(s, 16.0 * f.rows * C,
+                       (bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums)));
         HLMC_LAUNCHED();
     } else {
         auto k = mask ? bn_bwd_moments_kernel<T, true> : bn_bwd_moments_kernel<T, false>;
-        k<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb, part);
+        HLMC_BN_PROBED(s, 2.0 * sizeof(T) * R * C + 16.0 * nblk * C,
+                       (k<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb,
+                                                    part)));
         HLMC_LAUNCHED();
         const Folded f = fold_parts(s, part, nblk, 2 * C, fw);
-        bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums);
+        HLMC_BN_PROBED(s, 16.0 * f.rows * C,
+                       (bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums)));
         HLMC_LAUNCHED();
     }
     double* bpart = bias_part ? bias_part : part;
     auto ka = mask ? bn_bwd_apply_kernel<T, true> : bn_bwd_apply_kernel<T, false>;
-    ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
-                                                     dy, rpb, bpart);
+    HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C + 8.0 * nblk * C,
+                   (ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
+                                                 dy, rpb, bpart)));
     HLMC_LAUNCHED();
     if (dbias && !bias_part) {
         const Folded f = fold_parts(s, part, nblk, C, fw);
-        colsum_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dbias);
+        HLMC_BN_PROBED(s, 8.0 * f.rows * C, (colsum_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dbias)));
         HLMC_LAUNCHED();
     }
     return HLMC_OK;
@@ -989,7 +1025,7 @@ int bn_bias_parts(int64_t R, int C) { return bn_blocks(R, C); }
 int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out, Ws fold) {
     HLMC_CHECK_ARG(part && out && nparts > 0 && C > 0, "colsum_finalize: bad arguments");
     const Folded f = fold_parts(s, part, nparts, C, fold);
-    colsum_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, out);
+    HLMC_BN_PROBED(s, 8.0 * f.rows * C, (colsum_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, out)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

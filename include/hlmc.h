@@ -177,7 +177,8 @@ int hlmc_net_bucket_wait(hlmc_net* net, int k, void* stream);
 
 /* ============================================================== live kernel timing (measurement only)
  * Arm: launches of the op kinds in `mask` (1 conv_s2 GEMM, 2 sub-pixel GEMM, 4 conv weight-gradient GEMM,
- * 8 linear GEMM, 16 linear weight-gradient GEMM, 32 STFT-mel) are bracketed by HIP events on their launch
+ * 8 linear GEMM, 16 linear weight-gradient GEMM, 32 STFT-mel, 64 BatchNorm / reduction streaming family) are
+ * bracketed by HIP events on their launch
  * stream (up to max_launches; their algorithmic flops / bytes are summed).  Read: synchronises on the last
  * event, returns the count, the summed kernel time and work (and per-launch ms into ms_each[cap_each]), and
  * disarms.  bench.py uses this for the roofline of its dominant kernel inside the timed region. */

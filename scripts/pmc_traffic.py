@@ -1,12 +1,16 @@
 """HBM traffic per launch of every probed kernel kind from rocprofv3 PMC passes over bench.py, and the
 rocprofv3 kernel-trace average duration of the same kinds (the check on bench.py's live HIP-event timing).
 
-    python scripts/pmc_traffic.py OUT_JSON FETCH_DIR WRITE_DIR TRACE_DIR [--steps N]
+    python scripts/pmc_traffic.py OUT_JSON FETCH_DIR WRITE_DIR TRACE_DIR [MFMA_DIR]
 
 FETCH_DIR / WRITE_DIR: `rocprofv3 --kernel-trace --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` output directories;
 TRACE_DIR: a `--kernel-trace --stats` run of the bench command.  HBM bytes per dispatch =
 (2 x FETCH_SIZE + WRITE_SIZE) x 1024: rocprofv3 reports both in KiB, and on gfx950 FETCH_SIZE counts half the
 bytes of 16-B-per-lane streaming reads (/opt/skills/guides/MI355X_MICROARCH.md, HBM section).
+MFMA_DIR (optional): a `--kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE` pass.
+MFMA busy per dispatch = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the MFMA-unit cycles
+(MI355X_MICROARCH.md: "counts cycles") over the SIMD-cycles of the dispatch (GRBM_GUI_ACTIVE is summed over
+the 8 XCDs; 256 CUs x 4 SIMDs), i.e. the fraction of the dense MFMA peak the kernel's MFMAs occupy.
 """
 import csv
 import glob
@@ -21,6 +25,8 @@ KINDS = {  # op kind of include/hlmc.h hlmc_probe_arm -> kernel-name pattern
     "linear": r"gemm_nt\w*<[^<>]*, hlmc::DenseLoader<",
     "linear_wgrad": r"gemm_tn_kernel<[^<>]*, hlmc::(\(anonymous namespace\)::)?KRowDenseV?<[^<>]*>, hlmc::(\(anonymous namespace\)::)?KRowDenseV?<",
     "stft_mel": r"stft_mel_kernel",
+    "bn": r"(bn_act_kernel|bn_bwd_moments_kernel|bn_bwd_apply_kernel|col_moments_kernel|parts_fold_kernel|"
+          r"bn_finalize_kernel|bn_bwd_finalize_kernel|colsum_finalize_kernel)",
 }
 
 
@@ -56,9 +62,14 @@ def trace_avg(d):
 
 def main():
     out, fdir, wdir, tdir = sys.argv[1:5]
+    mdir = sys.argv[5] if len(sys.argv) > 5 else None
     fetch, nf = counters(fdir, "FETCH_SIZE")
     write, nw = counters(wdir, "WRITE_SIZE")
     tr = trace_avg(tdir)
+    mf, gr, nm = {}, {}, {}
+    if mdir:
+        mf, nm = counters(mdir, "SQ_VALU_MFMA_BUSY_CYCLES")
+        gr, _ = counters(mdir, "GRBM_GUI_ACTIVE")
     kinds = {}
     for k in KINDS:
         e = {}
@@ -70,6 +81,11 @@ def main():
         if k in tr:
             e["trace_avg_us"] = round(tr[k][0], 2)
             e["trace_dispatches"] = tr[k][1]
+        if k in mf and gr.get(k):
+            e["mfma_busy_cycles"] = round(mf[k], 1)
+            e["grbm_gui_active"] = round(gr[k], 1)
+            e["mfma_busy"] = round(mf[k] / (gr[k] / 8.0 * 1024.0), 4)
+            e["mfma_dispatches"] = nm[k]
         if e:
             kinds[k] = e
     res = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py ({fdir}, {wdir}); "

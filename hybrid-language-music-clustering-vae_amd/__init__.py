@@ -11,6 +11,8 @@ Drop-in surface (reference names):
   normalized_mutual_info_score / calculate_purity   (the sklearn.metrics evaluation calls)
   Adam                                         (torch.optim.Adam of the train loops)
   Trainer                                      (fused train step + RCCL data parallel)
+  pipeline.run_pipeline                        (BASELINE config[4]: 30 s clips -> mel -> scaler -> ConvVAE train ->
+                                                latents -> KMeans, resident in HBM)
 All compute runs in libhlmc.so (hand-written HIP for gfx950); see include/hlmc.h.
 """
 from . import _lib
@@ -24,6 +26,7 @@ from .losses import cvae_loss_function, loss_function, vae_loss
 from .models import VAE, ConditionalVAE, HybridVAE
 from .optim import Adam
 from .train import GraphedStep, Trainer
+from . import pipeline
 
 __all__ = ["HybridVAE", "ConditionalVAE", "VAE", "loss_function", "cvae_loss_function", "vae_loss", "melspectrogram",
            "power_to_db", "mfcc", "extract_mel_spectrogram", "mean_std_pool", "mel_filterbank", "StandardScaler",

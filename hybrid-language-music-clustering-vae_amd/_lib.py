@@ -78,6 +78,8 @@ _SIGS = {
     "hlmc_km_sqdist_rows": (c_int, [c_vp, c_vp, c_i64, c_int, P_i64, c_int, c_vp]),
     "hlmc_km_assign": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
     "hlmc_km_sums": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp]),
+    "hlmc_km_sums_workspace": (c_i64, [c_i64, c_int]),
+    "hlmc_km_sums_part": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_i64]),
     "hlmc_km_rowdist": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),
     "hlmc_km_inertia": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
     "hlmc_silhouette_workspace": (c_i64, [c_i64, c_int]),

@@ -122,6 +122,9 @@ class KMeans:
         pack = torch.empty(k * d + k + 1, dtype=torch.float32, device=dev)
         sums, wts = pack[:k * d], pack[k * d:k * d + k]
         changed = pack[k * d + k:].view(torch.int32)
+        # M-step workspace: per-tile cluster histograms + bases, cluster offsets, the label-partitioned row list
+        ws_bytes = int(L.lib().hlmc_km_sums_workspace(n, k))
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         old_c = centers.cpu().numpy()
         strict = False
         it = 0
@@ -129,8 +132,8 @@ class KMeans:
             changed.zero_()
             L.check(L.lib().hlmc_km_assign(L.stream(), Xc.data_ptr(), n, d, centers.data_ptr(), k,
                                            labels_new.data_ptr(), labels.data_ptr(), changed.data_ptr()))
-            L.check(L.lib().hlmc_km_sums(L.stream(), Xc.data_ptr(), n, d, labels_new.data_ptr(), k, sums.data_ptr(),
-                                         wts.data_ptr()))
+            L.check(L.lib().hlmc_km_sums_part(L.stream(), Xc.data_ptr(), n, d, labels_new.data_ptr(), k,
+                                              sums.data_ptr(), wts.data_ptr(), ws.data_ptr(), ws_bytes))
             pack_h = pack.cpu().numpy()
             new = pack_h[:k * d].reshape(k, d)
             wic = pack_h[k * d:k * d + k]

@@ -348,6 +348,11 @@ int hlmc_km_assign(void* stream, const float* X, int64_t n, int d, const float* 
 int hlmc_km_sums(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sums, float* w) {
     return km::sums(S(stream), X, n, d, labels, k, sums, w);
 }
+int64_t hlmc_km_sums_workspace(int64_t n, int k) { return (int64_t)km::sums_ws(n, k); }
+int hlmc_km_sums_part(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sums,
+                      float* w, void* ws, int64_t ws_bytes) {
+    return km::sums_part(S(stream), X, n, d, labels, k, sums, w, ws, (size_t)ws_bytes);
+}
 int hlmc_km_inertia(void* stream, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out,
                     float* tmp) {
     return km::inertia(S(stream), X, n, d, C, labels, out, tmp);

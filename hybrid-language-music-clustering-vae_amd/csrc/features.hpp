@@ -57,6 +57,9 @@ int sqdist_rows(hipStream_t s, const float* X, int64_t n, int d, const int64_t* 
 int assign(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, int32_t* labels, const int32_t* old,
            int32_t* n_changed);
 int sums(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w);
+size_t sums_ws(int64_t n, int k);
+int sums_part(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w,
+              void* ws, size_t ws_bytes);
 int inertia(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out,
             float* tmp);
 int rowdist(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out);

@@ -11,55 +11,6 @@
 namespace hlmc {
 namespace {
 
-// X.mean(axis=0) in numpy: sequential float32 row accumulation, then / n; Xc = X - mean.
-// np.var(X, axis=0): sequential float32 sum of (x - mean)^2, then / n (sklearn's tolerance input).
-// One block (4 waves) per 64 columns: all 4 waves load a 256-row group (64 rows each, all loads in flight,
-// the next group prefetched in registers) into LDS; wave 0 adds the group in row order, one float32
-// accumulator per column.
-constexpr int kCmRows = 256;
-__global__ __launch_bounds__(256) void km_colmean_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                         float* __restrict__ mean, float* __restrict__ var) {
-    __shared__ float tile[kCmRows][64];
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int c = blockIdx.x * 64 + l;
-    const float* __restrict__ Xc = X + (c < d ? c : d - 1);
-    float m = 0.f;
-    for (int pass = 0; pass < (var ? 2 : 1); ++pass) {
-        float acc = 0.f;
-        float v[64];
-#pragma unroll
-        for (int t = 0; t < 64; ++t) v[t] = Xc[min((int64_t)(w * 64 + t), n - 1) * d];
-        for (int64_t g = 0; g < n; g += kCmRows) {
-            __syncthreads();
-#pragma unroll
-            for (int t = 0; t < 64; ++t) tile[w * 64 + t][l] = v[t];
-            __syncthreads();
-            if (g + kCmRows < n) {
-#pragma unroll
-                for (int t = 0; t < 64; ++t) v[t] = Xc[min(g + kCmRows + w * 64 + t, n - 1) * d];
-            }
-            if (w == 0) {
-                const int rows = (int)min((int64_t)kCmRows, n - g);
-                if (pass == 0) {
-#pragma unroll 8
-                    for (int r = 0; r < rows; ++r) acc += tile[r][l];
-                } else {
-#pragma unroll 8
-                    for (int r = 0; r < rows; ++r) {
-                        const float e = tile[r][l] - m;
-                        acc += e * e;
-                    }
-                }
-            }
-        }
-        if (pass == 0) {
-            m = acc / (float)n;
-            if (w == 0 && c < d) mean[c] = m;
-        } else if (w == 0 && c < d) {
-            var[c] = acc / (float)n;
-        }
-    }
-}
 __global__ void km_sub_kernel(const float* __restrict__ X, int64_t n, int d, const float* __restrict__ mean,
                               float* __restrict__ Xc) {
     const int64_t tot = n * d;
@@ -314,6 +265,222 @@ __global__ __launch_bounds__(64) void km_sums_kernel(const float* __restrict__ X
     if (blockIdx.x == 0 && lane == 0) weight[j] = (float)count;
 }
 
+// ---- M-step via a stable partition of the rows by label (row order kept inside every cluster), then one
+// block per (64-column slab, cluster) walking the cluster's contiguous row list.  The sum is a serial float32
+// chain per column (sklearn's single-thread order), so the block is a producer/consumer ring: 15 loader waves
+// gather 64-row chunks (one row per load instruction, 64 in flight per lane) into an 8-slot LDS ring and wave 0
+// adds the slots in chunk order, handing slots back through LDS flags -- the add chain never waits on HBM.
+constexpr int kPartTile = 1024;   // rows per partition tile (one wave, 16 chunks of 64)
+// lanes holding the same label as this lane, from one ballot per label bit (no loop over the clusters)
+__device__ __forceinline__ uint64_t km_same_label(int lab, int nbits, bool valid) {
+    uint64_t eq = __ballot(valid);
+    for (int bit = 0; bit < nbits; ++bit) {
+        const uint64_t m = __ballot(valid && ((lab >> bit) & 1));
+        eq &= ((lab >> bit) & 1) ? m : ~m;
+    }
+    return eq;
+}
+// hist[tile][c] = rows of cluster c in the tile
+__global__ __launch_bounds__(64) void km_part_hist_kernel(const int32_t* __restrict__ labels, int n, int k, int nbits,
+                                                          int* __restrict__ hist) {
+    extern __shared__ int cnt[];  // [k]
+    const int lane = threadIdx.x, tile = blockIdx.x;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int c = lane; c < k; c += 64) cnt[c] = 0;
+    int lab[kPartTile / 64];
+#pragma unroll
+    for (int q = 0; q < kPartTile / 64; ++q) {
+        const int row = tile * kPartTile + q * 64 + lane;
+        lab[q] = row < n ? labels[row] : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPartTile / 64; ++q) {
+        const bool valid = lab[q] >= 0;
+        const uint64_t eq = km_same_label(lab[q], nbits, valid);
+        if (valid && (eq & lt) == 0) atomicAdd(&cnt[lab[q]], __popcll(eq));   // one add per label, no return
+    }
+    __syncthreads();
+    for (int c = lane; c < k; c += 64) hist[(int64_t)tile * k + c] = cnt[c];
+}
+// base[tile][c] = (rows of clusters < c) + (rows of cluster c in tiles < tile); off[c] = first row of cluster c.
+// 16 waves: per cluster a wave-level scan over the tiles (no block barriers inside), cluster totals in LDS.
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+__global__ __launch_bounds__(1024) void km_part_scan_kernel(const int* __restrict__ hist, int tiles, int k,
+                                                            int* __restrict__ base, int* __restrict__ off) {
+    extern __shared__ int tot[];  // [k + 1]
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (int c = wave; c < k; c += 16) {
+        int run = 0;
+        for (int t0 = 0; t0 < tiles; t0 += 64) {
+            const int v = (t0 + lane < tiles) ? hist[(int64_t)(t0 + lane) * k + c] : 0;
+            run += __shfl(wave_incl_scan(v, lane), 63, 64);
+        }
+        if (lane == 0) tot[c] = run;
+    }
+    __syncthreads();
+    if (wave == 0) {   // exclusive scan of the cluster totals
+        int run = 0;
+        for (int c0 = 0; c0 < k; c0 += 64) {
+            const int v = (c0 + lane < k) ? tot[c0 + lane] : 0;
+            const int inc = wave_incl_scan(v, lane);
+            if (c0 + lane < k) {
+                off[c0 + lane] = run + inc - v;
+                tot[c0 + lane] = run + inc - v;
+            }
+            run += __shfl(inc, 63, 64);
+        }
+        if (lane == 0) off[k] = run;
+    }
+    __syncthreads();
+    for (int c = wave; c < k; c += 16) {
+        int run = tot[c];
+        for (int t0 = 0; t0 < tiles; t0 += 64) {
+            const int v = (t0 + lane < tiles) ? hist[(int64_t)(t0 + lane) * k + c] : 0;
+            const int inc = wave_incl_scan(v, lane);
+            if (t0 + lane < tiles) base[(int64_t)(t0 + lane) * k + c] = run + inc - v;
+            run += __shfl(inc, 63, 64);
+        }
+    }
+}
+// order[base[tile][c] + rank] = row, rank = rows of cluster c before it in the tile (ballot prefix, row order)
+__global__ __launch_bounds__(64) void km_part_scatter_kernel(const int32_t* __restrict__ labels, int n, int k,
+                                                             int nbits, const int* __restrict__ base,
+                                                             int* __restrict__ order) {
+    extern __shared__ int cur[];  // [k] next free position per cluster
+    const int lane = threadIdx.x, tile = blockIdx.x;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int c = lane; c < k; c += 64) cur[c] = base[(int64_t)tile * k + c];
+    int lab[kPartTile / 64];
+#pragma unroll
+    for (int q = 0; q < kPartTile / 64; ++q) {
+        const int row = tile * kPartTile + q * 64 + lane;
+        lab[q] = row < n ? labels[row] : -1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPartTile / 64; ++q) {
+        const bool valid = lab[q] >= 0;
+        const uint64_t eq = km_same_label(lab[q], nbits, valid);
+        const int b0 = valid ? cur[lab[q]] : 0;
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): every lane's read of cur[] returned (one wave)
+        if (valid && (eq & lt) == 0) cur[lab[q]] = b0 + __popcll(eq);
+        if (valid) order[b0 + __popcll(eq & lt)] = tile * kPartTile + q * 64 + lane;
+    }
+}
+constexpr int kRingSlots = 8, kRingLoaders = 15, kRingPitch = 68;   // slot [column][row], rows padded to 68
+__device__ __forceinline__ int lds_acquire(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// kMode 0: cluster j = blockIdx.y, entries order[off[j] .. off[j+1]) -> out0[j][c] = sum, out1[j] = count.
+// kMode 1: all n rows in order, one pass (out1 == nullptr) or two -> out0[c] = X.mean(axis=0) and
+// out1[c] = np.var(X, axis=0) (numpy: sequential float32 sums, / n; the second pass adds (x - mean)^2).
+template <int kMode>
+__global__ __launch_bounds__(64 * (kRingLoaders + 1)) void km_ring_kernel(
+    const float* __restrict__ X, int n, int d, const int* __restrict__ order, const int* __restrict__ off,
+    float* __restrict__ out0, float* __restrict__ out1) {
+    // [slot][column][row]: a lane's 64 rows of its column are contiguous (b128 writes and reads; the 68-float
+    // pitch puts 16 consecutive lanes' 16-byte accesses in distinct banks), 139 KB
+    __shared__ __align__(16) float ring[kRingSlots][64][kRingPitch];
+    __shared__ int ready[kRingSlots];            // chunk held by the slot (-1: none yet)
+    __shared__ int done;                         // chunks the adder has consumed
+    const int j = blockIdx.y;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+    const int c = blockIdx.x * 64 + l;
+    const float* __restrict__ Xc = X + (c < d ? c : d - 1);
+    const int r0 = kMode == 0 ? off[j] : 0, m = kMode == 0 ? off[j + 1] - r0 : n;
+    const int nch = (m + 63) / 64;
+    const int total = (kMode == 1 && out1) ? 2 * nch : nch;   // chunk ch covers entries (ch % nch) * 64 + 0..63
+    if (threadIdx.x < kRingSlots) ready[threadIdx.x] = -1;
+    if (threadIdx.x == 0) done = 0;
+    __syncthreads();   // the only block-wide barrier: every wave reaches it before the roles split
+    if (w == 0) {
+        float acc = 0.f, mean = 0.f;
+        for (int ch = 0; ch < total; ++ch) {
+            const int s = ch % kRingSlots;
+            const bool sq = kMode == 1 && ch >= nch;
+            if (kMode == 1 && ch == nch) {   // pass 2 of X.mean / np.var
+                mean = acc / (float)m;
+                acc = 0.f;
+            }
+            auto add = [&](float x) {
+                if (sq) {
+                    const float e = x - mean;
+                    acc = __fadd_rn(acc, __fmul_rn(e, e));
+                } else {
+                    acc += x;
+                }
+            };
+            while (lds_acquire(&ready[s]) != ch) __builtin_amdgcn_s_sleep(1);
+            const float4* col = reinterpret_cast<const float4*>(&ring[s][l][0]);
+            const int e0 = (ch % nch) * 64;
+            if (e0 + 64 <= m) {
+                float4 q[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) q[r] = col[r];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    add(q[r].x);
+                    add(q[r].y);
+                    add(q[r].z);
+                    add(q[r].w);
+                }
+            } else {
+                const float* cf = &ring[s][l][0];
+                for (int r = 0; r < m - e0; ++r) add(cf[r]);
+            }
+            if (l == 0) lds_release(&done, ch + 1);
+        }
+        if (kMode == 0) {
+            if (c < d) out0[(int64_t)j * d + c] = acc;
+            if (blockIdx.x == 0 && l == 0) out1[j] = (float)m;
+        } else if (c < d) {
+            if (out1) {
+                out0[c] = mean;
+                out1[c] = acc / (float)m;
+            } else {
+                out0[c] = acc / (float)m;
+            }
+        }
+        return;
+    }
+    // loader w - 1: chunks w - 1, w - 1 + 15, ...; entries past the list end re-read its last row (never added)
+    auto row_of = [&](int ch) {
+        const int e = min((ch % nch) * 64 + l, m - 1);
+        return kMode == 0 ? order[r0 + e] : e;
+    };
+    int ch = w - 1;
+    if (ch >= total) return;
+    float v[64];
+    int idx = row_of(ch);
+#pragma unroll
+    for (int t = 0; t < 64; ++t) v[t] = Xc[(int64_t)__builtin_amdgcn_readlane(idx, t) * d];
+    for (; ch < total; ch += kRingLoaders) {
+        const int nx = ch + kRingLoaders;
+        if (nx < total) idx = row_of(nx);
+        const int s = ch % kRingSlots;
+        while (lds_acquire(&done) < ch - kRingSlots + 1) __builtin_amdgcn_s_sleep(1);   // slot's last chunk added
+        float4* col = reinterpret_cast<float4*>(&ring[s][l][0]);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) col[t] = make_float4(v[4 * t], v[4 * t + 1], v[4 * t + 2], v[4 * t + 3]);
+        if (l == 0) lds_release(&ready[s], ch);
+        if (nx < total) {
+#pragma unroll
+            for (int t = 0; t < 64; ++t) v[t] = Xc[(int64_t)__builtin_amdgcn_readlane(idx, t) * d];
+        }
+    }
+}
+
 // _euclidean_dense_dense(squared=True): float32 sum of 4-element groups, then the tail
 __global__ void km_rowdist_kernel(const float* __restrict__ X, int64_t n, int d, const float* __restrict__ C,
                                   const int32_t* __restrict__ labels, float* __restrict__ out) {
@@ -337,7 +504,7 @@ __global__ void km_rowdist_kernel(const float* __restrict__ X, int64_t n, int d,
 // float32 sum of v[0..n) in index order: one wave stages 1024 values per round in LDS (coalesced loads,
 // the next round prefetched in registers); lane 0 adds them sequentially from LDS.
 __global__ __launch_bounds__(64) void km_seqsum_kernel(const float* __restrict__ v, int64_t n, float* out) {
-    __shared__ float buf[64 * kLabQ];
+    __shared__ __align__(16) float buf[64 * kLabQ];
     const int lane = threadIdx.x;
     float cur[kLabQ], nxt[kLabQ];
 #pragma unroll
@@ -358,7 +525,21 @@ __global__ __launch_bounds__(64) void km_seqsum_kernel(const float* __restrict__
         __syncthreads();
         if (lane == 0) {
             const int m = (int)((n - base) < 64 * kLabQ ? (n - base) : 64 * kLabQ);
-            for (int t = 0; t < m; ++t) s += buf[t];
+            int t = 0;
+            // 64 values per batch: 16 b128 reads in flight, then the in-order adds
+            for (; t + 64 <= m; t += 64) {
+                float4 q[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) q[r] = reinterpret_cast<const float4*>(buf + t)[r];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    s += q[r].x;
+                    s += q[r].y;
+                    s += q[r].z;
+                    s += q[r].w;
+                }
+            }
+            for (; t < m; ++t) s += buf[t];
         }
         __syncthreads();
 #pragma unroll
@@ -373,7 +554,9 @@ namespace km {
 
 int center(hipStream_t s, const float* X, int64_t n, int d, float* mean, float* var, float* Xc) {
     HLMC_CHECK_ARG(X && mean && Xc && n > 0 && d > 0, "bad km_center arguments");
-    km_colmean_kernel<<<(d + 63) / 64, 256, 0, s>>>(X, n, d, mean, var);
+    HLMC_CHECK_ARG(n < (int64_t)1 << 30, "km_center: n too large");
+    km_ring_kernel<1><<<(unsigned)((d + 63) / 64), 64 * (kRingLoaders + 1), 0, s>>>(X, (int)n, d, nullptr, nullptr,
+                                                                                   mean, var);
     HLMC_LAUNCHED();
     km_sub_kernel<<<(unsigned)std::min<int64_t>(8192, (n * d + 255) / 256), 256, 0, s>>>(X, n, d, mean, Xc);
     HLMC_LAUNCHED();
@@ -408,6 +591,37 @@ int sums(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels,
     HLMC_CHECK_ARG(X && labels && sm && w && k > 0, "bad km_sums arguments");
     HLMC_CHECK_ARG(n > 0 && n < (int64_t)1 << 30 && d > 0 && k <= 65535, "bad km_sums sizes");
     km_sums_kernel<<<dim3((unsigned)((d + 63) / 64), (unsigned)k), 64, 0, s>>>(X, (int)n, d, labels, k, sm, w);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+constexpr int64_t kPartMinRows = 4096;
+size_t sums_ws(int64_t n, int k) {
+    const int64_t tiles = (n + kPartTile - 1) / kPartTile;
+    return (size_t)(2 * tiles * k + (k + 1) + n) * sizeof(int) + 256;
+}
+int sums_part(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w,
+              void* ws, size_t ws_bytes) {
+    HLMC_CHECK_ARG(X && labels && sm && w && ws && k > 0 && d > 0, "bad km_sums_part arguments");
+    HLMC_CHECK_ARG(n > 0 && n < (int64_t)1 << 30 && k <= 8192, "bad km_sums_part sizes");
+    HLMC_CHECK_ARG(ws_bytes >= sums_ws(n, k), "km_sums_part workspace too small");
+    if (n <= kPartMinRows) return sums(s, X, n, d, labels, k, sm, w);   // one pass beats four launches here
+    const int tiles = (int)((n + kPartTile - 1) / kPartTile);
+    int* hist = reinterpret_cast<int*>(ws);
+    int* base = hist + (int64_t)tiles * k;
+    int* off = base + (int64_t)tiles * k;
+    int* order = off + (k + 1);
+    const size_t klds = (size_t)k * sizeof(int);
+    int nbits = 0;
+    while ((1 << nbits) < k) ++nbits;
+    km_part_hist_kernel<<<tiles, 64, klds, s>>>(labels, (int)n, k, nbits, hist);
+    HLMC_LAUNCHED();
+    km_part_scan_kernel<<<1, 1024, klds + sizeof(int), s>>>(hist, tiles, k, base, off);
+    HLMC_LAUNCHED();
+    km_part_scatter_kernel<<<tiles, 64, klds, s>>>(labels, (int)n, k, nbits, base, order);
+    HLMC_LAUNCHED();
+    km_ring_kernel<0><<<dim3((unsigned)((d + 63) / 64), (unsigned)k), 64 * (kRingLoaders + 1), 0, s>>>(
+        X, (int)n, d, order, off, sm, w);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

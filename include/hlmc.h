@@ -223,6 +223,12 @@ int hlmc_km_assign(void* stream, const float* X, int64_t n, int d, const float* 
 /* M-step sums in index order (float32, as sklearn's single-thread loop): sums [k][d], weight [k] */
 int hlmc_km_sums(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sums,
                  float* weight);
+/* The same sums through a stable partition of the rows by label (device workspace of
+ * hlmc_km_sums_workspace(n, k) bytes): the rows of each cluster become one contiguous list in row order and
+ * one block per (64-column slab, cluster) gathers 256-row groups into LDS and adds them in order (k <= 4096). */
+int64_t hlmc_km_sums_workspace(int64_t n, int k);
+int hlmc_km_sums_part(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sums,
+                      float* weight, void* ws, int64_t ws_bytes);
 /* per-row ||x_i - c_{l_i}||^2 in sklearn's _euclidean_dense_dense float32 order -> out [n] */
 int hlmc_km_rowdist(void* stream, const float* X, int64_t n, int d, const float* centers, const int32_t* labels,
                     float* out);

@@ -2,7 +2,7 @@
 latent-like blobs [N, D] f32, the reference's call (src/Convolutional_VAE.py:317-319, cfg 5 at N=100k).
 
 Prints one JSON line per case: whole-fit wall time, Lloyd iterations run (all restarts), and the E-step
-(hlmc_km_assign) and M-step (hlmc_km_sums) kernels timed alone with HIP events on the launch stream,
+(hlmc_km_assign) and M-step (hlmc_km_sums direct, hlmc_km_sums_part partitioned -- the fit's) kernels timed alone with HIP events on the launch stream,
 each against the HBM roofline (algorithmic bytes per launch = N*D*4 read + N*4 labels written / read).
 sklearn (threadpool default) is timed beside it where it finishes in seconds."""
 import json
@@ -69,6 +69,13 @@ def case(n, d, k, n_init, sklearn_too):
                                                             sums.data_ptr(), wts.data_ptr())))
     heavy_us = _time_kernel(lambda: L.check(lib.hlmc_km_sums(L.stream(), Xd.data_ptr(), n, d, heavy.data_ptr(), k,
                                                              sums.data_ptr(), wts.data_ptr())))
+    nb = int(lib.hlmc_km_sums_workspace(n, k))
+    ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    part_us = _time_kernel(lambda: L.check(lib.hlmc_km_sums_part(L.stream(), Xd.data_ptr(), n, d, lab.data_ptr(), k,
+                                                                 sums.data_ptr(), wts.data_ptr(), ws.data_ptr(), nb)))
+    part_heavy_us = _time_kernel(lambda: L.check(lib.hlmc_km_sums_part(L.stream(), Xd.data_ptr(), n, d,
+                                                                       heavy.data_ptr(), k, sums.data_ptr(),
+                                                                       wts.data_ptr(), ws.data_ptr(), nb)))
     a_bytes = n * d * 4 + 2 * n * 4
     s_bytes = n * d * 4 + n * 4
     out = {"case": f"N={n} D={d} k={k} n_init={n_init}", "fit_ms": round(fit_ms, 2), "lloyd_iters": iters,
@@ -77,7 +84,9 @@ def case(n, d, k, n_init, sklearn_too):
            "assign_frac": round(a_bytes / assign_us / 1e3 / HBM_PEAK_GBS, 4),
            "sums_us": round(sums_us, 2), "sums_GBs": round(s_bytes / sums_us / 1e3, 1),
            "sums_frac": round(s_bytes / sums_us / 1e3 / HBM_PEAK_GBS, 4),
-           "sums_one_cluster_us": round(heavy_us, 2)}
+           "sums_one_cluster_us": round(heavy_us, 2),
+           "sums_part_us": round(part_us, 2), "sums_part_frac": round(s_bytes / part_us / 1e3 / HBM_PEAK_GBS, 4),
+           "sums_part_one_cluster_us": round(part_heavy_us, 2)}
     if sklearn_too:
         from sklearn.cluster import KMeans as SK
         t0 = time.perf_counter()

@@ -85,20 +85,33 @@ def test_kmeans_restarts_sharded_two_ranks(cuda):
         assert float(r["inertia"]) == single.inertia_ and int(r["n_iter"]) == single.n_iter_
 
 
-@pytest.mark.parametrize("n,d,k", [(20000, 80, 7), (3000, 130, 3), (1025, 64, 1), (5000, 16, 100)])
-def test_km_sums_row_order_bitexact(cuda, n, d, k):
-    """hlmc_km_sums = sklearn's single-thread float32 centre sums: per cluster and column a strictly
-    sequential row-order add (np.add.accumulate), counts exact; ragged column slabs and super-tiles."""
+@pytest.mark.parametrize("path", ["direct", "part"])
+@pytest.mark.parametrize("n,d,k", [(20000, 80, 7), (3000, 130, 3), (1025, 64, 1), (5000, 16, 100), (70001, 3, 11),
+                                   (300, 200, 40)])
+def test_km_sums_row_order_bitexact(cuda, n, d, k, path):
+    """hlmc_km_sums / hlmc_km_sums_part = sklearn's single-thread float32 centre sums: per cluster and column a
+    strictly sequential row-order add (np.add.accumulate), counts exact; ragged column slabs and tiles, a heavy
+    cluster, empty clusters (k > distinct labels at n=300, k=40)."""
     import torch
     from hlmc_amd import _lib as L
     rng = np.random.default_rng(n + d + k)
     X = rng.normal(0, 2.0, (n, d)).astype(np.float32)
     lab = rng.integers(0, k, n).astype(np.int32)
     lab[: n // 3] = 0                                     # one heavy cluster
+    if k == 40:
+        lab[lab % 3 == 1] = 2                             # some clusters left empty
     Xd, ld = torch.as_tensor(X, device="cuda"), torch.as_tensor(lab, device="cuda")
     sums = torch.empty(k, d, device="cuda")
     w = torch.empty(k, device="cuda")
-    L.check(L.lib().hlmc_km_sums(L.stream(), Xd.data_ptr(), n, d, ld.data_ptr(), k, sums.data_ptr(), w.data_ptr()))
+    sums.fill_(float("nan"))
+    w.fill_(float("nan"))
+    if path == "direct":
+        L.check(L.lib().hlmc_km_sums(L.stream(), Xd.data_ptr(), n, d, ld.data_ptr(), k, sums.data_ptr(), w.data_ptr()))
+    else:
+        nb = int(L.lib().hlmc_km_sums_workspace(n, k))
+        ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        L.check(L.lib().hlmc_km_sums_part(L.stream(), Xd.data_ptr(), n, d, ld.data_ptr(), k, sums.data_ptr(),
+                                          w.data_ptr(), ws.data_ptr(), nb))
     got = sums.cpu().numpy()
     for j in range(k):
         rows = X[lab == j]

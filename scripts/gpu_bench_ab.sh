@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests/test_models_gpu.py tests/test_traine
 for r in 1 2; do
   for spec in "$@"; do
     tag=${spec%%:*}; envs=${spec#*:}; envs=${envs//,/ }
-    env $envs timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/ab_$tag.log 2>&1; rc=$?
+    env $envs timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras > gpurun_out/ab_$tag.log 2>&1; rc=$?
     echo "r$r $tag rc=$rc $(python -c "import json;d=json.loads(open('gpurun_out/ab_$tag.log').read().strip().splitlines()[-1]);print(d['value'], d['ms_per_step'])")"
     [ $rc -eq 0 ] || exit $rc
   done

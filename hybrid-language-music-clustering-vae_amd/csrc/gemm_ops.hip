@@ -14,6 +14,7 @@ namespace {
 // 92.8k at 1024, 90.7k at 2048
 constexpr int kNtTargetBlocks = 256;
 constexpr int kTnTargetBlocks = 512;
+constexpr int kTnLongK = 131072;
 constexpr int kXcdRemapDefault = probe::kWgradS2 | probe::kLinearWgrad;  // measured: helps the TN (wgrad) family, hurts sub-pixel
 
 // Split-K plan shared by the launcher and the workspace query (must agree).
@@ -38,11 +39,15 @@ inline Plan plan_nt(int tiles, int Kmax, int BK) {
 }
 inline Plan plan_tn(int tiles, int K, int BK) {
     // weight gradients: long K (= batch x pixels), tiny M x N: split K until the grid fills the chip
-    // (>= 4 k-tiles per split); the slab reduction keeps 4 loads in flight.  HLMC_TN_BLOCKS: target grid
-    static const int target = [] {
+    // (>= 4 k-tiles per split); the slab reduction keeps 4 loads in flight.  The longest reductions (the
+    // 32 / 64-channel layers, K = 262 144) take a 1024-block grid: per layer (scripts/gpu_wgrad_blocks.sh,
+    // bench_gemm.py) 47 vs 60 us at 512, while every shorter layer is fastest at 512 (1024: +10-20 %).
+    // HLMC_TN_BLOCKS: one target grid for every layer (measurement aid).
+    static const int forced = [] {
         const char* e = std::getenv("HLMC_TN_BLOCKS");
-        return e ? std::max(64, std::atoi(e)) : kTnTargetBlocks;
+        return e ? std::max(64, std::atoi(e)) : 0;
     }();
+    const int target = forced ? forced : (K >= kTnLongK ? 2 * kTnTargetBlocks : kTnTargetBlocks);
     int S = cdiv(target, tiles);
     S = std::max(1, std::min(S, K / (4 * BK)));
     int ksl = cdiv(cdiv(K, S), BK) * BK;

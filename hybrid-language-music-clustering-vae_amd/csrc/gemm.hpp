@@ -875,13 +875,28 @@ struct KRowConvS2 {
 };
 
 // ============================================================================ TN main loop
+// XOR swizzle of the 16-byte chunks of a bf16 k-row (CPR chunks per row, 8 or 16) for the ds_read_b64_tr_b16
+// fragment reads: the 8 k-rows one 32-lane half reads (q = 0..3, g = 0..1) land on disjoint bank groups.
+template <int CPR>
+__device__ __forceinline__ int tn_swz(int row) {
+    if constexpr (CPR == 16) return 2 * ((row & 3) | (((row >> 3) & 1) << 2));
+    else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+}
+
 // Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_kernel).
-template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL>
+// PF: K-steps of global loads in flight (1: one register set; 2: two sets, the loop unrolled by two so each
+// step's loads are issued two steps ahead of their LDS store).
+template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, int PF = 1>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;            // k rows per tile (KCH 16-byte chunks of one column)
-    constexpr int LDA = BM + V;             // padded LDS row (elements)
-    constexpr int LDB = BN + V;
+    constexpr int ACPR = BM / V, BCPR = BN / V;  // chunks per k-row
+    // bf16 rows of 8 / 16 chunks: unpadded, XOR-swizzled chunks (tn_swz); otherwise one chunk of padding
+    // (measured: the padded 136-element rows put 2-way bank conflicts on a third of the LDS cycles)
+    constexpr bool SWA = sizeof(T) == 2 && (ACPR == 8 || ACPR == 16);
+    constexpr bool SWB = sizeof(T) == 2 && (BCPR == 8 || BCPR == 16);
+    constexpr int LDA = SWA ? BM : BM + V;  // LDS row (elements)
+    constexpr int LDB = SWB ? BN : BN + V;
     constexpr int WAVES_N = BN / WN;
     static_assert((BM / WM) * WAVES_N == 4, "4 waves per block");
     constexpr int TM = WM / 16, TN = WN / 16;
@@ -907,95 +922,139 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    uint4 ra[AR], rb[BR];
-    constexpr int ACPR = BM / V, BCPR = BN / V;  // chunks per k-row
+    struct Regs {
+        uint4 a[AR], b[BR];
+    };
     typename LL::Col acol[AR];
     typename HL::Col bcol[BR];
 #pragma unroll
     for (int i = 0; i < AR; ++i) acol[i] = ll.prep(m0 + ((tid + i * 256) % ACPR) * V);
 #pragma unroll
     for (int i = 0; i < BR; ++i) bcol[i] = hl.prep(n0 + ((tid + i * 256) % BCPR) * V);
-    auto gload = [&](int k0) {
+    auto gload = [&](Regs& rg, int k0) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) ra[i] = ll.load(k0 + c / ACPR, acol[i]);
+            if (c < ACH) rg.a[i] = ll.load(k0 + c / ACPR, acol[i]);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) rb[i] = hl.load(k0 + c / BCPR, bcol[i]);
+            if (c < BCH) rg.b[i] = hl.load(k0 + c / BCPR, bcol[i]);
         }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](const Regs& rg, int buf) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) *reinterpret_cast<uint4*>(&Ls[buf][(c / ACPR) * LDA + (c % ACPR) * V]) = ra[i];
+            if (c < ACH) {
+                const int row = c / ACPR, cc = c % ACPR;
+                const int pc = SWA ? (cc ^ tn_swz<ACPR>(row)) : cc;
+                *reinterpret_cast<uint4*>(&Ls[buf][row * LDA + pc * V]) = rg.a[i];
+            }
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) *reinterpret_cast<uint4*>(&Hs[buf][(c / BCPR) * LDB + (c % BCPR) * V]) = rb[i];
+            if (c < BCH) {
+                const int row = c / BCPR, cc = c % BCPR;
+                const int pc = SWB ? (cc ^ tn_swz<BCPR>(row)) : cc;
+                *reinterpret_cast<uint4*>(&Hs[buf][row * LDB + pc * V]) = rg.b[i];
+            }
+        }
+    };
+    // element offset of (k-row, column col) in a tile image (the fragment reads stay inside one 16-byte chunk)
+    auto aoff = [](int row, int col) {
+        if constexpr (SWA) return row * LDA + (((col >> 3) ^ tn_swz<ACPR>(row)) << 3) + (col & 7);
+        else return row * LDA + col;
+    };
+    auto boff = [](int row, int col) {
+        if constexpr (SWB) return row * LDB + (((col >> 3) ^ tn_swz<BCPR>(row)) << 3) + (col & 7);
+        else return row * LDB + col;
+    };
+    const int g = lane >> 4, li = lane & 15;
+    auto mma_step = [&](int cur) {
+        const T* A = Ls[cur];
+        const T* B = Hs[cur];
+        if constexpr (sizeof(T) == 2) {
+            // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses row q, cols 4p..4p+3;
+            // lane i receives column i of the 4 rows.
+            const int q = li >> 2, p = li & 3;
+#pragma unroll
+            for (int s = 0; s < BK / 32; ++s) {
+                bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int col = wm0 + i * 16 + 4 * p;
+                    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(A + aoff(32 * s + 8 * g + q, col)));
+                    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(A + aoff(32 * s + 8 * g + q + 4, col)));
+                    af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int col = wn0 + j * 16 + 4 * p;
+                    s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(B + boff(32 * s + 8 * g + q, col)));
+                    s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(B + boff(32 * s + 8 * g + q + 4, col)));
+                    bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < BK / 4; ++s) {
+                float af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[i] = A[(s * 4 + g) * LDA + wm0 + i * 16 + li];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bfr[j] = B[(s * 4 + g) * LDB + wn0 + j * 16 + li];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
         }
     };
 
-    if (kb < ke) {
-        gload(kb);
-        lstore(0);
-        __syncthreads();
-        int it = 0;
-        const int g = lane >> 4, li = lane & 15;
-        for (int k0 = kb; k0 < ke; k0 += BK, ++it) {
-            const int cur = it & 1;
-            const bool more = k0 + BK < ke;
-            if (more) gload(k0 + BK);
-            const T* A = Ls[cur];
-            const T* B = Hs[cur];
-            if constexpr (sizeof(T) == 2) {
-                // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses row q, cols 4p..4p+3;
-                // lane i receives column i of the 4 rows.
-                const int q = li >> 2, p = li & 3;
-#pragma unroll
-                for (int s = 0; s < BK / 32; ++s) {
-                    bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) {
-                        const T* base = &A[(32 * s + 8 * g + q) * LDA + wm0 + i * 16 + 4 * p];
-                        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base));
-                        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + 4 * LDA));
-                        af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    }
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const T* base = &B[(32 * s + 8 * g + q) * LDB + wn0 + j * 16 + 4 * p];
-                        s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base));
-                        s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + 4 * LDB));
-                        bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                    }
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-                }
-            } else {
-#pragma unroll
-                for (int s = 0; s < BK / 4; ++s) {
-                    float af[TM], bfr[TN];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i) af[i] = A[(s * 4 + g) * LDA + wm0 + i * 16 + li];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) bfr[j] = B[(s * 4 + g) * LDB + wn0 + j * 16 + li];
-#pragma unroll
-                    for (int i = 0; i < TM; ++i)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-                }
-            }
-            if (more) lstore(cur ^ 1);
+    if constexpr (PF == 1) {
+        Regs r0;
+        if (kb < ke) {
+            gload(r0, kb);
+            lstore(r0, 0);
             __syncthreads();
+            int it = 0;
+            for (int k0 = kb; k0 < ke; k0 += BK, ++it) {
+                const int cur = it & 1;
+                const bool more = k0 + BK < ke;
+                if (more) gload(r0, k0 + BK);
+                mma_step(cur);
+                if (more) lstore(r0, cur ^ 1);
+                __syncthreads();
+            }
+        }
+    } else {
+        // two register sets: x holds step k0 + BK while y's loads for k0 + 2 BK are in flight
+        Regs r0, r1;
+        if (kb < ke) {
+            gload(r0, kb);
+            if (kb + BK < ke) gload(r1, kb + BK);
+            lstore(r0, 0);
+            __syncthreads();
+            for (int k0 = kb; k0 < ke; k0 += 2 * BK) {
+                if (k0 + 2 * BK < ke) gload(r0, k0 + 2 * BK);
+                mma_step(0);
+                if (k0 + BK < ke) lstore(r1, 1);
+                __syncthreads();
+                if (k0 + BK >= ke) break;
+                if (k0 + 3 * BK < ke) gload(r1, k0 + 3 * BK);
+                mma_step(1);
+                if (k0 + 2 * BK < ke) lstore(r0, 0);
+                __syncthreads();
+            }
         }
     }
     float* slab = ws + (int64_t)bz * M * N;
@@ -1048,11 +1107,6 @@ __device__ __forceinline__ void lgkm_wait_tied(bf16x8_t (&af)[TM], bf16x8_t (&bf
         static_assert(TM == 0, "unsupported fragment counts");
 }
 
-template <int CPR>
-__device__ __forceinline__ int tn_swz(int row) {
-    if constexpr (CPR == 16) return 2 * ((row & 3) | (((row >> 3) & 1) << 2));
-    else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
-}
 
 template <int BM, int BN, int NS, class LL, class HL, class EP>
 __global__ __launch_bounds__(256) void gemm_tn_dma_kernel(LL ll, HL hl, EP ep, float* ws, int M, int N, int K,

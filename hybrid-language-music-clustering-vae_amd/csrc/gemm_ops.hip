@@ -235,11 +235,26 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "wgrad workspace too small");
     dim3 grid(tiles, 1, pl.S);
     const int rm = xcd_remap_for_site();
+    static const int pf = [] {  // HLMC_TN_PF=2: two K-steps of loads in flight (A/B)
+        const char* e = std::getenv("HLMC_TN_PF");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
+    static const int kch8_min = [] {  // HLMC_TN_KCH8_MIN: smallest split length on the 64-deep K-step (A/B)
+        const char* e = std::getenv("HLMC_TN_KCH8_MIN");
+        return e ? std::atoi(e) : 1024;
+    }();
     HLMC_PROBE_BEGIN(s);
-    if (pl.ksl >= 1024)
-        gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-    else
-        gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    if (pl.ksl >= kch8_min) {
+        if (pf == 2)
+            gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, 2><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        else
+            gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    } else {
+        if (pf == 2)
+            gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, 2><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        else
+            gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    }
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     reduce_splits(s, ws.p, ep, M, N, pl.S);

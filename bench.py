@@ -109,7 +109,7 @@ PROBE_KINDS = {
     4: ("wgrad_s2", "gemm_tn KRowConvS2 (conv / convT weight gradient)", "mfma"),
     8: ("linear", "gemm_nt DenseLoader (Linear fwd / dgrad)", "mfma"),
     16: ("linear_wgrad", "gemm_tn KRowDense (Linear weight gradient)", "mfma"),
-    32: ("stft_mel", "stft_mel_kernel (STFT + mel)", "hbm"),
+    32: ("stft_mel", "stft_mel0_kernel (STFT + mel)", "hbm"),
     64: ("bn", "BatchNorm / reduction streaming family (bn_act, bn_bwd_moments, bn_bwd_apply, col_moments, "
                "parts_fold, finalizers)", "hbm"),
 }

@@ -291,7 +291,7 @@ __device__ __forceinline__ void piptrack_frame(const float* pw, int ln, const Pi
 // kMode 0: banded mel (stored [b][m][t]) + per-clip max/min.  kMode 1: spectral shape of |X| (power 1):
 // centroid, bandwidth (p = 2) and rolloff per frame, stored f64 [b][3][t] (sout); the mel tables are unused.
 template <int kMode>
-__global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__ pcm, int64_t n_samples, int T,
+__device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int64_t n_samples, int T,
                                                        int hop, const float* __restrict__ window,
                                                        const float2* __restrict__ rtw, const float2* __restrict__ tw23,
                                                        const int* __restrict__ band,
@@ -300,22 +300,22 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
                                                        unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min,
                                                        double bin_hz, double roll, double* __restrict__ sout,
                                                        PipArgs pa) {
-    __shared__ float2 stw[kFFT + 1];
+    // LDS: stage-2/3 twiddles + the wave-private exchange buffers (43 KB static) + band info and mel staging
+    // (dynamic), 52 KB in all: 3 blocks per CU.  The real-split twiddles (rtw) and the chunk-transposed
+    // filterbank (wts, [c][lane][4]) are read from global memory (L1/L2-resident tables); in LDS they held the
+    // kernel at 2 blocks per CU.
     __shared__ float2 stw23[kTw2 + kTw3];
     __shared__ __align__(16) float2 zb[kWaves][kZ];
-    // dynamic: chunk-transposed filterbank W[c][lane][4] (nnz floats) | per-lane band info int4[64] |
-    // mel staging [kFpb][n_mels + 1]
-    extern __shared__ float4 sw4[];
-    int4* sbl = reinterpret_cast<int4*>(sw4 + nnz / 4);
+    // dynamic: per-lane band info int4[64] | mel staging [kFpb][n_mels + 1]
+    extern __shared__ int4 sbl[];
     float* smel = reinterpret_cast<float*>(sbl + kMelLanes);
+    const float4* __restrict__ gw4 = reinterpret_cast<const float4*>(wts);
     const int b = blockIdx.y;
     const int t0 = blockIdx.x * kFpb;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const float* x = pcm + (int64_t)b * n_samples;
-    for (int i = threadIdx.x; i <= kFFT; i += 256) stw[i] = rtw[i];
     for (int i = threadIdx.x; i < kTw2 + kTw3; i += 256) stw23[i] = tw23[i];
     if constexpr (kMode == 0) {
-        for (int i = threadIdx.x; i < nnz / 4; i += 256) sw4[i] = reinterpret_cast<const float4*>(wts)[i];
         for (int l = threadIdx.x; l < kMelLanes; l += 256) sbl[l] = reinterpret_cast<const int4*>(band)[l];
     }
     __syncthreads();
@@ -396,6 +396,10 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
         wave_lds_fence();
         // ---- real-FFT split: X[f] = E[f] + e^{-2 pi i f / 2048} O[f], f = 0..1024
         float p[17];
+        float2 w[17];   // real-split twiddles from global (issued before the LDS reads they pair with)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) w[q] = rtw[ln + 64 * q];
+        w[16] = rtw[kFFT];
         // conjugate partner 1024 - f of f = ln + 64 q: zpad = 68 (16 - q) + bcj (f = 0 pairs with itself)
         const int bcj = -ln + ((-ln) >> 4);
         auto split = [&](float2 zf, float2 zc, float2 w) -> float {
@@ -410,11 +414,11 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
             const float2 zf = z[brd + 68 * q];
             const int ic = (q == 0 && ln == 0) ? 0 : 68 * (16 - q) + bcj;  // index select, one LDS read
             const float2 zc = z[ic];
-            p[q] = split(zf, zc, stw[ln + 64 * q]);
+            p[q] = split(zf, zc, w[q]);
         }
         {
             const float2 z0 = z[0];
-            p[16] = split(z0, z0, stw[kFFT]);  // Nyquist bin (every lane computes it; lane 0 stores it)
+            p[16] = split(z0, z0, w[16]);  // Nyquist bin (every lane computes it; lane 0 stores it)
         }
         wave_lds_fence();
 #pragma unroll
@@ -433,7 +437,7 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
             float acc0 = 0.f, acc1 = 0.f;
             for (int c = 0; c < bl.y; c += 2) {
                 const float4 p0 = pw4[(bl.x >> 2) + c], p1 = pw4[(bl.x >> 2) + c + 1];
-                const float4 w0 = sw4[c * kMelLanes + ln], w1 = sw4[(c + 1) * kMelLanes + ln];
+                const float4 w0 = gw4[c * kMelLanes + ln], w1 = gw4[(c + 1) * kMelLanes + ln];
                 acc0 = fmaf(p0.x, w0.x, acc0); acc0 = fmaf(p0.y, w0.y, acc0);
                 acc0 = fmaf(p0.z, w0.z, acc0); acc0 = fmaf(p0.w, w0.w, acc0);
                 acc0 = fmaf(p1.x, w1.x, acc0); acc0 = fmaf(p1.y, w1.y, acc0);
@@ -442,7 +446,7 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
             for (int c = 0; c < bl.w; c += 2) {
                 const int cw = bl.y + c;
                 const float4 p0 = pw4[(bl.z >> 2) + c], p1 = pw4[(bl.z >> 2) + c + 1];
-                const float4 w0 = sw4[cw * kMelLanes + ln], w1 = sw4[(cw + 1) * kMelLanes + ln];
+                const float4 w0 = gw4[cw * kMelLanes + ln], w1 = gw4[(cw + 1) * kMelLanes + ln];
                 acc1 = fmaf(p0.x, w0.x, acc1); acc1 = fmaf(p0.y, w0.y, acc1);
                 acc1 = fmaf(p0.z, w0.z, acc1); acc1 = fmaf(p0.w, w0.w, acc1);
                 acc1 = fmaf(p1.x, w1.x, acc1); acc1 = fmaf(p1.y, w1.y, acc1);
@@ -478,6 +482,32 @@ __global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__
         if (lmax > 0.f) atomicMax(clip_max + b, __float_as_uint(lmax));
         if (lmin < INFINITY) atomicMin(clip_min + b, __float_as_uint(lmin));
     }
+}
+
+// kMode 0 (the mel hot path) is built for 3 waves per SIMD (168 VGPRs, no spills; LDS 52 KB: 3 blocks per CU);
+// the spectral-shape / piptrack modes keep the default register budget (they would spill at 168).
+template <int kMode>
+__global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__ pcm, int64_t n_samples, int T,
+                                                       int hop, const float* __restrict__ window,
+                                                       const float2* __restrict__ rtw, const float2* __restrict__ tw23,
+                                                       const int* __restrict__ band,
+                                                       const int* __restrict__ woff, const float* __restrict__ wts,
+                                                       int n_mels, int nnz, float* __restrict__ out,
+                                                       unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min,
+                                                       double bin_hz, double roll, double* __restrict__ sout,
+                                                       PipArgs pa) {
+    stft_mel_body<kMode>(pcm, n_samples, T, hop, window, rtw, tw23, band, woff, wts, n_mels, nnz, out, clip_max, clip_min, bin_hz, roll, sout, pa);
+}
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stft_mel0_kernel(const float* __restrict__ pcm, int64_t n_samples, int T,
+                                                       int hop, const float* __restrict__ window,
+                                                       const float2* __restrict__ rtw, const float2* __restrict__ tw23,
+                                                       const int* __restrict__ band,
+                                                       const int* __restrict__ woff, const float* __restrict__ wts,
+                                                       int n_mels, int nnz, float* __restrict__ out,
+                                                       unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min,
+                                                       double bin_hz, double roll, double* __restrict__ sout,
+                                                       PipArgs pa) {
+    stft_mel_body<0>(pcm, n_samples, T, hop, window, rtw, tw23, band, woff, wts, n_mels, nnz, out, clip_max, clip_min, bin_hz, roll, sout, pa);
 }
 
 __device__ __forceinline__ float db_of(float S, float amin) { return 10.f * log10f(fmaxf(amin, S)); }
@@ -847,17 +877,16 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
     const int T = (int)frames(p, n);
     init_minmax_kernel<<<(unsigned)((B + 255) / 256), 256, 0, s>>>(cmax, cmin, B);  // 0x7f7f7f7f: large positive float
     HLMC_LAUNCHED();
-    HLMC_CHECK_ARG(p->nnz <= kMaxW, "filterbank too large for the LDS-resident mel stage");
     HLMC_CHECK_ARG(p->n_mels <= 2 * kMelLanes, "n_mels <= 128");
     dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
-    const size_t dyn = ((size_t)p->nnz + 4 * kMelLanes + (size_t)kFpb * (p->n_mels + 1)) * 4;
+    const size_t dyn = (4 * kMelLanes + (size_t)kFpb * (p->n_mels + 1)) * 4;
     {  // algorithmic work: radix-2-equivalent FFT 2.5 N log2 N + window + |X|^2 + banded mel; PCM in, mel out
         const double nf = p->n_fft, lg = std::log2(nf);
         probe::site(probe::kStftMel, (double)B * T * (2.5 * nf * lg + nf + 3.0 * (nf / 2 + 1) + 2.0 * p->nnz),
                     (double)B * ((double)n * 4 + (double)p->n_mels * T * 4));
     }
     HLMC_PROBE_BEGIN(s);
-    stft_mel_kernel<0><<<grid, 256, dyn, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
+    stft_mel0_kernel<<<grid, 256, dyn, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
                                               p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0, nullptr, PipArgs{});
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();

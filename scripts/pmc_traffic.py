@@ -24,7 +24,7 @@ KINDS = {  # op kind of include/hlmc.h hlmc_probe_arm -> kernel-name pattern
     "wgrad_s2": r"gemm_tn_kernel<.*KRowConvS2",
     "linear": r"gemm_nt\w*<[^<>]*, hlmc::DenseLoader<",
     "linear_wgrad": r"gemm_tn_kernel<[^<>]*, hlmc::(\(anonymous namespace\)::)?KRowDenseV?<[^<>]*>, hlmc::(\(anonymous namespace\)::)?KRowDenseV?<",
-    "stft_mel": r"stft_mel_kernel",
+    "stft_mel": r"stft_mel0?_kernel",
     "bn": r"(bn_act_kernel|bn_bwd_moments_kernel|bn_bwd_apply_kernel|col_moments_kernel|parts_fold_kernel|"
           r"bn_finalize_kernel|bn_bwd_finalize_kernel|colsum_finalize_kernel)",
 }

@@ -92,7 +92,7 @@ __device__ __forceinline__ double block_sum_partials(const double* __restrict__ 
 // a block pass covers rpp = 256 / (C/V) consecutive rows (one contiguous 4 KB span); each thread keeps its
 // V channels' parameters in registers and has kU rows in flight.
 constexpr int kU = 4;   // rows in flight, forward streaming kernels
-constexpr int kUb = 4;  // backward (two operands per row)
+constexpr int kUb = 2;  // backward (two operands per row, the next step's rows prefetched as well)
 
 template <typename T>
 __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ y, int64_t R, int C, int64_t rows_per_blk,
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
                                                              const uint8_t* __restrict__ mask, float mscale,
                                                              int64_t rows_per_blk, double* __restrict__ part) {
     constexpr int V = Vec16<T>::N;
-    __shared__ double s1[2048], s2[2048];
+    __shared__ double s1[2048];
     const int tpr = C / V, rpp = kThreads / tpr;
     const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
     const int c0 = cg * V;
@@ -274,9 +274,12 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
     BnChan::load(invstd, c0, is);
     BnChan::load(gamma, c0, ga);
     BnChan::load(beta, c0, be);
-    double a[V], b[V];
+    // f32 per thread (rows_per_blk / rpp rows: 16 at the bench shapes, <= 128 at 128 x 1024 mel), f64 across
+    // the block's threads and the blocks:
+    // the lean register / LDS footprint lets more blocks share a CU with the weight-gradient GEMMs
+    float a[V], b[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) a[v] = b[v] = 0.0;
+    for (int v = 0; v < V; ++v) a[v] = b[v] = 0.f;
     uint4 nx[kUb], ng[kUb];  // next step's rows (clamped, always in-bounds)
     auto fetch = [&](int64_t rb) {
 #pragma unroll
@@ -292,11 +295,6 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
 #pragma unroll
         for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
         if (r + kUb * rpp < r1) fetch(r + kUb * rpp);
-        // the kUb rows of this step are added in f32, then once into the f64 accumulators (a per-element f64
-        // update made this pass FP64-bound: 1.6 TB/s against 4+ TB/s for the apply pass over the same operands)
-        float fa[V], fb[V];
-#pragma unroll
-        for (int v = 0; v < V; ++v) fa[v] = fb[v] = 0.f;
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t ru = r + u * rpp;
@@ -310,15 +308,17 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
                 float z = xh * ga[v] + be[v];
                 float dz = g[0][v] * act_grad(z, act);
                 if constexpr (kMask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
-                fa[v] += dz;
-                fb[v] = fmaf(dz, xh, fb[v]);
+                a[v] += dz;
+                b[v] = fmaf(dz, xh, b[v]);
             }
         }
-#pragma unroll
-        for (int v = 0; v < V; ++v) { a[v] += fa[v]; b[v] += fb[v]; }
     }
-    block_colsum<V>(a, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C);
-    block_colsum<V>(b, tpr, C, s2, part + (int64_t)blockIdx.x * 2 * C + C);
+    double da_[V], db_[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) { da_[v] = a[v]; db_[v] = b[v]; }
+    block_colsum<V>(da_, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C);
+    __syncthreads();   // s1 reused
+    block_colsum<V>(db_, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C + C);
 }
 
 // backward partials [nblk][2C]: sum dz (-> dbeta), sum dz*xhat (-> dgamma); grid ceil(C / 64) x 1024
@@ -360,9 +360,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     BnChan::load(beta, c0, be);
     BnChan::load(sums, c0, s0);
     BnChan::load(sums + C, c0, sx);
-    double a[V];
+    float a[V];   // f32 per thread, f64 across threads and blocks (see bn_bwd_moments_kernel)
 #pragma unroll
-    for (int v = 0; v < V; ++v) a[v] = 0.0;
+    for (int v = 0; v < V; ++v) a[v] = 0.f;
     uint4 nx[kUb], ng[kUb];  // next step's rows (clamped, always in-bounds)
     auto fetch = [&](int64_t rb) {
 #pragma unroll
@@ -378,9 +378,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
         for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
         if (r + kUb * rpp < r1) fetch(r + kUb * rpp);
-        float fa[V];  // this step's rows in f32, then once into the f64 accumulators
-#pragma unroll
-        for (int v = 0; v < V; ++v) fa[v] = 0.f;
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t ru = r + u * rpp;
@@ -400,12 +397,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
             store16_f32(dy + ru * C + c0, o);
             // the bias grad is the sum of the dy actually stored (rounded to T)
 #pragma unroll
-            for (int v = 0; v < V; ++v) fa[v] += to_f32<T>(from_f32<T>(o[v]));
+            for (int v = 0; v < V; ++v) a[v] += to_f32<T>(from_f32<T>(o[v]));
         }
-#pragma unroll
-        for (int v = 0; v < V; ++v) a[v] += fa[v];
     }
-    block_colsum<V>(a, tpr, C, s1, part + (int64_t)blockIdx.x * C);
+    double ad[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) ad[v] = a[v];
+    block_colsum<V>(ad, tpr, C, s1, part + (int64_t)blockIdx.x * C);
 }
 
 // out[c] = sum_k part[k][c] over [nblk][C] partials; grid ceil(C / 64) x 1024

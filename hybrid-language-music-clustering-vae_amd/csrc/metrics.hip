@@ -26,15 +26,17 @@ __global__ void sil_count_kernel(const int32_t* __restrict__ labels, int64_t n, 
 
 // S[i][c] (f64) for the block's 64 rows: thread (row r = tid / 4, sub = tid % 4) holds x_i in registers and
 // takes every 4th j of each LDS tile; its per-cluster sums live in LDS (private row, padded), and the 4
-// subs are combined in order at the end.
+// subs are combined in order at the end.  One launch covers the label window [c0, c0 + kw) (as many
+// accumulator rows as LDS holds); rows j outside it are skipped, so over all windows every distance is
+// computed exactly once.
 template <int DMAX>
 __global__ __launch_bounds__(256) void sil_sums_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                       const int32_t* __restrict__ labels, int k,
+                                                       const int32_t* __restrict__ labels, int k, int c0, int kw,
                                                        double* __restrict__ S) {
     extern __shared__ double sil_sh[];
     constexpr int DS = DMAX + 4;                   // tile row stride: the 4 rows one wave reads at once
                                                    // land on disjoint bank groups (16-B reads stay aligned)
-    const int kp = k + 1;                          // padded accumulator row
+    const int kp = kw + 1;                         // padded accumulator row
     double* acc = sil_sh;                          // [256][kp]
     float* xt = reinterpret_cast<float*>(acc + 256 * kp);  // [kSilTile][DS]
     int* lt = reinterpret_cast<int*>(xt + kSilTile * DS);
@@ -51,7 +53,10 @@ __global__ __launch_bounds__(256) void sil_sums_kernel(const float* __restrict__
             const int64_t j = j0 + jr;
             xt[jr * DS + c] = (j < n && c < d) ? X[j * d + c] : 0.f;
         }
-        for (int e = tid; e < kSilTile; e += 256) lt[e] = (j0 + e < n) ? labels[j0 + e] : -1;
+        for (int e = tid; e < kSilTile; e += 256) {
+            const int l = (j0 + e < n) ? labels[j0 + e] - c0 : -1;
+            lt[e] = (l >= 0 && l < kw) ? l : -1;
+        }
         __syncthreads();
         if (i >= n) continue;
         for (int q = sub; q < kSilTile; q += 4) {
@@ -74,11 +79,11 @@ __global__ __launch_bounds__(256) void sil_sums_kernel(const float* __restrict__
     }
     __syncthreads();
     if (i >= n || sub != 0) return;
-    for (int c = 0; c < k; ++c) {
+    for (int c = 0; c < kw; ++c) {
         double v = 0.0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) v += acc[(tid + u) * kp + c];
-        S[i * k + c] = v;
+        S[i * k + c0 + c] = v;
     }
 }
 
@@ -134,19 +139,24 @@ constexpr int kSilFinalBlocks = 512;
 // then the k x k finish.  Block partials over contiguous row ranges, reduced in block order.
 constexpr int kCluBlocks = 64;
 
-// part[blk][c][d] = sum of x[i][d] over the block's rows with label c (thread d owns column d)
+// part[blk][c][d] = sum of x[i][d] over the block's rows with label c (thread d owns column d), for the
+// labels of the window [c0, c0 + kw)
 __global__ __launch_bounds__(256) void clu_sums_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                       const int32_t* __restrict__ labels, int k,
+                                                       const int32_t* __restrict__ labels, int k, int c0, int kw,
                                                        double* __restrict__ part) {
-    extern __shared__ double clu_sh[];  // [k][d]
-    for (int e = threadIdx.x; e < k * d; e += blockDim.x) clu_sh[e] = 0.0;
+    extern __shared__ double clu_sh[];  // [kw][d]
+    for (int e = threadIdx.x; e < kw * d; e += blockDim.x) clu_sh[e] = 0.0;
     __syncthreads();
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t r0 = blockIdx.x * per, r1 = min(n, r0 + per);
     for (int c = threadIdx.x; c < d; c += blockDim.x)
-        for (int64_t i = r0; i < r1; ++i) clu_sh[labels[i] * d + c] += (double)X[i * d + c];
+        for (int64_t i = r0; i < r1; ++i) {
+            const int l = labels[i] - c0;
+            if (l >= 0 && l < kw) clu_sh[l * d + c] += (double)X[i * d + c];
+        }
     __syncthreads();
-    for (int e = threadIdx.x; e < k * d; e += blockDim.x) part[(int64_t)blockIdx.x * k * d + e] = clu_sh[e];
+    for (int e = threadIdx.x; e < kw * d; e += blockDim.x)
+        part[(int64_t)blockIdx.x * k * d + (int64_t)c0 * d + e] = clu_sh[e];
 }
 
 // centroids[c][d] = sum_blk part / count[c]; mean[d] = sum over all rows / n
@@ -199,9 +209,9 @@ __global__ __launch_bounds__(256) void clu_dist_kernel(const float* __restrict__
 // out[0] = Davies-Bouldin, out[1] = Calinski-Harabasz (sklearn 1.7 definitions, f64)
 __global__ void clu_finish_kernel(const double* __restrict__ part2, int nblk, int k, int d,
                                   const int32_t* __restrict__ counts, int64_t n, const double* __restrict__ cent,
-                                  const double* __restrict__ mean, double* __restrict__ out) {
+                                  const double* __restrict__ mean, double* __restrict__ intra,
+                                  double* __restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double intra[64];
     double extra_disp = 0.0, intra_disp = 0.0;
     bool intra_zero = true;
     for (int l = 0; l < k; ++l) {
@@ -243,34 +253,41 @@ __global__ void clu_finish_kernel(const double* __restrict__ part2, int nblk, in
 
 template <int DMAX>
 int launch_sums(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, double* S) {
-    const size_t sh = (size_t)256 * (k + 1) * sizeof(double) + (size_t)kSilTile * (DMAX + 4) * sizeof(float) +
-                      kSilTile * sizeof(int);
-    HLMC_CHECK_ARG(sh <= 160 * 1024, "silhouette: too many clusters for the LDS accumulators");
+    const size_t tile = (size_t)kSilTile * (DMAX + 4) * sizeof(float) + kSilTile * sizeof(int);
+    const int kw_max = std::min(64, (int)((160 * 1024 - tile) / (256 * sizeof(double))) - 1);
     const unsigned grid = (unsigned)((n + kSilRows - 1) / kSilRows);
-    sil_sums_kernel<DMAX><<<grid, 256, sh, s>>>(X, n, d, labels, k, S);
-    HLMC_LAUNCHED();
+    for (int c0 = 0; c0 < k; c0 += kw_max) {   // label windows (one launch for k <= kw_max)
+        const int kw = std::min(kw_max, k - c0);
+        const size_t sh = (size_t)256 * (kw + 1) * sizeof(double) + tile;
+        sil_sums_kernel<DMAX><<<grid, 256, sh, s>>>(X, n, d, labels, k, c0, kw, S);
+        HLMC_LAUNCHED();
+    }
     return HLMC_OK;
 }
+
+size_t counts_bytes(int k) { return ((size_t)k * sizeof(int32_t) + 255) / 256 * 256; }
+
+constexpr int kCluWin = 96 * 1024 / sizeof(double);   // doubles of the clu_sums LDS label window
 
 }  // namespace
 
 namespace metrics {
 
 size_t silhouette_workspace(int64_t n, int k) {
-    return ((size_t)n * k * sizeof(double) + 255) / 256 * 256 + 256 + kSilFinalBlocks * sizeof(double);
+    return ((size_t)n * k * sizeof(double) + 255) / 256 * 256 + counts_bytes(k) + kSilFinalBlocks * sizeof(double);
 }
 
 int silhouette(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, double* samples,
                double* score, void* ws, size_t ws_bytes) {
     HLMC_CHECK_ARG(X && labels && score && ws, "silhouette: NULL argument");
     HLMC_CHECK_ARG(n >= 2 && d >= 1 && d <= 128, "silhouette: need n >= 2 and 1 <= d <= 128 (row held in registers)");
-    HLMC_CHECK_ARG(k >= 2 && k <= 64, "silhouette: number of labels must be in [2, 64] (sklearn: 2..n-1)");
+    HLMC_CHECK_ARG(k >= 2 && k <= n - 1, "silhouette: number of labels must be in [2, n - 1] (sklearn)");
     HLMC_CHECK_ARG(ws_bytes >= silhouette_workspace(n, k), "silhouette: workspace too small");
     char* w = static_cast<char*>(ws);
     double* S = reinterpret_cast<double*>(w);
     int32_t* counts = reinterpret_cast<int32_t*>(w + ((size_t)n * k * sizeof(double) + 255) / 256 * 256);
-    double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(counts) + 256);
-    HLMC_HIP(hipMemsetAsync(counts, 0, 256, s));
+    double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(counts) + counts_bytes(k));
+    HLMC_HIP(hipMemsetAsync(counts, 0, counts_bytes(k), s));
     sil_count_kernel<<<(unsigned)std::min<int64_t>(1024, (n + 255) / 256), 256, 0, s>>>(labels, n, k, counts);
     HLMC_LAUNCHED();
     if (d <= 32) HLMC_TRY(launch_sums<32>(s, X, n, d, labels, k, S));
@@ -286,31 +303,36 @@ int silhouette(hipStream_t s, const float* X, int64_t n, int d, const int32_t* l
 
 size_t cluster_scores_workspace(int k, int d) {
     return (size_t)kCluBlocks * k * d * sizeof(double) + (size_t)kCluBlocks * k * 2 * sizeof(double) +
-           (size_t)k * d * sizeof(double) + (size_t)d * sizeof(double) + 256 + 1024;
+           (size_t)k * d * sizeof(double) + (size_t)d * sizeof(double) + counts_bytes(k) + (size_t)k * sizeof(double);
 }
 
 int cluster_scores(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, double* out2,
                    void* ws, size_t ws_bytes) {
     HLMC_CHECK_ARG(X && labels && out2 && ws, "cluster_scores: NULL argument");
     HLMC_CHECK_ARG(n >= 2 && d >= 1 && d <= 4096, "cluster_scores: need n >= 2, 1 <= d <= 4096");
-    HLMC_CHECK_ARG(k >= 2 && k <= 64 && k < n, "cluster_scores: number of labels must be in [2, min(64, n-1)]");
-    HLMC_CHECK_ARG((size_t)k * d * sizeof(double) <= 96 * 1024, "cluster_scores: k * d too large for LDS");
+    HLMC_CHECK_ARG(k >= 2 && k < n, "cluster_scores: number of labels must be in [2, n - 1]");
+    HLMC_CHECK_ARG(4 * 2 * (size_t)k * sizeof(double) <= 64 * 1024, "cluster_scores: k too large (<= 1024)");
     HLMC_CHECK_ARG(ws_bytes >= cluster_scores_workspace(k, d), "cluster_scores: workspace too small");
     double* part = static_cast<double*>(ws);
     double* part2 = part + (size_t)kCluBlocks * k * d;
     double* cent = part2 + (size_t)kCluBlocks * k * 2;
     double* mean = cent + (size_t)k * d;
     int32_t* counts = reinterpret_cast<int32_t*>(mean + d);
-    HLMC_HIP(hipMemsetAsync(counts, 0, 256, s));
+    double* intra = reinterpret_cast<double*>(reinterpret_cast<char*>(counts) + counts_bytes(k));
+    HLMC_HIP(hipMemsetAsync(counts, 0, counts_bytes(k), s));
     sil_count_kernel<<<(unsigned)std::min<int64_t>(1024, (n + 255) / 256), 256, 0, s>>>(labels, n, k, counts);
     HLMC_LAUNCHED();
-    clu_sums_kernel<<<kCluBlocks, 256, (size_t)k * d * sizeof(double), s>>>(X, n, d, labels, k, part);
-    HLMC_LAUNCHED();
+    const int kw_max = std::max(1, kCluWin / d);
+    for (int c0 = 0; c0 < k; c0 += kw_max) {   // label windows of the LDS accumulators (one launch usually)
+        const int kw = std::min(kw_max, k - c0);
+        clu_sums_kernel<<<kCluBlocks, 256, (size_t)kw * d * sizeof(double), s>>>(X, n, d, labels, k, c0, kw, part);
+        HLMC_LAUNCHED();
+    }
     clu_centroid_kernel<<<1, 256, 0, s>>>(part, kCluBlocks, k, d, counts, n, cent, mean);
     HLMC_LAUNCHED();
     clu_dist_kernel<<<kCluBlocks, 256, (size_t)4 * k * 2 * sizeof(double), s>>>(X, n, d, labels, k, cent, part2);
     HLMC_LAUNCHED();
-    clu_finish_kernel<<<1, 64, 0, s>>>(part2, kCluBlocks, k, d, counts, n, cent, mean, out2);
+    clu_finish_kernel<<<1, 64, 0, s>>>(part2, kCluBlocks, k, d, counts, n, cent, mean, intra, out2);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

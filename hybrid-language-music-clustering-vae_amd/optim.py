@@ -24,8 +24,7 @@ class Adam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for group in self.param_groups:
-            ps, gs, ms, vs, ns = [], [], [], [], []
-            steps = set()
+            ps, gs, ms, vs, ns, ks = [], [], [], [], [], []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -36,8 +35,9 @@ class Adam(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                # 'step' is a host (CPU) tensor as in torch.optim.Adam (non-capturable): no device sync
                 st["step"] += 1
-                steps.add(int(st["step"].item()))
+                ks.append(int(st["step"]))
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 ps.append(p)
                 gs.append(g)
@@ -47,8 +47,8 @@ class Adam(torch.optim.Optimizer):
             if not ps:
                 continue
             b1, b2 = group["betas"]
-            for step in sorted(steps):
-                idx = [i for i, p in enumerate(ps) if int(self.state[p]["step"].item()) == step]
+            for step in sorted(set(ks)):
+                idx = [i for i, k in enumerate(ks) if k == step]
                 L.check(L.lib().hlmc_adam_step(
                     L.stream(), len(idx), L.vp_array([ps[i].data_ptr() for i in idx]),
                     L.vp_array([gs[i].data_ptr() for i in idx]), L.vp_array([ms[i].data_ptr() for i in idx]),

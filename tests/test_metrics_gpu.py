@@ -71,3 +71,18 @@ def test_silhouette_larger_n_vs_oracle(cuda):
     y = FX.blob_labels(6000, 32, 7, seed=21)
     np.testing.assert_allclose(M.silhouette_samples(torch.from_numpy(X).to(cuda), y).cpu().numpy(),
                                MO.silhouette_samples(X, y), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("d", [16, 128])
+def test_many_clusters_label_windows(cuda, d):
+    """k = 150 > the 64 LDS accumulator rows of one launch: the label windows (silhouette) and the clu_sums
+    windows (Davies-Bouldin / Calinski-Harabasz) against the float64 oracle; sklearn allows k up to n - 1."""
+    rng = np.random.default_rng(d)
+    X = rng.normal(0, 1, (900, d)).astype(np.float32)
+    y = rng.integers(0, 150, 900)
+    Xd = torch.from_numpy(X).to(cuda)
+    np.testing.assert_allclose(M.silhouette_samples(Xd, y).cpu().numpy(), MO.silhouette_samples(X, y),
+                               rtol=1e-5, atol=1e-6)
+    db, ch = M.davies_bouldin_score(Xd, y), M.calinski_harabasz_score(Xd, y)
+    assert abs(db - MO.davies_bouldin_score(X, y)) <= 1e-6 * abs(MO.davies_bouldin_score(X, y))
+    assert abs(ch - MO.calinski_harabasz_score(X, y)) <= 1e-6 * abs(MO.calinski_harabasz_score(X, y))

@@ -327,13 +327,14 @@ class NetT : public NetBase {
                const uint8_t* mask, float mscale, T* a, int lda, const ops::ColStats* st = nullptr) {
         float* mean = AF(bb.mean);
         float* inv = AF(bb.inv);
-        if (train && st && st->nparts > 0)
-            HLMC_TRY(ops::bn_stats_from_parts(s, st->part, st->nparts, R, C, mean, inv, RM[bn], RV[bn], NBT[bn],
-                                              kBnMomentum, kBnEps, after_parts(st->part, (size_t)st->nparts * 2 * C)));
-        else if (train)
-            HLMC_TRY(ops::bn_stats<T>(s, y, R, C, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps, scratch));
-        else
-            HLMC_TRY(ops::bn_eval_stats(s, RM[bn], RV[bn], C, kBnEps, mean, inv));
+        if (train && st && st->nparts > 0)  // statistics finalized inside the activation kernel
+            return ops::bn_act_train<T>(s, y, R, C, st->part, st->nparts, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum,
+                                        kBnEps, P[g], P[beta], act, mask, mscale, a, lda,
+                                        after_parts(st->part, (size_t)st->nparts * 2 * C));
+        if (train)
+            return ops::bn_act_train<T>(s, y, R, C, nullptr, 0, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps,
+                                        P[g], P[beta], act, mask, mscale, a, lda, scratch);
+        HLMC_TRY(ops::bn_eval_stats(s, RM[bn], RV[bn], C, kBnEps, mean, inv));
         return ops::bn_act<T>(s, y, R, C, mean, inv, P[g], P[beta], act, mask, mscale, a, lda);
     }
     // fused: moments emitted by the GEMM that wrote da (nullable); bias_part: per-layer buffer of the conv bias

@@ -57,14 +57,17 @@ inline Plan plan_tn(int tiles, int K, int BK) {
 
 // NT pipeline: 0 register-staged (gemm_nt_kernel), 3/4 = LDS-DMA ring of that many stages (gemm_nt_glds_kernel).
 // Measured (scripts/bench_gemm.py): the 4-stage DMA ring wins when a block reduces >= 1024 (16 K-steps),
-// the register path below that (short reductions: more co-resident blocks hide the pipeline prologue).
+// the register path below that (short reductions: more co-resident blocks hide the pipeline prologue) --
+// except on split-K grids of <= 256 blocks (one block per CU: no co-residency to lose), where the ring's
+// three K-steps in flight win even on 9-step reductions (the 4x4x512 conv / its data gradient: 21.5 vs 31.8 us).
 // HLMC_GEMM_PIPE=0/3/4 forces one (A/B measurement aid).
-inline int nt_pipe_select(int ksl) {
+inline int nt_pipe_select(int ksl, int S, int blocks) {
     static const int forced = [] {
         const char* e = std::getenv("HLMC_GEMM_PIPE");
         return e ? std::atoi(e) : -1;
     }();
     if (forced >= 0) return forced;
+    if (S > 1 && blocks <= 256) return 4;
     return ksl >= 1024 ? 4 : 0;
 }
 
@@ -103,7 +106,7 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     dim3 grid(tmn, phases, pl.S);
     // register path: short reductions keep the 4-chunk K-step (more co-resident blocks), long ones 8 chunks
     const bool long_k = Kmax >= 1024;
-    const int pipe = (dma_ok && BN >= 32 && BM >= 64) ? nt_pipe_select(pl.ksl) : 0;
+    const int pipe = (dma_ok && BN >= 32 && BM >= 64) ? nt_pipe_select(pl.ksl, pl.S, tmn * phases * pl.S) : 0;
     if (st) st->nparts = 0;
     if (bf) bf->nparts = 0;
     if (pl.S == 1 && bf && bf->part) {  // single pass: the epilogue also emits the BN-backward moments

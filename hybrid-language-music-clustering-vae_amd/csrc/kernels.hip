@@ -138,19 +138,23 @@ __global__ __launch_bounds__(256) void parts_fold_kernel(const double* __restric
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
     const int r0 = blockIdx.y * rp, r1 = min(nrows, r0 + rp);
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0, a5 = 0.0, a6 = 0.0, a7 = 0.0;
     if (c < ncols) {
         const double* p = part + c;
         int r = r0 + w;
-        for (; r + 12 < r1; r += 16) {
+        for (; r + 28 < r1; r += 32) {  // 8 row loads in flight per lane
             a0 += p[(int64_t)r * ncols];
             a1 += p[(int64_t)(r + 4) * ncols];
             a2 += p[(int64_t)(r + 8) * ncols];
             a3 += p[(int64_t)(r + 12) * ncols];
+            a4 += p[(int64_t)(r + 16) * ncols];
+            a5 += p[(int64_t)(r + 20) * ncols];
+            a6 += p[(int64_t)(r + 24) * ncols];
+            a7 += p[(int64_t)(r + 28) * ncols];
         }
         for (; r < r1; r += 4) a0 += p[(int64_t)r * ncols];
     }
-    red[w][lane] = (a0 + a1) + (a2 + a3);
+    red[w][lane] = ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7));
     __syncthreads();
     if (w == 0 && c < ncols) out[(int64_t)blockIdx.y * ncols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
@@ -207,6 +211,95 @@ __global__ void bn_eval_kernel(const float* rmean, const float* rvar, int C, flo
     invstd[c] = 1.f / sqrtf(rvar[c] + eps);
 }
 
+// Consumer-side BatchNorm finalize: the streaming kernel that needs the per-channel statistics (bn_act: mean /
+// invstd; bn_bwd_apply: sum dz / sum dz*xhat) folds the <= kFinRows-row [rows][2C] f64 partial table itself,
+// in a fixed row order, into LDS -- instead of a separate one-block-per-64-channels finalize launch (every
+// such launch costs >= 5 us on the critical path).  Every block computes the same values in the same order;
+// block 0 also stores the ones later kernels read (mean / invstd and the running statistics; dgamma / dbeta).
+constexpr int kFinRows = 8;       // rows one thread folds
+// rows a consumer folds itself: channels C <= 256 spread every channel over 256 / C threads (row groups)
+inline int fin_max_rows(int C) { return kFinRows * (C <= 256 ? 256 / C : 1); }
+struct BnFin {
+    const double* part = nullptr;  // [rows][2C]
+    int rows = 0;
+    int64_t R = 0;                 // rows of the normalised map (forward)
+    float *mean = nullptr, *invstd = nullptr, *rmean = nullptr, *rvar = nullptr;  // forward outputs (block 0)
+    int64_t* nbt = nullptr;
+    float momentum = 0.f, eps = 0.f;
+    float *dgamma = nullptr, *dbeta = nullptr;  // backward outputs (block 0)
+};
+// x0[c] / x1[c] (LDS, c < C <= 512) = the two folded columns c and C + c; fwd: -> mean / invstd (+ running stats).
+// C <= 256: thread (c = t % C, g = t / C) sums rows g, g + G, ... (G = 256 / C), then the G group sums are added
+// in group order; C > 256: each thread folds channels t and t + 256 alone.  red: >= 512 doubles of LDS.
+template <bool kFwd>
+__device__ __forceinline__ void bn_fin_prologue(const BnFin& f, int C, float* x0, float* x1, double* red) {
+    const int tid = threadIdx.x;
+    const int G = C <= 256 ? kThreads / C : 1;
+    auto fold = [&](int c, int g, double& s, double& q) {
+        double ps[kFinRows], pq[kFinRows];
+#pragma unroll
+        for (int i = 0; i < kFinRows; ++i) {  // every row load issued before the adds
+            const int r = g + i * G;
+            ps[i] = r < f.rows ? f.part[(int64_t)r * 2 * C + c] : 0.0;
+            pq[i] = r < f.rows ? f.part[(int64_t)r * 2 * C + C + c] : 0.0;
+        }
+        s = 0.0;
+        q = 0.0;
+#pragma unroll
+        for (int i = 0; i < kFinRows; ++i) { s += ps[i]; q += pq[i]; }
+    };
+    auto finish = [&](int c, double s, double q) {
+        if constexpr (kFwd) {
+            const double m = s / (double)f.R;
+            double var = q / (double)f.R - m * m;
+            if (var < 0.0) var = 0.0;
+            const float mf = (float)m, inv = (float)(1.0 / sqrt(var + (double)f.eps));
+            x0[c] = mf;
+            x1[c] = inv;
+            if (blockIdx.x == 0) {
+                f.mean[c] = mf;
+                f.invstd[c] = inv;
+                if (f.rmean) {
+                    const double unb = f.R > 1 ? var * (double)f.R / (double)(f.R - 1) : var;
+                    f.rmean[c] = (float)((1.0 - f.momentum) * f.rmean[c] + f.momentum * m);
+                    f.rvar[c] = (float)((1.0 - f.momentum) * f.rvar[c] + f.momentum * unb);
+                }
+                if (c == 0 && f.nbt) f.nbt[0] += 1;
+            }
+        } else {
+            x0[c] = (float)s;
+            x1[c] = (float)q;
+            if (blockIdx.x == 0) {
+                f.dbeta[c] = (float)s;
+                f.dgamma[c] = (float)q;
+            }
+        }
+    };
+    if (C <= 256) {
+        const int c = tid % C, g = tid / C;
+        double s, q;
+        fold(c, g, s, q);
+        red[g * C + c] = s;
+        red[kThreads + g * C + c] = q;
+        __syncthreads();
+        if (tid < C) {
+            double ss = 0.0, qq = 0.0;
+            for (int k = 0; k < G; ++k) {
+                ss += red[k * C + tid];
+                qq += red[kThreads + k * C + tid];
+            }
+            finish(tid, ss, qq);
+        }
+    } else {
+        for (int c = tid; c < C; c += kThreads) {
+            double s, q;
+            fold(c, 0, s, q);
+            finish(c, s, q);
+        }
+    }
+    __syncthreads();
+}
+
 struct BnChan {  // one thread's V channels of BatchNorm parameters
     template <int V>
     __device__ static void load(const float* __restrict__ src, int c0, float (&dst)[V]) {
@@ -215,27 +308,41 @@ struct BnChan {  // one thread's V channels of BatchNorm parameters
     }
 };
 
-// a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale]; grid-stride over row passes
-template <typename T, bool kMask>
+// a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale]; grid-stride over row passes.
+// kFin: train mode, mean / invstd folded here from the partial table (bn_fin_prologue).
+template <typename T, bool kMask, bool kFin>
 __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ y, int64_t R, int C,
                                                      const float* __restrict__ mean, const float* __restrict__ invstd,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      int act, const uint8_t* __restrict__ mask, float mscale,
-                                                     T* __restrict__ a, int lda) {
+                                                     T* __restrict__ a, int lda, BnFin fin) {
     constexpr int V = Vec16<T>::N;
+    __shared__ float fin_sh[kFin ? 1024 : 1];
+    __shared__ double fin_red[kFin ? 2 * kThreads : 1];
     const int tpr = C / V, rpp = kThreads / tpr;
     const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
     const int c0 = cg * V;
-    float mu[V], is[V], ga[V], be[V];
-    BnChan::load(mean, c0, mu);
-    BnChan::load(invstd, c0, is);
-    BnChan::load(gamma, c0, ga);
-    BnChan::load(beta, c0, be);
     const int64_t step = (int64_t)gridDim.x * rpp;
-    for (int64_t r = (int64_t)blockIdx.x * rpp + rr; r < R; r += kU * step) {
-        uint4 raw[kU];
+    const int64_t rfirst = (int64_t)blockIdx.x * rpp + rr;
+    uint4 raw[kU];
+    auto load_rows = [&](int64_t r) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) raw[u] = load16_raw(y + min(r + u * step, R - 1) * C + c0);
+    };
+    if (rfirst < R) load_rows(rfirst);  // the first pass's rows are in flight during the finalize prologue
+    float mu[V], is[V], ga[V], be[V];
+    if constexpr (kFin) {
+        bn_fin_prologue<true>(fin, C, fin_sh, fin_sh + 512, fin_red);
+        BnChan::load(fin_sh, c0, mu);
+        BnChan::load(fin_sh + 512, c0, is);
+    } else {
+        BnChan::load(mean, c0, mu);
+        BnChan::load(invstd, c0, is);
+    }
+    BnChan::load(gamma, c0, ga);
+    BnChan::load(beta, c0, be);
+    for (int64_t r = rfirst; r < R; r += kU * step) {
+        if (r != rfirst) load_rows(r);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int64_t ru = r + u * step;
@@ -337,7 +444,9 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const double* __r
 }
 
 // dy = gamma*invstd*(dz - sum_dz/R - xhat*sum_dzxh/R); also column partial sums of dy (bias grad)
-template <typename T, bool kMask>
+// kFin: sum dz / sum dz*xhat folded here from the moments' partial table (bn_fin_prologue; block 0 stores
+// dgamma / dbeta) instead of read from `sums`
+template <typename T, bool kMask, bool kFin>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
                                                            int64_t R, int C, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -345,7 +454,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ beta, int act,
                                                            const uint8_t* __restrict__ mask, float mscale,
                                                            const float* __restrict__ sums, T* __restrict__ dy,
-                                                           int64_t rows_per_blk, double* __restrict__ part) {
+                                                           int64_t rows_per_blk, double* __restrict__ part, BnFin fin) {
     constexpr int V = Vec16<T>::N;
     __shared__ double s1[2048];
     const int tpr = C / V, rpp = kThreads / tpr;
@@ -358,8 +467,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     BnChan::load(invstd, c0, is);
     BnChan::load(gamma, c0, ga);
     BnChan::load(beta, c0, be);
-    BnChan::load(sums, c0, s0);
-    BnChan::load(sums + C, c0, sx);
     float a[V];   // f32 per thread, f64 across threads and blocks (see bn_bwd_moments_kernel)
 #pragma unroll
     for (int v = 0; v < V; ++v) a[v] = 0.f;
@@ -372,7 +479,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
             ng[u] = load16_raw(da + rc * lda + c0);
         }
     };
-    if (r0 + rr < r1) fetch(r0 + rr);
+    if (r0 + rr < r1) fetch(r0 + rr);  // in flight during the finalize prologue
+    if constexpr (kFin) {
+        float* fsh = reinterpret_cast<float*>(s1 + 2 * kThreads);  // s1 is free until the closing block_colsum
+        bn_fin_prologue<false>(fin, C, fsh, fsh + 512, s1);
+        BnChan::load(fsh, c0, s0);
+        BnChan::load(fsh + 512, c0, sx);
+        __syncthreads();  // every thread has its sums before block_colsum reuses s1
+    } else {
+        BnChan::load(sums, c0, s0);
+        BnChan::load(sums + C, c0, sx);
+    }
     for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
         uint4 rx[kUb], rg[kUb];
 #pragma unroll
@@ -435,6 +552,19 @@ struct Folded {
 Folded fold_parts(hipStream_t s, const double* part, int nrows, int ncols, Ws ws) {
     if (nrows <= kFoldMin || !ws.p || ws.bytes < fold_bytes(ncols)) return Folded{part, nrows};
     int G = std::min(kFoldRows, cdiv(nrows, 64));  // >= 64 rows per fold block: one 4-load round per wave
+    const int rp = cdiv(nrows, G);
+    G = cdiv(nrows, rp);
+    double* out = reinterpret_cast<double*>(ws.p);
+    HLMC_BN_PROBED(s, 8.0 * ((double)nrows + G) * ncols,
+                   (parts_fold_kernel<<<dim3(cdiv(ncols, 64), G), 256, 0, s>>>(part, nrows, ncols, rp, out)));
+    return Folded{out, G};
+}
+// Fold to at most maxrows rows (a consumer-side finalize reads <= fin_max_rows(C) rows); tables already that
+// short are returned as they are unless `copy` (the consumer overwrites the table).
+Folded fold_parts_to(hipStream_t s, const double* part, int nrows, int ncols, Ws ws, int maxrows, bool copy = false) {
+    if (nrows <= maxrows && !copy) return Folded{part, nrows};
+    if (!ws.p || ws.bytes < (size_t)maxrows * ncols * sizeof(double)) return Folded{nullptr, 0};
+    int G = maxrows;
     const int rp = cdiv(nrows, G);
     G = cdiv(nrows, rp);
     double* out = reinterpret_cast<double*>(ws.p);
@@ -968,11 +1098,55 @@ int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const
     const unsigned g = grid_for(R, rpp * kU);
     const double by = 2.0 * sizeof(T) * R * C;
     if (mask)
-        HLMC_BN_PROBED(s, by, (bn_act_kernel<T, true><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act, mask,
-                                                                            mscale, a, lda)));
+        HLMC_BN_PROBED(s, by, (bn_act_kernel<T, true, false><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act,
+                                                                                   mask, mscale, a, lda, BnFin{})));
     else
-        HLMC_BN_PROBED(s, by, (bn_act_kernel<T, false><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act,
-                                                                             mask, mscale, a, lda)));
+        HLMC_BN_PROBED(s, by, (bn_act_kernel<T, false, false><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta,
+                                                                                    act, mask, mscale, a, lda, BnFin{})));
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+template <typename T>
+int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, const double* part, int nparts, float* mean, float* invstd,
+                 float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, const float* gamma,
+                 const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda, Ws ws) {
+    HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act: output row stride must be a multiple of 16 bytes");
+    Ws fw = ws;
+    if (!part) {  // no statistics from the producer: a moments pass into ws first
+        const int nblk = bn_blocks(R, C);
+        HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
+        double* p = reinterpret_cast<double*>(ws.p);
+        HLMC_BN_PROBED(s, (double)sizeof(T) * R * C + 16.0 * nblk * C,
+                       (col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), p)));
+        HLMC_LAUNCHED();
+        part = p;
+        nparts = nblk;
+        fw = ws_from(ws, bn_fold_off(R, C));
+    }
+    Folded f = C <= 512 ? fold_parts_to(s, part, nparts, 2 * C, fw, fin_max_rows(C)) : Folded{nullptr, 0};
+    if (!f.p) {  // wide channels / no fold space: separate finalize
+        const Folded f2 = fold_parts(s, part, nparts, 2 * C, fw);
+        HLMC_BN_PROBED(s, 16.0 * f2.rows * C,
+                       (bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f2.p, f2.rows, C, R, mean, invstd, run_mean,
+                                                                        run_var, nbt, momentum, eps)));
+        HLMC_LAUNCHED();
+        return bn_act<T>(s, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
+    }
+    BnFin fin;
+    fin.part = f.p; fin.rows = f.rows; fin.R = R;
+    fin.mean = mean; fin.invstd = invstd; fin.rmean = run_mean; fin.rvar = run_var; fin.nbt = nbt;
+    fin.momentum = momentum; fin.eps = eps;
+    const int rpp = kThreads / (C / Vec16<T>::N);
+    const unsigned g = grid_for(R, rpp * kU);
+    const double by = 2.0 * sizeof(T) * R * C + 16.0 * f.rows * C;
+    if (mask)
+        HLMC_BN_PROBED(s, by, (bn_act_kernel<T, true, true><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act,
+                                                                                  mask, mscale, a, lda, fin)));
+    else
+        HLMC_BN_PROBED(s, by, (bn_act_kernel<T, false, true><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta,
+                                                                                   act, mask, mscale, a, lda, fin)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -989,6 +1163,7 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
     double* part = reinterpret_cast<double*>(ws.p);
     float* sums = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
     const Ws fw = ws_from(ws, bn_fold_off(R, C));
+    Folded fin{nullptr, 0};
     if (fused && fused->nparts > 0) {  // moments came with the producing GEMM's epilogue
         HLMC_CHECK_ARG(lda == C && !mask && act == 0, "bn_act_bwd: fused moments need a dense lrelu layer");
         const Folded f = fold_parts(s, fused->part, fused->nparts, 2 * C, fw);
@@ -1001,16 +1176,28 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
                        (k<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb,
                                                     part)));
         HLMC_LAUNCHED();
-        const Folded f = fold_parts(s, part, nblk, 2 * C, fw);
-        HLMC_BN_PROBED(s, 16.0 * f.rows * C,
-                       (bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums)));
-        HLMC_LAUNCHED();
+        // the apply kernel folds the (<= fin_max_rows(C)-row) table itself: no finalize launch
+        // (without bias_part the apply kernel writes its bias partials over `part`: fold into fw even when short)
+        fin = C <= 512 ? fold_parts_to(s, part, nblk, 2 * C, fw, fin_max_rows(C), bias_part == nullptr)
+                       : Folded{nullptr, 0};
+        if (!fin.p) {
+            const Folded f = fold_parts(s, part, nblk, 2 * C, fw);
+            HLMC_BN_PROBED(s, 16.0 * f.rows * C,
+                           (bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums)));
+            HLMC_LAUNCHED();
+        }
     }
     double* bpart = bias_part ? bias_part : part;
-    auto ka = mask ? bn_bwd_apply_kernel<T, true> : bn_bwd_apply_kernel<T, false>;
+    BnFin bf;
+    if (fin.p) {
+        bf.part = fin.p; bf.rows = fin.rows; bf.dgamma = dgamma; bf.dbeta = dbeta;
+    }
+    HLMC_CHECK_ARG(!fin.p || fin.p != bpart, "bn_act_bwd: the folded table aliases the bias partials");
+    auto ka = mask ? (fin.p ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
+                   : (fin.p ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
     HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C + 8.0 * nblk * C,
                    (ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
-                                                 dy, rpb, bpart)));
+                                                 dy, rpb, bpart, bf)));
     HLMC_LAUNCHED();
     if (dbias && !bias_part) {
         const Folded f = fold_parts(s, part, nblk, C, fw);
@@ -1288,6 +1475,9 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
                              float, Ws);                                                                              \
     template int bn_act<T>(hipStream_t, const T*, int64_t, int, const float*, const float*, const float*, const float*, \
                            int, const uint8_t*, float, T*, int);                                                      \
+    template int bn_act_train<T>(hipStream_t, const T*, int64_t, int, const double*, int, float*, float*, float*,    \
+                                 float*, int64_t*, float, float, const float*, const float*, int, const uint8_t*, float, \
+                                 T*, int, Ws);                                                                       \
     template int bn_act_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,          \
                                const float*, const float*, int, const uint8_t*, float, T*, float*, float*, float*, Ws, \
                                const BnBwdFuse*, double*);                                                           \

@@ -373,6 +373,14 @@ class NetT : public NetBase {
             return f(q, sc);
         });
     }
+    // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
+    static bool tail_on_main() {
+        static const bool on = [] {
+            const char* e = std::getenv("HLMC_TAIL_MAIN");
+            return !(e && e[0] == '0');
+        }();
+        return on;
+    }
     // fused BN-backward moments request for the GEMM that writes the grad of a BN layer's output
     // Off by default: measured on MI355X (scripts/gpu_ab_env.sh, 3 alternating rounds) the epilogue's extra
     // y reads in the low-occupancy DMA GEMMs plus the finalize over phases x M-tiles partial rows cost more
@@ -473,7 +481,14 @@ class NetT : public NetBase {
             HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
                             &fuse, reinterpret_cast<double*>(ws + enc.bpart[l]), true));
             float* gw = G[enc.w[l]];
-            if (l == 0) {
+            if (l == 0 && tail_on_main()) {
+                // the last weight gradient of backward: on the main stream, which would otherwise only wait for
+                // the weight-gradient stream here (that stream is still reducing layer 1's gradient)
+                const PendingBias pb = pend_bias;
+                pend_bias = PendingBias{};
+                if (pb.bp) HLMC_TRY(ops::colsum_finalize(s, pb.bp, pb.np, pb.C, pb.gb, scratch));
+                HLMC_TRY(ops::wgrad_c1<T>(s, dy, B, ho, wo, co, audio, gw, scratch));
+            } else if (l == 0) {
                 HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
             } else {
                 const T* xin = AT(enc.a[l - 1]);

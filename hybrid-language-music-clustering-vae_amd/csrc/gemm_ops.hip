@@ -10,9 +10,9 @@ namespace hlmc {
 namespace {
 
 // split-K grid targets (A/B on the bench step, scripts in DESIGN.md §8): NT (forward / data-gradient convs,
-// linears) 256 = one block per CU: 94.7k vs 93.3k at 512, 92.1k at 128; TN (weight gradients) 512: 93.2k vs
-// 92.8k at 1024, 90.7k at 2048
-constexpr int kNtTargetBlocks = 256;
+// linears) 512: 101.8k vs 101.2k at 256 (round 2, after the small split-K grids moved to the LDS-DMA ring;
+// round 1 measured 256 ahead of 512 and 128); TN (weight gradients) 512: 93.2k vs 92.8k at 1024, 90.7k at 2048
+constexpr int kNtTargetBlocks = 512;
 constexpr int kTnTargetBlocks = 512;
 constexpr int kTnLongK = 131072;
 constexpr int kXcdRemapDefault = probe::kWgradS2 | probe::kLinearWgrad;  // measured: helps the TN (wgrad) family, hurts sub-pixel

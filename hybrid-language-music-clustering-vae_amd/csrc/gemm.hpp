@@ -432,8 +432,12 @@ __device__ __forceinline__ int nt_lds_chunk(int row, int c) {
 }
 
 // ============================================================================ NT main loop
+// ploop > 1: the grid has one y-slice and every block runs all ploop phases of its tile in turn (the sub-pixel
+// phases of one M-tile gather overlapping low-res rows: the later phases find them in L2 instead of every
+// phase's blocks streaming the whole input again).
 template <typename T, int BM, int BN, int WM, int WN, int KCH, class AL, class BL, class EP>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap) {
+__global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap,
+                                                      int ploop) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;  // LDS rows of KCH 16-byte chunks, chunk positions swizzled (nt_lds_chunk)
     constexpr int WAVES_N = BN / WN;
@@ -448,7 +452,15 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
     const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
     const int tiles_n = (N + BN - 1) / BN;
     NT_BLOCK_COORDS();
-    al.set_phase(phase); bl.set_phase(phase); ep.set_phase(phase); ep.set_split(bz);
+    typename AL::Row arow[AR];   // row preparation does not depend on the phase
+    typename BL::Row brow[BR];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) arow[i] = al.prep(m0 + ((tid + i * 256) / KCH));
+#pragma unroll
+    for (int i = 0; i < BR; ++i) brow[i] = bl.prep(n0 + ((tid + i * 256) / KCH));
+    const int ph0 = ploop > 1 ? 0 : phase, ph1 = ploop > 1 ? ploop : phase + 1;
+    for (int ph = ph0; ph < ph1; ++ph) {
+    al.set_phase(ph); bl.set_phase(ph); ep.set_phase(ph); ep.set_split(bz);
     const int K = al.K();
     const int kb = bz * ksplit_len;
     const int ke = min(K, kb + ksplit_len);
@@ -464,12 +476,6 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
     };
     Regs r0;  // staging set: one K-step of global loads in flight (measured: a second set, two steps in
               // flight, was 1.2-1.6x slower on every short-K layer — lower occupancy)
-    typename AL::Row arow[AR];
-    typename BL::Row brow[BR];
-#pragma unroll
-    for (int i = 0; i < AR; ++i) arow[i] = al.prep(m0 + ((tid + i * 256) / KCH));
-#pragma unroll
-    for (int i = 0; i < BR; ++i) brow[i] = bl.prep(n0 + ((tid + i * 256) / KCH));
     const int kc = (tid % KCH) * V;  // this thread's chunk column (256 % KCH == 0: the same for every i)
     auto gload = [&](Regs& rg, int k0) {
         const typename AL::Ctx ax = al.ctx(k0 + kc);
@@ -582,7 +588,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
             }
         }
         __syncthreads();
-        const int row = phase * ep.mtiles + tile_m_;
+        const int row = ph * ep.mtiles + tile_m_;
         for (int c = tid; c < BN; c += 256) {
             const int n = n0 + c;
             if (n >= N) continue;
@@ -595,6 +601,8 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
             ep.part[(int64_t)row * 2 * N + n] = a;
             ep.part[(int64_t)row * 2 * N + N + n] = q;
         }
+    }
+    if (ph + 1 < ph1) __syncthreads();  // the next phase's LDS fills / statistics scratch
     }
 }
 

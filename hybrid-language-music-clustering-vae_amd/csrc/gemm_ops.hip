@@ -81,19 +81,34 @@ inline int xcd_remap_for_site() {
     return (mask & probe::g_site.kind) ? 1 : 0;
 }
 
+// Register-path launches with 4 sub-pixel phases and >= kPloopTiles M x N tiles (>= 4 blocks per CU without
+// the phases) run the phases inside each block (gemm_nt_kernel ploop): the 64 x 64 / 32 x 32 layers' phases
+// otherwise stream the low-res input from HBM once per phase.  HLMC_SP_PLOOP=0 / 2: never / always (A/B aid).
+constexpr int kPloopTiles = 1024;
+inline bool use_ploop(int phases, int tmn, int pipe) {
+    static const int mode = [] {
+        const char* e = std::getenv("HLMC_SP_PLOOP");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (phases < 2 || pipe != 0 || mode == 0) return false;
+    return mode == 2 || tmn >= kPloopTiles;
+}
+
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class E>
 void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
                       bool long_k, int pipe) {
     const int rm = xcd_remap_for_site();
+    const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe) ? (int)grid.y : 1;
+    if (ploop > 1) grid.y = 1;
     HLMC_PROBE_BEGIN(s);
     if (pipe == 3)
         gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (pipe == 4)
         gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (long_k)
-        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     else
-        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     HLMC_PROBE_END(s);
 }
 

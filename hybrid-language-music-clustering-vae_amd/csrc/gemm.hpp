@@ -894,8 +894,13 @@ __device__ __forceinline__ int tn_swz(int row) {
 // Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_kernel).
 // PF: K-steps of global loads in flight (1: one register set; 2: two sets, the loop unrolled by two so each
 // step's loads are issued two steps ahead of their LDS store).
-template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, int PF = 1>
-__global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len, int remap) {
+// NG = 2 (PF 1 only): 512 threads as two 4-wave groups over the even / odd K-steps of the block's split, each
+// with its own LDS double buffer: twice the loads in flight per block without more split-K slabs; group 1
+// hands its accumulators to group 0 through LDS at the end (fixed order: group 0 + group 1).
+template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, int PF = 1, int NG = 1>
+__global__ __launch_bounds__(256 * NG) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len,
+                                                           int remap) {
+    static_assert(NG == 1 || PF == 1, "two wave groups only with one register set");
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;            // k rows per tile (KCH 16-byte chunks of one column)
     constexpr int ACPR = BM / V, BCPR = BN / V;  // chunks per k-row
@@ -910,10 +915,16 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
     constexpr int TM = WM / 16, TN = WN / 16;
     constexpr int ACH = BK * BM / V, BCH = BK * BN / V;
     constexpr int AR = (ACH + 255) / 256, BR = (BCH + 255) / 256;
-    __shared__ __attribute__((aligned(16))) T Ls[2][BK * LDA];
-    __shared__ __attribute__((aligned(16))) T Hs[2][BK * LDB];
+    constexpr int LSZ = BK * LDA, HSZ = BK * LDB;
+    __shared__ __attribute__((aligned(16))) T tn_sm[NG * 2 * (LSZ + HSZ)];
+    static_assert(NG == 1 || (size_t)NG * 2 * (LSZ + HSZ) * sizeof(T) >= (size_t)BM * BN * sizeof(float),
+                  "the group hand-off fits the staging buffers");
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
+    const int grp = NG > 1 ? (int)(threadIdx.x >> 8) : 0;
+    T* const Lg = tn_sm + grp * 2 * (LSZ + HSZ);  // this group's buffers: L0 H0 L1 H1
+    auto Lbuf = [&](int buf) { return Lg + buf * (LSZ + HSZ); };
+    auto Hbuf = [&](int buf) { return Lg + buf * (LSZ + HSZ) + LSZ; };
     const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
     const int tiles_n = (N + BN - 1) / BN;
     // XCD remap: the tiles of one K-split (which share L and H rows) run consecutively on one XCD
@@ -958,7 +969,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
             if (c < ACH) {
                 const int row = c / ACPR, cc = c % ACPR;
                 const int pc = SWA ? (cc ^ tn_swz<ACPR>(row)) : cc;
-                *reinterpret_cast<uint4*>(&Ls[buf][row * LDA + pc * V]) = rg.a[i];
+                *reinterpret_cast<uint4*>(&Lbuf(buf)[row * LDA + pc * V]) = rg.a[i];
             }
         }
 #pragma unroll
@@ -967,7 +978,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
             if (c < BCH) {
                 const int row = c / BCPR, cc = c % BCPR;
                 const int pc = SWB ? (cc ^ tn_swz<BCPR>(row)) : cc;
-                *reinterpret_cast<uint4*>(&Hs[buf][row * LDB + pc * V]) = rg.b[i];
+                *reinterpret_cast<uint4*>(&Hbuf(buf)[row * LDB + pc * V]) = rg.b[i];
             }
         }
     };
@@ -982,8 +993,8 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
     };
     const int g = lane >> 4, li = lane & 15;
     auto mma_step = [&](int cur) {
-        const T* A = Ls[cur];
-        const T* B = Hs[cur];
+        const T* A = Lbuf(cur);
+        const T* B = Hbuf(cur);
         if constexpr (sizeof(T) == 2) {
             // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses row q, cols 4p..4p+3;
             // lane i receives column i of the 4 rows.
@@ -1030,19 +1041,43 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
 
     if constexpr (PF == 1) {
         Regs r0;
-        if (kb < ke) {
-            gload(r0, kb);
-            lstore(r0, 0);
+        // group g takes K-steps g, g + NG, ...; both groups run the same iteration count (one barrier each)
+        const int nsteps = kb < ke ? (ke - kb + BK - 1) / BK : 0;
+        const int iters = (nsteps + NG - 1) / NG;
+        if (iters > 0) {
+            if (grp < nsteps) {
+                gload(r0, kb + grp * BK);
+                lstore(r0, 0);
+            }
             __syncthreads();
-            int it = 0;
-            for (int k0 = kb; k0 < ke; k0 += BK, ++it) {
+            for (int it = 0; it < iters; ++it) {
+                const int st = grp + it * NG;
                 const int cur = it & 1;
-                const bool more = k0 + BK < ke;
-                if (more) gload(r0, k0 + BK);
-                mma_step(cur);
+                const bool more = st + NG < nsteps;
+                if (more) gload(r0, kb + (st + NG) * BK);
+                if (st < nsteps) mma_step(cur);
                 if (more) lstore(r0, cur ^ 1);
                 __syncthreads();
             }
+        }
+        if constexpr (NG > 1) {  // group 1's accumulators to group 0 (the loop ended on a barrier: LDS is free)
+            float* red = reinterpret_cast<float*>(tn_sm);
+            if (grp == 1) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) red[((i * TN + j) * 4 + r) * 256 + tid] = acc[i][j][r];
+            }
+            __syncthreads();
+            if (grp == 1) return;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((i * TN + j) * 4 + r) * 256 + tid];
         }
     } else {
         // two register sets: x holds step k0 + BK while y's loads for k0 + 2 BK are in flight

@@ -261,8 +261,17 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
         const char* e = std::getenv("HLMC_TN_KCH8_MIN");
         return e ? std::atoi(e) : 1024;
     }();
+    static const int ng = [] {  // HLMC_TN_NG=2: two 4-wave groups per block over alternate K-steps (A/B)
+        const char* e = std::getenv("HLMC_TN_NG");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
     HLMC_PROBE_BEGIN(s);
-    if (pl.ksl >= kch8_min) {
+    if (ng == 2 && pf == 1) {
+        if (pl.ksl >= kch8_min)
+            gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, 1, 2><<<grid, 512, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        else
+            gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, 1, 2><<<grid, 512, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    } else if (pl.ksl >= kch8_min) {
         if (pf == 2)
             gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, 2><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
         else

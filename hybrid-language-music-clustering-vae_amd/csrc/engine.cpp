@@ -211,7 +211,21 @@ class NetT : public NetBase {
         }();
         use_side = !env_off;
         if (use_side && !s2) {
-            HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+            // HLMC_SIDE_CU_EVERY=k (A/B aid): the weight-gradient stream may only use every k-th CU
+            static const int cu_every = [] {
+                const char* e = std::getenv("HLMC_SIDE_CU_EVERY");
+                return e ? std::max(1, std::atoi(e)) : 1;
+            }();
+            if (cu_every > 1) {
+                int dev = 0, ncu = 0;
+                HLMC_HIP(hipGetDevice(&dev));
+                HLMC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+                std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+                for (int c = 0; c < ncu; c += cu_every) mask[c / 32] |= 1u << (c % 32);
+                HLMC_HIP(hipExtStreamCreateWithCUMask(&s2, (uint32_t)mask.size(), mask.data()));
+            } else {
+                HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+            }
             evs.resize(32);
             for (auto& e : evs) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             HLMC_HIP(hipEventCreateWithFlags(&prelate_ev, hipEventDisableTiming));

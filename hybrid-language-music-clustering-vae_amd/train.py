@@ -104,9 +104,11 @@ class Trainer:
             self._cache[B] = dict(out=out, d=d, ws=ws, lws=lws, sums=sums, coef=coef, n=(na, nt, nl))
         return self._cache[B]
 
-    def step(self, in0, in1=None, in2=None, eps=None, dropout=None):
+    def step(self, in0, in1=None, in2=None, eps=None, dropout=None, before_adam=None):
         """One optimisation step on a batch; returns device float64 sums (sum sq audio err, sum sq text err,
-        sum(1+lv-mu^2-e^lv)) from which the reference's loss tuple follows."""
+        sum(1+lv-mu^2-e^lv)) from which the reference's loss tuple follows.  before_adam (optional callable)
+        is invoked once the backward pass is enqueued, before the optimizer update (the inputs are no longer
+        read from there on: a caller may start refilling them on another stream)."""
         lib = L.lib()
         s = L.stream()
         B = in0.shape[0]
@@ -137,6 +139,8 @@ class Trainer:
                 self._allreduce_overlapped(bcast)
             else:
                 self.allreduce_grads()
+        if before_adam is not None:
+            before_adam()
         if self._graph:  # coefficients staged by prepare_step_coefficients()
             L.check(lib.hlmc_net_adam_step_dev(self.net.h, s, *self._mv, self._coef_dev.data_ptr()),
                     "hlmc_net_adam_step_dev")

@@ -341,6 +341,9 @@ class NetT : public NetBase {
                const uint8_t* mask, float mscale, T* a, int lda, const ops::ColStats* st = nullptr) {
         float* mean = AF(bb.mean);
         float* inv = AF(bb.inv);
+        if (train && !mask && small_bn(R, C))  // one launch: statistics + apply by channel-slab blocks
+            return ops::bn_small_fwd<T>(s, y, R, C, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps, P[g],
+                                        P[beta], act, a, lda);
         if (train && st && st->nparts > 0)  // statistics finalized inside the activation kernel
             return ops::bn_act_train<T>(s, y, R, C, st->part, st->nparts, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum,
                                         kBnEps, P[g], P[beta], act, mask, mscale, a, lda,
@@ -358,6 +361,9 @@ class NetT : public NetBase {
     int bn_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const BnBufs& bb, int g, int beta,
                int act, const uint8_t* mask, float mscale, T* dy, int bias, const ops::BnBwdFuse* fused = nullptr,
                double* bias_part = nullptr, bool defer_bias = false) {
+        if (!mask && small_bn(R, C) && !(fused && fused->nparts > 0))  // one launch, bias grad included
+            return ops::bn_small_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, dy, G[g],
+                                        G[beta], bias >= 0 ? G[bias] : nullptr);
         double* bp = (bias >= 0 && use_side) ? bias_part : nullptr;
         HLMC_TRY(ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask, mscale, dy,
                                     G[g], G[beta], bias >= 0 ? G[bias] : nullptr, scratch, fused, bp));
@@ -386,6 +392,16 @@ class NetT : public NetBase {
             if (pb.bp) HLMC_TRY(ops::colsum_finalize(q, pb.bp, pb.np, pb.C, pb.gb, sc));
             return f(q, sc);
         });
+    }
+    // HLMC_BN_SMALL=1: small BatchNorm layers on the single-launch channel-slab kernels.  Measured 4.3% slower
+    // (100.5k vs 105.1k, 3 alternating rounds): <= 32 blocks cannot keep enough loads in flight; the
+    // 1024-block partial-table path wins despite its extra launches.  Off by default.
+    static bool small_bn(int64_t R, int C) {
+        static const bool on = [] {
+            const char* e = std::getenv("HLMC_BN_SMALL");
+            return e && e[0] == '1';
+        }();
+        return on && ops::bn_small(R, C);
     }
     // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
     static bool tail_on_main() {
@@ -465,7 +481,9 @@ class NetT : public NetBase {
         for (int l = 0; l < 6; ++l) {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             T* y = AT(enc.y[l]);
-            ops::ColStats st{train ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
+            // GEMM-epilogue statistics only for layers the single-launch small-BN kernels do not take
+            const bool want_st = train && !small_bn((int64_t)B * (h / 2) * (w / 2), co);
+            ops::ColStats st{want_st ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
             if (l == 0)
                 HLMC_TRY(ops::conv_c1_s2<T>(s, audio, B, h, w, P[enc.w[0]], P[enc.b[0]], co, y));
             else
@@ -575,7 +593,8 @@ class NetT : public NetBase {
             const int ci = DEC_CH[l], co = DEC_CH[l + 1];
             if (l < 5) {
                 T* y = AT(dec.y[l]);
-                ops::ColStats st{train ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
+                const bool want_st = train && !small_bn((int64_t)B * 4 * h * w, co);
+                ops::ColStats st{want_st ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
                 HLMC_TRY(ops::subpixel<T>(s, x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co, y, scratch, &st));
                 HLMC_TRY(bn_fwd(s, train, y, (int64_t)B * 4 * h * w, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0,
                                 nullptr, 1.f, AT(dec.a[l]), co, &st));

@@ -523,6 +523,193 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     block_colsum<V>(ad, tpr, C, s1, part + (int64_t)blockIdx.x * C);
 }
 
+// ---------------------------------------------------------------- small BatchNorm layers: one launch each way
+// Layers with R * C <= kSmallBnElems (the 2x2 / 4x4 / 8x8 conv layers at B = 256, the BN1d layers): block b owns
+// channels [b * CPB, (b + 1) * CPB) over ALL R rows, so nothing crosses blocks (no partial table, fold or
+// finalize launch): pass 1 reduces the channels' statistics (per-thread accumulators, then the block's fixed
+// xor-shuffle / LDS tree), pass 2 walks the rows again (L2-resident) and applies.  Deterministic.
+constexpr int64_t kSmallBnElems = (int64_t)1 << 21;
+inline bool bn_small_ok(int64_t R, int C) { return R * C <= kSmallBnElems && R > 0; }
+template <typename T>
+inline int bn_small_cpb(int C) { return std::max(Vec16<T>::N, std::min(C, C / 32)); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_small_fwd_kernel(const T* __restrict__ y, int64_t R, int C, int cpb,
+                                                           float* __restrict__ mean, float* __restrict__ invstd,
+                                                           float* __restrict__ rmean, float* __restrict__ rvar,
+                                                           int64_t* __restrict__ nbt, float momentum, float eps,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, int act,
+                                                           T* __restrict__ a, int lda) {
+    constexpr int V = Vec16<T>::N;
+    __shared__ double red[4 * 512];
+    __shared__ double st[2][512];
+    __shared__ float fm[512], fi[512];
+    const int gpr = cpb / V, rpp = kThreads / gpr;
+    const int tid = threadIdx.x, cg = tid % gpr, rr = tid / gpr;
+    const int cb = blockIdx.x * cpb, c0 = cb + cg * V;
+    double sa[V], sb[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) sa[v] = sb[v] = 0.0;
+    for (int64_t r = rr; r < R; r += kU * rpp) {
+        uint4 raw[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) raw[u] = load16_raw(y + min(r + u * rpp, R - 1) * C + c0);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (r + u * rpp >= R) break;
+            float x[V];
+            cvt16_f32<T>(raw[u], x);
+#pragma unroll
+            for (int v = 0; v < V; ++v) { sa[v] += x[v]; sb[v] += (double)x[v] * x[v]; }
+        }
+    }
+    block_colsum<V>(sa, gpr, cpb, red, st[0]);
+    __syncthreads();
+    block_colsum<V>(sb, gpr, cpb, red, st[1]);
+    __syncthreads();
+    for (int j = tid; j < cpb; j += kThreads) {
+        const int c = cb + j;
+        const double m = st[0][j] / (double)R;
+        double var = st[1][j] / (double)R - m * m;
+        if (var < 0.0) var = 0.0;
+        const float mf = (float)m, inv = (float)(1.0 / sqrt(var + (double)eps));
+        fm[j] = mf;
+        fi[j] = inv;
+        mean[c] = mf;
+        invstd[c] = inv;
+        if (rmean) {
+            const double unb = R > 1 ? var * (double)R / (double)(R - 1) : var;
+            rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * m);
+            rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
+        }
+        if (c == 0 && nbt) nbt[0] += 1;
+    }
+    __syncthreads();
+    float mu[V], is[V], ga[V], be[V];
+    BnChan::load(fm, cg * V, mu);
+    BnChan::load(fi, cg * V, is);
+    BnChan::load(gamma, c0, ga);
+    BnChan::load(beta, c0, be);
+    for (int64_t r = rr; r < R; r += kU * rpp) {
+        uint4 raw[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) raw[u] = load16_raw(y + min(r + u * rpp, R - 1) * C + c0);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t ru = r + u * rpp;
+            if (ru >= R) break;
+            float x[V], o[V];
+            cvt16_f32<T>(raw[u], x);
+#pragma unroll
+            for (int v = 0; v < V; ++v) o[v] = act_fwd((x[v] - mu[v]) * is[v] * ga[v] + be[v], act);
+            store16_f32(a + ru * lda + c0, o);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_small_bwd_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
+                                                           int64_t R, int C, int cpb, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, int act,
+                                                           T* __restrict__ dy, float* __restrict__ dgamma,
+                                                           float* __restrict__ dbeta, float* __restrict__ dbias) {
+    constexpr int V = Vec16<T>::N;
+    __shared__ double red[4 * 512];
+    __shared__ double st[2][512];
+    const int gpr = cpb / V, rpp = kThreads / gpr;
+    const int tid = threadIdx.x, cg = tid % gpr, rr = tid / gpr;
+    const int cb = blockIdx.x * cpb, c0 = cb + cg * V;
+    float mu[V], is[V], ga[V], be[V];
+    BnChan::load(mean, c0, mu);
+    BnChan::load(invstd, c0, is);
+    BnChan::load(gamma, c0, ga);
+    BnChan::load(beta, c0, be);
+    float fa[V], fb[V];  // f32 per thread, f64 across threads (as bn_bwd_moments_kernel)
+#pragma unroll
+    for (int v = 0; v < V; ++v) fa[v] = fb[v] = 0.f;
+    for (int64_t r = rr; r < R; r += kUb * rpp) {
+        uint4 rx[kUb], rg[kUb];
+#pragma unroll
+        for (int u = 0; u < kUb; ++u) {
+            const int64_t rc = min(r + u * rpp, R - 1);
+            rx[u] = load16_raw(y + rc * C + c0);
+            rg[u] = load16_raw(da + rc * lda + c0);
+        }
+#pragma unroll
+        for (int u = 0; u < kUb; ++u) {
+            if (r + u * rpp >= R) break;
+            float x[V], g[V];
+            cvt16_f32<T>(rx[u], x);
+            cvt16_f32<T>(rg[u], g);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const float xh = (x[v] - mu[v]) * is[v];
+                const float dz = g[v] * act_grad(xh * ga[v] + be[v], act);
+                fa[v] += dz;
+                fb[v] = fmaf(dz, xh, fb[v]);
+            }
+        }
+    }
+    double da_[V], db_[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) { da_[v] = fa[v]; db_[v] = fb[v]; }
+    block_colsum<V>(da_, gpr, cpb, red, st[0]);
+    __syncthreads();
+    block_colsum<V>(db_, gpr, cpb, red, st[1]);
+    __syncthreads();
+    for (int j = tid; j < cpb; j += kThreads) {
+        dbeta[cb + j] = (float)st[0][j];
+        dgamma[cb + j] = (float)st[1][j];
+    }
+    const float invR = 1.f / (float)R;
+    float s0[V], sx[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        s0[v] = (float)st[0][cg * V + v];
+        sx[v] = (float)st[1][cg * V + v];
+    }
+    float bs[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) bs[v] = 0.f;
+    for (int64_t r = rr; r < R; r += kUb * rpp) {
+        uint4 rx[kUb], rg[kUb];
+#pragma unroll
+        for (int u = 0; u < kUb; ++u) {
+            const int64_t rc = min(r + u * rpp, R - 1);
+            rx[u] = load16_raw(y + rc * C + c0);
+            rg[u] = load16_raw(da + rc * lda + c0);
+        }
+#pragma unroll
+        for (int u = 0; u < kUb; ++u) {
+            const int64_t ru = r + u * rpp;
+            if (ru >= R) break;
+            float x[V], g[V], o[V];
+            cvt16_f32<T>(rx[u], x);
+            cvt16_f32<T>(rg[u], g);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const float xh = (x[v] - mu[v]) * is[v];
+                const float dz = g[v] * act_grad(xh * ga[v] + be[v], act);
+                o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
+            }
+            store16_f32(dy + ru * C + c0, o);
+#pragma unroll
+            for (int v = 0; v < V; ++v) bs[v] += to_f32<T>(from_f32<T>(o[v]));  // the bias grad sums the stored dy
+        }
+    }
+    if (!dbias) return;
+    double bd[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) bd[v] = bs[v];
+    __syncthreads();
+    block_colsum<V>(bd, gpr, cpb, red, st[0]);
+    __syncthreads();
+    for (int j = tid; j < cpb; j += kThreads) dbias[cb + j] = (float)st[0][j];
+}
+
 // out[c] = sum_k part[k][c] over [nblk][C] partials; grid ceil(C / 64) x 1024
 __global__ __launch_bounds__(1024) void colsum_finalize_kernel(const double* __restrict__ part, int nblk, int C,
                                                                float* out) {
@@ -1151,6 +1338,36 @@ int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, const double* part
     return HLMC_OK;
 }
 
+bool bn_small(int64_t R, int C) { return bn_small_ok(R, C) && C <= 512; }
+
+template <typename T>
+int bn_small_fwd(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean,
+                 float* run_var, int64_t* nbt, float momentum, float eps, const float* gamma, const float* beta,
+                 int act, T* a, int lda) {
+    HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_CHECK_ARG(bn_small(R, C) && lda % Vec16<T>::N == 0, "bn_small_fwd: layer too large / bad stride");
+    const int cpb = bn_small_cpb<T>(C);
+    HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C,
+                   (bn_small_fwd_kernel<T><<<C / cpb, kThreads, 0, s>>>(y, R, C, cpb, mean, invstd, run_mean, run_var,
+                                                                       nbt, momentum, eps, gamma, beta, act, a, lda)));
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+template <typename T>
+int bn_small_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean,
+                 const float* invstd, const float* gamma, const float* beta, int act, T* dy, float* dgamma,
+                 float* dbeta, float* dbias) {
+    HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_CHECK_ARG(bn_small(R, C) && lda % Vec16<T>::N == 0, "bn_small_bwd: layer too large / bad stride");
+    const int cpb = bn_small_cpb<T>(C);
+    HLMC_BN_PROBED(s, 5.0 * sizeof(T) * R * C,
+                   (bn_small_bwd_kernel<T><<<C / cpb, kThreads, 0, s>>>(da, lda, y, R, C, cpb, mean, invstd, gamma,
+                                                                       beta, act, dy, dgamma, dbeta, dbias)));
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
@@ -1475,6 +1692,10 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
                              float, Ws);                                                                              \
     template int bn_act<T>(hipStream_t, const T*, int64_t, int, const float*, const float*, const float*, const float*, \
                            int, const uint8_t*, float, T*, int);                                                      \
+    template int bn_small_fwd<T>(hipStream_t, const T*, int64_t, int, float*, float*, float*, float*, int64_t*,     \
+                                 float, float, const float*, const float*, int, T*, int);                            \
+    template int bn_small_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,     \
+                                 const float*, const float*, int, T*, float*, float*, float*);                       \
     template int bn_act_train<T>(hipStream_t, const T*, int64_t, int, const double*, int, float*, float*, float*,    \
                                  float*, int64_t*, float, float, const float*, const float*, int, const uint8_t*, float, \
                                  T*, int, Ws);                                                                       \

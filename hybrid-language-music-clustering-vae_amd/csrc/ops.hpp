@@ -89,6 +89,17 @@ size_t fold_ws(int ncols);  // scratch bytes to fold a [rows][ncols] f64 partial
 // Eval-mode statistics from running buffers.
 int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, int C, float eps, float* mean, float* invstd);
 // a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale];  act: 0 lrelu(0.01), 1 relu, 2 none
+// Small train-mode BatchNorm layers (R * C <= 2^21, C <= 512): one launch per direction, each block owning a
+// channel slab over all rows (statistics + apply; backward also writes dgamma / dbeta / dbias (nullable)).
+bool bn_small(int64_t R, int C);
+template <typename T>
+int bn_small_fwd(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean,
+                 float* run_var, int64_t* nbt, float momentum, float eps, const float* gamma, const float* beta,
+                 int act, T* a, int lda);
+template <typename T>
+int bn_small_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean,
+                 const float* invstd, const float* gamma, const float* beta, int act, T* dy, float* dgamma,
+                 float* dbeta, float* dbias);
 // Train-mode BatchNorm + activation with the statistics finalized inside the activation kernel: `part`
 // [nparts][2C] f64 column sums / sums of squares from the producer (nullptr: a moments pass over y into ws
 // first), folded to <= 8 rows; writes mean / invstd and updates the running statistics like bn_stats.

@@ -424,6 +424,7 @@ class NetT : public NetBase {
                               on ? reinterpret_cast<double*>(ws + bnb_part_off) : nullptr, 0};
     }
     size_t bnb_part_off = 0, bnb_part_bytes = 0;
+    ops::BnBwdFuse fuse4{};  // the decoder's last BN layer: moments from the output convT's data gradient
     void need_bnb(size_t b) { bnb_part_bytes = std::max(bnb_part_bytes, b); }
 
     // ---------------------------------------------------------------- conv encoder (6 x conv-BN-LReLU)
@@ -456,6 +457,8 @@ class NetT : public NetBase {
                 need(ops::wgrad_s2_ws<T>((int)B, h / 2, w / 2, co, ci));
             } else {
                 need(ops::wgrad_c1_ws((int)B, h / 2, w / 2, co));
+                // the edge conv's fused statistics rows + their fold (bn_act_train reads them from scratch)
+                need((size_t)(ops::conv_c1_fused_rows((int)B, h, w) + 64) * 2 * co * sizeof(double) + 256);
             }
             h /= 2;
             w /= 2;
@@ -484,8 +487,8 @@ class NetT : public NetBase {
             // GEMM-epilogue statistics only for layers the single-launch small-BN kernels do not take
             const bool want_st = train && !small_bn((int64_t)B * (h / 2) * (w / 2), co);
             ops::ColStats st{want_st ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
-            if (l == 0)
-                HLMC_TRY(ops::conv_c1_s2<T>(s, audio, B, h, w, P[enc.w[0]], P[enc.b[0]], co, y));
+            if (l == 0)  // BN statistics from the edge conv itself (no col_moments pass)
+                HLMC_TRY(ops::conv_c1_s2<T>(s, audio, B, h, w, P[enc.w[0]], P[enc.b[0]], co, y, &st));
             else
                 HLMC_TRY(ops::conv_s2<T>(s, AT(enc.a[l - 1]), B, h, w, ci, P0(enc.w[l]), P[enc.b[l]], co, y, scratch,
                                          &st));
@@ -579,6 +582,8 @@ class NetT : public NetBase {
             } else {
                 need(ops::wgrad_c1_ws((int)B, h, w, ci));
                 need(ops::colsum_ws((int)(B * 4 * h * w), 1));
+                // the output convT's data gradient carries layer 4's BN-backward moments (edge conv rows)
+                need_bnb((size_t)ops::conv_c1_fused_rows((int)B, 2 * h, 2 * w) * 2 * ci * sizeof(double));
             }
             h *= 2;
             w *= 2;
@@ -624,9 +629,13 @@ class NetT : public NetBase {
                 HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
                 return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
             }));
-            HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA));
+            // layer 4's BN-backward moments come with the edge conv that writes its output gradient
+            fuse4 = ops::BnBwdFuse{AT(dec.y[4]), AF(dec.bb[4].mean), AF(dec.bb[4].inv), P[dec.g[4]], P[dec.beta[4]],
+                                   reinterpret_cast<double*>(ws + bnb_part_off), 0};
+            HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA, nullptr,
+                                        &fuse4));
         }
-        ops::BnBwdFuse fuse{};  // layer 4's output grad comes from the single-channel edge conv (separate pass)
+        ops::BnBwdFuse fuse = fuse4;
         for (int l = 4; l >= 0; --l) {
             const int ci = DEC_CH[l], co = DEC_CH[l + 1];
             const int hl = hs[l], wl = ws_[l];

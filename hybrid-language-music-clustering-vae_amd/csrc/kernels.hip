@@ -6,12 +6,14 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 namespace hlmc {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kC1FusedBlocks = 4096;  // grid of the statistics-fused edge conv (partial rows it writes)
 
 inline int grid_for(int64_t n, int per_block = kThreads, int cap = 8192) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(cap, (n + per_block - 1) / per_block));
@@ -784,12 +786,35 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
 // y[b, oh, ow, co] = bias[co] + sum_taps x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + tap]  (1 input channel, CO = 32)
 // Four threads per output pixel, each computing 8 channels (one 16-byte store): a wave's store instruction
 // writes 1 KB contiguous; the 9 input taps are re-read by the 4 threads from L1.
-template <typename T, int CO>
+// MODE 1 (encoder input conv): also the BatchNorm statistics of the stored outputs, one [sum | sum of squares]
+// f64 partial row per block (the col_moments pass it replaces).  MODE 2 (data gradient of the decoder's output
+// convT, which writes the gradient of the last BatchNorm layer's output): also that layer's backward moments
+// [sum dz | sum dz * xhat] (bn_bwd_moments_kernel's partial rows), with ybn / mean / invstd / gamma / beta of
+// the layer (LeakyReLU 0.01).  Both: per-thread accumulators over the grid-stride pixels, block_colsum rows.
+struct C1Fuse {
+    double* part = nullptr;
+    const void* ybn = nullptr;
+    const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
+};
+template <typename T, int CO, int MODE>
 __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
-                                                         T* __restrict__ y, FastDiv dWo, FastDiv dHo) {
+                                                         T* __restrict__ y, FastDiv dWo, FastDiv dHo, C1Fuse fz) {
     constexpr int V = Vec16<T>::N, G = CO / V;  // threads per pixel
     __shared__ float wsh[CO * 9], bsh[CO];       // per-lane channel groups: LDS broadcast reads, not global
+    __shared__ double fred[MODE ? 4 * CO : 1];
+    using Acc = typename std::conditional<MODE == 1, double, float>::type;
+    Acc fa[V], fb[V];
+    float bmu[V], bis[V], bga[V], bbe[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) fa[v] = fb[v] = Acc(0);
+    if constexpr (MODE == 2) {  // a thread's channels are fixed (the grid stride is a multiple of G)
+        const int cf = (int)((blockIdx.x * blockDim.x + threadIdx.x) % G) * V;
+        BnChan::load(fz.mean, cf, bmu);
+        BnChan::load(fz.invstd, cf, bis);
+        BnChan::load(fz.gamma, cf, bga);
+        BnChan::load(fz.beta, cf, bbe);
+    }
     for (int i = threadIdx.x; i < CO * 9; i += blockDim.x) wsh[i] = w[i];
     for (int i = threadIdx.x; i < CO; i += blockDim.x) bsh[i] = bias ? bias[i] : 0.f;
     __syncthreads();
@@ -807,6 +832,8 @@ __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict
                 const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
                 in[kh * 3 + kw] = (ih >= 0 && iw >= 0) ? x[((int64_t)b * Hi + ih) * Wi + iw] : 0.f;  // ih, iw < Hi, Wi
             }
+        uint4 yraw;
+        if constexpr (MODE == 2) yraw = load16_raw(static_cast<const T*>(fz.ybn) + (int64_t)p * CO + c0);
         float o[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) {
@@ -816,6 +843,33 @@ __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict
             o[v] = s;
         }
         store16_f32(y + (int64_t)p * CO + c0, o);
+        if constexpr (MODE == 1) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const double q = (double)to_f32<T>(from_f32<T>(o[v]));  // statistics of the stored values
+                fa[v] += q;
+                fb[v] += q * q;
+            }
+        } else if constexpr (MODE == 2) {
+            float xb[V];
+            cvt16_f32<T>(yraw, xb);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const float g = to_f32<T>(from_f32<T>(o[v]));  // the stored gradient
+                const float xh = (xb[v] - bmu[v]) * bis[v];
+                const float dz = g * (xh * bga[v] + bbe[v] > 0.f ? 1.f : 0.01f);
+                fa[v] += dz;
+                fb[v] = fmaf(dz, xh, fb[v]);
+            }
+        }
+    }
+    if constexpr (MODE != 0) {
+        double da_[V], db_[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) { da_[v] = fa[v]; db_[v] = fb[v]; }
+        block_colsum<V>(da_, G, CO, fred, fz.part + (int64_t)blockIdx.x * 2 * CO);
+        __syncthreads();
+        block_colsum<V>(db_, G, CO, fred, fz.part + (int64_t)blockIdx.x * 2 * CO + CO);
     }
 }
 
@@ -1383,10 +1437,15 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
     Folded fin{nullptr, 0};
     if (fused && fused->nparts > 0) {  // moments came with the producing GEMM's epilogue
         HLMC_CHECK_ARG(lda == C && !mask && act == 0, "bn_act_bwd: fused moments need a dense lrelu layer");
-        const Folded f = fold_parts(s, fused->part, fused->nparts, 2 * C, fw);
-        HLMC_BN_PROBED(s, 16.0 * f.rows * C,
-                       (bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums)));
-        HLMC_LAUNCHED();
+        fin = C <= 512 ? fold_parts_to(s, fused->part, fused->nparts, 2 * C, fw, fin_max_rows(C),
+                                       bias_part == nullptr)
+                       : Folded{nullptr, 0};
+        if (!fin.p) {
+            const Folded f = fold_parts(s, fused->part, fused->nparts, 2 * C, fw);
+            HLMC_BN_PROBED(s, 16.0 * f.rows * C,
+                           (bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums)));
+            HLMC_LAUNCHED();
+        }
     } else {
         auto k = mask ? bn_bwd_moments_kernel<T, true> : bn_bwd_moments_kernel<T, false>;
         HLMC_BN_PROBED(s, 2.0 * sizeof(T) * R * C + 16.0 * nblk * C,
@@ -1432,13 +1491,36 @@ int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float*
     return HLMC_OK;
 }
 
+int conv_c1_fused_rows(int B, int Hi, int Wi) {
+    return grid_for((int64_t)B * (Hi / 2) * (Wi / 2) * 4, kThreads, kC1FusedBlocks);
+}
+
 template <typename T>
-int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y) {
+int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y,
+               ColStats* st, BnBwdFuse* bf) {
     HLMC_CHECK_ARG(Co == 32 && Hi % 2 == 0 && Wi % 2 == 0, "conv_c1_s2: only Co == 32, even H/W");
     int64_t nthr = (int64_t)B * (Hi / 2) * (Wi / 2) * (32 / Vec16<T>::N);
     HLMC_CHECK_ARG(nthr < (int64_t)1 << 31, "conv_c1_s2: too many pixels");
-    conv_c1_s2_kernel<T, 32><<<grid_for(nthr, kThreads, 16384), kThreads, 0, s>>>(
-        x, B, Hi, Wi, w, bias, y, FastDiv((uint32_t)(Wi / 2)), FastDiv((uint32_t)(Hi / 2)));
+    const FastDiv dW((uint32_t)(Wi / 2)), dH((uint32_t)(Hi / 2));
+    C1Fuse fz;
+    if (st) st->nparts = 0;
+    if (bf) bf->nparts = 0;
+    if (st && st->part) {
+        // fewer, longer-running blocks: one partial row each (the fold reads them)
+        const int g = grid_for(nthr, kThreads, kC1FusedBlocks);
+        fz.part = st->part;
+        conv_c1_s2_kernel<T, 32, 1><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
+        st->nparts = g;
+    } else if (bf && bf->part) {
+        const int g = grid_for(nthr, kThreads, kC1FusedBlocks);
+        fz.part = bf->part;
+        fz.ybn = bf->y; fz.mean = bf->mean; fz.invstd = bf->invstd; fz.gamma = bf->gamma; fz.beta = bf->beta;
+        conv_c1_s2_kernel<T, 32, 2><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
+        bf->nparts = g;
+    } else {
+        conv_c1_s2_kernel<T, 32, 0><<<grid_for(nthr, kThreads, 16384), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH,
+                                                                                        fz);
+    }
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1702,7 +1784,8 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
     template int bn_act_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,          \
                                const float*, const float*, int, const uint8_t*, float, T*, float*, float*, float*, Ws, \
                                const BnBwdFuse*, double*);                                                           \
-    template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*);        \
+    template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*,        \
+                               ColStats*, BnBwdFuse*);                                                               \
     template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);          \
     template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws);                    \
     template int cast_from_f32<T>(hipStream_t, const float*, T*, int64_t);                                           \

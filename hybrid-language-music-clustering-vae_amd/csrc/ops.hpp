@@ -66,7 +66,9 @@ size_t linear_wgrad_ws(int Mb, int N, int K);
 // ---------------------------------------------------------------- edge convs with one channel (kernels.hip)
 // y[B,Hi/2,Wi/2,32] = sum_taps x[B,Hi,Wi] * w[co*9+tap] (+ bias)  (conv1 fwd, convT6 dgrad)
 template <typename T>
-int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y);
+int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y,
+               ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
+int conv_c1_fused_rows(int B, int Hi, int Wi);  // partial rows conv_c1_s2 writes with st / bf
 // y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel)
 template <typename T>
 int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y);

@@ -71,6 +71,8 @@ _SIGS = {
     "hlmc_loss_sums": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "hlmc_loss_backward": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                                    c_vp, c_vp, c_vp]),
+    "hlmc_loss_sums_backward": (c_int, [c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
+                                        c_vp, c_vp, c_vp, c_vp, c_vp]),
     "hlmc_adam_scratch_bytes": (c_i64, [c_int]),
     "hlmc_adam_step": (c_int, [c_vp, c_int, P_vp, P_vp, P_vp, P_vp, P_i64, c_f32, c_f32, c_f32, c_f32, c_f32,
                                c_int, c_vp]),

@@ -325,6 +325,14 @@ int hlmc_loss_backward(void* stream, const float* ra, const float* a, int64_t na
                        (nl == 0 || (mu && lv && dmu && dlv)), "bad arguments");
     return ops::vae_loss_bwd(S(stream), ra, a, na, dra, rt, t, nt, drt, mu, lv, nl, coef, dmu, dlv);
 }
+int hlmc_loss_sums_backward(void* stream, const float* ra, const float* a, int64_t na, float* dra, const float* rt,
+                            const float* t, int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl,
+                            const float* coef, float* dmu, float* dlv, double* sums3, void* ws) {
+    HLMC_CHECK_ARG(coef && sums3 && ws && (na == 0 || (ra && a && dra)) && (nt == 0 || (rt && t && drt)) &&
+                       (nl == 0 || (mu && lv && dmu && dlv)), "bad arguments");
+    return ops::vae_sums_bwd(S(stream), ra, a, na, dra, rt, t, nt, drt, mu, lv, nl, coef, dmu, dlv, sums3,
+                             Ws{reinterpret_cast<float*>(ws), ops::vae_sums_ws(na, nt, nl)});
+}
 int64_t hlmc_adam_scratch_bytes(int) { return 0; }
 int hlmc_adam_step(void* stream, int n, float* const* p, const float* const* g, float* const* m, float* const* v,
                    const int64_t* numel, float lr, float b1, float b2, float eps, float wd, int step, void* scratch) {

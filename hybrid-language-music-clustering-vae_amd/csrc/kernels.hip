@@ -1112,6 +1112,47 @@ __global__ __launch_bounds__(256) void vae_sums_kernel(const float* __restrict__
         part[blockIdx.x * 3 + threadIdx.x] = s;
     }
 }
+// loss sums and their gradient in one pass over (ra, a), (rt, t), (mu, lv): vae_sums_kernel's partial rows plus
+// vae_bwd_kernel's outputs (the gradient does not depend on the sums: d ra = ca (ra - a), ...)
+__global__ __launch_bounds__(256) void vae_sums_bwd_kernel(const float* __restrict__ ra, const float* __restrict__ a,
+                                                           int64_t na, float* __restrict__ dra,
+                                                           const float* __restrict__ rt, const float* __restrict__ t,
+                                                           int64_t nt, float* __restrict__ drt,
+                                                           const float* __restrict__ mu, const float* __restrict__ lv,
+                                                           int64_t nl, const float* __restrict__ coef,
+                                                           float* __restrict__ dmu, float* __restrict__ dlv,
+                                                           double* __restrict__ part) {
+    __shared__ double red[3][4];
+    const float ca = coef[0], ct = coef[1], ck = coef[2];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = i0; i < na; i += stride) {
+        const float d = ra[i] - a[i];
+        s0 += (double)d * d;
+        dra[i] = ca * d;
+    }
+    for (int64_t i = i0; i < nt; i += stride) {
+        const float d = rt[i] - t[i];
+        s1 += (double)d * d;
+        drt[i] = ct * d;
+    }
+    for (int64_t i = i0; i < nl; i += stride) {
+        const float e = expf(lv[i]);
+        s2 += (double)(1.f + lv[i] - mu[i] * mu[i] - e);
+        dmu[i] = ck * mu[i];
+        dlv[i] = -0.5f * ck * (1.f - e);
+    }
+    s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { red[0][w] = s0; red[1][w] = s1; red[2][w] = s2; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        double s = 0.0;
+        for (int k = 0; k < 4; ++k) s += red[threadIdx.x][k];
+        part[blockIdx.x * 3 + threadIdx.x] = s;
+    }
+}
 __global__ __launch_bounds__(256) void vae_sums_finalize_kernel(const double* __restrict__ part, int nblk, double* out) {
     __shared__ double sh[256];
     const int j = blockIdx.x;
@@ -1705,6 +1746,19 @@ int vae_loss_bwd(hipStream_t s, const float* ra, const float* a, int64_t na, flo
     int64_t n = std::max(na, std::max(nt, nl));
     vae_bwd_kernel<<<grid_for(n, kThreads, 4096), kThreads, 0, s>>>(ra, a, na, dra, rt, t, nt, drt, mu, lv, nl, coef,
                                                                      dmu, dlv);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+int vae_sums_bwd(hipStream_t s, const float* ra, const float* a, int64_t na, float* dra, const float* rt, const float* t,
+                 int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl, const float* coef, float* dmu,
+                 float* dlv, double* out3, Ws ws) {
+    int nblk = vae_blocks(std::max(na, std::max(nt, nl)));
+    HLMC_CHECK_ARG(ws.bytes >= vae_sums_ws(na, nt, nl), "loss workspace");
+    double* part = reinterpret_cast<double*>(ws.p);
+    vae_sums_bwd_kernel<<<nblk, kThreads, 0, s>>>(ra, a, na, dra, rt, t, nt, drt, mu, lv, nl, coef, dmu, dlv, part);
+    HLMC_LAUNCHED();
+    vae_sums_finalize_kernel<<<3, 256, 0, s>>>(part, nblk, out3);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -160,6 +160,10 @@ size_t vae_sums_ws(int64_t na, int64_t nt, int64_t nl);
 int vae_loss_bwd(hipStream_t s, const float* ra, const float* a, int64_t na, float* dra, const float* rt, const float* t,
                  int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl, const float* coef, float* dmu,
                  float* dlv);
+// both in one pass: the sums (out3) and the gradients
+int vae_sums_bwd(hipStream_t s, const float* ra, const float* a, int64_t na, float* dra, const float* rt, const float* t,
+                 int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl, const float* coef, float* dmu,
+                 float* dlv, double* out3, Ws ws);
 
 // ---------------------------------------------------------------- optimizer / packing (kernels.hip)
 struct AdamArgs {

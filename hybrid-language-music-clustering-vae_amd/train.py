@@ -127,11 +127,12 @@ class Trainer:
             bcast = self._broadcast_buffers_after_forward()
         na, nt, nl = c["n"]
         rt, t = out.get("recon_text"), (in1 if nt else None)
-        L.check(lib.hlmc_loss_sums(s, L.ptr(out["recon"]), L.ptr(in0), na, L.ptr(rt), L.ptr(t), nt, L.ptr(out["mu"]),
-                                   L.ptr(out["logvar"]), nl, c["sums"].data_ptr(), c["lws"].data_ptr()), "hlmc_loss_sums")
-        L.check(lib.hlmc_loss_backward(s, L.ptr(out["recon"]), L.ptr(in0), na, L.ptr(d["recon"]), L.ptr(rt), L.ptr(t),
-                                       nt, L.ptr(d.get("recon_text")), L.ptr(out["mu"]), L.ptr(out["logvar"]), nl,
-                                       c["coef"].data_ptr(), L.ptr(d["mu"]), L.ptr(d["logvar"])), "hlmc_loss_backward")
+        # the loss sums and their gradient in one pass (hlmc_loss_sums + hlmc_loss_backward fused)
+        L.check(lib.hlmc_loss_sums_backward(s, L.ptr(out["recon"]), L.ptr(in0), na, L.ptr(d["recon"]), L.ptr(rt),
+                                            L.ptr(t), nt, L.ptr(d.get("recon_text")), L.ptr(out["mu"]),
+                                            L.ptr(out["logvar"]), nl, c["coef"].data_ptr(), L.ptr(d["mu"]),
+                                            L.ptr(d["logvar"]), c["sums"].data_ptr(), c["lws"].data_ptr()),
+                "hlmc_loss_sums_backward")
         L.check(lib.hlmc_net_backward(self.net.h, s, B, L.ptr(d["recon"]), L.ptr(d.get("recon_text")), L.ptr(d["mu"]),
                                       L.ptr(d["logvar"]), c["ws"].data_ptr()), "hlmc_net_backward")
         if self.distributed:

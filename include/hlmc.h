@@ -198,6 +198,11 @@ int64_t hlmc_loss_workspace(int64_t na, int64_t nt, int64_t nl);
 int hlmc_loss_backward(void* stream, const float* ra, const float* a, int64_t na, float* dra, const float* rt,
                        const float* t, int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl,
                        const float* coef, float* dmu, float* dlv);
+/* hlmc_loss_sums and hlmc_loss_backward in one pass over the inputs (same outputs; the gradient does not
+ * depend on the sums).  Used by the fused train step; ws as for hlmc_loss_sums. */
+int hlmc_loss_sums_backward(void* stream, const float* ra, const float* a, int64_t na, float* dra, const float* rt,
+                            const float* t, int64_t nt, float* drt, const float* mu, const float* lv, int64_t nl,
+                            const float* coef, float* dmu, float* dlv, double* sums3, void* ws);
 
 /* ============================================================== optimizer
  * torch.optim.Adam(lr, betas, eps, weight_decay) step (src/Convolutional_VAE.py:208,235) over

@@ -185,3 +185,40 @@ def test_edge_convs(cuda, ws, dt):
     L.check(L.lib().hlmc_op_wgrad_c1(L.stream(), code, dyd.data_ptr(), B, H // 2, W // 2, 32, imgd.data_ptr(),
                                      dW.data_ptr(), ws.data_ptr(), WS_BYTES))
     assert rel(dW, refw) < 1e-5
+
+
+@pytest.mark.parametrize("nt", [0, 4 * 384])
+def test_loss_sums_backward_fused_equals_separate(cuda, nt):
+    """hlmc_loss_sums_backward (one pass) == hlmc_loss_sums + hlmc_loss_backward, bit for bit (same grid, same
+    per-element arithmetic and partial order)."""
+    g = torch.Generator(device=cuda).manual_seed(11)
+    na, nl = 4 * 128 * 128, 4 * 128
+    ra, a = torch.randn(na, device=cuda, generator=g), torch.randn(na, device=cuda, generator=g)
+    rt, t = torch.randn(max(nt, 1), device=cuda, generator=g), torch.randn(max(nt, 1), device=cuda, generator=g)
+    mu, lv = torch.randn(nl, device=cuda, generator=g), torch.randn(nl, device=cuda, generator=g) * 0.3
+    coef = torch.tensor([2.0, 0.7, 4.0], device=cuda)
+    lib = L.lib()
+    ws = torch.empty(int(lib.hlmc_loss_workspace(na, nt, nl)), dtype=torch.uint8, device=cuda)
+    outs = []
+    for fused in (False, True):
+        sums = torch.zeros(3, dtype=torch.float64, device=cuda)
+        dra, drt = torch.empty_like(ra), torch.empty_like(rt)
+        dmu, dlv = torch.empty_like(mu), torch.empty_like(lv)
+        ptr_t = (rt.data_ptr(), t.data_ptr(), drt.data_ptr()) if nt else (None, None, None)
+        if fused:
+            L.check(lib.hlmc_loss_sums_backward(L.stream(), ra.data_ptr(), a.data_ptr(), na, dra.data_ptr(), ptr_t[0],
+                                                ptr_t[1], nt, ptr_t[2], mu.data_ptr(), lv.data_ptr(), nl,
+                                                coef.data_ptr(), dmu.data_ptr(), dlv.data_ptr(), sums.data_ptr(),
+                                                ws.data_ptr()))
+        else:
+            L.check(lib.hlmc_loss_sums(L.stream(), ra.data_ptr(), a.data_ptr(), na, ptr_t[0], ptr_t[1], nt,
+                                       mu.data_ptr(), lv.data_ptr(), nl, sums.data_ptr(), ws.data_ptr()))
+            L.check(lib.hlmc_loss_backward(L.stream(), ra.data_ptr(), a.data_ptr(), na, dra.data_ptr(), ptr_t[0],
+                                           ptr_t[1], nt, ptr_t[2], mu.data_ptr(), lv.data_ptr(), nl, coef.data_ptr(),
+                                           dmu.data_ptr(), dlv.data_ptr()))
+        outs.append((sums.cpu(), dra.cpu(), drt.cpu() if nt else None, dmu.cpu(), dlv.cpu()))
+    for x, y in zip(*outs):
+        if x is not None:
+            assert torch.equal(x, y)
+    ref = float(((ra - a).double() ** 2).sum())
+    assert abs(float(outs[1][0][0]) - ref) <= 1e-9 * ref

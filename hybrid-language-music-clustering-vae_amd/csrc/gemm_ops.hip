@@ -90,8 +90,12 @@ inline bool use_ploop(int phases, int tmn, int pipe) {
         const char* e = std::getenv("HLMC_SP_PLOOP");
         return e ? std::atoi(e) : 1;
     }();
+    static const int min_tiles = [] {  // HLMC_SP_PLOOP_TILES: the tile threshold (A/B aid)
+        const char* e = std::getenv("HLMC_SP_PLOOP_TILES");
+        return e ? std::atoi(e) : kPloopTiles;
+    }();
     if (phases < 2 || pipe != 0 || mode == 0) return false;
-    return mode == 2 || tmn >= kPloopTiles;
+    return mode == 2 || tmn >= min_tiles;
 }
 
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class E>

@@ -425,6 +425,19 @@ class NetT : public NetBase {
     }
     size_t bnb_part_off = 0, bnb_part_bytes = 0;
     ops::BnBwdFuse fuse4{};  // the decoder's last BN layer: moments from the output convT's data gradient
+    ops::BnApply dec_ba{};       // ... and its forward BN + LeakyReLU applied inside the output convT
+    bool dec_a4_fused = false;   // the last full forward left a4 unmaterialised (backward reads y4 instead)
+    // HLMC_LAST_BN_CONSUMER=1: the output convT and its weight gradient apply the decoder's last BN + LeakyReLU
+    // to y4 themselves (no bn_act pass, no a4 map).  Parity green, but measured 3.3% slower (101.7k vs 105.0k,
+    // 4 alternating rounds): the convT re-reads every input 2.25 times and pays the per-channel transform (LDS
+    // parameter reads + VALU) on each read, more than the 26 us streaming pass it removes.  Off by default.
+    static bool last_bn_in_consumers() {
+        static const bool on = [] {
+            const char* e = std::getenv("HLMC_LAST_BN_CONSUMER");
+            return e && e[0] == '1';
+        }();
+        return on;
+    }
     void need_bnb(size_t b) { bnb_part_bytes = std::max(bnb_part_bytes, b); }
 
     // ---------------------------------------------------------------- conv encoder (6 x conv-BN-LReLU)
@@ -598,14 +611,26 @@ class NetT : public NetBase {
             const int ci = DEC_CH[l], co = DEC_CH[l + 1];
             if (l < 5) {
                 T* y = AT(dec.y[l]);
-                const bool want_st = train && !small_bn((int64_t)B * 4 * h * w, co);
+                const int64_t R = (int64_t)B * 4 * h * w;
+                const bool want_st = train && !small_bn(R, co);
                 ops::ColStats st{want_st ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
                 HLMC_TRY(ops::subpixel<T>(s, x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co, y, scratch, &st));
-                HLMC_TRY(bn_fwd(s, train, y, (int64_t)B * 4 * h * w, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0,
-                                nullptr, 1.f, AT(dec.a[l]), co, &st));
-                x = AT(dec.a[l]);
+                if (l == 4 && train && st.nparts > 0 && last_bn_in_consumers()) {
+                    // the output convT applies this layer's BN + LeakyReLU itself (no bn_act pass, no a4 map)
+                    dec_ba = ops::BnApply{st.part, st.nparts, R, AF(dec.bb[4].mean), AF(dec.bb[4].inv), RM[dec.bn[4]],
+                                          RV[dec.bn[4]], NBT[dec.bn[4]], kBnMomentum, kBnEps, P[dec.g[4]],
+                                          P[dec.beta[4]], after_parts(st.part, (size_t)st.nparts * 2 * co)};
+                    dec_a4_fused = true;
+                    x = y;
+                } else {
+                    HLMC_TRY(bn_fwd(s, train, y, R, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f,
+                                    AT(dec.a[l]), co, &st));
+                    if (l == 4) dec_a4_fused = false;
+                    x = AT(dec.a[l]);
+                }
             } else {
-                HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon));
+                HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon,
+                                          dec_a4_fused ? &dec_ba : nullptr));
             }
             h *= 2;
             w *= 2;
@@ -621,12 +646,14 @@ class NetT : public NetBase {
         // last layer (1 output channel): input a4 [B, hs5, ws5, 32]
         {
             const int hl = hs[5], wl = ws_[5];
-            const T* a4 = AT(dec.a[4]);
+            // the forward did not materialise a4: the weight gradient applies the BN + LeakyReLU to y4 itself
+            const T* a4 = dec_a4_fused ? AT(dec.y[4]) : AT(dec.a[4]);
+            const ops::BnAct a4act{AF(dec.bb[4].mean), AF(dec.bb[4].inv), P[dec.g[4]], P[dec.beta[4]]};
             float* gw = G[dec.w[5]];
             float* gb = G[dec.b[5]];
             const int npix = B * hs[6] * ws_[6];
             HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) {
-                HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
+                HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc, dec_a4_fused ? &a4act : nullptr));
                 return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
             }));
             // layer 4's BN-backward moments come with the edge conv that writes its output gradient

@@ -876,12 +876,26 @@ __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict
 // y[b, oh, ow] = bias + sum_ci sum_taps x[b, ih, iw, ci] * w[ci*9 + kh*3 + kw]  (transposed, 1 output channel).
 // (Measured: one thread per output pixel beats one thread per low-res pixel computing the 2 x 2 block, whose
 // long per-accumulator FMA chains leave it latency-bound: 47 vs 61 us at B = 256.)
-template <typename T, int CI>
+// kBn: x is the PRE-BatchNorm map y of the decoder's last BN layer: its statistics are finalized here from the
+// (folded) partial table (bn_fin_prologue; block 0 stores mean / invstd / running stats) and every input value
+// goes through BN + LeakyReLU + rounding to T exactly as bn_act_kernel would have stored it.
+template <typename T, int CI, bool kBn>
 __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
-                                                       float* __restrict__ y, FastDiv dWo, FastDiv dHo) {
+                                                       float* __restrict__ y, FastDiv dWo, FastDiv dHo, BnFin fin,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta) {
     __shared__ float ws[CI * 9];
+    __shared__ float bnp[kBn ? 4 * CI : 1];
+    __shared__ double bred[kBn ? 2 * kThreads : 1];
     for (int i = threadIdx.x; i < CI * 9; i += blockDim.x) ws[i] = w[i];
+    if constexpr (kBn) {
+        bn_fin_prologue<true>(fin, CI, bnp, bnp + CI, bred);
+        for (int c = threadIdx.x; c < CI; c += blockDim.x) {
+            bnp[2 * CI + c] = gamma[c];
+            bnp[3 * CI + c] = beta[c];
+        }
+    }
     __syncthreads();
     const float b0 = bias ? bias[0] : 0.f;
     const int Ho = 2 * Hi, Wo = 2 * Wi;
@@ -906,6 +920,14 @@ __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, 
                 for (int c0 = 0; c0 < CI; c0 += V) {
                     float v[V];
                     load16_f32(src + c0, v);
+                    if constexpr (kBn) {
+#pragma unroll
+                        for (int q = 0; q < V; ++q) {
+                            const int c = c0 + q;
+                            v[q] = to_f32<T>(from_f32<T>(
+                                act_fwd((v[q] - bnp[c]) * bnp[CI + c] * bnp[2 * CI + c] + bnp[3 * CI + c], 0)));
+                        }
+                    }
 #pragma unroll
                     for (int q = 0; q < V; ++q) s = fmaf(v[q], ws[(c0 + q) * 9 + tap], s);
                 }
@@ -918,15 +940,30 @@ __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, 
 // dW[m*9+tap] partials: block = chunk of low-res rows (b,r,c); Xh single-channel high-res [B, 2Hl, 2Wl].
 // Rows are staged in LDS 256 at a time; thread (mg, rg) accumulates a 4(m) x 9(tap) register block over
 // rows rg, rg+32, ... (13 LDS reads per 36 FMAs); the 32 row-groups are combined in a fixed order.
+// BN + LeakyReLU(0.01) applied to a consumer's operand on the fly: a = T(lrelu((y - mean) * invstd * gamma + beta))
+// (bn_act_kernel's arithmetic and rounding, so the result equals the materialised activation)
+struct BnXf {
+    const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
+};
 template <typename T, int M>
 __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, int B, int Hl, int Wl,
                                                        const float* __restrict__ Xh, int rows_per_blk,
-                                                       float* __restrict__ part, FastDiv dWl, FastDiv dHl) {
+                                                       float* __restrict__ part, FastDiv dWl, FastDiv dHl, BnXf xf) {
     static_assert(M == 32, "one 8 x 4 channel tiling");
     constexpr int RC = 256;
     // one LDS block: [RC][M+1] rows + [RC][9] taps during accumulation, [32][M*9] partials afterwards
     constexpr int kAcc = RC * (M + 1) + RC * 9, kRed = 32 * M * 9;
     __shared__ float smem[kAcc > kRed ? kAcc : kRed];
+    __shared__ float xfp[4][M];  // mean / invstd / gamma / beta of L's BN layer (xf.mean set)
+    if (xf.mean) {
+        for (int c = threadIdx.x; c < M; c += blockDim.x) {
+            xfp[0][c] = xf.mean[c];
+            xfp[1][c] = xf.invstd[c];
+            xfp[2][c] = xf.gamma[c];
+            xfp[3][c] = xf.beta[c];
+        }
+        __syncthreads();
+    }
     float (*Ls)[M + 1] = reinterpret_cast<float (*)[M + 1]>(smem);
     float (*Hs)[9] = reinterpret_cast<float (*)[9]>(smem + RC * (M + 1));
     const int64_t K = (int64_t)B * Hl * Wl;
@@ -968,6 +1005,13 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, 
             const int i = threadIdx.x + u * 256, rr = i / (M / V), cg = i % (M / V);
             float v[V];
             cvt16_f32<T>(nl[u], v);
+            if (xf.mean) {
+#pragma unroll
+                for (int q = 0; q < V; ++q) {
+                    const int c = cg * V + q;
+                    v[q] = to_f32<T>(from_f32<T>(act_fwd((v[q] - xfp[0][c]) * xfp[1][c] * xfp[2][c] + xfp[3][c], 0)));
+                }
+            }
             const bool ok = kb + rr < k1;
 #pragma unroll
             for (int q = 0; q < V; ++q) Ls[rr][cg * V + q] = ok ? v[q] : 0.f;
@@ -1567,12 +1611,26 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
 }
 
 template <typename T>
-int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y) {
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y,
+             const BnApply* ba) {
     HLMC_CHECK_ARG(Ci == 32, "convT_c1: only Ci == 32");
     int64_t npix = (int64_t)B * 4 * Hi * Wi;
     HLMC_CHECK_ARG(npix < (int64_t)1 << 31, "convT_c1: too many pixels");
-    convT_c1_kernel<T, 32><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, FastDiv((uint32_t)(2 * Wi)),
-                                                               FastDiv((uint32_t)(2 * Hi)));
+    const FastDiv dW((uint32_t)(2 * Wi)), dH((uint32_t)(2 * Hi));
+    if (ba) {
+        HLMC_CHECK_ARG(ba->part && ba->nparts > 0, "convT_c1: BN statistics rows required");
+        const Folded f = fold_parts_to(s, ba->part, ba->nparts, 2 * Ci, ba->fold, fin_max_rows(Ci));
+        HLMC_CHECK_ARG(f.p != nullptr, "convT_c1: no fold space for the BN statistics");
+        BnFin fin;
+        fin.part = f.p; fin.rows = f.rows; fin.R = ba->R;
+        fin.mean = ba->mean; fin.invstd = ba->invstd; fin.rmean = ba->rmean; fin.rvar = ba->rvar; fin.nbt = ba->nbt;
+        fin.momentum = ba->momentum; fin.eps = ba->eps;
+        convT_c1_kernel<T, 32, true><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fin,
+                                                                         ba->gamma, ba->beta);
+    } else {
+        convT_c1_kernel<T, 32, false><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, BnFin{},
+                                                                          nullptr, nullptr);
+    }
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1583,15 +1641,20 @@ size_t wgrad_c1_ws(int B, int Hl, int Wl, int M) {
 }
 
 template <typename T>
-int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws) {
+int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws,
+             const BnAct* act) {
     HLMC_CHECK_ARG(M == 32, "wgrad_c1: only M == 32");
     int64_t K = (int64_t)B * Hl * Wl;
     int nblk = wgrad_c1_blocks(K);
     HLMC_CHECK_ARG(ws.bytes >= wgrad_c1_ws(B, Hl, Wl, M), "wgrad_c1 workspace");
     int rpb = (int)((K + nblk - 1) / nblk);
     HLMC_CHECK_ARG(K < (int64_t)1 << 31, "wgrad_c1: too many rows");
+    BnXf xf;
+    if (act) {
+        xf.mean = act->mean; xf.invstd = act->invstd; xf.gamma = act->gamma; xf.beta = act->beta;
+    }
     wgrad_c1_kernel<T, 32><<<nblk, kThreads, 0, s>>>(L, B, Hl, Wl, Xh, rpb, ws.p, FastDiv((uint32_t)Wl),
-                                                     FastDiv((uint32_t)Hl));
+                                                     FastDiv((uint32_t)Hl), xf);
     HLMC_LAUNCHED();
     sum_partials_f32_kernel<<<M * 9, 256, 0, s>>>(ws.p, nblk, M * 9, dW);
     HLMC_LAUNCHED();
@@ -1840,8 +1903,9 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
                                const BnBwdFuse*, double*);                                                           \
     template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*,        \
                                ColStats*, BnBwdFuse*);                                                               \
-    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);          \
-    template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws);                    \
+    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*,          \
+                             const BnApply*);                                                                        \
+    template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws, const BnAct*);      \
     template int cast_from_f32<T>(hipStream_t, const float*, T*, int64_t);                                           \
     template int cast_to_f32<T>(hipStream_t, const T*, float*, int64_t);                                             \
     template int copy2d<T>(hipStream_t, const T*, int, T*, int, int, int);                                           \

@@ -70,11 +70,30 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
                ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
 int conv_c1_fused_rows(int B, int Hi, int Wi);  // partial rows conv_c1_s2 writes with st / bf
 // y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel)
+// The consumer applies its input's train-mode BatchNorm + LeakyReLU(0.01) itself (no bn_act pass): `part`
+// [nparts][2C] statistics rows of the pre-BN map x, folded into `fold`; the consumer writes mean / invstd and the
+// running statistics like bn_stats, and rounds every activation to T as bn_act would have stored it.
+struct BnApply {
+    const double* part;
+    int nparts;
+    int64_t R;
+    float *mean, *invstd, *rmean, *rvar;
+    int64_t* nbt;
+    float momentum, eps;
+    const float *gamma, *beta;
+    Ws fold;
+};
+// the same transform from already-finalized statistics (backward consumers)
+struct BnAct {
+    const float *mean, *invstd, *gamma, *beta;
+};
 template <typename T>
-int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y);
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y,
+             const BnApply* ba = nullptr);
 // dW[m*9+tap] = sum L[b,r,c,m] * Xh[b, 2r-1+kh, 2c-1+kw]   (Xh single channel f32)
 template <typename T>
-int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws);
+int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws,
+             const BnAct* act = nullptr);
 size_t wgrad_c1_ws(int B, int Hl, int Wl, int M);
 
 // ---------------------------------------------------------------- batch norm / activation (kernels.hip)

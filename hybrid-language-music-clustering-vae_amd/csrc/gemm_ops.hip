@@ -85,7 +85,7 @@ inline int xcd_remap_for_site() {
 // the phases) run the phases inside each block (gemm_nt_kernel ploop): the 64 x 64 / 32 x 32 layers' phases
 // otherwise stream the low-res input from HBM once per phase.  HLMC_SP_PLOOP=0 / 2: never / always (A/B aid).
 constexpr int kPloopTiles = 1024;
-inline bool use_ploop(int phases, int tmn, int pipe) {
+inline bool use_ploop(int phases, int tmn, int pipe, bool with_stats) {
     static const int mode = [] {
         const char* e = std::getenv("HLMC_SP_PLOOP");
         return e ? std::atoi(e) : 1;
@@ -95,6 +95,8 @@ inline bool use_ploop(int phases, int tmn, int pipe) {
         return e ? std::atoi(e) : kPloopTiles;
     }();
     if (phases < 2 || pipe != 0 || mode == 0) return false;
+    if (mode == 3 && !with_stats) return false;  // A/B aid: forward (statistics epilogue) launches only
+    if (mode == 4 && with_stats) return false;   // A/B aid: data-gradient launches only
     return mode == 2 || tmn >= min_tiles;
 }
 
@@ -102,7 +104,7 @@ template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class 
 void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
                       bool long_k, int pipe) {
     const int rm = xcd_remap_for_site();
-    const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe) ? (int)grid.y : 1;
+    const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe, E::kStatMode == 1) ? (int)grid.y : 1;
     if (ploop > 1) grid.y = 1;
     HLMC_PROBE_BEGIN(s);
     if (pipe == 3)

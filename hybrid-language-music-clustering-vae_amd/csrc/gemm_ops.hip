@@ -425,6 +425,119 @@ size_t dispatch_tn_ws(int M, int N, int K) {
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline int log2_exact(int c) { return (c > 0 && (c & (c - 1)) == 0) ? __builtin_ctz(c) : -1; }
 
+// ---- stride-2 3x3 conv over LDS halo tiles (HLMC_CONV_HALO=0 disables): Ci = 32, Wo = 32, bf16, Co = CO.
+// Measured (scripts/bench_gemm.py): the 64x64x32 -> 64 conv and the matching decoder data gradient 46.3 / 44.1 ->
+// 36.7 / 34.2 us; bench A/B 106.4k vs 105.0k clips/s (3 alternating rounds).
+// A persistent block (one per CU) keeps the packed weights [CO][9 x 32] in LDS and walks 128-pixel M-tiles (4
+// output rows of one image).  Each tile's 9 input rows (plus the zero column left of the image) are staged in
+// LDS once, and every tap's A fragment is read from there: the input crosses L2 once per tile instead of once
+// per (tap, 16-byte chunk) gather.  The next tile's rows are loaded into registers while this tile computes.
+constexpr int kHaloCols = 65, kHaloPS = 40, kHaloRows = 9;  // 64 pixels + pad column; 32 channels + 8 pad (80 B)
+template <int CO, class EP>
+__global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
+                                                           const bf16* __restrict__ wp, EP ep, int M) {
+    const int tpi = Hi / 8;  // tiles per image: Ho / 4
+    constexpr int KP = 9 * 32 + 8;                     // weight row (592 B: the 16 n-rows of a fragment read
+                                                       // land on distinct 16-byte bank slots)
+    constexpr int HS = kHaloRows * kHaloCols * kHaloPS;  // one halo buffer (bf16)
+    constexpr int TM = 4, TN = CO / 32, WM = 64, WN = CO / 2;
+    __shared__ __attribute__((aligned(16))) bf16 Bs[CO * KP];
+    __shared__ __attribute__((aligned(16))) bf16 Hs[2 * HS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = (wave >> 1) * WM, wn0 = (wave & 1) * WN;
+    // weights: CO x 36 chunks
+    for (int c = tid; c < CO * 36; c += 256) {
+        const int n = c / 36, q = c - n * 36;
+        *reinterpret_cast<uint4*>(&Bs[n * KP + q * 8]) = *reinterpret_cast<const uint4*>(wp + (int64_t)n * 288 + q * 8);
+    }
+    // the pad column (input column -1) of both buffers stays zero
+    for (int c = tid; c < 2 * kHaloRows * 4; c += 256) {
+        const int bufr = c >> 2, q = c & 3;
+        *reinterpret_cast<uint4*>(&Hs[(bufr / kHaloRows) * HS + ((bufr % kHaloRows) * kHaloCols) * kHaloPS + q * 8]) =
+            make_uint4(0, 0, 0, 0);
+    }
+    uint4 hr[9];  // 9 rows x 256 chunks / 256 threads
+    auto load_rows = [&](int t) {
+        const int b = t / tpi, oh0 = (t - b * tpi) * 4;
+#pragma unroll
+        for (int u = 0; u < 9; ++u) {  // row u, chunk tid: pixel tid >> 2, channel group tid & 3
+            const int ih = 2 * oh0 - 1 + u;
+            hr[u] = ih >= 0 ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * 64 + (tid >> 2)) * 32 +
+                                                             (tid & 3) * 8)
+                            : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_rows = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 9; ++u)
+            *reinterpret_cast<uint4*>(&Hs[buf * HS + (u * kHaloCols + (tid >> 2) + 1) * kHaloPS + (tid & 3) * 8]) = hr[u];
+    };
+    int t = blockIdx.x, buf = 0;
+    if (t < ntiles) {
+        load_rows(t);
+        store_rows(0);
+    }
+    __syncthreads();
+    for (; t < ntiles; t += gridDim.x) {
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) load_rows(tn);  // in flight during this tile's MFMAs and stores
+        f32x4_t acc[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const bf16* H = Hs + buf * HS;
+        const int g8 = (lane >> 4) * 8;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) {
+            const int kh = tap / 3, kw = tap % 3;
+            bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int m = wm0 + i * 16 + (lane & 15);
+                const int hrow = 2 * (m >> 5) + kh, hcol = 2 * (m & 31) + kw;  // input (2oh-1+kh, 2ow-1+kw), col +1
+                af[i] = *reinterpret_cast<const bf16x8_t*>(&H[(hrow * kHaloCols + hcol) * kHaloPS + g8]);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int n = wn0 + j * 16 + (lane & 15);
+                bfr[j] = *reinterpret_cast<const bf16x8_t*>(&Bs[n * KP + tap * 32 + g8]);
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        double cs[TN], cq[TN];
+        epilogue_tile<TM, TN>(ep, acc, t * 128 + wm0, wn0, lane, M, CO, cs, cq);
+        if constexpr (EP::kStatMode == 1) {
+            __shared__ double sred[2][2][CO];
+            const int wmi = wave >> 1;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                double a = cs[j], q = cq[j];
+                a += __shfl_xor(a, 16, 64);
+                q += __shfl_xor(q, 16, 64);
+                a += __shfl_xor(a, 32, 64);
+                q += __shfl_xor(q, 32, 64);
+                if (lane < 16) {
+                    sred[wmi][0][wn0 + j * 16 + lane] = a;
+                    sred[wmi][1][wn0 + j * 16 + lane] = q;
+                }
+            }
+            __syncthreads();
+            for (int c = tid; c < CO; c += 256) {
+                ep.part[(int64_t)t * 2 * CO + c] = sred[0][0][c] + sred[1][0][c];
+                ep.part[(int64_t)t * 2 * CO + CO + c] = sred[0][1][c] + sred[1][1][c];
+            }
+        }
+        if (tn < ntiles) store_rows(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+}
+
 }  // namespace
 
 namespace ops {
@@ -441,6 +554,32 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     StoreRM<T> ep{y, bias, Co, 0, 0};
     probe::site(probe::kConvS2, 2.0 * M * Co * K,
                 (double)sizeof(T) * ((double)B * Hi * Wi * Ci + (double)Co * K + (double)M * Co));
+    if constexpr (std::is_same<T, bf16>::value) {
+        static const bool halo = [] {
+            const char* e = std::getenv("HLMC_CONV_HALO");
+            return !(e && e[0] == '0');
+        }();
+        if (halo && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0 && !(bf && bf->part)) {
+            const int ntiles = M / 128;  // 4 output rows of 32 pixels; Ho % 4 == 0: tiles stay inside an image
+            const int grid = std::min(ntiles, 256);
+            if (bf) bf->nparts = 0;
+            HLMC_PROBE_BEGIN(s);
+            if (st && st->part) {
+                WithStats<StoreRM<T>> eps;
+                static_cast<StoreRM<T>&>(eps) = ep;
+                eps.part = st->part;
+                eps.mtiles = ntiles;
+                conv_s2_halo_kernel<64, WithStats<StoreRM<T>>><<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M);
+                st->nparts = ntiles;
+            } else {
+                if (st) st->nparts = 0;
+                conv_s2_halo_kernel<64, StoreRM<T>><<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M);
+            }
+            HLMC_PROBE_END(s);
+            HLMC_LAUNCHED();
+            return HLMC_OK;
+        }
+    }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st, bf);
 }
 // partial rows (phases x 64-row tiles, the smallest BM) | fold scratch for their reduction

@@ -32,8 +32,9 @@ def ws(cuda):
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 @pytest.mark.parametrize("B,Hi,Wi,Ci,Co", [(2, 16, 16, 32, 64), (2, 8, 8, 64, 128), (3, 4, 4, 128, 256),
                                           (2, 4, 4, 256, 512), (2, 2, 2, 512, 512), (1, 8, 32, 32, 32),
-                                          (5, 4, 8, 64, 64)])
+                                          (5, 4, 8, 64, 64), (3, 16, 64, 32, 64), (2, 64, 64, 32, 64)])
 def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
+    """(also the shapes of the opt-in LDS halo-tile kernel, HLMC_CONV_HALO=1: Ci 32, Co 64, Wi 64)"""
     code, tdt, tol = DT[dt]
     g = torch.Generator().manual_seed(B * 1000 + Ci)
     x = torch.randn(B, Hi, Wi, Ci, generator=g)

@@ -538,6 +538,131 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
     }
 }
 
+// ---- sub-pixel (stride-2 transposed 3x3) conv over LDS halo tiles (HLMC_SP_HALO=0 disables): Ci = 64,
+// Co = 32, low-res width 32, bf16 (the decoder's last sub-pixel layer and the encoder layer-2 data gradient).
+// A persistent block keeps the packed weights [32][9 x 64] in LDS and walks 128-pixel low-res tiles (4 rows);
+// each tile's 5 input rows (the 4 plus the next, and a zero column right of the image) are staged once, and all
+// 4 phases' taps (1 + 2 + 2 + 4) read their fragments from there.
+constexpr int kSpCols = 33, kSpPS = 72, kSpRows = 5;  // 32 pixels + pad column; 64 channels + 8 pad (144 B)
+template <class EP>
+__global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
+                                                            const bf16* __restrict__ wp, EP ep, int M) {
+    constexpr int CO = 32, KP = 9 * 64 + 8;               // weight row 1168 B: fragment rows on distinct slots
+    constexpr int HS = kSpRows * kSpCols * kSpPS;
+    constexpr int TM = 2, TN = 2;                         // 4 waves x (32 rows x 32 channels)
+    __shared__ __attribute__((aligned(16))) bf16 Bs[CO * KP];
+    __shared__ __attribute__((aligned(16))) bf16 Hs[2 * HS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm0 = wave * 32;
+    const int tpi = Hi / 4;                               // tiles per image
+    for (int c = tid; c < CO * 72; c += 256) {            // weights: 32 x 72 chunks
+        const int n = c / 72, q = c - n * 72;
+        *reinterpret_cast<uint4*>(&Bs[n * KP + q * 8]) = *reinterpret_cast<const uint4*>(wp + (int64_t)n * 576 + q * 8);
+    }
+    for (int c = tid; c < 2 * kSpRows * 8; c += 256) {    // the pad column (c = 32) of both buffers stays zero
+        const int bufr = c >> 3, q = c & 7;
+        *reinterpret_cast<uint4*>(&Hs[(bufr / kSpRows) * HS + ((bufr % kSpRows) * kSpCols + 32) * kSpPS + q * 8]) =
+            make_uint4(0, 0, 0, 0);
+    }
+    uint4 hr[5];  // 5 rows x 256 chunks (32 pixels x 8) / 256 threads
+    auto load_rows = [&](int t) {
+        const int b = t / tpi, r0 = (t - b * tpi) * 4;
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int ih = r0 + u;
+            hr[u] = ih < Hi ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * 32 + (tid >> 3)) * 64 +
+                                                             (tid & 7) * 8)
+                            : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto store_rows = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < 5; ++u)
+            *reinterpret_cast<uint4*>(&Hs[buf * HS + (u * kSpCols + (tid >> 3)) * kSpPS + (tid & 7) * 8]) = hr[u];
+    };
+    int t = blockIdx.x, buf = 0;
+    if (t < ntiles) {
+        load_rows(t);
+        store_rows(0);
+    }
+    __syncthreads();
+    const int g8 = (lane >> 4) * 8;
+    for (; t < ntiles; t += gridDim.x) {
+        const int tn = t + gridDim.x;
+        if (tn < ntiles) load_rows(tn);
+        const bf16* H = Hs + buf * HS;
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+            const int py = ph >> 1, px = ph & 1;
+            f32x4_t acc[TM][TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ty = 0; ty < 2; ++ty) {
+                if (ty == 1 && !py) continue;
+                const int kh = py ? (ty ? 2 : 0) : 1, dr = (py && ty == 0) ? 1 : 0;
+#pragma unroll
+                for (int tx = 0; tx < 2; ++tx) {
+                    if (tx == 1 && !px) continue;
+                    const int kw = px ? (tx ? 2 : 0) : 1, dc = (px && tx == 0) ? 1 : 0;
+#pragma unroll
+                    for (int kc = 0; kc < 2; ++kc) {
+                        bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+                        for (int i = 0; i < TM; ++i) {
+                            const int m = wm0 + i * 16 + (lane & 15);
+                            af[i] = *reinterpret_cast<const bf16x8_t*>(
+                                &H[(((m >> 5) + dr) * kSpCols + (m & 31) + dc) * kSpPS + kc * 32 + g8]);
+                        }
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            const int n = j * 16 + (lane & 15);
+                            bfr[j] = *reinterpret_cast<const bf16x8_t*>(&Bs[n * KP + (kh * 3 + kw) * 64 + kc * 32 + g8]);
+                        }
+#pragma unroll
+                        for (int i = 0; i < TM; ++i)
+#pragma unroll
+                            for (int j = 0; j < TN; ++j)
+                                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    }
+                }
+            }
+            EP e = ep;
+            e.set_phase(ph);
+            double cs[TN], cq[TN];
+            epilogue_tile<TM, TN>(e, acc, t * 128 + wm0, 0, lane, M, CO, cs, cq);
+            if constexpr (EP::kStatMode == 1) {
+                __shared__ double sred[4][2][CO];
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    double a = cs[j], q = cq[j];
+                    a += __shfl_xor(a, 16, 64);
+                    q += __shfl_xor(q, 16, 64);
+                    a += __shfl_xor(a, 32, 64);
+                    q += __shfl_xor(q, 32, 64);
+                    if (lane < 16) {
+                        sred[wave][0][j * 16 + lane] = a;
+                        sred[wave][1][j * 16 + lane] = q;
+                    }
+                }
+                __syncthreads();
+                const int row = ph * ep.mtiles + t;
+                for (int c = tid; c < CO; c += 256) {
+                    ep.part[(int64_t)row * 2 * CO + c] = (sred[0][0][c] + sred[1][0][c]) + (sred[2][0][c] + sred[3][0][c]);
+                    ep.part[(int64_t)row * 2 * CO + CO + c] =
+                        (sred[0][1][c] + sred[1][1][c]) + (sred[2][1][c] + sred[3][1][c]);
+                }
+                __syncthreads();  // sred is reused by the next phase
+            }
+        }
+        if (tn < ntiles) store_rows(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+}
+
 }  // namespace
 
 namespace ops {
@@ -605,6 +730,32 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
     // the 4 phases hold 1 + 2 + 2 + 4 = 9 taps: 9 Ci MACs per (low-res pixel, output channel)
     probe::site(probe::kSubpixel, 2.0 * M * Co * 9.0 * Ci,
                 (double)sizeof(T) * ((double)M * Ci + 9.0 * Ci * Co + 4.0 * M * Co));
+    if constexpr (std::is_same<T, bf16>::value) {
+        static const bool halo = [] {
+            const char* e = std::getenv("HLMC_SP_HALO");
+            return !(e && e[0] == '0');
+        }();
+        if (halo && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0 && !(bf && bf->part)) {
+            const int ntiles = M / 128;  // 4 low-res rows of 32 pixels per tile, inside one image
+            const int grid = std::min(ntiles, 256);
+            if (bf) bf->nparts = 0;
+            HLMC_PROBE_BEGIN(s);
+            if (st && st->part) {
+                WithStats<StoreSubpixel<T>> eps;
+                static_cast<StoreSubpixel<T>&>(eps) = ep;
+                eps.part = st->part;
+                eps.mtiles = ntiles;
+                subpixel_halo_kernel<WithStats<StoreSubpixel<T>>><<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M);
+                st->nparts = 4 * ntiles;
+            } else {
+                if (st) st->nparts = 0;
+                subpixel_halo_kernel<StoreSubpixel<T>><<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M);
+            }
+            HLMC_PROBE_END(s);
+            HLMC_LAUNCHED();
+            return HLMC_OK;
+        }
+    }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st, bf);
 }
 template <typename T>

@@ -432,54 +432,60 @@ inline int log2_exact(int c) { return (c > 0 && (c & (c - 1)) == 0) ? __builtin_
 // output rows of one image).  Each tile's 9 input rows (plus the zero column left of the image) are staged in
 // LDS once, and every tap's A fragment is read from there: the input crosses L2 once per tile instead of once
 // per (tap, 16-byte chunk) gather.  The next tile's rows are loaded into registers while this tile computes.
-constexpr int kHaloCols = 65, kHaloPS = 40, kHaloRows = 9;  // 64 pixels + pad column; 32 channels + 8 pad (80 B)
-template <int CO, class EP>
+// Template: CI input channels, COB output channels per block (NSPL blocks share a tile's Co = NSPL * COB), WO
+// output width, ROWS output rows per tile (TP = ROWS * WO pixels), DB: double-buffered halo (else one buffer and
+// an extra barrier).  Shapes: 2 WO * CI / 8 == 256 (one 16-byte chunk per thread per input row).
+template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP>
 __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
                                                            const bf16* __restrict__ wp, EP ep, int M) {
-    const int tpi = Hi / 8;  // tiles per image: Ho / 4
-    constexpr int KP = 9 * 32 + 8;                     // weight row (592 B: the 16 n-rows of a fragment read
-                                                       // land on distinct 16-byte bank slots)
-    constexpr int HS = kHaloRows * kHaloCols * kHaloPS;  // one halo buffer (bf16)
-    constexpr int TM = 4, TN = CO / 32, WM = 64, WN = CO / 2;
-    __shared__ __attribute__((aligned(16))) bf16 Bs[CO * KP];
-    __shared__ __attribute__((aligned(16))) bf16 Hs[2 * HS];
+    constexpr int WI = 2 * WO, HR = 2 * ROWS + 1, HC = WI + 1, PS = CI + 8;  // halo rows / cols / pixel pitch
+    constexpr int TP = ROWS * WO, CPP = CI / 8;                             // tile pixels, chunks per pixel
+    static_assert(WI * CPP == 256 && TP % 32 == 0 && COB == 64, "halo chunk map / wave tiling");
+    constexpr int KP = 9 * CI + 8;      // weight row: 16 n-rows of a fragment read on distinct 16-byte slots
+    constexpr int HS = HR * HC * PS;    // one halo buffer (bf16)
+    constexpr int TM = TP / 32, TN = 2, WM = TP / 2, WN = 32;
+    constexpr int CO = NSPL * COB;
+    __shared__ __attribute__((aligned(16))) bf16 Bs[COB * KP];
+    __shared__ __attribute__((aligned(16))) bf16 Hs[(DB ? 2 : 1) * HS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = (wave >> 1) * WM, wn0 = (wave & 1) * WN;
-    // weights: CO x 36 chunks
-    for (int c = tid; c < CO * 36; c += 256) {
-        const int n = c / 36, q = c - n * 36;
-        *reinterpret_cast<uint4*>(&Bs[n * KP + q * 8]) = *reinterpret_cast<const uint4*>(wp + (int64_t)n * 288 + q * 8);
+    const int tpi = (Hi / 2) / ROWS;   // tiles per image
+    const int nh = blockIdx.x % NSPL, n0 = nh * COB;
+    const int bstep = gridDim.x / NSPL;
+    for (int c = tid; c < COB * 9 * CPP; c += 256) {  // this block's weight rows
+        const int n = c / (9 * CPP), q = c - n * (9 * CPP);
+        *reinterpret_cast<uint4*>(&Bs[n * KP + q * 8]) =
+            *reinterpret_cast<const uint4*>(wp + (int64_t)(n0 + n) * 9 * CI + q * 8);
     }
-    // the pad column (input column -1) of both buffers stays zero
-    for (int c = tid; c < 2 * kHaloRows * 4; c += 256) {
-        const int bufr = c >> 2, q = c & 3;
-        *reinterpret_cast<uint4*>(&Hs[(bufr / kHaloRows) * HS + ((bufr % kHaloRows) * kHaloCols) * kHaloPS + q * 8]) =
-            make_uint4(0, 0, 0, 0);
+    for (int c = tid; c < (DB ? 2 : 1) * HR * CPP; c += 256) {  // the pad column (input column -1) stays zero
+        const int bufr = c / CPP, q = c - bufr * CPP;
+        *reinterpret_cast<uint4*>(&Hs[(bufr / HR) * HS + ((bufr % HR) * HC) * PS + q * 8]) = make_uint4(0, 0, 0, 0);
     }
-    uint4 hr[9];  // 9 rows x 256 chunks / 256 threads
+    uint4 hr[HR];  // HR rows x 256 chunks / 256 threads
     auto load_rows = [&](int t) {
-        const int b = t / tpi, oh0 = (t - b * tpi) * 4;
+        const int b = t / tpi, oh0 = (t - b * tpi) * ROWS;
 #pragma unroll
-        for (int u = 0; u < 9; ++u) {  // row u, chunk tid: pixel tid >> 2, channel group tid & 3
+        for (int u = 0; u < HR; ++u) {
             const int ih = 2 * oh0 - 1 + u;
-            hr[u] = ih >= 0 ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * 64 + (tid >> 2)) * 32 +
-                                                             (tid & 3) * 8)
+            hr[u] = ih >= 0 ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * WI + tid / CPP) * CI +
+                                                             (tid % CPP) * 8)
                             : make_uint4(0, 0, 0, 0);
         }
     };
     auto store_rows = [&](int buf) {
 #pragma unroll
-        for (int u = 0; u < 9; ++u)
-            *reinterpret_cast<uint4*>(&Hs[buf * HS + (u * kHaloCols + (tid >> 2) + 1) * kHaloPS + (tid & 3) * 8]) = hr[u];
+        for (int u = 0; u < HR; ++u)
+            *reinterpret_cast<uint4*>(&Hs[buf * HS + (u * HC + tid / CPP + 1) * PS + (tid % CPP) * 8]) = hr[u];
     };
-    int t = blockIdx.x, buf = 0;
+    int t = blockIdx.x / NSPL, buf = 0;
     if (t < ntiles) {
         load_rows(t);
         store_rows(0);
     }
     __syncthreads();
-    for (; t < ntiles; t += gridDim.x) {
-        const int tn = t + gridDim.x;
+    const int g8 = (lane >> 4) * 8;
+    for (; t < ntiles; t += bstep) {
+        const int tn = t + bstep;
         if (tn < ntiles) load_rows(tn);  // in flight during this tile's MFMAs and stores
         f32x4_t acc[TM][TN];
 #pragma unroll
@@ -487,32 +493,34 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         const bf16* H = Hs + buf * HS;
-        const int g8 = (lane >> 4) * 8;
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
             const int kh = tap / 3, kw = tap % 3;
-            bf16x8_t af[TM], bfr[TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int m = wm0 + i * 16 + (lane & 15);
-                const int hrow = 2 * (m >> 5) + kh, hcol = 2 * (m & 31) + kw;  // input (2oh-1+kh, 2ow-1+kw), col +1
-                af[i] = *reinterpret_cast<const bf16x8_t*>(&H[(hrow * kHaloCols + hcol) * kHaloPS + g8]);
+            for (int kc = 0; kc < CI / 32; ++kc) {
+                bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int m = wm0 + i * 16 + (lane & 15);
+                    const int hrow = 2 * (m / WO) + kh, hcol = 2 * (m % WO) + kw;  // (2oh-1+kh, 2ow-1+kw), col +1
+                    af[i] = *reinterpret_cast<const bf16x8_t*>(&H[(hrow * HC + hcol) * PS + kc * 32 + g8]);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int n = wn0 + j * 16 + (lane & 15);
+                    bfr[j] = *reinterpret_cast<const bf16x8_t*>(&Bs[n * KP + tap * CI + kc * 32 + g8]);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
             }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n = wn0 + j * 16 + (lane & 15);
-                bfr[j] = *reinterpret_cast<const bf16x8_t*>(&Bs[n * KP + tap * 32 + g8]);
-            }
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
         double cs[TN], cq[TN];
-        epilogue_tile<TM, TN>(ep, acc, t * 128 + wm0, wn0, lane, M, CO, cs, cq);
+        epilogue_tile<TM, TN>(ep, acc, t * TP + wm0, n0 + wn0, lane, M, CO, cs, cq);
         if constexpr (EP::kStatMode == 1) {
-            __shared__ double sred[2][2][CO];
+            __shared__ double sred[2][2][COB];
             const int wmi = wave >> 1;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
@@ -527,14 +535,20 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
                 }
             }
             __syncthreads();
-            for (int c = tid; c < CO; c += 256) {
-                ep.part[(int64_t)t * 2 * CO + c] = sred[0][0][c] + sred[1][0][c];
-                ep.part[(int64_t)t * 2 * CO + CO + c] = sred[0][1][c] + sred[1][1][c];
+            for (int c = tid; c < COB; c += 256) {
+                ep.part[(int64_t)t * 2 * CO + n0 + c] = sred[0][0][c] + sred[1][0][c];
+                ep.part[(int64_t)t * 2 * CO + CO + n0 + c] = sred[0][1][c] + sred[1][1][c];
             }
         }
-        if (tn < ntiles) store_rows(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
+        if constexpr (DB) {
+            if (tn < ntiles) store_rows(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        } else {
+            __syncthreads();  // every wave is done with this tile's halo (and the statistics scratch)
+            if (tn < ntiles) store_rows(0);
+            __syncthreads();
+        }
     }
 }
 
@@ -543,52 +557,57 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
 // A persistent block keeps the packed weights [32][9 x 64] in LDS and walks 128-pixel low-res tiles (4 rows);
 // each tile's 5 input rows (the 4 plus the next, and a zero column right of the image) are staged once, and all
 // 4 phases' taps (1 + 2 + 2 + 4) read their fragments from there.
-constexpr int kSpCols = 33, kSpPS = 72, kSpRows = 5;  // 32 pixels + pad column; 64 channels + 8 pad (144 B)
-template <class EP>
+// Template: CI input channels, COB output channels per block (NSPL blocks per tile), WI low-res width, ROWS
+// low-res rows per tile (TP = ROWS * WI = 128 pixels), DB: double-buffered halo.  WI * CI / 8 == 256.
+template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP>
 __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
                                                             const bf16* __restrict__ wp, EP ep, int M) {
-    constexpr int CO = 32, KP = 9 * 64 + 8;               // weight row 1168 B: fragment rows on distinct slots
-    constexpr int HS = kSpRows * kSpCols * kSpPS;
-    constexpr int TM = 2, TN = 2;                         // 4 waves x (32 rows x 32 channels)
-    __shared__ __attribute__((aligned(16))) bf16 Bs[CO * KP];
-    __shared__ __attribute__((aligned(16))) bf16 Hs[2 * HS];
+    constexpr int HR = ROWS + 1, HC = WI + 1, PS = CI + 8, CPP = CI / 8, TP = ROWS * WI;
+    static_assert(WI * CPP == 256 && TP == 128 && COB == 32, "halo chunk map / wave tiling");
+    constexpr int KP = 9 * CI + 8;                        // weight row: fragment rows on distinct 16-byte slots
+    constexpr int HS = HR * HC * PS;
+    constexpr int TM = 2, TN = 2, CO = NSPL * COB;        // 4 waves x (32 pixels x 32 channels)
+    __shared__ __attribute__((aligned(16))) bf16 Bs[COB * KP];
+    __shared__ __attribute__((aligned(16))) bf16 Hs[(DB ? 2 : 1) * HS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm0 = wave * 32;
-    const int tpi = Hi / 4;                               // tiles per image
-    for (int c = tid; c < CO * 72; c += 256) {            // weights: 32 x 72 chunks
-        const int n = c / 72, q = c - n * 72;
-        *reinterpret_cast<uint4*>(&Bs[n * KP + q * 8]) = *reinterpret_cast<const uint4*>(wp + (int64_t)n * 576 + q * 8);
+    const int tpi = Hi / ROWS;                            // tiles per image
+    const int nh = blockIdx.x % NSPL, n0 = nh * COB;
+    const int bstep = gridDim.x / NSPL;
+    for (int c = tid; c < COB * 9 * CPP; c += 256) {      // this block's weight rows
+        const int n = c / (9 * CPP), q = c - n * (9 * CPP);
+        *reinterpret_cast<uint4*>(&Bs[n * KP + q * 8]) =
+            *reinterpret_cast<const uint4*>(wp + (int64_t)(n0 + n) * 9 * CI + q * 8);
     }
-    for (int c = tid; c < 2 * kSpRows * 8; c += 256) {    // the pad column (c = 32) of both buffers stays zero
-        const int bufr = c >> 3, q = c & 7;
-        *reinterpret_cast<uint4*>(&Hs[(bufr / kSpRows) * HS + ((bufr % kSpRows) * kSpCols + 32) * kSpPS + q * 8]) =
-            make_uint4(0, 0, 0, 0);
+    for (int c = tid; c < (DB ? 2 : 1) * HR * CPP; c += 256) {  // the pad column (c = WI) stays zero
+        const int bufr = c / CPP, q = c - bufr * CPP;
+        *reinterpret_cast<uint4*>(&Hs[(bufr / HR) * HS + ((bufr % HR) * HC + WI) * PS + q * 8]) = make_uint4(0, 0, 0, 0);
     }
-    uint4 hr[5];  // 5 rows x 256 chunks (32 pixels x 8) / 256 threads
+    uint4 hr[HR];  // HR rows x 256 chunks / 256 threads
     auto load_rows = [&](int t) {
-        const int b = t / tpi, r0 = (t - b * tpi) * 4;
+        const int b = t / tpi, r0 = (t - b * tpi) * ROWS;
 #pragma unroll
-        for (int u = 0; u < 5; ++u) {
+        for (int u = 0; u < HR; ++u) {
             const int ih = r0 + u;
-            hr[u] = ih < Hi ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * 32 + (tid >> 3)) * 64 +
-                                                             (tid & 7) * 8)
+            hr[u] = ih < Hi ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * WI + tid / CPP) * CI +
+                                                             (tid % CPP) * 8)
                             : make_uint4(0, 0, 0, 0);
         }
     };
     auto store_rows = [&](int buf) {
 #pragma unroll
-        for (int u = 0; u < 5; ++u)
-            *reinterpret_cast<uint4*>(&Hs[buf * HS + (u * kSpCols + (tid >> 3)) * kSpPS + (tid & 7) * 8]) = hr[u];
+        for (int u = 0; u < HR; ++u)
+            *reinterpret_cast<uint4*>(&Hs[buf * HS + (u * HC + tid / CPP) * PS + (tid % CPP) * 8]) = hr[u];
     };
-    int t = blockIdx.x, buf = 0;
+    int t = blockIdx.x / NSPL, buf = 0;
     if (t < ntiles) {
         load_rows(t);
         store_rows(0);
     }
     __syncthreads();
     const int g8 = (lane >> 4) * 8;
-    for (; t < ntiles; t += gridDim.x) {
-        const int tn = t + gridDim.x;
+    for (; t < ntiles; t += bstep) {
+        const int tn = t + bstep;
         if (tn < ntiles) load_rows(tn);
         const bf16* H = Hs + buf * HS;
 #pragma unroll
@@ -608,18 +627,18 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
                     if (tx == 1 && !px) continue;
                     const int kw = px ? (tx ? 2 : 0) : 1, dc = (px && tx == 0) ? 1 : 0;
 #pragma unroll
-                    for (int kc = 0; kc < 2; ++kc) {
+                    for (int kc = 0; kc < CI / 32; ++kc) {
                         bf16x8_t af[TM], bfr[TN];
 #pragma unroll
                         for (int i = 0; i < TM; ++i) {
                             const int m = wm0 + i * 16 + (lane & 15);
                             af[i] = *reinterpret_cast<const bf16x8_t*>(
-                                &H[(((m >> 5) + dr) * kSpCols + (m & 31) + dc) * kSpPS + kc * 32 + g8]);
+                                &H[((m / WI + dr) * HC + m % WI + dc) * PS + kc * 32 + g8]);
                         }
 #pragma unroll
                         for (int j = 0; j < TN; ++j) {
                             const int n = j * 16 + (lane & 15);
-                            bfr[j] = *reinterpret_cast<const bf16x8_t*>(&Bs[n * KP + (kh * 3 + kw) * 64 + kc * 32 + g8]);
+                            bfr[j] = *reinterpret_cast<const bf16x8_t*>(&Bs[n * KP + (kh * 3 + kw) * CI + kc * 32 + g8]);
                         }
 #pragma unroll
                         for (int i = 0; i < TM; ++i)
@@ -632,9 +651,9 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
             EP e = ep;
             e.set_phase(ph);
             double cs[TN], cq[TN];
-            epilogue_tile<TM, TN>(e, acc, t * 128 + wm0, 0, lane, M, CO, cs, cq);
+            epilogue_tile<TM, TN>(e, acc, t * TP + wm0, n0, lane, M, CO, cs, cq);
             if constexpr (EP::kStatMode == 1) {
-                __shared__ double sred[4][2][CO];
+                __shared__ double sred[4][2][COB];
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     double a = cs[j], q = cq[j];
@@ -649,17 +668,24 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
                 }
                 __syncthreads();
                 const int row = ph * ep.mtiles + t;
-                for (int c = tid; c < CO; c += 256) {
-                    ep.part[(int64_t)row * 2 * CO + c] = (sred[0][0][c] + sred[1][0][c]) + (sred[2][0][c] + sred[3][0][c]);
-                    ep.part[(int64_t)row * 2 * CO + CO + c] =
+                for (int c = tid; c < COB; c += 256) {
+                    ep.part[(int64_t)row * 2 * CO + n0 + c] =
+                        (sred[0][0][c] + sred[1][0][c]) + (sred[2][0][c] + sred[3][0][c]);
+                    ep.part[(int64_t)row * 2 * CO + CO + n0 + c] =
                         (sred[0][1][c] + sred[1][1][c]) + (sred[2][1][c] + sred[3][1][c]);
                 }
                 __syncthreads();  // sred is reused by the next phase
             }
         }
-        if (tn < ntiles) store_rows(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
+        if constexpr (DB) {
+            if (tn < ntiles) store_rows(buf ^ 1);
+            __syncthreads();
+            buf ^= 1;
+        } else {
+            __syncthreads();  // every wave is done with this tile's halo
+            if (tn < ntiles) store_rows(0);
+            __syncthreads();
+        }
     }
 }
 
@@ -684,9 +710,15 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             const char* e = std::getenv("HLMC_CONV_HALO");
             return !(e && e[0] == '0');
         }();
-        if (halo && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0 && !(bf && bf->part)) {
-            const int ntiles = M / 128;  // 4 output rows of 32 pixels; Ho % 4 == 0: tiles stay inside an image
-            const int grid = std::min(ntiles, 256);
+        static const bool halo2 = [] {  // HLMC_CONV_HALO2=0: the 32x32x64 -> 128 layers on the gather GEMM (A/B)
+            const char* e = std::getenv("HLMC_CONV_HALO2");
+            return !(e && e[0] == '0');
+        }();
+        // (CI, Co, Wi): (32, 64, 64) 128-pixel tiles, double-buffered halo; (64, 128, 32) two 64-channel halves per
+        // 64-pixel tile, one halo buffer (the weights take half the LDS)
+        auto run = [&](auto kern_plain, auto kern_stats, int tp, int nspl) -> int {
+            const int ntiles = M / tp;  // whole output rows: tiles stay inside an image
+            const int grid = std::min(ntiles * nspl, 256);
             if (bf) bf->nparts = 0;
             HLMC_PROBE_BEGIN(s);
             if (st && st->part) {
@@ -694,16 +726,23 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
                 static_cast<StoreRM<T>&>(eps) = ep;
                 eps.part = st->part;
                 eps.mtiles = ntiles;
-                conv_s2_halo_kernel<64, WithStats<StoreRM<T>>><<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M);
+                kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M);
                 st->nparts = ntiles;
             } else {
                 if (st) st->nparts = 0;
-                conv_s2_halo_kernel<64, StoreRM<T>><<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M);
+                kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M);
             }
             HLMC_PROBE_END(s);
             HLMC_LAUNCHED();
-            return HLMC_OK;
-        }
+            return (int)HLMC_OK;
+        };
+        const bool nofuse = !(bf && bf->part);
+        if (halo && nofuse && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0)
+            return run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>>,
+                       conv_s2_halo_kernel<32, 64, 1, 32, 4, true, WithStats<StoreRM<T>>>, 128, 1);
+        if (halo2 && nofuse && Ci == 64 && Co == 128 && Wi == 32 && Hi % 8 == 0)
+            return run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>>,
+                       conv_s2_halo_kernel<64, 64, 2, 16, 4, false, WithStats<StoreRM<T>>>, 64, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st, bf);
 }
@@ -735,9 +774,13 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
             const char* e = std::getenv("HLMC_SP_HALO");
             return !(e && e[0] == '0');
         }();
-        if (halo && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0 && !(bf && bf->part)) {
-            const int ntiles = M / 128;  // 4 low-res rows of 32 pixels per tile, inside one image
-            const int grid = std::min(ntiles, 256);
+        static const bool halo2 = [] {  // HLMC_SP_HALO2=0: the 16x16x128 -> 64 layers on the gather GEMM (A/B)
+            const char* e = std::getenv("HLMC_SP_HALO2");
+            return !(e && e[0] == '0');
+        }();
+        auto run = [&](auto kern_plain, auto kern_stats, int nspl) -> int {
+            const int ntiles = M / 128;  // 128 low-res pixels (whole rows) per tile, inside one image
+            const int grid = std::min(ntiles * nspl, 256);
             if (bf) bf->nparts = 0;
             HLMC_PROBE_BEGIN(s);
             if (st && st->part) {
@@ -745,16 +788,23 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
                 static_cast<StoreSubpixel<T>&>(eps) = ep;
                 eps.part = st->part;
                 eps.mtiles = ntiles;
-                subpixel_halo_kernel<WithStats<StoreSubpixel<T>>><<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M);
+                kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M);
                 st->nparts = 4 * ntiles;
             } else {
                 if (st) st->nparts = 0;
-                subpixel_halo_kernel<StoreSubpixel<T>><<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M);
+                kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M);
             }
             HLMC_PROBE_END(s);
             HLMC_LAUNCHED();
-            return HLMC_OK;
-        }
+            return (int)HLMC_OK;
+        };
+        const bool nofuse = !(bf && bf->part);
+        if (halo && nofuse && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0)
+            return run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>>,
+                       subpixel_halo_kernel<64, 32, 1, 32, 4, true, WithStats<StoreSubpixel<T>>>, 1);
+        if (halo2 && nofuse && Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0)
+            return run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>>,
+                       subpixel_halo_kernel<128, 32, 2, 16, 8, false, WithStats<StoreSubpixel<T>>>, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st, bf);
 }

@@ -32,9 +32,11 @@ def ws(cuda):
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 @pytest.mark.parametrize("B,Hi,Wi,Ci,Co", [(2, 16, 16, 32, 64), (2, 8, 8, 64, 128), (3, 4, 4, 128, 256),
                                           (2, 4, 4, 256, 512), (2, 2, 2, 512, 512), (1, 8, 32, 32, 32),
-                                          (5, 4, 8, 64, 64), (3, 16, 64, 32, 64), (2, 64, 64, 32, 64)])
+                                          (5, 4, 8, 64, 64), (3, 16, 64, 32, 64), (2, 64, 64, 32, 64),
+                                          (2, 32, 32, 64, 128), (3, 8, 32, 64, 128)])
 def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
-    """(also the shapes of the opt-in LDS halo-tile kernel, HLMC_CONV_HALO=1: Ci 32, Co 64, Wi 64)"""
+    """(also the shapes of the LDS halo-tile kernels: Ci 32 -> Co 64 at Wi 64 (default on), Ci 64 -> Co 128 at
+    Wi 32 (HLMC_CONV_HALO2=1))"""
     code, tdt, tol = DT[dt]
     g = torch.Generator().manual_seed(B * 1000 + Ci)
     x = torch.randn(B, Hi, Wi, Ci, generator=g)
@@ -53,7 +55,8 @@ def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 @pytest.mark.parametrize("B,Hi,Wi,Ci,Co", [(2, 2, 2, 512, 512), (2, 4, 4, 512, 256), (2, 8, 8, 256, 128),
                                           (3, 16, 16, 128, 64), (2, 32, 32, 64, 32), (1, 2, 16, 512, 512),
-                                          (2, 4, 4, 32, 64), (3, 8, 32, 64, 32)])
+                                          (2, 4, 4, 32, 64), (3, 8, 32, 64, 32), (2, 16, 16, 128, 64),
+                                          (3, 8, 16, 128, 64)])
 def test_subpixel_convT(cuda, ws, dt, B, Hi, Wi, Ci, Co):
     """(the Ci 64 -> Co 32, 32-wide shapes run the LDS halo-tile kernel in bf16; HLMC_SP_HALO=0 disables it)"""
     code, tdt, tol = DT[dt]

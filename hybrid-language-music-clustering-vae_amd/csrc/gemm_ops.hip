@@ -563,10 +563,10 @@ template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP>
 __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
                                                             const bf16* __restrict__ wp, EP ep, int M) {
     constexpr int HR = ROWS + 1, HC = WI + 1, PS = CI + 8, CPP = CI / 8, TP = ROWS * WI;
-    static_assert(WI * CPP == 256 && TP == 128 && COB == 32, "halo chunk map / wave tiling");
+    static_assert(WI * CPP == 256 && TP == 128 && (COB == 32 || COB == 16), "halo chunk map / wave tiling");
     constexpr int KP = 9 * CI + 8;                        // weight row: fragment rows on distinct 16-byte slots
     constexpr int HS = HR * HC * PS;
-    constexpr int TM = 2, TN = 2, CO = NSPL * COB;        // 4 waves x (32 pixels x 32 channels)
+    constexpr int TM = 2, TN = COB / 16, CO = NSPL * COB;  // 4 waves x (32 pixels x COB channels)
     __shared__ __attribute__((aligned(16))) bf16 Bs[COB * KP];
     __shared__ __attribute__((aligned(16))) bf16 Hs[(DB ? 2 : 1) * HS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

@@ -56,7 +56,7 @@ def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
 @pytest.mark.parametrize("B,Hi,Wi,Ci,Co", [(2, 2, 2, 512, 512), (2, 4, 4, 512, 256), (2, 8, 8, 256, 128),
                                           (3, 16, 16, 128, 64), (2, 32, 32, 64, 32), (1, 2, 16, 512, 512),
                                           (2, 4, 4, 32, 64), (3, 8, 32, 64, 32), (2, 16, 16, 128, 64),
-                                          (3, 8, 16, 128, 64)])
+                                          (3, 8, 16, 128, 64), (2, 16, 8, 256, 128)])
 def test_subpixel_convT(cuda, ws, dt, B, Hi, Wi, Ci, Co):
     """(the Ci 64 -> Co 32, 32-wide shapes run the LDS halo-tile kernel in bf16; HLMC_SP_HALO=0 disables it)"""
     code, tdt, tol = DT[dt]

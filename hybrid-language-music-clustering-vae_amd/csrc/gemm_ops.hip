@@ -440,15 +440,17 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
                                                            const bf16* __restrict__ wp, EP ep, int M) {
     constexpr int WI = 2 * WO, HR = 2 * ROWS + 1, HC = WI + 1, PS = CI + 8;  // halo rows / cols / pixel pitch
     constexpr int TP = ROWS * WO, CPP = CI / 8;                             // tile pixels, chunks per pixel
-    static_assert(WI * CPP == 256 && TP % 32 == 0 && COB == 64, "halo chunk map / wave tiling");
+    static_assert(WI * CPP == 256 && (COB == 64 || COB == 32), "halo chunk map / wave tiling");
     constexpr int KP = 9 * CI + 8;      // weight row: 16 n-rows of a fragment read on distinct 16-byte slots
     constexpr int HS = HR * HC * PS;    // one halo buffer (bf16)
-    constexpr int TM = TP / 32, TN = 2, WM = TP / 2, WN = 32;
+    constexpr int WAVES_N = COB / 32;   // 4 waves: 2 x 2 over (TP x 64) or 4 x 1 over (TP x 32)
+    constexpr int WM = TP / (4 / WAVES_N), WN = 32, TM = WM / 16, TN = 2;
+    static_assert(WM % 16 == 0, "wave rows");
     constexpr int CO = NSPL * COB;
     __shared__ __attribute__((aligned(16))) bf16 Bs[COB * KP];
     __shared__ __attribute__((aligned(16))) bf16 Hs[(DB ? 2 : 1) * HS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm0 = (wave >> 1) * WM, wn0 = (wave & 1) * WN;
+    const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
     const int tpi = (Hi / 2) / ROWS;   // tiles per image
     const int nh = blockIdx.x % NSPL, n0 = nh * COB;
     const int bstep = gridDim.x / NSPL;
@@ -520,8 +522,9 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
         double cs[TN], cq[TN];
         epilogue_tile<TM, TN>(ep, acc, t * TP + wm0, n0 + wn0, lane, M, CO, cs, cq);
         if constexpr (EP::kStatMode == 1) {
-            __shared__ double sred[2][2][COB];
-            const int wmi = wave >> 1;
+            constexpr int WAVES_M = 4 / WAVES_N;
+            __shared__ double sred[WAVES_M][2][COB];
+            const int wmi = wave / WAVES_N;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 double a = cs[j], q = cq[j];
@@ -536,8 +539,14 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
             }
             __syncthreads();
             for (int c = tid; c < COB; c += 256) {
-                ep.part[(int64_t)t * 2 * CO + n0 + c] = sred[0][0][c] + sred[1][0][c];
-                ep.part[(int64_t)t * 2 * CO + CO + n0 + c] = sred[0][1][c] + sred[1][1][c];
+                double a = 0.0, q = 0.0;
+#pragma unroll
+                for (int w = 0; w < WAVES_M; ++w) {
+                    a += sred[w][0][c];
+                    q += sred[w][1][c];
+                }
+                ep.part[(int64_t)t * 2 * CO + n0 + c] = a;
+                ep.part[(int64_t)t * 2 * CO + CO + n0 + c] = q;
             }
         }
         if constexpr (DB) {
@@ -714,6 +723,10 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             const char* e = std::getenv("HLMC_CONV_HALO2");
             return !(e && e[0] == '0');
         }();
+        static const bool halo3 = [] {  // HLMC_CONV_HALO3=1: the 16x16x128 -> 256 layers too (A/B)
+            const char* e = std::getenv("HLMC_CONV_HALO3");
+            return e && e[0] == '1';
+        }();
         // (CI, Co, Wi): (32, 64, 64) 128-pixel tiles, double-buffered halo; (64, 128, 32) two 64-channel halves per
         // 64-pixel tile, one halo buffer (the weights take half the LDS)
         auto run = [&](auto kern_plain, auto kern_stats, int tp, int nspl) -> int {
@@ -743,6 +756,10 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
         if (halo2 && nofuse && Ci == 64 && Co == 128 && Wi == 32 && Hi % 8 == 0)
             return run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>>,
                        conv_s2_halo_kernel<64, 64, 2, 16, 4, false, WithStats<StoreRM<T>>>, 64, 2);
+        // Ci 128 -> Co 256 at 16-wide input: 64-pixel tiles (8 output rows), eight 32-channel slices per tile
+        if (halo3 && nofuse && Ci == 128 && Co == 256 && Wi == 16 && Hi % 16 == 0)
+            return run(conv_s2_halo_kernel<128, 32, 8, 8, 8, false, StoreRM<T>>,
+                       conv_s2_halo_kernel<128, 32, 8, 8, 8, false, WithStats<StoreRM<T>>>, 64, 8);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st, bf);
 }

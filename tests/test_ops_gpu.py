@@ -33,7 +33,8 @@ def ws(cuda):
 @pytest.mark.parametrize("B,Hi,Wi,Ci,Co", [(2, 16, 16, 32, 64), (2, 8, 8, 64, 128), (3, 4, 4, 128, 256),
                                           (2, 4, 4, 256, 512), (2, 2, 2, 512, 512), (1, 8, 32, 32, 32),
                                           (5, 4, 8, 64, 64), (3, 16, 64, 32, 64), (2, 64, 64, 32, 64),
-                                          (2, 32, 32, 64, 128), (3, 8, 32, 64, 128)])
+                                          (2, 32, 32, 64, 128), (3, 8, 32, 64, 128), (2, 16, 16, 128, 256),
+                                          (3, 32, 16, 128, 256)])
 def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
     """(also the shapes of the LDS halo-tile kernels: Ci 32 -> Co 64 at Wi 64 (default on), Ci 64 -> Co 128 at
     Wi 32 (HLMC_CONV_HALO2=1))"""

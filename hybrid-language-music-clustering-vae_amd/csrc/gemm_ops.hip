@@ -67,7 +67,11 @@ inline int nt_pipe_select(int ksl, int S, int blocks) {
         return e ? std::atoi(e) : -1;
     }();
     if (forced >= 0) return forced;
-    if (S > 1 && blocks <= 256) return 4;
+    static const int split_max = [] {  // HLMC_GLDS_SPLIT_MAX: largest split-K grid on the ring (A/B aid)
+        const char* e = std::getenv("HLMC_GLDS_SPLIT_MAX");
+        return e ? std::atoi(e) : 256;
+    }();
+    if (S > 1 && blocks <= split_max) return 4;
     return ksl >= 1024 ? 4 : 0;
 }
 

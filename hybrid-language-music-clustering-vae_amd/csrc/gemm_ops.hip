@@ -69,7 +69,7 @@ inline int nt_pipe_select(int ksl, int S, int blocks) {
     if (forced >= 0) return forced;
     static const int split_max = [] {  // HLMC_GLDS_SPLIT_MAX: largest split-K grid on the ring (A/B aid)
         const char* e = std::getenv("HLMC_GLDS_SPLIT_MAX");
-        return e ? std::atoi(e) : 256;
+        return e ? std::atoi(e) : 512;
     }();
     if (S > 1 && blocks <= split_max) return 4;
     return ksl >= 1024 ? 4 : 0;

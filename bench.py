@@ -7,11 +7,14 @@ with fp32 accumulation and fp32 master weights; for N > 1 ranks the flat fp32 gr
 (RCCL over xGMI) before Adam.  Weak scaling: 256 clips per GPU per step.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload audio|hybrid|cvae] [--dtype bf16|fp32]
-                    [--no-cpu-baseline] [--no-roofline] [--no-extras]
+                    [--grad-dtype bf16|fp32] [--no-cpu-baseline] [--no-roofline] [--no-extras] [--graph]
 N > 1 is launched by torch.distributed.run (one process per GPU); rank 0 prints ONE JSON line.
 Besides the headline (BASELINE config[1]), the default run times three more workloads on the same mel stage and
 reports them under "extras" (never as `value`): the headline in fp32 (the parity precision), the hybrid ConvVAE
-with 384-d lyrics (config[2]) and the genre-conditioned ConditionalVAE (config[3]), each bs=256 per GPU.
+with 384-d lyrics (config[2]) and the genre-conditioned ConditionalVAE (config[3]), each bs=256 per GPU; the
+K-Means fit of config[3]/[4]'s clustering scale (N = 100 000 x 128, k = 10, n_init = 10) beside sklearn's on the
+host cores; and config[4] end to end (run_pipeline: 30 s PCM -> mel -> scaler -> HybridVAE 128x1024 training ->
+latents -> K-Means) on --e2e-clips clips.
 """
 from __future__ import annotations
 
@@ -71,64 +74,6 @@ class MelStage:
         return self.audio
 
 
-class MelPipeline:
-    """Double-buffered mel stage on its own HIP stream: the mel-dB + z-score of step k+1's clips runs while
-    step k trains (the GPU-side counterpart of the reference's preprocess-then-train split).  Slot s is
-    rewritten only after the step that last read it has finished (event `free[s]`)."""
-
-    def __init__(self, batch, device, scaler):
-        self.stages = [MelStage(batch, device, scaler), MelStage(batch, device, scaler)]
-        self.stream = torch.cuda.Stream(device=device)
-        self.ready = [torch.cuda.Event(), torch.cuda.Event()]
-        self.free = [torch.cuda.Event(), torch.cuda.Event()]
-
-    def launch(self, pcm, slot):
-        with torch.cuda.stream(self.stream):
-            self.stream.wait_event(self.free[slot])
-            self.stages[slot](pcm)
-            self.ready[slot].record(self.stream)
-
-    def run(self, trainer, pcm, text, steps):
-        """`steps` train steps, each on freshly computed mel features; returns the last step's loss sums."""
-        sums = None
-        self.launch(pcm, 0)
-        for k in range(steps):
-            slot = k & 1
-            torch.cuda.current_stream().wait_event(self.ready[slot])
-            if k + 1 < steps:
-                self.launch(pcm, slot ^ 1)
-            sums = trainer.step(self.stages[slot].audio, text)
-            self.free[slot].record(torch.cuda.current_stream())
-        return sums
-
-
-class MelUnderAdam:
-    """The next step's mel-dB + z-score on its own stream, started once the current step's backward is enqueued
-    (Trainer.step before_adam): the STFT runs under Adam + weight packing (streaming, no dependency on the
-    mel input) instead of ahead of the forward.  One mel buffer: the step's inputs are last read by the loss,
-    which precedes the backward.  Every timed step still computes one batch's mel features."""
-
-    def __init__(self, stage, device):
-        self.stage = stage
-        self.stream = torch.cuda.Stream(device=device)
-        self.go, self.ready = torch.cuda.Event(), torch.cuda.Event()
-        self.primed = False
-
-    def launch(self, pcm):
-        self.go.record(torch.cuda.current_stream())
-        with torch.cuda.stream(self.stream):
-            self.stream.wait_event(self.go)
-            self.stage(pcm)
-            self.ready.record(self.stream)
-
-    def step(self, trainer, pcm, text, cond):
-        if not self.primed:
-            self.launch(pcm)
-            self.primed = True
-        torch.cuda.current_stream().wait_event(self.ready)
-        return trainer.step(self.stage.audio, text, cond, before_adam=lambda: self.launch(pcm))
-
-
 # Op kinds of the live kernel probe (include/hlmc.h hlmc_probe_arm) and the kernel each one launches
 PROBE_KINDS = {
     1: ("conv_s2", "gemm_nt ConvS2Loader (conv fwd / convT dgrad)", "mfma"),
@@ -149,7 +94,7 @@ WORKLOADS = {
 }
 
 
-def build_workload(name, dtype, B, device, world, seed=42):
+def build_workload(name, dtype, B, device, world, seed=42, grad_dtype=torch.float32):
     """Model (seed-42 init), fused Trainer and the synthetic side inputs (lyrics embeddings ~ N(0, 1/td), one-hot
     genres) of one BASELINE workload at 128 x 128 mel."""
     torch.manual_seed(seed)
@@ -163,21 +108,22 @@ def build_workload(name, dtype, B, device, world, seed=42):
         model = hlmc_amd.HybridVAE(128, 384, (128, 128), audio_only=name == "audio", compute_dtype=dtype).to(device)
         if name == "hybrid":
             text = torch.randn(B, 384, device=device, generator=g) / 384 ** 0.5
-    trainer = hlmc_amd.Trainer(model, lr=1e-4, distributed=world > 1)
+    trainer = hlmc_amd.Trainer(model, lr=1e-4, distributed=world > 1, grad_dtype=grad_dtype)
     return model, trainer, text, cond
 
 
-def time_workload(name, dtype, B, device, world, mel, pcm, dist, steps=10, warmup=3):
-    """Whole-job clips/s of one extra workload (same mel stage, same timing protocol as the headline)."""
-    model, trainer, text, cond = build_workload(name, dtype, B, device, world)
-    for _ in range(warmup):
-        trainer.step(mel(pcm), text, cond)
+def time_workload(name, dtype, B, device, world, mel, pcms, dist, steps=10, warmup=3, grad_dtype=torch.float32):
+    """Whole-job clips/s of one extra workload (same mel stage, same rotating PCM batches, same timing protocol as
+    the headline)."""
+    model, trainer, text, cond = build_workload(name, dtype, B, device, world, grad_dtype=grad_dtype)
+    for k in range(warmup):
+        trainer.step(mel(pcms[k % len(pcms)]), text, cond)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        sums = trainer.step(mel(pcm), text, cond)
+    for k in range(steps):
+        sums = trainer.step(mel(pcms[k % len(pcms)]), text, cond)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -194,6 +140,78 @@ def time_workload(name, dtype, B, device, world, mel, pcm, dist, steps=10, warmu
     del trainer, model
     torch.cuda.empty_cache()
     return out
+
+
+def _kmeans_data(n=100000, d=128, k=10, spread=0.3, seed=5):
+    """Latent-like rows: N(0, 1) points around k centres drawn from N(0, spread^2) (overlapping clusters, the
+    tests/golden N = 100k recipe), float32."""
+    rng = np.random.default_rng(seed)
+    c = rng.normal(0, spread, (k, d))
+    lab = rng.integers(0, k, n)
+    return (c[lab] + rng.normal(0, 1.0, (n, d))).astype(np.float32)
+
+
+def time_kmeans(device, dist, world, rank, cpu_leg=True):
+    """KMeans(10, random_state=42, n_init=10).fit on 100 000 x 128 latents (src/Convolutional_VAE.py:317-319 at
+    BASELINE config[4]'s clustering scale): the HIP E/M-step kernels + the host k-means++ (restarts sharded over
+    ranks), against sklearn's fit on the host cores (rank 0, N = 1)."""
+    X = _kmeans_data()
+    Xd = torch.from_numpy(X).to(device)
+    group = dist.group.WORLD if dist else None
+    hlmc_amd.KMeans(10, random_state=42, n_init=10, process_group=group).fit(Xd)      # warm-up (allocations)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    km = hlmc_amd.KMeans(10, random_state=42, n_init=10, process_group=group).fit(Xd)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    out = {"workload": "KMeans(n_clusters=10, random_state=42, n_init=10).fit, N=100000 x 128 f32 latents",
+           "fit_ms": round(1e3 * el, 2), "n_iter": int(km.n_iter_), "inertia": float(km.inertia_),
+           "higher_is_better": False}
+    if cpu_leg and rank == 0 and world == 1:
+        from sklearn.cluster import KMeans as SkKMeans
+        from sklearn.metrics import adjusted_rand_score
+        from threadpoolctl import threadpool_limits
+        cores, _ = host_cpu_share()
+        with threadpool_limits(limits=cores):
+            t0 = time.perf_counter()
+            sk = SkKMeans(10, random_state=42, n_init=10).fit(X)
+            sk_s = time.perf_counter() - t0
+        out["sklearn_cpu"] = {"fit_ms": round(1e3 * sk_s, 1), "cores": cores, "n_iter": int(sk.n_iter_),
+                              "inertia": float(sk.inertia_)}
+        out["speedup_vs_sklearn"] = round(sk_s / el, 1)
+        # sklearn at `cores` threads sums centres in a thread-dependent order; the bit-exact label contract is pinned
+        # against single-thread sklearn in tests/test_kmeans_gpu.py — here the agreement is reported as ARI
+        out["ari_vs_sklearn"] = round(float(adjusted_rand_score(sk.labels_, km.labels_)), 6)
+    return out
+
+
+def time_e2e(device, dist, world, n_clips, grad_dtype):
+    """BASELINE config[4] end to end (hlmc_amd.pipeline.run_pipeline): synthetic 30 s PCM -> HIP mel-dB (1024 kept
+    frames) -> per-pixel StandardScaler -> HybridVAE 128x1024 (768-d lyrics) bf16 training, one epoch, bs 256 per
+    GPU -> eval latents -> KMeans(10, n_init=10).  Strong scaling: n_clips in total, sharded over the ranks."""
+    group = dist.group.WORLD if dist else None
+    hlmc_amd.pipeline.run_pipeline(512 * world, batch=256, epochs=1, process_group=group, grad_dtype=grad_dtype)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    r = hlmc_amd.pipeline.run_pipeline(n_clips, batch=256, epochs=1, process_group=group, grad_dtype=grad_dtype)
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return {"workload": "config[4] end to end: 30 s PCM -> mel-dB -> scaler -> HybridVAE 128x1024 bf16 train (1 epoch) "
+                        "-> eval latents -> KMeans(10, n_init=10)",
+            "n_clips": n_clips, "value": round(n_clips / el, 2), "unit": "clips/s", "seconds": round(el, 3),
+            "stages_s_rank0": {k: round(v, 4) for k, v in r["stages_s"].items()}, "train_steps": r["train_steps"],
+            "final_loss": r["final_loss"], "kmeans_n_iter": int(r["kmeans_n_iter"])}
 
 
 def probe_read(cap=4096):
@@ -251,8 +269,10 @@ def host_cpu_share():
     return cores, quota
 
 
-def cpu_baseline(batch=256, steps=5):
-    """Oracle (torch-CPU restatement of the reference model + numpy restatement of librosa) on host cores."""
+def cpu_baseline(batch=256, steps=5, warmup=2):
+    """Oracle (torch-CPU restatement of the reference model + numpy restatement of librosa) on host cores:
+    SURVEY §8(d) protocol (2 warm-up steps, >= 5 timed), the mel stage and the VAE step timed separately so the
+    VAE-only rate (the reference's Convolutional_VAE.py train step alone) is reported beside the whole step."""
     from multiprocessing import Pool
 
     from oracle import mel_oracle, models_oracle
@@ -264,27 +284,39 @@ def cpu_baseline(batch=256, steps=5):
     model = models_oracle.HybridVAE(128, 768, (128, 128), audio_only=True)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     with Pool(cores) as pool:
-        def one_step():
+        def mel_stage():
             mel = np.stack(pool.map(mel_oracle.extract_mel_spectrogram, list(pcm)))
-            x = torch.from_numpy((mel - mel.mean(0)) / (mel.std(0) + 1e-8)).float()[:, None]
+            return torch.from_numpy((mel - mel.mean(0)) / (mel.std(0) + 1e-8)).float()[:, None]
+
+        def vae_step(x):
             opt.zero_grad()
             ra, _, mu, lv = model(x)
             loss = models_oracle.loss_function(ra, x, None, None, mu, lv)[0]
             loss.backward()
             opt.step()
-        one_step()
-        t0 = time.perf_counter()
+
+        for _ in range(warmup):
+            vae_step(mel_stage())
+        t_mel = t_vae = 0.0
         for _ in range(steps):
-            one_step()
-        dt = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            x = mel_stage()
+            t1 = time.perf_counter()
+            vae_step(x)
+            t2 = time.perf_counter()
+            t_mel += t1 - t0
+            t_vae += t2 - t1
+    dt = t_mel + t_vae
     return {"value": round(batch * steps / dt, 2), "unit": "clips/s", "cores": cores, "kind": "port",
+            "vae_only_value": round(batch * steps / t_vae, 2), "mel_only_value": round(batch * steps / t_mel, 2),
             "affinity_cores": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota,
             "sample": f"audio-only HybridVAE 128x128 torch-CPU restatement fwd+bwd+Adam ({cores} torch threads) + "
                       f"numpy librosa-mel restatement ({cores}-process pool), bs={batch}, {steps} timed steps after "
-                      f"1 warmup ({dt:.1f} s)"}
+                      f"{warmup} warm-up steps ({dt:.1f} s: mel {t_mel:.1f} s, VAE {t_vae:.1f} s)"}
 
 
 PROBE_STEPS = int(os.environ.get("HLMC_PROBE_STEPS", "3"))  # timed steps whose dominant-kernel launches are timed
+PCM_BATCHES = 5
 
 
 def main():
@@ -298,9 +330,10 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--prefetch", action="store_true",
-                    help="overlap step k+1's mel stage with step k on a third stream (measured 6%% slower on MI355X: "
-                         "the STFT blocks delay the forward's critical-path GEMMs)")
+    ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default=None,
+                    help="gradient all-reduce wire for N > 1 (default bf16: half the xGMI bytes, DESIGN.md §7; the "
+                         "fp32 master gradient is what Adam reads either way)")
+    ap.add_argument("--e2e-clips", type=int, default=20000, help="clips of the config[4] end-to-end extra line")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (N = 1 only; measured 12%% slower on ROCm 7: the graph "
                          "executor serialises the weight-gradient stream's branch, see DESIGN.md)")
@@ -330,23 +363,22 @@ def main():
     B = args.batch
     audio_only = args.workload == "audio"
     # ---- setup (untimed): model, optimizer state, scaler fit on a calibration batch
-    pcm = synthetic_pcm(B, N_SAMPLES, seed=1000 + rank, device=device)
+    # PCM_BATCHES distinct batches (5 x 66.6 MB = 333 MB at B = 256, more than the 256 MiB Infinity Cache), one per
+    # step in rotation: every step's STFT streams its PCM from HBM, not from a cache that held the last step's
+    pcms = [synthetic_pcm(B, N_SAMPLES, seed=1000 + 17 * j + rank, device=device) for j in range(PCM_BATCHES)]
+    pcm = pcms[0]
     calib = hlmc_amd.extract_mel_spectrogram(pcm, fixed_time_steps=FRAMES)
     scaler = hlmc_amd.StandardScaler().fit(calib.reshape(B, -1))
     mel = MelStage(B, device, scaler)
-    model, trainer, text, cond = build_workload(args.workload, args.dtype, B, device, world)
-    prefetch = args.prefetch and not args.graph and args.workload != "cvae"
-    pipe = MelPipeline(B, device, scaler) if prefetch else None
-
-    # HLMC_MEL_OVERLAP=1: the next step's mel stage under this step's Adam (measured 2.4% slower: 102.6k vs
-    # 105.2k, 3 alternating rounds; the default keeps it ahead of each forward on the step's stream)
-    under_adam = MelUnderAdam(mel, device) if (os.environ.get("HLMC_MEL_OVERLAP", "0") == "1" and not args.graph
-                                               and not prefetch) else None
+    gd = args.grad_dtype or ("bf16" if world > 1 else "fp32")
+    grad_dtype = torch.bfloat16 if gd == "bf16" else torch.float32
+    model, trainer, text, cond = build_workload(args.workload, args.dtype, B, device, world, grad_dtype=grad_dtype)
+    nstep = [0]
 
     def step():
-        if under_adam is not None:
-            return under_adam.step(trainer, pcm, text, cond)
-        x = mel(pcm)
+        p = pcms[nstep[0] % PCM_BATCHES]
+        nstep[0] += 1
+        x = mel(p)
         return trainer.step(x, text, cond)
 
     for _ in range(args.warmup):
@@ -391,15 +423,10 @@ def main():
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    if pipe is not None:
-        if probe_from >= 0:
-            L.check(L.lib().hlmc_probe_arm(dominant, 64 * args.steps), "hlmc_probe_arm")
-        sums = pipe.run(trainer, pcm, text, args.steps)
-    else:
-        for k in range(args.steps):
-            if k == probe_from:
-                L.check(L.lib().hlmc_probe_arm(dominant, 64 * probe_steps), "hlmc_probe_arm")
-            sums = run_step()
+    for k in range(args.steps):
+        if k == probe_from:
+            L.check(L.lib().hlmc_probe_arm(dominant, 64 * probe_steps), "hlmc_probe_arm")
+        sums = run_step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -430,7 +457,9 @@ def main():
         torch.cuda.empty_cache()
         for key, (wl, dt) in {"audio_fp32": ("audio", "fp32"), "hybrid_td384_bf16": ("hybrid", "bf16"),
                               "cvae_bf16": ("cvae", "bf16")}.items():
-            extras[key] = time_workload(wl, dt, B, device, world, mel, pcm, dist)
+            extras[key] = time_workload(wl, dt, B, device, world, mel, pcms, dist, grad_dtype=grad_dtype)
+        extras["kmeans_n100k_k10"] = time_kmeans(device, dist, world, rank)
+        extras["config4_e2e_n20k"] = time_e2e(device, dist, world, args.e2e_clips, grad_dtype)
 
     if rank == 0:
         n_params = params_of_headline
@@ -445,11 +474,12 @@ def main():
                "config": {"workload": WORKLOADS[args.workload] +
                                       ": PCM[256,65024] -> HIP mel-dB 128x128 -> z-score -> VAE fwd+bwd+Adam",
                           "per_gpu_batch": B, "global_batch": B * world, "mel": "128x128", "params": n_params,
-                          "parallelism": f"dp{world}", **({"backend": backend} if world > 1 else {}),
+                          "parallelism": f"dp{world}",
+                          **({"backend": backend, "grad_wire": gd} if world > 1 else {}),
+                          "pcm_batches": f"{PCM_BATCHES} distinct batches in rotation "
+                                         f"({PCM_BATCHES * B * N_SAMPLES * 4 / 1e6:.0f} MB)",
                           "final_loss": round(loss, 3),
-                          "execution": ("HIP graph replay of the whole step" if graphed else
-                                        "eager launches; mel stage of step k+1 on its own stream during step k"
-                                        if pipe is not None else "eager launches"),
+                          "execution": "HIP graph replay of the whole step" if graphed else "eager launches",
                           "step_mfma_frac": (round(value / world * flops_clip / 1e12 / PEAK_BF16_TFLOPS, 4)
                                              if flops_clip else None)}}
         if live is not None:

@@ -15,11 +15,13 @@ sgemm call (oracle/kmeans_oracle.py estep_dist), per-cluster sums in sklearn's s
 inertia.
 
 Multi-GPU (``process_group=``): the n_init restarts are independent objects, so they shard across ranks
-with no collective on the data path.  Every rank holds the same (small, [N, D] f32) latents and runs ALL
-k-means++ seedings -- sklearn draws every restart's seeds from one RandomState stream, and a seeding costs
-k distance rows against a Lloyd run's up-to-300 E/M passes -- but runs Lloyd only for restarts
-``i % world == rank``.  One ``all_gather_object`` of (restart, labels, inertia, centres, n_iter) at the end
-feeds sklearn's sequential best-of rule in restart order, so the result is bit-identical for any world size.
+with no collective on the data path.  Every rank holds the same (small, [N, D] f32) latents and runs the
+k-means++ seeding and Lloyd iterations of restarts ``i % world == rank`` only.  sklearn draws every restart's
+seeds from one RandomState stream; a seeding consumes a data-independent number of doubles
+(``seeding_draws``), so a rank skips another rank's seeding by drawing and discarding exactly that many and
+its own restarts see the same random numbers as in a single process.  One ``all_gather_object`` of (restart,
+labels, inertia, centres, n_iter) at the end feeds sklearn's sequential best-of rule in restart order, so the
+result is bit-identical for any world size.
 """
 from __future__ import annotations
 
@@ -180,6 +182,13 @@ class KMeans:
         return labels, float(inertia.item()), centers, it + 1
 
     @staticmethod
+    def seeding_draws(k):
+        """Doubles one k-means++ seeding takes from the RandomState stream: choice(n, p) draws one, then each of
+        the k - 1 further centres draws n_local_trials = 2 + int(ln k) (uniform(size=trials)); the count does
+        not depend on the data."""
+        return 1 + (k - 1) * (2 + int(np.log(k)))
+
+    @staticmethod
     def _select_best(runs, k):
         """sklearn's best-of-n_init rule applied in restart order (sklearn/cluster/_kmeans.py, KMeans.fit):
         a later restart wins only with strictly lower inertia AND a different partition."""
@@ -210,10 +219,14 @@ class KMeans:
             world = dist.get_world_size(self.process_group)
             rank = dist.get_rank(self.process_group)
         runs = []
+        draws = self.seeding_draws(self.n_clusters)
         for i in range(n_init):
-            c0, _ = self._kmeans_plusplus(Xc, rs, w)      # every rank: keeps the one RandomState stream
             if i % world != rank:
+                # another rank's restart: advance the one RandomState stream past its seeding (a fixed count of
+                # doubles) instead of computing it, so every rank seeds only its own restarts
+                rs.random_sample(draws)
                 continue
+            c0, _ = self._kmeans_plusplus(Xc, rs, w)
             labels, inertia, centers, n_iter = self._lloyd(Xc, c0, tol)
             runs.append((i, labels.cpu().numpy(), inertia, centers.cpu().numpy(), n_iter))
         if world > 1:

@@ -49,31 +49,87 @@ def _sync():
     return time.perf_counter()
 
 
+def shard_bounds(n_clips, world):
+    """Contiguous clip shards [lo, hi) per rank: sizes n // world, the first n % world ranks one more."""
+    q, r = divmod(n_clips, world)
+    out, lo = [], 0
+    for k in range(world):
+        hi = lo + q + (1 if k < r else 0)
+        out.append((lo, hi))
+        lo = hi
+    return out
+
+
+def local_batches(shard_sizes, rank, batch):
+    """Per-step slices [a, b) of rank `rank`'s epoch order such that every rank takes the SAME number of steps
+    (each step all-reduces gradients): steps = ceil(smallest shard / batch); a larger shard (by one clip) folds its
+    extra clips into its last batch.  A last batch under 2 rows on any rank (train-mode BatchNorm needs >= 2) is
+    merged into the step before it on every rank."""
+    smin = min(shard_sizes)
+    steps = max(1, -(-smin // batch))
+    if steps > 1 and any(s - (steps - 1) * batch < 2 for s in shard_sizes):
+        steps -= 1
+    n = shard_sizes[rank]
+    return [(k * batch, n if k == steps - 1 else (k + 1) * batch) for k in range(steps)]
+
+
+def _all_gather_rows(t, group, bounds):
+    """[hi - lo, ...] per rank -> [n, ...] in clip order (every rank).  gloo gathers host copies."""
+    import torch.distributed as dist
+    world = len(bounds)
+    width = max(hi - lo for lo, hi in bounds)
+    gloo = dist.get_backend(group) == "gloo"
+    src = t if not gloo else t.cpu()
+    pad = torch.zeros((width,) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+    pad[:t.shape[0]] = src
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    return torch.cat([p[:hi - lo] for p, (lo, hi) in zip(parts, bounds)]).to(t.device)
+
+
 def run_pipeline(n_clips, batch=256, epochs=1, text_dim=768, latent_dim=128, compute_dtype="bf16", k=10,
                  n_init=10, seed=0, pcm_fn=None, lyrics=None, eps_fn=None, order_fn=None, keep_outputs=False,
-                 device=None):
+                 device=None, process_group=None, grad_dtype=torch.float32):
     """Run config[4] on `n_clips` clips; returns a dict of per-stage seconds and results.
 
     pcm_fn(i, b) -> [b, 661500] float32 device PCM of clips i..i+b (default: synthetic_clips seeded per batch);
     lyrics: [n_clips, text_dim] lyric embeddings (default: seeded N(0, 1/text_dim), on the device);
     eps_fn(step, b) -> reparameterisation noise (default torch.randn, as the reference's randn_like);
-    order_fn(epoch) -> clip order of that epoch (default a seeded torch.randperm: DataLoader(shuffle=True))."""
+    order_fn(epoch) -> clip order of that epoch over the rank's shard (local indices; default a seeded
+    torch.randperm: DataLoader(shuffle=True)).
+
+    process_group (data parallel, one process per GPU): the clips are cut into contiguous shards, one per rank
+    (shard_bounds).  Each rank computes the mel-dB of its own shard only; the per-pixel StandardScaler all-reduces
+    its f64 pass sums (every rank gets the global statistics, as the reference's whole-dataset fit,
+    src/1_preprocessing_advanced.py:376-382); training is Trainer(distributed=True) — every step each rank takes
+    `batch` clips of its shard (local_batches), gradients are SUM all-reduced (RCCL over xGMI) and rank 0's
+    BatchNorm running statistics broadcast (DDP semantics); each rank encodes its shard with the (identical)
+    trained model, the latents are all-gathered in clip order and KMeans(process_group) shards the n_init
+    restarts, so every rank returns the same labels."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    world, rank = 1, 0
+    if process_group is not None:
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(process_group), dist.get_rank(process_group)
+    bounds = shard_bounds(n_clips, world)
+    lo, hi = bounds[rank]
+    n_local = hi - lo
     if pcm_fn is None:
         def pcm_fn(i, b):
             return synthetic_clips(b, CLIP_SAMPLES, seed * 1000003 + i, dev)
-    out = {"n_clips": n_clips, "batch": batch, "epochs": epochs, "compute_dtype": compute_dtype, "stages_s": {}}
+    out = {"n_clips": n_clips, "batch": batch, "epochs": epochs, "compute_dtype": compute_dtype, "world": world,
+           "shard": (lo, hi), "stages_s": {}}
     st = out["stages_s"]
 
-    # ---- 1. mel-dB of every clip (1292 frames, ref = max over all of them, 1024 kept), resident in HBM
+    # ---- 1. mel-dB of this rank's clips (1292 frames, ref = max over all of them, 1024 kept), resident in HBM
     t0 = _sync()
-    mel = torch.empty(n_clips, 128, KEEP_FRAMES, device=dev)
+    mel = torch.empty(n_local, 128, KEEP_FRAMES, device=dev)
     evs = []   # per batch: (before the clip source, after it = before the mel kernels, after them)
-    for i in range(0, n_clips, batch):
-        b = min(batch, n_clips - i)
+    for i in range(0, n_local, batch):
+        b = min(batch, n_local - i)
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         e[0].record()
-        pcm = pcm_fn(i, b)
+        pcm = pcm_fn(lo + i, b)
         e[1].record()
         mel[i:i + b] = extract_mel_spectrogram(pcm, fixed_time_steps=KEEP_FRAMES)
         e[2].record()
@@ -83,8 +139,8 @@ def run_pipeline(n_clips, batch=256, epochs=1, text_dim=768, latent_dim=128, com
     st["mel_only"] = sum(e[1].elapsed_time(e[2]) for e in evs) / 1e3     # GPU time of the STFT/mel/dB kernels
     st["pcm_source"] = sum(e[0].elapsed_time(e[1]) for e in evs) / 1e3   # synthetic clip generation (torch)
 
-    # ---- 2. per-pixel StandardScaler over [N, 131072] (float64 accumulators)
-    scaler = StandardScaler().fit(mel.view(n_clips, -1))
+    # ---- 2. per-pixel StandardScaler over [N, 131072] (float64 accumulators; all-reduced over the shards)
+    scaler = StandardScaler(process_group=process_group).fit(mel.view(n_local, -1))
     t2 = _sync()
     st["scaler_fit"] = t2 - t1
 
@@ -92,12 +148,14 @@ def run_pipeline(n_clips, batch=256, epochs=1, text_dim=768, latent_dim=128, com
     if lyrics is None:
         g = torch.Generator(device=dev).manual_seed(seed + 17)
         lyrics = torch.randn(n_clips, text_dim, device=dev, generator=g) / text_dim ** 0.5
-    lyrics = lyrics.to(dev).float().contiguous()
+    lyrics = lyrics.to(dev).float()[lo:hi].contiguous()
     torch.manual_seed(42)
     model = HybridVAE(latent_dim, text_dim, (128, KEEP_FRAMES), compute_dtype=compute_dtype).to(dev)
-    trainer = Trainer(model, lr=1e-4)
-    xb = torch.empty(batch, 1, 128, KEEP_FRAMES, device=dev)
-    tb = torch.empty(batch, text_dim, device=dev)
+    trainer = Trainer(model, lr=1e-4, process_group=process_group, grad_dtype=grad_dtype)
+    slices = local_batches([h - l for l, h in bounds], rank, batch)
+    bmax = max(b - a for a, b in slices)
+    xb = torch.empty(bmax, 1, 128, KEEP_FRAMES, device=dev)
+    tb = torch.empty(bmax, text_dim, device=dev)
 
     def zscore_into(idx):
         b = idx.numel()
@@ -107,15 +165,13 @@ def run_pipeline(n_clips, batch=256, epochs=1, text_dim=768, latent_dim=128, com
         tb[:b].copy_(lyrics.index_select(0, idx))
         return xb[:b], tb[:b]
 
-    gperm = torch.Generator(device=dev).manual_seed(seed + 29)
+    gperm = torch.Generator(device=dev).manual_seed(seed + 29 + 7919 * rank)
     step, sums = 0, None
     for ep in range(epochs):
         order = (order_fn(ep).to(dev) if order_fn is not None
-                 else torch.randperm(n_clips, device=dev, generator=gperm))   # DataLoader(shuffle=True)
-        for i in range(0, n_clips, batch):
-            idx = order[i:i + batch]
-            if idx.numel() < 2:      # BatchNorm in train mode needs >= 2 rows (the reference's last batch >= 2)
-                continue
+                 else torch.randperm(n_local, device=dev, generator=gperm))   # DataLoader(shuffle=True)
+        for a, b in slices:
+            idx = order[a:b]
             x, t = zscore_into(idx)
             eps = eps_fn(step, idx.numel()) if eps_fn is not None else None
             sums = trainer.step(x, t, eps=eps)
@@ -125,21 +181,23 @@ def run_pipeline(n_clips, batch=256, epochs=1, text_dim=768, latent_dim=128, com
     out["train_steps"] = step
     out["final_loss"] = trainer.loss_tuple(sums)[0] if sums is not None else None
 
-    # ---- 4. eval-mode latent extraction (mu of encode)
+    # ---- 4. eval-mode latent extraction (mu of encode) of this rank's clips, gathered in clip order
     trainer.release()
     model.eval()
-    latents = torch.empty(n_clips, latent_dim, device=dev)
-    ar = torch.arange(n_clips, device=dev)
+    latents = torch.empty(n_local, latent_dim, device=dev)
+    ar = torch.arange(n_local, device=dev)
     with torch.no_grad():
-        for i in range(0, n_clips, batch):
+        for i in range(0, n_local, batch):
             idx = ar[i:i + batch]
             x, t = zscore_into(idx)
             latents[i:i + idx.numel()] = model.encode(x, t)[0]
+    if world > 1:
+        latents = _all_gather_rows(latents, process_group, bounds)
     t4 = _sync()
     st["encode"] = t4 - t3
 
     # ---- 5. KMeans(k, random_state=42, n_init) on the latents (sklearn semantics, bit-exact labels)
-    km = KMeans(n_clusters=k, random_state=42, n_init=n_init).fit(latents)
+    km = KMeans(n_clusters=k, random_state=42, n_init=n_init, process_group=process_group).fit(latents)
     t5 = _sync()
     st["kmeans"] = t5 - t4
     st["total"] = t5 - t0

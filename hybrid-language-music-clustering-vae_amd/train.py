@@ -112,6 +112,8 @@ class Trainer:
         lib = L.lib()
         s = L.stream()
         B = in0.shape[0]
+        if self.broadcast_buffers:
+            self._check_bn_flat()
         c = self._buffers(B)
         out, d = c["out"], c["d"]
         if eps is None:
@@ -141,6 +143,9 @@ class Trainer:
             else:
                 self.allreduce_grads()
         if before_adam is not None:
+            # the inputs must be out of every reader's hands: with the tail weight gradients left on the side stream
+            # (overlap_adam) the encoder's first weight gradient still reads in0 -> join it first
+            L.check(lib.hlmc_net_settle(self.net.h, s), "hlmc_net_settle")
             before_adam()
         if self._graph:  # coefficients staged by prepare_step_coefficients()
             L.check(lib.hlmc_net_adam_step_dev(self.net.h, s, *self._mv, self._coef_dev.data_ptr()),
@@ -179,6 +184,15 @@ class Trainer:
             L.check(nb, "hlmc_net_grad_buckets")
         return bucket_ranges(list(starts)[:nb], offs)
 
+    def _check_bn_flat(self):
+        """The buffer broadcast sends the flat tensor the BatchNorm running statistics were re-pointed at when this
+        Trainer was built; a later module._apply (device move, .half()) or load_state_dict(assign=True) replaces
+        them with new tensors, and a silent broadcast of the stale flat copy would let the ranks drift apart."""
+        bns = [m for m in self.model.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)]
+        if bns and bns[0].running_mean.data_ptr() != self.bn_flat.data_ptr():
+            raise L.HLMCError("BatchNorm running statistics were replaced after the Trainer was built "
+                              "(module._apply / load_state_dict(assign=True)); build a new Trainer")
+
     def _broadcast_buffers_after_forward(self):
         """Rank 0's BatchNorm running statistics to every rank (DDP broadcast_buffers), issued right after the
         forward that updated them: on the comm stream (under the backward pass) on a GPU, else synchronously."""
@@ -209,8 +223,10 @@ class Trainer:
             for k, (lo, hi) in enumerate(self.buckets):
                 L.check(lib.hlmc_net_bucket_wait(self.net.h, k, self._comm.cuda_stream), "hlmc_net_bucket_wait")
                 works.append(_allreduce_sum(self.gflat[lo:hi], self.grad_dtype, self.process_group, async_op=True))
-        for w in works:
-            w.wait()
+            # every bucket's collective is in flight before the first wait; the wait makes the comm stream (not
+            # the host, under RCCL) wait for it, and a bf16 wire's copy-back follows on the comm stream
+            for w in works:
+                w.wait()
         torch.cuda.current_stream().wait_stream(self._comm)
 
     def allreduce_grads(self):
@@ -243,19 +259,32 @@ def bucket_ranges(starts, offsets):
 
 
 def _allreduce_sum(buf, grad_dtype, group, async_op=False):
-    """SUM all-reduce of a contiguous fp32 gradient slice (optionally on a bf16 wire copy: converted, reduced and
-    copied back on the current stream, which the caller must make its consumers wait for)."""
+    """SUM all-reduce of a contiguous fp32 gradient slice, optionally on a bf16 wire copy (half the bytes over
+    xGMI): converted on the current stream, reduced in place, and copied back into `buf` by the handle's wait()
+    on the stream wait() is called from (the caller makes its consumers wait for that stream)."""
     import torch.distributed as dist
     if grad_dtype == torch.float32:
         return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
     g = buf.to(grad_dtype)
-    dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
-    buf.copy_(g)
-    return _Done()
+    w = _WireWork(dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group, async_op=True), g, buf)
+    if not async_op:
+        w.wait()
+    return w
 
 
-class _Done:
+class _WireWork:
+    """Handle of a reduced-precision wire all-reduce: wait() orders the current stream after the collective
+    (RCCL: a stream wait, the host does not block) and copies the reduced wire values back into the fp32
+    buffer on that stream."""
+
+    def __init__(self, work, wire, buf):
+        self.work, self.wire, self.buf = work, wire, buf
+
     def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.buf.copy_(self.wire)
+            self.work = None
         return True
 
 

@@ -230,7 +230,9 @@ int hlmc_km_sums(void* stream, const float* X, int64_t n, int d, const int32_t* 
                  float* weight);
 /* The same sums through a stable partition of the rows by label (device workspace of
  * hlmc_km_sums_workspace(n, k) bytes): the rows of each cluster become one contiguous list in row order and
- * one block per (64-column slab, cluster) gathers 256-row groups into LDS and adds them in order (k <= 4096). */
+ * one 1024-thread block per (64-column slab, cluster) runs a loader/adder ring: 15 loader waves gather 64-row
+ * chunks into an 8-slot LDS ring, one adder wave adds them in row order.  Limits: 0 < n < 2^30, k <= 8192.
+ * n <= 4096 rows take hlmc_km_sums instead (one launch is faster there); the results are the same bits. */
 int64_t hlmc_km_sums_workspace(int64_t n, int k);
 int hlmc_km_sums_part(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sums,
                       float* weight, void* ws, int64_t ws_bytes);

@@ -12,7 +12,9 @@ Tolerances:
   * fp32 engine from the same z-scored input: mu / logvar / ELBO terms <= 1e-4 relative (north_star);
     gradients by the f64-yardstick rule of test_models_gpu.compare_step; Adam exact vs torch.optim.Adam on
     the same gradient; BatchNorm running statistics <= 1e-4;
-  * bf16 engine (the bench dtype): mu 3e-2, ELBO 2e-2, global gradient 0.15 relative L2 (test_models_gpu);
+  * bf16 engine (the bench dtype): mu / ELBO / global gradient within BF16_TOL (about 3x the measured errors)
+    and every weight tensor's gradient within 0.1 relative L2 of the fp32 oracle's;
+  * configs[2] (hybrid, 384-d lyrics) and [3] (CVAE) at the same B = 256 shapes, fp32 and bf16;
   * the whole oracle chain (oracle mel -> oracle f64 scaler -> oracle model) vs the HIP chain: the inputs
     differ by the mel tolerance, so ELBO / mu are compared at 1e-3 (fp32 engine).
 """
@@ -29,32 +31,59 @@ from tests.test_models_gpu import _bias_feeds_bn, oracle64_with_kink_envelope, r
 
 pytestmark = pytest.mark.gpu
 B = 256
-CASE = {"kind": "hybrid"}
 
 
-def _hip_chain(dtype):
+LATENT = {"audio": 128, "hybrid": 128, "cvae": 64}
+
+
+def _hip_chain(dtype, workload="audio"):
+    """The bench's own chain for one BASELINE workload (bench.build_workload: seed-42 model, fused Trainer, the
+    synthetic lyrics / one-hot genres) on the bench's PCM, one train step from eps ~ Generator(1)."""
     dev = torch.device("cuda", 0)
     pcm = bench.synthetic_pcm(B, bench.N_SAMPLES, seed=1000, device=dev)
     calib = hlmc_amd.extract_mel_spectrogram(pcm, fixed_time_steps=bench.FRAMES)
     scaler = hlmc_amd.StandardScaler().fit(calib.reshape(B, -1))
     stage = bench.MelStage(B, dev, scaler)
     x = stage(pcm)
-    torch.manual_seed(42)
-    model = hlmc_amd.HybridVAE(128, 384, (128, 128), audio_only=True, compute_dtype=dtype).to(dev)
-    trainer = hlmc_amd.Trainer(model, lr=1e-4)
-    eps = torch.randn(B, 128, generator=torch.Generator().manual_seed(1))
+    model, trainer, text, cond = bench.build_workload(workload, dtype, B, dev, 1)
+    eps = torch.randn(B, LATENT[workload], generator=torch.Generator().manual_seed(1))
     init = [p.detach().cpu().clone() for p in model.parameters()]
-    sums = trainer.step(x, None, eps=eps.to(dev))
+    sums = trainer.step(x, text, cond, eps=eps.to(dev))
     out = trainer._cache[B]["out"]
     torch.cuda.synchronize()
     return dict(pcm=pcm.cpu().numpy(), mel=stage.mel.cpu().numpy(), x=x.detach().cpu().clone(), eps=eps,
+                text=None if text is None else text.cpu(), cond=None if cond is None else cond.cpu(),
                 loss=trainer.loss_tuple(sums), mu=out["mu"].cpu(), logvar=out["logvar"].cpu(),
+                recon=out["recon"].cpu(), recon_text=out["recon_text"].cpu() if "recon_text" in out else None,
                 grad=trainer.gflat.detach().cpu().clone(), init=init, model=model)
 
 
-def _oracle_model():
+def _oracle_model(workload="audio"):
     torch.manual_seed(42)
-    return OM.HybridVAE(128, 384, (128, 128), audio_only=True)
+    if workload == "cvae":
+        return OM.ConditionalVAE(64, 768, 10, (128, 128))
+    return OM.HybridVAE(128, 384, (128, 128), audio_only=workload == "audio")
+
+
+def _case(workload):
+    return {"kind": "cvae" if workload == "cvae" else "hybrid"}
+
+
+def _ins(h, workload):
+    if workload == "cvae":
+        return (h["x"], h["text"], h["cond"])
+    return (h["x"], h["text"])
+
+
+def _oracle_step(ora, h, workload):
+    ins = _ins(h, workload)
+    out = ora(*ins, eps=h["eps"])
+    if workload == "cvae":
+        lo = OM.cvae_loss_function(out[0], ins[0], out[1], ins[1], out[2], out[3], beta=4.0)
+    else:
+        lo = OM.loss_function(out[0], ins[0], out[1], ins[1], out[2], out[3])
+    lo[0].backward()
+    return out, lo
 
 
 def test_bench_mel_stage_matches_oracle(cuda):
@@ -70,19 +99,24 @@ def test_bench_mel_stage_matches_oracle(cuda):
     np.testing.assert_allclose(h["x"].numpy(), z, rtol=1e-5, atol=1e-5)
 
 
-def test_bench_train_step_fp32_matches_oracle(cuda):
-    h = _hip_chain("fp32")
-    x, eps = h["x"], h["eps"]
-    ora = _oracle_model()
+@pytest.mark.parametrize("workload", ["audio", "hybrid", "cvae"])
+def test_bench_train_step_fp32_matches_oracle(cuda, workload):
+    """BASELINE configs[1] (audio), [2] (hybrid, 384-d lyrics) and [3] (CVAE, 10 genres) at the bench's B = 256
+    shapes and GEMM plans, fp32 engine: one fused Trainer.step vs the oracle (src/Convolutional_VAE.py:224-240,
+    src/Conditional_VAE.py:321-331)."""
+    h = _hip_chain("fp32", workload)
+    eps = h["eps"]
+    ora = _oracle_model(workload)
     for p, q in zip(ora.parameters(), h["init"]):
         assert torch.equal(p.detach(), q)
-    ora64, ora64f = oracle64_with_kink_envelope(CASE, ora, (x, None), eps, None)
-    out = ora(x, None, eps=eps)
-    lo = OM.loss_function(out[0], x, None, None, out[2], out[3])
-    lo[0].backward()
-    print(f"B={B} fp32: rel mu {rel(h['mu'], out[2].detach()):.2e}, rel logvar {rel(h['logvar'], out[3].detach()):.2e},"
-          f" ELBO {h['loss'][0]:.6e} vs {float(lo[0]):.6e}")
+    ora64, ora64f = oracle64_with_kink_envelope(_case(workload), ora, _ins(h, workload), eps, None)
+    out, lo = _oracle_step(ora, h, workload)
+    print(f"{workload} B={B} fp32: rel mu {rel(h['mu'], out[2].detach()):.2e}, rel logvar "
+          f"{rel(h['logvar'], out[3].detach()):.2e}, ELBO {h['loss'][0]:.6e} vs {float(lo[0]):.6e}")
     assert rel(h["mu"], out[2].detach()) < 1e-4 and rel(h["logvar"], out[3].detach()) < 1e-4
+    assert rel(h["recon"], out[0].detach()) < 1e-4
+    if h["recon_text"] is not None:
+        assert rel(h["recon_text"], out[1].detach()) < 1e-4
     for a, b in zip(h["loss"], lo):
         if b is not None and float(b) != 0.0:
             assert abs(a - float(b)) <= 1e-4 * abs(float(b)), (a, float(b))
@@ -102,7 +136,7 @@ def test_bench_train_step_fp32_matches_oracle(cuda):
         e_ref, e_ours, e_kink = rel(p.grad, g64), rel(g, g64), rel(o64f[name].grad, g64)
         worst = max(worst, e_ours)
         assert e_ours <= max(1e-3, 8 * e_ref) + 1.5 * e_kink, f"grad {name}: {e_ours:.3e} vs {e_ref:.3e} / {e_kink:.3e}"
-    print(f"B={B} fp32: worst per-tensor gradient error vs float64 {worst:.2e}")
+    print(f"{workload} B={B} fp32: worst per-tensor gradient error vs float64 {worst:.2e}")
     # Adam: exact torch.optim.Adam on the engine's own gradient
     ps = [q.clone().requires_grad_(True) for q in h["init"]]
     off = 0
@@ -119,16 +153,36 @@ def test_bench_train_step_fp32_matches_oracle(cuda):
             assert torch.equal(bm.cpu(), bo), n
 
 
-def test_bench_train_step_bf16_tracks_oracle(cuda):
-    h = _hip_chain("bf16")
-    ora = _oracle_model()
-    out = ora(h["x"], None, eps=h["eps"])
-    lo = OM.loss_function(out[0], h["x"], None, None, out[2], out[3])
-    lo[0].backward()
+# bf16 engine (the bench dtype) vs the fp32 oracle at B = 256: (mu, ELBO, global gradient) relative bounds, each
+# about 3x the error measured on MI355X.  Inputs are identical, so the gap is the bf16 rounding of
+# activations / MFMA operands (fp32 accumulation, fp32 BN statistics); a kernel that drops a K-split slab of one
+# layer moves the gradient of that layer by >= 1/S and the ELBO by far more than these bounds.
+BF16_TOL = {"audio": (2e-2, 5e-4, 3e-2), "hybrid": (2e-2, 5e-4, 3e-2), "cvae": (2e-2, 5e-4, 3e-2)}
+
+
+@pytest.mark.parametrize("workload", ["audio", "hybrid", "cvae"])
+def test_bench_train_step_bf16_tracks_oracle(cuda, workload):
+    h = _hip_chain("bf16", workload)
+    ora = _oracle_model(workload)
+    out, lo = _oracle_step(ora, h, workload)
     go = torch.cat([p.grad.reshape(-1) for p in ora.parameters()])
     e_mu, e_elbo, e_g = rel(h["mu"], out[2].detach()), abs(h["loss"][0] - float(lo[0])) / abs(float(lo[0])), rel(h["grad"], go)
-    print(f"B={B} bf16: rel mu {e_mu:.2e}, rel ELBO {e_elbo:.2e}, global grad rel L2 {e_g:.2e}")
-    assert e_mu < 3e-2 and e_elbo < 2e-2 and e_g < 0.15
+    # per-tensor gradient errors (BN-fed conv biases excluded: zero true gradient)
+    per = {}
+    off = 0
+    for name, p in ora.named_parameters():
+        g = h["grad"][off:off + p.numel()].view_as(p)
+        off += p.numel()
+        if not _bias_feeds_bn(ora, name):
+            per[name] = rel(g, p.grad)
+    worst = sorted(per.items(), key=lambda kv: -kv[1])[:4]
+    print(f"{workload} B={B} bf16: rel mu {e_mu:.2e}, rel ELBO {e_elbo:.2e}, global grad rel L2 {e_g:.2e}; "
+          f"worst tensors {[(n, round(e, 4)) for n, e in worst]}")
+    t_mu, t_elbo, t_g = BF16_TOL[workload]
+    assert e_mu < t_mu and e_elbo < t_elbo and e_g < t_g
+    # every weight tensor tracks its own fp32 gradient (a dropped slab / tile of one layer shows here)
+    bad = {n: e for n, e in per.items() if n.endswith("weight") and e > 0.1}
+    assert not bad, bad
 
 
 def test_bench_whole_oracle_chain(cuda):

@@ -89,6 +89,12 @@ def _worker(rank, port, outdir):
     hlmc_amd.Trainer.allreduce_grads(ns)
     ns16 = types.SimpleNamespace(gflat=flat.clone(), grad_dtype=torch.bfloat16, process_group=None, buckets=buckets)
     hlmc_amd.Trainer.allreduce_grads(ns16)
+    # the asynchronous bf16 wire handle: every bucket in flight first, then wait() copies the reduced wire back
+    from hlmc_amd.train import _allreduce_sum
+    ga = flat.clone()
+    works = [_allreduce_sum(ga[lo:hi], torch.bfloat16, None, async_op=True) for lo, hi in buckets]
+    for w in works:
+        assert w.wait() and w.wait()          # a second wait is a no-op
 
     # ---- BatchNorm running statistics: flat views + rank 0 broadcast (DDP broadcast_buffers)
     torch.manual_seed(42)
@@ -115,7 +121,7 @@ def _worker(rank, port, outdir):
     dist.all_reduce(corr)
     dist.all_reduce(m2)
     mean, var, scale = scaler_finalize(float(n.item()), s, corr, m2)
-    torch.save({"g32": ns.gflat, "g16": ns16.gflat, "mean": mean, "var": var, "scale": scale, "bn": bn_state},
+    torch.save({"g32": ns.gflat, "g16": ns16.gflat, "g16a": ga, "mean": mean, "var": var, "scale": scale, "bn": bn_state},
                os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
@@ -132,6 +138,7 @@ def test_dp_allreduce_and_distributed_scaler():
         assert torch.equal(r["g32"], ref), "fp32 SUM all-reduce must equal the per-shard gradient sum exactly"
         rel = float((r["g16"] - ref).norm() / ref.norm())
         assert rel < 1e-2, rel
+        assert torch.equal(r["g16a"], r["g16"]), "async bf16 wire == blocking bf16 wire"
     assert torch.equal(res[0]["g32"], res[1]["g32"])
     X, _ = _scaler_shard(0)
     sk = SkScaler().fit(X)
@@ -145,3 +152,21 @@ def test_dp_allreduce_and_distributed_scaler():
     means = [float(v.reshape(-1)[0]) for k, v in res[1]["bn"].items() if k.endswith("running_mean")]
     assert means == [float(i) for i in range(len(means))]           # rank 0 filled 10 * 0 + i
     assert all(float(v.max()) == float(v.min()) == 1.0 for k, v in res[1]["bn"].items() if k.endswith("running_var"))
+
+
+def test_pipeline_shards_and_equal_step_counts():
+    """run_pipeline's data-parallel split: contiguous shards covering every clip once, and every rank taking the
+    same number of train steps (each step all-reduces) with >= 2 rows per batch and every shard clip trained."""
+    from hlmc_amd.pipeline import local_batches, shard_bounds
+    for n, world, batch in [(16, 1, 16), (16, 2, 8), (17, 2, 8), (100, 8, 4), (9, 2, 4), (10, 3, 2), (7, 2, 2),
+                            (100000, 8, 256), (20000, 8, 256), (5, 2, 8), (3, 1, 2)]:
+        bounds = shard_bounds(n, world)
+        assert bounds[0][0] == 0 and bounds[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(bounds, bounds[1:]))
+        sizes = [hi - lo for lo, hi in bounds]
+        assert max(sizes) - min(sizes) <= 1
+        plans = [local_batches(sizes, r, batch) for r in range(world)]
+        assert len({len(p) for p in plans}) == 1
+        for p, size in zip(plans, sizes):
+            assert p[0][0] == 0 and p[-1][1] == size and all(a[1] == b[0] for a, b in zip(p, p[1:]))
+            assert all(b - a >= 2 for a, b in p)

@@ -85,3 +85,20 @@ def test_select_best_keeps_first_of_equal_partitions():
     assert KMeans._select_best(runs, 2)[0] == 0
     runs = [(0, a, 5.0, None, 3), (1, c, 4.5, None, 2)]
     assert KMeans._select_best(runs, 2)[0] == 1
+
+
+def test_seeding_draws_match_the_stream():
+    """A rank skips another rank's k-means++ seeding by drawing KMeans.seeding_draws(k) doubles: the RandomState
+    must then stand exactly where the seeding itself would have left it (any k, any data)."""
+    cls = _cpu_kmeans_cls()
+    X = _data()
+    Xc = torch.from_numpy(X - X.mean(axis=0))
+    w = np.ones(N, np.float32)
+    for k in (2, 3, 7, 10, 14):
+        a, b = np.random.RandomState(42), np.random.RandomState(42)
+        for _ in range(3):
+            cls(n_clusters=k)._kmeans_plusplus(Xc, a, w)
+        b.random_sample(3 * cls.seeding_draws(k))
+        sa, sb = a.get_state(), b.get_state()
+        assert np.array_equal(sa[1], sb[1]) and sa[2:] == sb[2:], k
+        assert a.random_sample() == b.random_sample()

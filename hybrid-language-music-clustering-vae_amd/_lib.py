@@ -60,6 +60,9 @@ _SIGS = {
     "hlmc_net_adam_step_dev": (c_int, [c_vp, c_vp, P_vp, P_vp, c_vp]),
     "hlmc_adam_coef": (c_int, [c_f32, c_f32, c_f32, c_f32, c_f32, c_int, c_vp]),
     "hlmc_net_set_overlap_adam": (c_int, [c_vp, c_int]),
+    "hlmc_net_set_rng": (c_int, [c_vp, C.c_uint64, C.c_uint64]),
+    "hlmc_net_get_rng": (c_int, [c_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "hlmc_randn": (c_int, [c_vp, c_vp, c_i64, C.c_uint64, C.c_uint64]),
     "hlmc_net_settle": (c_int, [c_vp, c_vp]),
     "hlmc_net_grad_buckets": (c_int, [c_vp, C.POINTER(c_int), c_int]),
     "hlmc_net_set_bucket_sync": (c_int, [c_vp, c_int]),

@@ -285,6 +285,21 @@ int hlmc_net_settle(hlmc_net* h, void* stream) {
     HLMC_CHECK_ARG(h, "net is NULL");
     return h->impl->settle(S(stream));
 }
+int hlmc_net_set_rng(hlmc_net* h, uint64_t seed, uint64_t offset) {
+    HLMC_CHECK_ARG(h && offset % 4 == 0, "net is NULL / offset not a multiple of 4");
+    h->impl->rng_seed = seed;
+    h->impl->rng_offset = offset;
+    return HLMC_OK;
+}
+int hlmc_net_get_rng(const hlmc_net* h, uint64_t* seed, uint64_t* offset) {
+    HLMC_CHECK_ARG(h && seed && offset, "NULL argument");
+    *seed = h->impl->rng_seed;
+    *offset = h->impl->rng_offset;
+    return HLMC_OK;
+}
+int hlmc_randn(void* stream, float* out, int64_t n, uint64_t seed, uint64_t offset) {
+    return ops::randn(S(stream), out, n, seed, offset);
+}
 int hlmc_net_set_overlap_adam(hlmc_net* h, int enable) {
     HLMC_CHECK_ARG(h, "net is NULL");
     h->impl->overlap_adam = enable != 0;

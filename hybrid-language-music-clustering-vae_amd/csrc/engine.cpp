@@ -211,21 +211,7 @@ class NetT : public NetBase {
         }();
         use_side = !env_off;
         if (use_side && !s2) {
-            // HLMC_SIDE_CU_EVERY=k (A/B aid): the weight-gradient stream may only use every k-th CU
-            static const int cu_every = [] {
-                const char* e = std::getenv("HLMC_SIDE_CU_EVERY");
-                return e ? std::max(1, std::atoi(e)) : 1;
-            }();
-            if (cu_every > 1) {
-                int dev = 0, ncu = 0;
-                HLMC_HIP(hipGetDevice(&dev));
-                HLMC_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-                std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-                for (int c = 0; c < ncu; c += cu_every) mask[c / 32] |= 1u << (c % 32);
-                HLMC_HIP(hipExtStreamCreateWithCUMask(&s2, (uint32_t)mask.size(), mask.data()));
-            } else {
-                HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-            }
+            HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
             evs.resize(32);
             for (auto& e : evs) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             HLMC_HIP(hipEventCreateWithFlags(&prelate_ev, hipEventDisableTiming));
@@ -287,6 +273,18 @@ class NetT : public NetBase {
         return HLMC_OK;
     }
 
+    // ---------------------------------------------------------------- reparameterisation
+    // z = mu + eps * exp(0.5 logvar): eps from the caller (copied to eps_keep by the forward's copy_segments) or,
+    // when the caller passes none, drawn on the device from the net's Philox stream (hlmc_net_set_rng) straight
+    // into eps_keep (the backward's copy) — no host / torch launch for the noise
+    int reparam(hipStream_t s, const float* eps_in, const float* mu, const float* lv, float* eps_keep, int B, int L,
+                T* z, int ldz) {
+        if (eps_in) return ops::reparam_fwd<T>(s, mu, lv, eps_keep, B, L, z, ldz);
+        const uint64_t off = this->rng_offset;
+        this->rng_offset += ((uint64_t)B * L + 3) & ~uint64_t(3);
+        return ops::reparam_rng<T>(s, mu, lv, this->rng_seed, off, B, L, eps_keep, z, ldz);
+    }
+
     // ---------------------------------------------------------------- layer helpers
     // y = act(x W^T + b)
     template <typename OutT>
@@ -341,9 +339,6 @@ class NetT : public NetBase {
                const uint8_t* mask, float mscale, T* a, int lda, const ops::ColStats* st = nullptr) {
         float* mean = AF(bb.mean);
         float* inv = AF(bb.inv);
-        if (train && !mask && small_bn(R, C))  // one launch: statistics + apply by channel-slab blocks
-            return ops::bn_small_fwd<T>(s, y, R, C, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps, P[g],
-                                        P[beta], act, a, lda);
         if (train && st && st->nparts > 0)  // statistics finalized inside the activation kernel
             return ops::bn_act_train<T>(s, y, R, C, st->part, st->nparts, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum,
                                         kBnEps, P[g], P[beta], act, mask, mscale, a, lda,
@@ -361,9 +356,6 @@ class NetT : public NetBase {
     int bn_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const BnBufs& bb, int g, int beta,
                int act, const uint8_t* mask, float mscale, T* dy, int bias, const ops::BnBwdFuse* fused = nullptr,
                double* bias_part = nullptr, bool defer_bias = false) {
-        if (!mask && small_bn(R, C) && !(fused && fused->nparts > 0))  // one launch, bias grad included
-            return ops::bn_small_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, dy, G[g],
-                                        G[beta], bias >= 0 ? G[bias] : nullptr);
         double* bp = (bias >= 0 && use_side) ? bias_part : nullptr;
         HLMC_TRY(ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask, mscale, dy,
                                     G[g], G[beta], bias >= 0 ? G[bias] : nullptr, scratch, fused, bp));
@@ -393,16 +385,6 @@ class NetT : public NetBase {
             return f(q, sc);
         });
     }
-    // HLMC_BN_SMALL=1: small BatchNorm layers on the single-launch channel-slab kernels.  Measured 4.3% slower
-    // (100.5k vs 105.1k, 3 alternating rounds): <= 32 blocks cannot keep enough loads in flight; the
-    // 1024-block partial-table path wins despite its extra launches.  Off by default.
-    static bool small_bn(int64_t R, int C) {
-        static const bool on = [] {
-            const char* e = std::getenv("HLMC_BN_SMALL");
-            return e && e[0] == '1';
-        }();
-        return on && ops::bn_small(R, C);
-    }
     // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
     static bool tail_on_main() {
         static const bool on = [] {
@@ -411,40 +393,18 @@ class NetT : public NetBase {
         }();
         return on;
     }
-    // fused BN-backward moments request for the GEMM that writes the grad of a BN layer's output
-    // Off by default: measured on MI355X (scripts/gpu_ab_env.sh, 3 alternating rounds) the epilogue's extra
-    // y reads in the low-occupancy DMA GEMMs plus the finalize over phases x M-tiles partial rows cost more
-    // than the moments pass they replace (87.4k vs 90.5k clips/s).  HLMC_BN_FUSE=1 enables it.
-    ops::BnBwdFuse bn_fuse(const T* y, const BnBufs& bb, int g, int beta) {
-        static const bool on = [] {
-            const char* e = std::getenv("HLMC_BN_FUSE");
-            return e && e[0] == '1';
-        }();
-        return ops::BnBwdFuse{y, AF(bb.mean), AF(bb.inv), P[g], P[beta],
-                              on ? reinterpret_cast<double*>(ws + bnb_part_off) : nullptr, 0};
-    }
     size_t bnb_part_off = 0, bnb_part_bytes = 0;
     ops::BnBwdFuse fuse4{};  // the decoder's last BN layer: moments from the output convT's data gradient
-    ops::BnApply dec_ba{};       // ... and its forward BN + LeakyReLU applied inside the output convT
-    bool dec_a4_fused = false;   // the last full forward left a4 unmaterialised (backward reads y4 instead)
-    // HLMC_LAST_BN_CONSUMER=1: the output convT and its weight gradient apply the decoder's last BN + LeakyReLU
-    // to y4 themselves (no bn_act pass, no a4 map).  Parity green, but measured 3.3% slower (101.7k vs 105.0k,
-    // 4 alternating rounds): the convT re-reads every input 2.25 times and pays the per-channel transform (LDS
-    // parameter reads + VALU) on each read, more than the 26 us streaming pass it removes.  Off by default.
-    static bool last_bn_in_consumers() {
-        static const bool on = [] {
-            const char* e = std::getenv("HLMC_LAST_BN_CONSUMER");
-            return e && e[0] == '1';
-        }();
-        return on;
-    }
     void need_bnb(size_t b) { bnb_part_bytes = std::max(bnb_part_bytes, b); }
 
     // ---------------------------------------------------------------- conv encoder (6 x conv-BN-LReLU)
     struct Enc {
         int w[6], b[6], g[6], beta[6], bn[6];
         int H = 0, W = 0;
-        size_t y[6], a[6], dy[6], bpart[6], audio = 0;  // dy: grad wrt the conv output (read by the forked wgrad)
+        size_t y[6], a[6], dy[6], bpart[6];  // dy: grad wrt the conv output (read by the forked wgrad)
+        // the caller's input of the last full forward: the first conv's weight gradient reads it in backward (the
+        // ABI contract keeps in0 alive and unchanged until then: hlmc.h hlmc_net_forward)
+        const float* audio = nullptr;
         BnBufs bb[6];
     };
     Enc enc;
@@ -461,7 +421,6 @@ class NetT : public NetBase {
     }
     void enc_plan(Arena& A, int64_t B) {
         int h = enc.H, w = enc.W;
-        enc.audio = A.take((size_t)B * h * w * sizeof(float));
         for (int l = 0; l < 6; ++l) {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             if (l > 0) {
@@ -481,8 +440,6 @@ class NetT : public NetBase {
             enc.a[l] = A.take(n * sizeof(T));
             enc.dy[l] = A.take(n * sizeof(T));
             enc.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * h * w, co) * co * sizeof(double));
-            // the sub-pixel data-gradient GEMM writing this layer's output grad (4 phases over the low grid)
-            need_bnb(ops::col_stats_bytes(B * (h / 2) * (w / 2), 4, co));
             enc.bb[l] = bn_plan(A, co);
             need(ops::bn_ws(B * h * w, co));
         }
@@ -491,15 +448,13 @@ class NetT : public NetBase {
     int enc_fwd(hipStream_t s, bool train, const float* audio_in, int B) {
         int h = enc.H, w = enc.W;
         HLMC_CHECK_ARG(audio_in, "audio input required");
-        // keep the input for the first conv's weight gradient
-        float* audio = AF(enc.audio);
-        HLMC_HIP(hipMemcpyAsync(audio, audio_in, (size_t)B * h * w * sizeof(float), hipMemcpyDeviceToDevice, s));
+        const float* audio = audio_in;
+        enc.audio = audio_in;
         for (int l = 0; l < 6; ++l) {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             T* y = AT(enc.y[l]);
-            // GEMM-epilogue statistics only for layers the single-launch small-BN kernels do not take
-            const bool want_st = train && !small_bn((int64_t)B * (h / 2) * (w / 2), co);
-            ops::ColStats st{want_st ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
+            // train mode: BN statistics from the producing conv's epilogue
+            ops::ColStats st{train ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
             if (l == 0)  // BN statistics from the edge conv itself (no col_moments pass)
                 HLMC_TRY(ops::conv_c1_s2<T>(s, audio, B, h, w, P[enc.w[0]], P[enc.b[0]], co, y, &st));
             else
@@ -515,19 +470,19 @@ class NetT : public NetBase {
     // gA: grad of the last activation on entry (overwritten: data-gradient chain buffer).  Bucket
     // `bucket_hi` (layers 3..5) is marked final after layer 3 (-1: no mark).
     int enc_bwd(hipStream_t s, int B, T* gA, int bucket_hi = -1) {
-        const float* audio = AF(enc.audio);
+        const float* audio = enc.audio;
+        HLMC_CHECK_ARG(audio, "backward: no forward input recorded");
         int hs[7], ws_[7];
         hs[0] = enc.H;
         ws_[0] = enc.W;
         for (int l = 0; l < 6; ++l) { hs[l + 1] = hs[l] / 2; ws_[l + 1] = ws_[l] / 2; }
-        ops::BnBwdFuse fuse{};  // nparts 0: layer 5's output grad comes from flat_to_nhwc (separate moments pass)
         for (int l = 5; l >= 0; --l) {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             const int ho = hs[l + 1], wo = ws_[l + 1];
             const int64_t R = (int64_t)B * ho * wo;
             T* dy = AT(enc.dy[l]);
             HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
-                            &fuse, reinterpret_cast<double*>(ws + enc.bpart[l]), true));
+                            nullptr, reinterpret_cast<double*>(ws + enc.bpart[l]), true));
             float* gw = G[enc.w[l]];
             if (l == 0 && tail_on_main()) {
                 // the last weight gradient of backward: on the main stream, which would otherwise only wait for
@@ -541,9 +496,8 @@ class NetT : public NetBase {
             } else {
                 const T* xin = AT(enc.a[l - 1]);
                 HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
-                // grad of layer l-1's activation, with layer l-1's BN-backward moments from the epilogue
-                fuse = bn_fuse(AT(enc.y[l - 1]), enc.bb[l - 1], enc.g[l - 1], enc.beta[l - 1]);
-                HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch, nullptr, &fuse));
+                // grad of layer l-1's activation
+                HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));
             }
             if (l == 3 && bucket_hi >= 0) HLMC_TRY(mark(s, bucket_hi));
             if (l == 2) HLMC_TRY(prelate(s));  // layers 0-1 (late_params) remain
@@ -587,8 +541,6 @@ class NetT : public NetBase {
                 dec.a[l] = A.take(n * sizeof(T));
                 dec.dy[l] = A.take(n * sizeof(T));
                 dec.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * 4 * h * w, co) * co * sizeof(double));
-                // the stride-2 conv data-gradient GEMM writing this layer's output grad (output grid 2h x 2w)
-                need_bnb(ops::col_stats_bytes(B * 4 * h * w, 1, co));
                 dec.bb[l] = bn_plan(A, co);
                 need(ops::bn_ws(B * 4 * h * w, co));
                 need(ops::col_stats_bytes(B * h * w, 4, co));
@@ -612,25 +564,13 @@ class NetT : public NetBase {
             if (l < 5) {
                 T* y = AT(dec.y[l]);
                 const int64_t R = (int64_t)B * 4 * h * w;
-                const bool want_st = train && !small_bn(R, co);
-                ops::ColStats st{want_st ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
+                ops::ColStats st{train ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
                 HLMC_TRY(ops::subpixel<T>(s, x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co, y, scratch, &st));
-                if (l == 4 && train && st.nparts > 0 && last_bn_in_consumers()) {
-                    // the output convT applies this layer's BN + LeakyReLU itself (no bn_act pass, no a4 map)
-                    dec_ba = ops::BnApply{st.part, st.nparts, R, AF(dec.bb[4].mean), AF(dec.bb[4].inv), RM[dec.bn[4]],
-                                          RV[dec.bn[4]], NBT[dec.bn[4]], kBnMomentum, kBnEps, P[dec.g[4]],
-                                          P[dec.beta[4]], after_parts(st.part, (size_t)st.nparts * 2 * co)};
-                    dec_a4_fused = true;
-                    x = y;
-                } else {
-                    HLMC_TRY(bn_fwd(s, train, y, R, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f,
-                                    AT(dec.a[l]), co, &st));
-                    if (l == 4) dec_a4_fused = false;
-                    x = AT(dec.a[l]);
-                }
+                HLMC_TRY(bn_fwd(s, train, y, R, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f,
+                                AT(dec.a[l]), co, &st));
+                x = AT(dec.a[l]);
             } else {
-                HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon,
-                                          dec_a4_fused ? &dec_ba : nullptr));
+                HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon));
             }
             h *= 2;
             w *= 2;
@@ -646,14 +586,12 @@ class NetT : public NetBase {
         // last layer (1 output channel): input a4 [B, hs5, ws5, 32]
         {
             const int hl = hs[5], wl = ws_[5];
-            // the forward did not materialise a4: the weight gradient applies the BN + LeakyReLU to y4 itself
-            const T* a4 = dec_a4_fused ? AT(dec.y[4]) : AT(dec.a[4]);
-            const ops::BnAct a4act{AF(dec.bb[4].mean), AF(dec.bb[4].inv), P[dec.g[4]], P[dec.beta[4]]};
+            const T* a4 = AT(dec.a[4]);
             float* gw = G[dec.w[5]];
             float* gb = G[dec.b[5]];
             const int npix = B * hs[6] * ws_[6];
             HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) {
-                HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc, dec_a4_fused ? &a4act : nullptr));
+                HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
                 return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
             }));
             // layer 4's BN-backward moments come with the edge conv that writes its output gradient
@@ -673,12 +611,8 @@ class NetT : public NetBase {
             const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
             float* gw = G[dec.w[l]];
             HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
-            if (l > 0) {
-                fuse = bn_fuse(AT(dec.y[l - 1]), dec.bb[l - 1], dec.g[l - 1], dec.beta[l - 1]);
-                HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch, nullptr, &fuse));
-            } else {
-                HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
-            }
+            HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
+            fuse = ops::BnBwdFuse{};  // the stride-2 conv data gradients carry no moments: a separate pass
         }
         *out = gA;
         return HLMC_OK;
@@ -864,8 +798,8 @@ class HybridNet : public NetT<T> {
                 HLMC_TRY(ops::copy_segments(s, cs, 3));
             }
             if (a.encode_only) return HLMC_OK;
-            HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
-            HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), L));
+            HLMC_CHECK_ARG(a.recon, "recon required");
+            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), L));
         }
         HLMC_TRY(this->template lin_fwd<T>(s, AT(z_), L, B, di_w, di_b, AT(d1_), 512, 1));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(d1_), 512, B, ds_w, ds_b, AT(s_), ldSP, 1));
@@ -1071,8 +1005,8 @@ class CvaeNet : public NetT<T> {
                 HLMC_TRY(ops::copy_segments(s, cs, 3));
             }
             if (a.encode_only) return HLMC_OK;
-            HLMC_CHECK_ARG(a.eps && a.recon && a.recon_text, "eps / recon / recon_text required");
-            HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(Z_), ldZ));
+            HLMC_CHECK_ARG(a.recon && a.recon_text, "recon / recon_text required");
+            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(Z_), ldZ));
         }
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in2, C, AT(Z_) + L, ldZ, B, C));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(S_), ldS, 0));
@@ -1286,8 +1220,8 @@ class SimpleNet : public NetT<T> {
                 HLMC_TRY(ops::copy_segments(s, cs, 3));
             }
             if (a.encode_only) return HLMC_OK;
-            HLMC_CHECK_ARG(a.eps && a.recon, "eps and recon required");
-            HLMC_TRY(ops::reparam_fwd<T>(s, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), pad8(L)));
+            HLMC_CHECK_ARG(a.recon, "recon required");
+            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), pad8(L)));
             if (a.z) HLMC_TRY(ops::reparam_fwd<float>(s, AF(mu_), AF(lv_), AF(eps_), B, L, a.z, L));
         }
         const T* x = AT(z_);

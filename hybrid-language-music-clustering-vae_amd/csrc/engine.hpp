@@ -100,6 +100,9 @@ class NetBase {
     int late_params = 0;
     bool overlap_adam = false;
     bool last_full_forward = false;  // the workspace holds a full forward (backward's precondition)
+    // reparameterisation noise drawn on the device when the caller passes no eps (ops::reparam_rng): Philox
+    // stream `rng_seed`, next element rng_offset (advanced by each such forward, kept a multiple of 4)
+    uint64_t rng_seed = 0, rng_offset = 0;
     virtual int settle(hipStream_t s) = 0;  // make every gradient of the last backward final on s
 };
 

@@ -308,19 +308,6 @@ struct WithStats : Base {
     int mtiles;
 };
 
-// Any epilogue whose output is the gradient da of a BatchNorm(+LeakyReLU 0.01) layer's output, plus that
-// layer's fused backward moments (what bn_bwd_moments_kernel computes): with y the layer's BN input at the
-// same NHWC position, xhat = (y - mean) * invstd, z = gamma * xhat + beta, dz = da * lrelu'(z):
-// part[(phase * mtiles + mtile) * 2N + n] = sum dz, [... + N + n] = sum dz * xhat  (f64, fixed order).
-template <class Base, typename YT>
-struct WithBnBwd : Base {
-    static constexpr int kStatMode = 2;
-    double* part;
-    int mtiles;
-    const YT* y;
-    const float *mean, *invstd, *gamma, *beta;
-};
-
 // Split-K partial slab: ws[((phase * S + split) * M + m) * N + n]
 struct StorePartial {
     static constexpr int kStatMode = 0;
@@ -348,30 +335,18 @@ struct StorePartial {
 
 // Store one wave's TM x TN grid of 16x16 accumulator tiles through the epilogue (C/D map: col = lane & 15,
 // rows (lane >> 4) * 4 + 0..3), bias hoisted per column, one quad() per 4-row group.  EP::kStatMode 1: per-column
-// sum / sum of squares of the stored values over this lane's rows into cs / cq (f64); 2: the fused BatchNorm
-// backward moments (WithBnBwd) of the stored gradient.
+// sum / sum of squares of the stored values over this lane's rows into cs / cq (f64).
 template <int TM, int TN, class EP>
 __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)[TM][TN], int mb, int nb, int lane,
                                               int M, int N, double (&cs)[TN], double (&cq)[TN]) {
     float bias[TN];
     int ncol[TN];
-    float mu[TN], is[TN], ga[TN], be[TN];
-    float fs[TN], fq[TN];  // mode 2: this lane's <= 4 TM rows summed in f32, widened once below
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         ncol[j] = nb + j * 16 + (lane & 15);
-        const bool ok = ncol[j] < N;
-        bias[j] = ok ? ep.colbias(ncol[j]) : 0.f;
+        bias[j] = ncol[j] < N ? ep.colbias(ncol[j]) : 0.f;
         cs[j] = 0.0;
         cq[j] = 0.0;
-        fs[j] = 0.f;
-        fq[j] = 0.f;
-        if constexpr (EP::kStatMode == 2) {
-            mu[j] = ok ? ep.mean[ncol[j]] : 0.f;
-            is[j] = ok ? ep.invstd[ncol[j]] : 0.f;
-            ga[j] = ok ? ep.gamma[ncol[j]] : 0.f;
-            be[j] = ok ? ep.beta[ncol[j]] : 0.f;
-        }
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -389,21 +364,8 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
                 if constexpr (EP::kStatMode == 1) {
                     cs[j] += v;
                     cq[j] += (double)v * v;
-                } else if constexpr (EP::kStatMode == 2) {
-                    const float xh = (to_f32(ep.y[ro + ncol[j]]) - mu[j]) * is[j];
-                    const float z = xh * ga[j] + be[j];
-                    const float dz = v * (z > 0.f ? 1.f : 0.01f);
-                    fs[j] += dz;
-                    fq[j] = fmaf(dz, xh, fq[j]);
                 }
             }
-        }
-    }
-    if constexpr (EP::kStatMode == 2) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            cs[j] = fs[j];
-            cq[j] = fq[j];
         }
     }
 }
@@ -626,19 +588,6 @@ __device__ __forceinline__ void wait_stage(int ahead) {  // ahead = stages still
         if (ahead >= 1) { wait_vmcnt<GPW>(); return; }
     }
     wait_vmcnt<0>();
-}
-// the same for any ring depth: allow `ahead` (<= A) later stages of GPW instructions each to stay in flight
-template <int GPW, int A>
-__device__ __forceinline__ void wait_ahead(int ahead) {
-    if constexpr (A <= 0) {
-        wait_vmcnt<0>();
-    } else {
-        if (ahead >= A) {
-            wait_vmcnt<A * GPW>();
-            return;
-        }
-        wait_ahead<GPW, A - 1>(ahead);
-    }
 }
 __device__ __forceinline__ void glds16(const void* g, void* l) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -891,16 +840,11 @@ __device__ __forceinline__ int tn_swz(int row) {
     else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
 }
 
-// Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_kernel).
-// PF: K-steps of global loads in flight (1: one register set; 2: two sets, the loop unrolled by two so each
-// step's loads are issued two steps ahead of their LDS store).
-// NG = 2 (PF 1 only): 512 threads as two 4-wave groups over the even / odd K-steps of the block's split, each
-// with its own LDS double buffer: twice the loads in flight per block without more split-K slabs; group 1
-// hands its accumulators to group 0 through LDS at the end (fixed order: group 0 + group 1).
-template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, int PF = 1, int NG = 1>
-__global__ __launch_bounds__(256 * NG) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len,
-                                                           int remap) {
-    static_assert(NG == 1 || PF == 1, "two wave groups only with one register set");
+// Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_grouped_kernel).
+// One K-step of global loads in flight in one register set, double-buffered LDS images.
+template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len,
+                                                      int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;            // k rows per tile (KCH 16-byte chunks of one column)
     constexpr int ACPR = BM / V, BCPR = BN / V;  // chunks per k-row
@@ -916,13 +860,10 @@ __global__ __launch_bounds__(256 * NG) void gemm_tn_kernel(LL ll, HL hl, float* 
     constexpr int ACH = BK * BM / V, BCH = BK * BN / V;
     constexpr int AR = (ACH + 255) / 256, BR = (BCH + 255) / 256;
     constexpr int LSZ = BK * LDA, HSZ = BK * LDB;
-    __shared__ __attribute__((aligned(16))) T tn_sm[NG * 2 * (LSZ + HSZ)];
-    static_assert(NG == 1 || (size_t)NG * 2 * (LSZ + HSZ) * sizeof(T) >= (size_t)BM * BN * sizeof(float),
-                  "the group hand-off fits the staging buffers");
+    __shared__ __attribute__((aligned(16))) T tn_sm[2 * (LSZ + HSZ)];
 
-    const int tid = threadIdx.x & 255, lane = tid & 63, wave = tid >> 6;
-    const int grp = NG > 1 ? (int)(threadIdx.x >> 8) : 0;
-    T* const Lg = tn_sm + grp * 2 * (LSZ + HSZ);  // this group's buffers: L0 H0 L1 H1
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    T* const Lg = tn_sm;  // L0 H0 L1 H1
     auto Lbuf = [&](int buf) { return Lg + buf * (LSZ + HSZ); };
     auto Hbuf = [&](int buf) { return Lg + buf * (LSZ + HSZ) + LSZ; };
     const int wm0 = (wave / WAVES_N) * WM, wn0 = (wave % WAVES_N) * WN;
@@ -1039,65 +980,19 @@ __global__ __launch_bounds__(256 * NG) void gemm_tn_kernel(LL ll, HL hl, float* 
         }
     };
 
-    if constexpr (PF == 1) {
-        Regs r0;
-        // group g takes K-steps g, g + NG, ...; both groups run the same iteration count (one barrier each)
-        const int nsteps = kb < ke ? (ke - kb + BK - 1) / BK : 0;
-        const int iters = (nsteps + NG - 1) / NG;
-        if (iters > 0) {
-            if (grp < nsteps) {
-                gload(r0, kb + grp * BK);
-                lstore(r0, 0);
-            }
+    Regs r0;
+    const int nsteps = kb < ke ? (ke - kb + BK - 1) / BK : 0;
+    if (nsteps > 0) {
+        gload(r0, kb);
+        lstore(r0, 0);
+        __syncthreads();
+        for (int st = 0; st < nsteps; ++st) {
+            const int cur = st & 1;
+            const bool more = st + 1 < nsteps;
+            if (more) gload(r0, kb + (st + 1) * BK);
+            mma_step(cur);
+            if (more) lstore(r0, cur ^ 1);
             __syncthreads();
-            for (int it = 0; it < iters; ++it) {
-                const int st = grp + it * NG;
-                const int cur = it & 1;
-                const bool more = st + NG < nsteps;
-                if (more) gload(r0, kb + (st + NG) * BK);
-                if (st < nsteps) mma_step(cur);
-                if (more) lstore(r0, cur ^ 1);
-                __syncthreads();
-            }
-        }
-        if constexpr (NG > 1) {  // group 1's accumulators to group 0 (the loop ended on a barrier: LDS is free)
-            float* red = reinterpret_cast<float*>(tn_sm);
-            if (grp == 1) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) red[((i * TN + j) * 4 + r) * 256 + tid] = acc[i][j][r];
-            }
-            __syncthreads();
-            if (grp == 1) return;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[i][j][r] += red[((i * TN + j) * 4 + r) * 256 + tid];
-        }
-    } else {
-        // two register sets: x holds step k0 + BK while y's loads for k0 + 2 BK are in flight
-        Regs r0, r1;
-        if (kb < ke) {
-            gload(r0, kb);
-            if (kb + BK < ke) gload(r1, kb + BK);
-            lstore(r0, 0);
-            __syncthreads();
-            for (int k0 = kb; k0 < ke; k0 += 2 * BK) {
-                if (k0 + 2 * BK < ke) gload(r0, k0 + 2 * BK);
-                mma_step(0);
-                if (k0 + BK < ke) lstore(r1, 1);
-                __syncthreads();
-                if (k0 + BK >= ke) break;
-                if (k0 + 3 * BK < ke) gload(r1, k0 + 3 * BK);
-                mma_step(1);
-                if (k0 + 2 * BK < ke) lstore(r0, 0);
-                __syncthreads();
-            }
         }
     }
     float* slab = ws + (int64_t)bz * M * N;
@@ -1109,168 +1004,6 @@ __global__ __launch_bounds__(256 * NG) void gemm_tn_kernel(LL ll, HL hl, float* 
             for (int r = 0; r < 4; ++r) {
                 int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
                 int n = n0 + wn0 + j * 16 + (lane & 15);
-                if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
-            }
-}
-
-// ============================================================================ TN main loop, LDS-DMA pipeline
-// bf16 weight gradients.  NS-stage ring of 32-k-row stages filled by global_load_lds_dwordx4 (no register
-// staging): one 1 KB wave-instruction writes 512/BM k-rows of the L tile (or 512/BN of the H tile), lane l at
-// physical chunk l % CPR of its row, fetching logical chunk pc ^ tn_swz(row) (the XOR swizzle lives on the
-// SOURCE address, so the LDS image stays lane-linear).  The swizzle makes the ds_read_b64_tr_b16 fragment
-// reads conflict-free: each 32-lane half reads 8 k-rows x 32 bytes, and the XOR spreads those rows' chunk
-// pairs over all 64 banks (256-B rows: the row's low bits pick the pair; 128-B rows: two rows per bank sweep).
-// 4 waves split the BM x BN tile 2 x 2.  Per stage: counted vmcnt wait for this wave's DMA, raw barrier, issue
-// the stage NS-1 ahead into the slot everyone just finished, 16x16x32 MFMAs.  S > 1: the block writes its
-// K-split's partial tile to ws[(split * M + m) * N + n] (reduced in fixed split order); S == 1: the epilogue
-// stores the final value.
-// Two ds_read_b64_tr_b16 (k-rows lo and lo + 4 of a 16-lane group) forming one 16x16x32 bf16 fragment; no wait
-// (see lgkm_wait_tied).  lo / hi: LDS byte addresses.
-__device__ __forceinline__ bf16x8_t ds_read_tr16_pair(uint32_t lo, uint32_t hi) {
-    s16x4_t a, b;
-    asm volatile("ds_read_b64_tr_b16 %0, %2\n\tds_read_b64_tr_b16 %1, %3" : "=v"(a), "=v"(b) : "v"(lo), "v"(hi));
-    return bf16x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-}
-// s_waitcnt lgkmcnt(0) that every fragment depends on (the MFMAs cannot be scheduled above it)
-template <int TM, int TN>
-__device__ __forceinline__ void lgkm_wait_tied(bf16x8_t (&af)[TM], bf16x8_t (&bf)[TN]) {
-    static_assert(TM <= 4 && TN <= 4, "at most 8 tied fragments");
-    if constexpr (TM == 4 && TN == 4)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bf[0]),
-                     "+v"(bf[1]), "+v"(bf[2]), "+v"(bf[3]));
-    else if constexpr (TM == 4 && TN == 2)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3]), "+v"(bf[0]),
-                     "+v"(bf[1]));
-    else if constexpr (TM == 2 && TN == 4)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bf[0]), "+v"(bf[1]), "+v"(bf[2]),
-                     "+v"(bf[3]));
-    else if constexpr (TM == 2 && TN == 2)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(bf[0]), "+v"(bf[1]));
-    else
-        static_assert(TM == 0, "unsupported fragment counts");
-}
-
-
-template <int BM, int BN, int NS, class LL, class HL, class EP>
-__global__ __launch_bounds__(256) void gemm_tn_dma_kernel(LL ll, HL hl, EP ep, float* ws, int M, int N, int K,
-                                                          int ksplit_len, int nsplit, int remap, int dbg) {
-    constexpr int BK = 32;
-    constexpr int ASZ = BK * BM * 2, BSZ = BK * BN * 2, STG = ASZ + BSZ;
-    constexpr int ACPR = BM / 8, BCPR = BN / 8;          // 16-byte chunks per k-row
-    constexpr int ARPI = 64 / ACPR, BRPI = 64 / BCPR;    // k-rows per 1 KB DMA instruction
-    constexpr int AI = ASZ / 1024, BI = BSZ / 1024, GI = AI + BI;
-    static_assert(GI % 4 == 0, "DMA instructions per stage must split over 4 waves");
-    constexpr int GPW = GI / 4;
-    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
-    __shared__ __attribute__((aligned(1024))) char smem[NS * STG];  // the only LDS object (see vmcnt traps)
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm0 = (wave >> 1) * WM, wn0 = (wave & 1) * WN;
-    const int tiles_n = (N + BN - 1) / BN;
-    const int gx_ = (int)gridDim.x;
-    const int lg_ = remap ? xcd_logical_block((int)blockIdx.x + gx_ * (int)blockIdx.z, gx_ * (int)gridDim.z) : 0;
-    const int tile_ = remap ? lg_ % gx_ : (int)blockIdx.x, bz = remap ? lg_ / gx_ : (int)blockIdx.z;
-    const int m0 = (tile_ / tiles_n) * BM, n0 = (tile_ % tiles_n) * BN;
-    const int kb = bz * ksplit_len;
-    const int ke = min(K, kb + ksplit_len);
-    const int nsteps = kb < ke ? (ke - kb + BK - 1) / BK : 0;
-
-    f32x4_t acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-    // this wave's DMA instructions g = wave * GPW + u (A first, then H): k-row within the stage and operand column
-    int drow[GPW];
-    typename LL::Col acol[GPW];
-    typename HL::Col bcol[GPW];
-#pragma unroll
-    for (int u = 0; u < GPW; ++u) {
-        const int g = wave * GPW + u;
-        if (g < AI) {
-            const int row = g * ARPI + lane / ACPR, pc = lane % ACPR;
-            drow[u] = row;
-            acol[u] = ll.prep(m0 + 8 * (pc ^ tn_swz<ACPR>(row)));
-        } else {
-            const int row = (g - AI) * BRPI + lane / BCPR, pc = lane % BCPR;
-            drow[u] = row;
-            bcol[u] = hl.prep(n0 + 8 * (pc ^ tn_swz<BCPR>(row)));
-        }
-    }
-    auto issue = [&](int slot, int k0) {
-        char* sb = smem + slot * STG;
-#pragma unroll
-        for (int u = 0; u < GPW; ++u) {
-            const int g = wave * GPW + u;
-            if (g < AI) glds16(ll.addr(k0 + drow[u], acol[u]), sb + g * 1024);
-            else glds16(hl.addr(k0 + drow[u], bcol[u]), sb + ASZ + (g - AI) * 1024);
-        }
-    };
-
-#pragma unroll
-    for (int p = 0; p < NS - 1; ++p)
-        if (p < nsteps) issue(p, kb + p * BK);
-    const int g4 = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-    const uint32_t lds_base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-    for (int t = 0; t < nsteps; ++t) {
-        wait_ahead<GPW, NS - 2>(min(NS - 2, nsteps - 1 - t));
-        __builtin_amdgcn_s_barrier();
-        if (t + NS - 1 < nsteps && !(dbg & 2)) issue((t + NS - 1) % NS, kb + (t + NS - 1) * BK);
-        if (dbg & 1) continue;
-        // Fragment reads as inline asm: hipcc cannot tie a ds_read_b64_tr_b16 builtin to the LDS-DMA slot it reads
-        // and drains the whole ring (vmcnt(0)) before it; the ring is ordered by the counted wait + barrier above,
-        // and the asm's own lgkmcnt wait (tied to the fragments) orders the MFMAs after the data.
-        const uint32_t sa = lds_base + (uint32_t)((t % NS) * STG);
-        const uint32_t sh = sa + ASZ;
-        bf16x8_t af[TM], bfr[TN];
-        const int rlo = 8 * g4 + q, rhi = rlo + 4;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int c = (wm0 + i * 16) / 8 + (pp >> 1);
-            const uint32_t lo = sa + rlo * (2 * BM) + ((c ^ tn_swz<ACPR>(rlo)) << 4) + 8 * (pp & 1);
-            const uint32_t hi = sa + rhi * (2 * BM) + ((c ^ tn_swz<ACPR>(rhi)) << 4) + 8 * (pp & 1);
-            af[i] = ds_read_tr16_pair(lo, hi);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int c = (wn0 + j * 16) / 8 + (pp >> 1);
-            const uint32_t lo = sh + rlo * (2 * BN) + ((c ^ tn_swz<BCPR>(rlo)) << 4) + 8 * (pp & 1);
-            const uint32_t hi = sh + rhi * (2 * BN) + ((c ^ tn_swz<BCPR>(rhi)) << 4) + 8 * (pp & 1);
-            bfr[j] = ds_read_tr16_pair(lo, hi);
-        }
-        lgkm_wait_tied<TM, TN>(af, bfr);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (nsplit == 1) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
-                if (m >= M) continue;
-                const typename EP::Row rw = ep.row(m);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = n0 + wn0 + j * 16 + (lane & 15);
-                    if (n < N) ep.store(rw, n, acc[i][j][r]);
-                }
-            }
-        return;
-    }
-    float* slab = ws + (int64_t)bz * M * N;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
-                const int n = n0 + wn0 + j * 16 + (lane & 15);
                 if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
             }
 }
@@ -1311,32 +1044,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(const float*
         EP e = ep;
         e.set_phase(0);
         e.store(e.row(m), n, acc);
-    }
-}
-
-// Split-K reduction of a conv weight gradient straight into torch's dW[m][ci][tap] layout: one thread per
-// (m, ci) sums the S partial slabs of its 9 columns n = tap * C + ci in split order (loads coalesced along ci)
-// and writes its 9 contiguous outputs (stores coalesced along ci x tap).
-__global__ void splitk_reduce_wgrad_kernel(const float* __restrict__ ws, float* __restrict__ dW, int M, int C, int S) {
-    const int64_t total = (int64_t)M * C;
-    const int N = 9 * C;
-    const int64_t st = (int64_t)M * N;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const int m = (int)(i / C), ci = (int)(i - (int64_t)m * C);
-        const float* p = ws + (int64_t)m * N + ci;
-        float s[9];
-#pragma unroll
-        for (int t = 0; t < 9; ++t) s[t] = 0.f;
-        for (int k = 0; k < S; ++k) {
-            float v[9];
-#pragma unroll
-            for (int t = 0; t < 9; ++t) v[t] = p[k * st + t * C];
-#pragma unroll
-            for (int t = 0; t < 9; ++t) s[t] += v[t];
-        }
-        float* o = dW + (int64_t)m * N + ci * 9;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) o[t] = s[t];
     }
 }
 

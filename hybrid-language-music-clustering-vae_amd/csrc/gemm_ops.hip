@@ -15,6 +15,7 @@ namespace {
 constexpr int kNtTargetBlocks = 512;
 constexpr int kTnTargetBlocks = 512;
 constexpr int kTnLongK = 131072;
+constexpr int kTnKch8Min = 1024;
 constexpr int kXcdRemapDefault = probe::kWgradS2 | probe::kLinearWgrad;  // measured: helps the TN (wgrad) family, hurts sub-pixel
 
 // Split-K plan shared by the launcher and the workspace query (must agree).
@@ -124,7 +125,7 @@ void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, cons
 
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
 int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
-              ops::ColStats* st = nullptr, bool dma_ok = true, ops::BnBwdFuse* bf = nullptr) {
+              ops::ColStats* st = nullptr, bool dma_ok = true) {
     constexpr int BK = gemm_bk<T>();
     const int tmn = cdiv(M, BM) * cdiv(N, BN);
     Plan pl = plan_nt(tmn * phases, Kmax, BK);
@@ -133,19 +134,6 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     const bool long_k = Kmax >= 1024;
     const int pipe = (dma_ok && BN >= 32 && BM >= 64) ? nt_pipe_select(pl.ksl, pl.S, tmn * phases * pl.S) : 0;
     if (st) st->nparts = 0;
-    if (bf) bf->nparts = 0;
-    if (pl.S == 1 && bf && bf->part) {  // single pass: the epilogue also emits the BN-backward moments
-        WithBnBwd<EP, T> epb;
-        static_cast<EP&>(epb) = ep;
-        epb.part = bf->part;
-        epb.mtiles = cdiv(M, BM);
-        epb.y = static_cast<const T*>(bf->y);
-        epb.mean = bf->mean; epb.invstd = bf->invstd; epb.gamma = bf->gamma; epb.beta = bf->beta;
-        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, epb, M, N, pl.ksl, long_k, pipe);
-        HLMC_LAUNCHED();
-        bf->nparts = phases * cdiv(M, BM);
-        return HLMC_OK;
-    }
     if (pl.S == 1 && st && st->part) {  // single pass: the epilogue also emits the column statistics
         WithStats<EP> eps;
         static_cast<EP&>(eps) = ep;
@@ -191,12 +179,12 @@ inline int nt_tile(int M, int N, int phases) {
 }
 template <typename T, class AL, class BL, class EP>
 int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
-                ops::ColStats* st = nullptr, ops::BnBwdFuse* bf = nullptr) {
+                ops::ColStats* st = nullptr) {
     switch (nt_tile(M, N, phases)) {
-        case 0: return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, bf);
-        case 1: return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, bf);
-        case 2: return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, bf);
-        default: return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, bf);
+        case 0: return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true);
+        case 1: return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true);
+        case 2: return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true);
+        default: return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true);
     }
 }
 template <typename T>
@@ -263,35 +251,13 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "wgrad workspace too small");
     dim3 grid(tiles, 1, pl.S);
     const int rm = xcd_remap_for_site();
-    static const int pf = [] {  // HLMC_TN_PF=2: two K-steps of loads in flight (A/B)
-        const char* e = std::getenv("HLMC_TN_PF");
-        return e && e[0] == '2' ? 2 : 1;
-    }();
-    static const int kch8_min = [] {  // HLMC_TN_KCH8_MIN: smallest split length on the 64-deep K-step (A/B)
-        const char* e = std::getenv("HLMC_TN_KCH8_MIN");
-        return e ? std::atoi(e) : 1024;
-    }();
-    static const int ng = [] {  // HLMC_TN_NG=2: two 4-wave groups per block over alternate K-steps (A/B)
-        const char* e = std::getenv("HLMC_TN_NG");
-        return e && e[0] == '2' ? 2 : 1;
-    }();
     HLMC_PROBE_BEGIN(s);
-    if (ng == 2 && pf == 1) {
-        if (pl.ksl >= kch8_min)
-            gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, 1, 2><<<grid, 512, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-        else
-            gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, 1, 2><<<grid, 512, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-    } else if (pl.ksl >= kch8_min) {
-        if (pf == 2)
-            gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, 2><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-        else
-            gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-    } else {
-        if (pf == 2)
-            gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, 2><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-        else
-            gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-    }
+    // the 64-deep K-step for splits of >= 1024 rows (measured: 490.9 vs 450.9 us for the 9 conv layers when
+    // every split took it), the 32-deep one below
+    if (pl.ksl >= kTnKch8Min)
+        gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    else
+        gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     reduce_splits(s, ws.p, ep, M, N, pl.S);
@@ -316,93 +282,6 @@ inline int tn_tile(int M, int N) {
     if (M > 32) return tn_n96(N) ? 2 : 1;
     return 3;
 }
-// ---- bf16 weight gradients on the LDS-DMA pipeline (gemm_tn_dma_kernel): OPT-IN (HLMC_TN_DMA=1), measured
-// slower than the register-staged kernel on every conv weight gradient of the step (scripts/bench_gemm.py,
-// 600-730 vs 478 us for the 10 layers; its compute phase alone ran at ~20 % of MFMA peak, the
-// fragment reads waiting on one lgkmcnt per 32-deep stage).  Kept as the measured alternative.
-// HLMC_TN_DMA_BLOCKS sets its grid target, HLMC_TN_DMA_NS its ring depth (4 / 8).
-constexpr int kTnDmaStages = 8;
-constexpr int kTnDmaTargetBlocks = 256;
-inline bool tn_dma_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HLMC_TN_DMA");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-inline bool tn_dma_linear() {  // HLMC_TN_DMA_LINEAR=0: linear weight gradients on the register-staged kernel
-    static const bool on = [] {
-        const char* e = std::getenv("HLMC_TN_DMA_LINEAR");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-inline Plan plan_tn_dma(int tiles, int K) {
-    static const int target = [] {
-        const char* e = std::getenv("HLMC_TN_DMA_BLOCKS");
-        return e ? std::max(16, std::atoi(e)) : kTnDmaTargetBlocks;
-    }();
-    constexpr int BK = 32;
-    int S = cdiv(target, tiles);
-    S = std::max(1, std::min(S, K / (8 * BK)));   // >= 8 stages per split
-    int ksl = cdiv(cdiv(K, S), BK) * BK;
-    S = cdiv(K, ksl);
-    return {S, ksl};
-}
-// tile: BM = 128 when M >= 128 else 64; BN = 64 when N is a multiple of 64 but not of 128 (N = 9 C: 288, 576)
-inline int tn_dma_tile(int M, int N) { return (M >= 128 ? 0 : 2) + ((N % 128 != 0 && N % 64 == 0) ? 1 : 0); }
-inline size_t tn_dma_ws(int M, int N, int K) {
-    const int bm = M >= 128 ? 128 : 64, bn = (N % 128 != 0 && N % 64 == 0) ? 64 : 128;
-    const Plan pl = plan_tn_dma(cdiv(M, bm) * cdiv(N, bn), K);
-    return pl.S > 1 ? (size_t)pl.S * M * N * sizeof(float) : 0;
-}
-struct ReduceWgradConv {  // S > 1 reduction of a conv weight gradient into torch's dW layout
-    float* dW;
-    int C;
-};
-template <int BM, int BN, class LL, class HL, class EP>
-int launch_tn_dma(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws,
-                  const ReduceWgradConv* rw) {
-    const int tiles = cdiv(M, BM) * cdiv(N, BN);
-    const Plan pl = plan_tn_dma(tiles, K);
-    if (pl.S > 1) {
-        const size_t need = (size_t)pl.S * M * N * sizeof(float);
-        HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "wgrad workspace too small");
-    }
-    dim3 grid(tiles, 1, pl.S);
-    const int rm = xcd_remap_for_site();
-    static const int dbg = [] {  // HLMC_TN_DMA_DBG: 1 skip fragment reads + MFMA, 2 skip the in-loop DMA (timing probes)
-        const char* e = std::getenv("HLMC_TN_DMA_DBG");
-        return e ? std::atoi(e) : 0;
-    }();
-    static const int stages = [] {  // HLMC_TN_DMA_NS = 4 or 8 (ring depth; measurement aid)
-        const char* e = std::getenv("HLMC_TN_DMA_NS");
-        return e ? std::atoi(e) : kTnDmaStages;
-    }();
-    HLMC_PROBE_BEGIN(s);
-    if (stages == 4)
-        gemm_tn_dma_kernel<BM, BN, 4, LL, HL, EP><<<grid, 256, 0, s>>>(ll, hl, ep, ws.p, M, N, K, pl.ksl, pl.S, rm, dbg);
-    else
-        gemm_tn_dma_kernel<BM, BN, 8, LL, HL, EP><<<grid, 256, 0, s>>>(ll, hl, ep, ws.p, M, N, K, pl.ksl, pl.S, rm, dbg);
-    HLMC_PROBE_END(s);
-    HLMC_LAUNCHED();
-    if (pl.S == 1) return HLMC_OK;
-    (void)rw;
-    reduce_splits(s, ws.p, ep, M, N, pl.S);
-    HLMC_LAUNCHED();
-    return HLMC_OK;
-}
-template <class LL, class HL, class EP>
-int dispatch_tn_dma(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws,
-                    const ReduceWgradConv* rw) {
-    switch (tn_dma_tile(M, N)) {
-        case 0: return launch_tn_dma<128, 128>(s, ll, hl, ep, M, N, K, ws, rw);
-        case 1: return launch_tn_dma<128, 64>(s, ll, hl, ep, M, N, K, ws, rw);
-        case 2: return launch_tn_dma<64, 128>(s, ll, hl, ep, M, N, K, ws, rw);
-        default: return launch_tn_dma<64, 64>(s, ll, hl, ep, M, N, K, ws, rw);
-    }
-}
-
 template <typename T, class LL, class HL, class EP>
 int dispatch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, int N, int K, Ws ws) {
     switch (tn_tile(M, N)) {
@@ -422,7 +301,6 @@ size_t dispatch_tn_ws(int M, int N, int K) {
         case 2: w = tn_ws<64, 96>(M, N, K, BK); break;
         default: w = tn_ws<32, 128>(M, N, K, BK); break;
     }
-    if constexpr (sizeof(T) == 2) w = std::max(w, tn_dma_ws(M, N, K));  // either path may run (alignment decides)
     return w;
 }
 
@@ -708,7 +586,7 @@ namespace ops {
 
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-            ColStats* st, BnBwdFuse* bf) {
+            ColStats* st) {
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % V == 0, "conv_s2: need even H/W and Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "conv_s2: 16-byte alignment");
@@ -727,16 +605,11 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             const char* e = std::getenv("HLMC_CONV_HALO2");
             return !(e && e[0] == '0');
         }();
-        static const bool halo3 = [] {  // HLMC_CONV_HALO3=1: the 16x16x128 -> 256 layers too (A/B)
-            const char* e = std::getenv("HLMC_CONV_HALO3");
-            return e && e[0] == '1';
-        }();
         // (CI, Co, Wi): (32, 64, 64) 128-pixel tiles, double-buffered halo; (64, 128, 32) two 64-channel halves per
         // 64-pixel tile, one halo buffer (the weights take half the LDS)
         auto run = [&](auto kern_plain, auto kern_stats, int tp, int nspl) -> int {
             const int ntiles = M / tp;  // whole output rows: tiles stay inside an image
             const int grid = std::min(ntiles * nspl, 256);
-            if (bf) bf->nparts = 0;
             HLMC_PROBE_BEGIN(s);
             if (st && st->part) {
                 WithStats<StoreRM<T>> eps;
@@ -753,19 +626,14 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
-        const bool nofuse = !(bf && bf->part);
-        if (halo && nofuse && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0)
+        if (halo && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0)
             return run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>>,
                        conv_s2_halo_kernel<32, 64, 1, 32, 4, true, WithStats<StoreRM<T>>>, 128, 1);
-        if (halo2 && nofuse && Ci == 64 && Co == 128 && Wi == 32 && Hi % 8 == 0)
+        if (halo2 && Ci == 64 && Co == 128 && Wi == 32 && Hi % 8 == 0)
             return run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>>,
                        conv_s2_halo_kernel<64, 64, 2, 16, 4, false, WithStats<StoreRM<T>>>, 64, 2);
-        // Ci 128 -> Co 256 at 16-wide input: 64-pixel tiles (8 output rows), eight 32-channel slices per tile
-        if (halo3 && nofuse && Ci == 128 && Co == 256 && Wi == 16 && Hi % 16 == 0)
-            return run(conv_s2_halo_kernel<128, 32, 8, 8, 8, false, StoreRM<T>>,
-                       conv_s2_halo_kernel<128, 32, 8, 8, 8, false, WithStats<StoreRM<T>>>, 64, 8);
     }
-    return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st, bf);
+    return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
 }
 // partial rows (phases x 64-row tiles, the smallest BM) | fold scratch for their reduction
 size_t col_stats_bytes(int64_t M, int phases, int C) {
@@ -779,7 +647,7 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {
 
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-             ColStats* st, BnBwdFuse* bf) {
+             ColStats* st) {
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(Ci % V == 0, "subpixel: Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "subpixel: 16-byte alignment");
@@ -802,7 +670,6 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
         auto run = [&](auto kern_plain, auto kern_stats, int nspl) -> int {
             const int ntiles = M / 128;  // 128 low-res pixels (whole rows) per tile, inside one image
             const int grid = std::min(ntiles * nspl, 256);
-            if (bf) bf->nparts = 0;
             HLMC_PROBE_BEGIN(s);
             if (st && st->part) {
                 WithStats<StoreSubpixel<T>> eps;
@@ -819,15 +686,14 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
-        const bool nofuse = !(bf && bf->part);
-        if (halo && nofuse && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0)
+        if (halo && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0)
             return run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>>,
                        subpixel_halo_kernel<64, 32, 1, 32, 4, true, WithStats<StoreSubpixel<T>>>, 1);
-        if (halo2 && nofuse && Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0)
+        if (halo2 && Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0)
             return run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>>,
                        subpixel_halo_kernel<128, 32, 2, 16, 8, false, WithStats<StoreSubpixel<T>>>, 2);
     }
-    return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st, bf);
+    return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
 }
 template <typename T>
 size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co) {
@@ -844,12 +710,6 @@ int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* X
     StoreWgradConv ep{dW, C};
     probe::site(probe::kWgradS2, 2.0 * M * N * K,
                 (double)sizeof(T) * ((double)K * M + 4.0 * K * C) + 4.0 * M * N);
-    if constexpr (sizeof(T) == 2) {
-        if (tn_dma_enabled() && ll.vec && aligned16(Xh)) {
-            const ReduceWgradConv rw{dW, C};
-            return dispatch_tn_dma(s, ll, hl, ep, M, N, K, ws, &rw);
-        }
-    }
     return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
 }
 template <typename T>
@@ -881,10 +741,6 @@ int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int 
     KRowDense<T> hl{x, ldx, Mb, K, (ldx % V == 0) && aligned16(x)};
     StoreRM<float> ep{dW, nullptr, K, 0, 0};
     probe::site(probe::kLinearWgrad, 2.0 * N * K * Mb, (double)sizeof(T) * ((double)Mb * N + (double)Mb * K) + 4.0 * N * K);
-    if constexpr (sizeof(T) == 2) {
-        if (tn_dma_enabled() && tn_dma_linear() && ll.vec && hl.vec && N % 8 == 0 && K % 8 == 0)
-            return dispatch_tn_dma(s, ll, hl, ep, N, K, Mb, ws, nullptr);
-    }
     return dispatch_tn<T>(s, ll, hl, ep, N, K, Mb, ws);
 }
 template <typename T>
@@ -894,10 +750,10 @@ size_t linear_wgrad_ws(int Mb, int N, int K) {
 
 #define INST(T)                                                                                                     \
     template int conv_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,         \
-                            ColStats*, BnBwdFuse*);                                                                  \
+                            ColStats*);                                                                              \
     template size_t conv_s2_ws<T>(int, int, int, int, int);                                                        \
     template int subpixel<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,        \
-                             ColStats*, BnBwdFuse*);                                                                 \
+                             ColStats*);                                                                             \
     template size_t subpixel_ws<T>(int, int, int, int, int);                                                       \
     template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws);                \
     template size_t wgrad_s2_ws<T>(int, int, int, int, int);                                                       \

@@ -525,192 +525,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     block_colsum<V>(ad, tpr, C, s1, part + (int64_t)blockIdx.x * C);
 }
 
-// ---------------------------------------------------------------- small BatchNorm layers: one launch each way
-// Layers with R * C <= kSmallBnElems (the 2x2 / 4x4 / 8x8 conv layers at B = 256, the BN1d layers): block b owns
-// channels [b * CPB, (b + 1) * CPB) over ALL R rows, so nothing crosses blocks (no partial table, fold or
-// finalize launch): pass 1 reduces the channels' statistics (per-thread accumulators, then the block's fixed
-// xor-shuffle / LDS tree), pass 2 walks the rows again (L2-resident) and applies.  Deterministic.
-constexpr int64_t kSmallBnElems = (int64_t)1 << 21;
-inline bool bn_small_ok(int64_t R, int C) { return R * C <= kSmallBnElems && R > 0; }
-template <typename T>
-inline int bn_small_cpb(int C) { return std::max(Vec16<T>::N, std::min(C, C / 32)); }
-
-template <typename T>
-__global__ __launch_bounds__(256) void bn_small_fwd_kernel(const T* __restrict__ y, int64_t R, int C, int cpb,
-                                                           float* __restrict__ mean, float* __restrict__ invstd,
-                                                           float* __restrict__ rmean, float* __restrict__ rvar,
-                                                           int64_t* __restrict__ nbt, float momentum, float eps,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, int act,
-                                                           T* __restrict__ a, int lda) {
-    constexpr int V = Vec16<T>::N;
-    __shared__ double red[4 * 512];
-    __shared__ double st[2][512];
-    __shared__ float fm[512], fi[512];
-    const int gpr = cpb / V, rpp = kThreads / gpr;
-    const int tid = threadIdx.x, cg = tid % gpr, rr = tid / gpr;
-    const int cb = blockIdx.x * cpb, c0 = cb + cg * V;
-    double sa[V], sb[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) sa[v] = sb[v] = 0.0;
-    for (int64_t r = rr; r < R; r += kU * rpp) {
-        uint4 raw[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) raw[u] = load16_raw(y + min(r + u * rpp, R - 1) * C + c0);
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            if (r + u * rpp >= R) break;
-            float x[V];
-            cvt16_f32<T>(raw[u], x);
-#pragma unroll
-            for (int v = 0; v < V; ++v) { sa[v] += x[v]; sb[v] += (double)x[v] * x[v]; }
-        }
-    }
-    block_colsum<V>(sa, gpr, cpb, red, st[0]);
-    __syncthreads();
-    block_colsum<V>(sb, gpr, cpb, red, st[1]);
-    __syncthreads();
-    for (int j = tid; j < cpb; j += kThreads) {
-        const int c = cb + j;
-        const double m = st[0][j] / (double)R;
-        double var = st[1][j] / (double)R - m * m;
-        if (var < 0.0) var = 0.0;
-        const float mf = (float)m, inv = (float)(1.0 / sqrt(var + (double)eps));
-        fm[j] = mf;
-        fi[j] = inv;
-        mean[c] = mf;
-        invstd[c] = inv;
-        if (rmean) {
-            const double unb = R > 1 ? var * (double)R / (double)(R - 1) : var;
-            rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * m);
-            rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unb);
-        }
-        if (c == 0 && nbt) nbt[0] += 1;
-    }
-    __syncthreads();
-    float mu[V], is[V], ga[V], be[V];
-    BnChan::load(fm, cg * V, mu);
-    BnChan::load(fi, cg * V, is);
-    BnChan::load(gamma, c0, ga);
-    BnChan::load(beta, c0, be);
-    for (int64_t r = rr; r < R; r += kU * rpp) {
-        uint4 raw[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) raw[u] = load16_raw(y + min(r + u * rpp, R - 1) * C + c0);
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int64_t ru = r + u * rpp;
-            if (ru >= R) break;
-            float x[V], o[V];
-            cvt16_f32<T>(raw[u], x);
-#pragma unroll
-            for (int v = 0; v < V; ++v) o[v] = act_fwd((x[v] - mu[v]) * is[v] * ga[v] + be[v], act);
-            store16_f32(a + ru * lda + c0, o);
-        }
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void bn_small_bwd_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
-                                                           int64_t R, int C, int cpb, const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd,
-                                                           const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, int act,
-                                                           T* __restrict__ dy, float* __restrict__ dgamma,
-                                                           float* __restrict__ dbeta, float* __restrict__ dbias) {
-    constexpr int V = Vec16<T>::N;
-    __shared__ double red[4 * 512];
-    __shared__ double st[2][512];
-    const int gpr = cpb / V, rpp = kThreads / gpr;
-    const int tid = threadIdx.x, cg = tid % gpr, rr = tid / gpr;
-    const int cb = blockIdx.x * cpb, c0 = cb + cg * V;
-    float mu[V], is[V], ga[V], be[V];
-    BnChan::load(mean, c0, mu);
-    BnChan::load(invstd, c0, is);
-    BnChan::load(gamma, c0, ga);
-    BnChan::load(beta, c0, be);
-    float fa[V], fb[V];  // f32 per thread, f64 across threads (as bn_bwd_moments_kernel)
-#pragma unroll
-    for (int v = 0; v < V; ++v) fa[v] = fb[v] = 0.f;
-    for (int64_t r = rr; r < R; r += kUb * rpp) {
-        uint4 rx[kUb], rg[kUb];
-#pragma unroll
-        for (int u = 0; u < kUb; ++u) {
-            const int64_t rc = min(r + u * rpp, R - 1);
-            rx[u] = load16_raw(y + rc * C + c0);
-            rg[u] = load16_raw(da + rc * lda + c0);
-        }
-#pragma unroll
-        for (int u = 0; u < kUb; ++u) {
-            if (r + u * rpp >= R) break;
-            float x[V], g[V];
-            cvt16_f32<T>(rx[u], x);
-            cvt16_f32<T>(rg[u], g);
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-                const float xh = (x[v] - mu[v]) * is[v];
-                const float dz = g[v] * act_grad(xh * ga[v] + be[v], act);
-                fa[v] += dz;
-                fb[v] = fmaf(dz, xh, fb[v]);
-            }
-        }
-    }
-    double da_[V], db_[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) { da_[v] = fa[v]; db_[v] = fb[v]; }
-    block_colsum<V>(da_, gpr, cpb, red, st[0]);
-    __syncthreads();
-    block_colsum<V>(db_, gpr, cpb, red, st[1]);
-    __syncthreads();
-    for (int j = tid; j < cpb; j += kThreads) {
-        dbeta[cb + j] = (float)st[0][j];
-        dgamma[cb + j] = (float)st[1][j];
-    }
-    const float invR = 1.f / (float)R;
-    float s0[V], sx[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-        s0[v] = (float)st[0][cg * V + v];
-        sx[v] = (float)st[1][cg * V + v];
-    }
-    float bs[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) bs[v] = 0.f;
-    for (int64_t r = rr; r < R; r += kUb * rpp) {
-        uint4 rx[kUb], rg[kUb];
-#pragma unroll
-        for (int u = 0; u < kUb; ++u) {
-            const int64_t rc = min(r + u * rpp, R - 1);
-            rx[u] = load16_raw(y + rc * C + c0);
-            rg[u] = load16_raw(da + rc * lda + c0);
-        }
-#pragma unroll
-        for (int u = 0; u < kUb; ++u) {
-            const int64_t ru = r + u * rpp;
-            if (ru >= R) break;
-            float x[V], g[V], o[V];
-            cvt16_f32<T>(rx[u], x);
-            cvt16_f32<T>(rg[u], g);
-#pragma unroll
-            for (int v = 0; v < V; ++v) {
-                const float xh = (x[v] - mu[v]) * is[v];
-                const float dz = g[v] * act_grad(xh * ga[v] + be[v], act);
-                o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
-            }
-            store16_f32(dy + ru * C + c0, o);
-#pragma unroll
-            for (int v = 0; v < V; ++v) bs[v] += to_f32<T>(from_f32<T>(o[v]));  // the bias grad sums the stored dy
-        }
-    }
-    if (!dbias) return;
-    double bd[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) bd[v] = bs[v];
-    __syncthreads();
-    block_colsum<V>(bd, gpr, cpb, red, st[0]);
-    __syncthreads();
-    for (int j = tid; j < cpb; j += kThreads) dbias[cb + j] = (float)st[0][j];
-}
 
 // out[c] = sum_k part[k][c] over [nblk][C] partials; grid ceil(C / 64) x 1024
 __global__ __launch_bounds__(1024) void colsum_finalize_kernel(const double* __restrict__ part, int nblk, int C,
@@ -876,26 +690,12 @@ __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict
 // y[b, oh, ow] = bias + sum_ci sum_taps x[b, ih, iw, ci] * w[ci*9 + kh*3 + kw]  (transposed, 1 output channel).
 // (Measured: one thread per output pixel beats one thread per low-res pixel computing the 2 x 2 block, whose
 // long per-accumulator FMA chains leave it latency-bound: 47 vs 61 us at B = 256.)
-// kBn: x is the PRE-BatchNorm map y of the decoder's last BN layer: its statistics are finalized here from the
-// (folded) partial table (bn_fin_prologue; block 0 stores mean / invstd / running stats) and every input value
-// goes through BN + LeakyReLU + rounding to T exactly as bn_act_kernel would have stored it.
-template <typename T, int CI, bool kBn>
+template <typename T, int CI>
 __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
-                                                       float* __restrict__ y, FastDiv dWo, FastDiv dHo, BnFin fin,
-                                                       const float* __restrict__ gamma,
-                                                       const float* __restrict__ beta) {
+                                                       float* __restrict__ y, FastDiv dWo, FastDiv dHo) {
     __shared__ float ws[CI * 9];
-    __shared__ float bnp[kBn ? 4 * CI : 1];
-    __shared__ double bred[kBn ? 2 * kThreads : 1];
     for (int i = threadIdx.x; i < CI * 9; i += blockDim.x) ws[i] = w[i];
-    if constexpr (kBn) {
-        bn_fin_prologue<true>(fin, CI, bnp, bnp + CI, bred);
-        for (int c = threadIdx.x; c < CI; c += blockDim.x) {
-            bnp[2 * CI + c] = gamma[c];
-            bnp[3 * CI + c] = beta[c];
-        }
-    }
     __syncthreads();
     const float b0 = bias ? bias[0] : 0.f;
     const int Ho = 2 * Hi, Wo = 2 * Wi;
@@ -920,14 +720,6 @@ __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, 
                 for (int c0 = 0; c0 < CI; c0 += V) {
                     float v[V];
                     load16_f32(src + c0, v);
-                    if constexpr (kBn) {
-#pragma unroll
-                        for (int q = 0; q < V; ++q) {
-                            const int c = c0 + q;
-                            v[q] = to_f32<T>(from_f32<T>(
-                                act_fwd((v[q] - bnp[c]) * bnp[CI + c] * bnp[2 * CI + c] + bnp[3 * CI + c], 0)));
-                        }
-                    }
 #pragma unroll
                     for (int q = 0; q < V; ++q) s = fmaf(v[q], ws[(c0 + q) * 9 + tap], s);
                 }
@@ -940,30 +732,15 @@ __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, 
 // dW[m*9+tap] partials: block = chunk of low-res rows (b,r,c); Xh single-channel high-res [B, 2Hl, 2Wl].
 // Rows are staged in LDS 256 at a time; thread (mg, rg) accumulates a 4(m) x 9(tap) register block over
 // rows rg, rg+32, ... (13 LDS reads per 36 FMAs); the 32 row-groups are combined in a fixed order.
-// BN + LeakyReLU(0.01) applied to a consumer's operand on the fly: a = T(lrelu((y - mean) * invstd * gamma + beta))
-// (bn_act_kernel's arithmetic and rounding, so the result equals the materialised activation)
-struct BnXf {
-    const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
-};
 template <typename T, int M>
 __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, int B, int Hl, int Wl,
                                                        const float* __restrict__ Xh, int rows_per_blk,
-                                                       float* __restrict__ part, FastDiv dWl, FastDiv dHl, BnXf xf) {
+                                                       float* __restrict__ part, FastDiv dWl, FastDiv dHl) {
     static_assert(M == 32, "one 8 x 4 channel tiling");
     constexpr int RC = 256;
     // one LDS block: [RC][M+1] rows + [RC][9] taps during accumulation, [32][M*9] partials afterwards
     constexpr int kAcc = RC * (M + 1) + RC * 9, kRed = 32 * M * 9;
     __shared__ float smem[kAcc > kRed ? kAcc : kRed];
-    __shared__ float xfp[4][M];  // mean / invstd / gamma / beta of L's BN layer (xf.mean set)
-    if (xf.mean) {
-        for (int c = threadIdx.x; c < M; c += blockDim.x) {
-            xfp[0][c] = xf.mean[c];
-            xfp[1][c] = xf.invstd[c];
-            xfp[2][c] = xf.gamma[c];
-            xfp[3][c] = xf.beta[c];
-        }
-        __syncthreads();
-    }
     float (*Ls)[M + 1] = reinterpret_cast<float (*)[M + 1]>(smem);
     float (*Hs)[9] = reinterpret_cast<float (*)[9]>(smem + RC * (M + 1));
     const int64_t K = (int64_t)B * Hl * Wl;
@@ -1005,13 +782,6 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, 
             const int i = threadIdx.x + u * 256, rr = i / (M / V), cg = i % (M / V);
             float v[V];
             cvt16_f32<T>(nl[u], v);
-            if (xf.mean) {
-#pragma unroll
-                for (int q = 0; q < V; ++q) {
-                    const int c = cg * V + q;
-                    v[q] = to_f32<T>(from_f32<T>(act_fwd((v[q] - xfp[0][c]) * xfp[1][c] * xfp[2][c] + xfp[3][c], 0)));
-                }
-            }
             const bool ok = kb + rr < k1;
 #pragma unroll
             for (int q = 0; q < V; ++q) Ls[rr][cg * V + q] = ok ? v[q] : 0.f;
@@ -1119,6 +889,66 @@ __global__ void reparam_fwd_kernel(const float* __restrict__ mu, const float* __
         z[(int64_t)r * ldz + c] = from_f32<T>(mu[i] + eps[i] * sd);
     }
 }
+// ---------------------------------------------------------------- reparameterisation noise (Philox4x32-10)
+// eps ~ N(0, 1) drawn on the device instead of a host/torch launch: element g = offset + i of the (seed) stream is
+// component g % 4 of Philox4x32-10(counter = {g / 4 (64 bits), 0, 0}, key = seed) (Salmon et al., SC'11: 10 rounds,
+// multipliers 0xD2511F53 / 0xCD9E8D57, key bumps 0x9E3779B9 / 0xBB67AE85), the 4 words mapped to 2 Box-Muller
+// pairs: u1 = (w0 + 1) 2^-32 in (0, 1], u2 = w1 2^-32, n0 = sqrt(-2 ln u1) cos(2 pi u2), n1 = ... sin(2 pi u2).
+// Counter-based, so any element is computed independently (no generator state on the device).
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+__device__ __forceinline__ void philox_normal4(uint64_t seed, uint64_t q, float (&n)[4]) {
+    const uint4 w = philox4x32_10(make_uint4((uint32_t)q, (uint32_t)(q >> 32), 0u, 0u), (uint32_t)seed,
+                                  (uint32_t)(seed >> 32));
+    const float k = 2.3283064365386963e-10f;  // 2^-32
+    const float r0 = sqrtf(-2.f * logf(((float)w.x + 1.f) * k)), a0 = 6.283185307179586f * ((float)w.y * k);
+    const float r1 = sqrtf(-2.f * logf(((float)w.z + 1.f) * k)), a1 = 6.283185307179586f * ((float)w.w * k);
+    n[0] = r0 * cosf(a0);
+    n[1] = r0 * sinf(a0);
+    n[2] = r1 * cosf(a1);
+    n[3] = r1 * sinf(a1);
+}
+// out[i] = element offset + i of the stream (offset % 4 == 0): one thread per group of 4
+__global__ void randn_kernel(float* __restrict__ out, int64_t n, uint64_t seed, uint64_t offset) {
+    const int64_t groups = (n + 3) / 4;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < groups; t += (int64_t)gridDim.x * blockDim.x) {
+        float v[4];
+        philox_normal4(seed, offset / 4 + t, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (4 * t + j < n) out[4 * t + j] = v[j];
+    }
+}
+// z = mu + eps * exp(0.5 lv) with eps drawn here (element i of the [n_rows][L] block = stream element offset + i)
+// and stored to eps_out for the backward pass
+template <typename T>
+__global__ void reparam_rng_kernel(const float* __restrict__ mu, const float* __restrict__ lv, uint64_t seed,
+                                   uint64_t offset, int n_rows, int L, float* __restrict__ eps_out, T* __restrict__ z,
+                                   int ldz) {
+    const int64_t n = (int64_t)n_rows * L, groups = (n + 3) / 4;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < groups; t += (int64_t)gridDim.x * blockDim.x) {
+        float v[4];
+        philox_normal4(seed, offset / 4 + t, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t i = 4 * t + j;
+            if (i >= n) break;
+            const int r = (int)(i / L), c = (int)(i - (int64_t)r * L);
+            eps_out[i] = v[j];
+            z[(int64_t)r * ldz + c] = from_f32<T>(mu[i] + v[j] * expf(0.5f * lv[i]));
+        }
+    }
+}
+
 template <typename T>
 __global__ void reparam_bwd_kernel(const T* __restrict__ dz, int lddz, const float* __restrict__ lv,
                                    const float* __restrict__ eps, int n_rows, int L, float* __restrict__ dmu,
@@ -1477,36 +1307,6 @@ int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, const double* part
     return HLMC_OK;
 }
 
-bool bn_small(int64_t R, int C) { return bn_small_ok(R, C) && C <= 512; }
-
-template <typename T>
-int bn_small_fwd(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean,
-                 float* run_var, int64_t* nbt, float momentum, float eps, const float* gamma, const float* beta,
-                 int act, T* a, int lda) {
-    HLMC_TRY(check_bn_shape<T>(C));
-    HLMC_CHECK_ARG(bn_small(R, C) && lda % Vec16<T>::N == 0, "bn_small_fwd: layer too large / bad stride");
-    const int cpb = bn_small_cpb<T>(C);
-    HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C,
-                   (bn_small_fwd_kernel<T><<<C / cpb, kThreads, 0, s>>>(y, R, C, cpb, mean, invstd, run_mean, run_var,
-                                                                       nbt, momentum, eps, gamma, beta, act, a, lda)));
-    HLMC_LAUNCHED();
-    return HLMC_OK;
-}
-
-template <typename T>
-int bn_small_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean,
-                 const float* invstd, const float* gamma, const float* beta, int act, T* dy, float* dgamma,
-                 float* dbeta, float* dbias) {
-    HLMC_TRY(check_bn_shape<T>(C));
-    HLMC_CHECK_ARG(bn_small(R, C) && lda % Vec16<T>::N == 0, "bn_small_bwd: layer too large / bad stride");
-    const int cpb = bn_small_cpb<T>(C);
-    HLMC_BN_PROBED(s, 5.0 * sizeof(T) * R * C,
-                   (bn_small_bwd_kernel<T><<<C / cpb, kThreads, 0, s>>>(da, lda, y, R, C, cpb, mean, invstd, gamma,
-                                                                       beta, act, dy, dgamma, dbeta, dbias)));
-    HLMC_LAUNCHED();
-    return HLMC_OK;
-}
-
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
@@ -1611,26 +1411,12 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
 }
 
 template <typename T>
-int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y,
-             const BnApply* ba) {
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y) {
     HLMC_CHECK_ARG(Ci == 32, "convT_c1: only Ci == 32");
     int64_t npix = (int64_t)B * 4 * Hi * Wi;
     HLMC_CHECK_ARG(npix < (int64_t)1 << 31, "convT_c1: too many pixels");
     const FastDiv dW((uint32_t)(2 * Wi)), dH((uint32_t)(2 * Hi));
-    if (ba) {
-        HLMC_CHECK_ARG(ba->part && ba->nparts > 0, "convT_c1: BN statistics rows required");
-        const Folded f = fold_parts_to(s, ba->part, ba->nparts, 2 * Ci, ba->fold, fin_max_rows(Ci));
-        HLMC_CHECK_ARG(f.p != nullptr, "convT_c1: no fold space for the BN statistics");
-        BnFin fin;
-        fin.part = f.p; fin.rows = f.rows; fin.R = ba->R;
-        fin.mean = ba->mean; fin.invstd = ba->invstd; fin.rmean = ba->rmean; fin.rvar = ba->rvar; fin.nbt = ba->nbt;
-        fin.momentum = ba->momentum; fin.eps = ba->eps;
-        convT_c1_kernel<T, 32, true><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fin,
-                                                                         ba->gamma, ba->beta);
-    } else {
-        convT_c1_kernel<T, 32, false><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, BnFin{},
-                                                                          nullptr, nullptr);
-    }
+    convT_c1_kernel<T, 32><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1641,20 +1427,15 @@ size_t wgrad_c1_ws(int B, int Hl, int Wl, int M) {
 }
 
 template <typename T>
-int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws,
-             const BnAct* act) {
+int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws) {
     HLMC_CHECK_ARG(M == 32, "wgrad_c1: only M == 32");
     int64_t K = (int64_t)B * Hl * Wl;
     int nblk = wgrad_c1_blocks(K);
     HLMC_CHECK_ARG(ws.bytes >= wgrad_c1_ws(B, Hl, Wl, M), "wgrad_c1 workspace");
     int rpb = (int)((K + nblk - 1) / nblk);
     HLMC_CHECK_ARG(K < (int64_t)1 << 31, "wgrad_c1: too many rows");
-    BnXf xf;
-    if (act) {
-        xf.mean = act->mean; xf.invstd = act->invstd; xf.gamma = act->gamma; xf.beta = act->beta;
-    }
     wgrad_c1_kernel<T, 32><<<nblk, kThreads, 0, s>>>(L, B, Hl, Wl, Xh, rpb, ws.p, FastDiv((uint32_t)Wl),
-                                                     FastDiv((uint32_t)Hl), xf);
+                                                     FastDiv((uint32_t)Hl));
     HLMC_LAUNCHED();
     sum_partials_f32_kernel<<<M * 9, 256, 0, s>>>(ws.p, nblk, M * 9, dW);
     HLMC_LAUNCHED();
@@ -1780,6 +1561,22 @@ int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* ep
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
+int randn(hipStream_t s, float* out, int64_t n, uint64_t seed, uint64_t offset) {
+    HLMC_CHECK_ARG(out && n >= 0 && offset % 4 == 0, "randn: bad arguments (offset must be a multiple of 4)");
+    if (n == 0) return HLMC_OK;
+    randn_kernel<<<grid_for((n + 3) / 4), kThreads, 0, s>>>(out, n, seed, offset);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+template <typename T>
+int reparam_rng(hipStream_t s, const float* mu, const float* lv, uint64_t seed, uint64_t offset, int n_rows, int L,
+                float* eps_out, T* z, int ldz) {
+    HLMC_CHECK_ARG(offset % 4 == 0, "reparam_rng: offset must be a multiple of 4");
+    reparam_rng_kernel<T><<<grid_for(((int64_t)n_rows * L + 3) / 4), kThreads, 0, s>>>(mu, lv, seed, offset, n_rows, L,
+                                                                                       eps_out, z, ldz);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
 template <typename T>
 int reparam_bwd(hipStream_t s, const T* dz, int lddz, const float* lv, const float* eps, int n_rows, int L, float* dmu,
                 float* dlv) {
@@ -1891,10 +1688,6 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
                              float, Ws);                                                                              \
     template int bn_act<T>(hipStream_t, const T*, int64_t, int, const float*, const float*, const float*, const float*, \
                            int, const uint8_t*, float, T*, int);                                                      \
-    template int bn_small_fwd<T>(hipStream_t, const T*, int64_t, int, float*, float*, float*, float*, int64_t*,     \
-                                 float, float, const float*, const float*, int, T*, int);                            \
-    template int bn_small_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,     \
-                                 const float*, const float*, int, T*, float*, float*, float*);                       \
     template int bn_act_train<T>(hipStream_t, const T*, int64_t, int, const double*, int, float*, float*, float*,    \
                                  float*, int64_t*, float, float, const float*, const float*, int, const uint8_t*, float, \
                                  T*, int, Ws);                                                                       \
@@ -1903,9 +1696,8 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
                                const BnBwdFuse*, double*);                                                           \
     template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*,        \
                                ColStats*, BnBwdFuse*);                                                               \
-    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*,          \
-                             const BnApply*);                                                                        \
-    template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws, const BnAct*);      \
+    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);         \
+    template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws);                    \
     template int cast_from_f32<T>(hipStream_t, const float*, T*, int64_t);                                           \
     template int cast_to_f32<T>(hipStream_t, const T*, float*, int64_t);                                             \
     template int copy2d<T>(hipStream_t, const T*, int, T*, int, int, int);                                           \
@@ -1915,6 +1707,7 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
     template int relu_bwd<T>(hipStream_t, T*, int, const T*, int, int, int);                                         \
     template int colsum<T>(hipStream_t, const T*, int, int, int, float*, Ws);                                        \
     template int reparam_fwd<T>(hipStream_t, const float*, const float*, const float*, int, int, T*, int);           \
+    template int reparam_rng<T>(hipStream_t, const float*, const float*, uint64_t, uint64_t, int, int, float*, T*, int); \
     template int reparam_bwd<T>(hipStream_t, const T*, int, const float*, const float*, int, int, float*, float*);   \
     template int pack<T>(hipStream_t, const AdamJob*, int, int);                                                     \
     template int adam_pack<T>(hipStream_t, const AdamJob*, int, int, AdamArgs, const float*, int);

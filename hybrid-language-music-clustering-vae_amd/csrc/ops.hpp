@@ -20,9 +20,9 @@ struct ColStats {
     int nparts;
 };
 size_t col_stats_bytes(int64_t M, int phases, int C);  // bytes of part for M output rows x phases
-// Optional fused BatchNorm(+LeakyReLU 0.01) backward moments of a data-gradient GEMM's output da (see
-// WithBnBwd): y / mean / invstd / gamma / beta of the BN layer whose output gradient the GEMM writes.  When
-// the launch is single-pass, part receives nparts rows of [sum dz | sum dz*xhat] (else nparts = 0).
+// Fused BatchNorm(+LeakyReLU 0.01) backward moments of a data-gradient producer's output da (conv_c1_s2 as the
+// output convT's data gradient): y / mean / invstd / gamma / beta of the BN layer whose output gradient it
+// writes; part receives nparts rows of [sum dz | sum dz*xhat] (nparts = 0: compute them separately).
 struct BnBwdFuse {
     const void* y;
     const float *mean, *invstd, *gamma, *beta;
@@ -32,7 +32,7 @@ struct BnBwdFuse {
 // y[B, Hi/2, Wi/2, Co] = conv3x3_s2_p1(x[B,Hi,Wi,Ci]) + bias ; wp packed [Co][3][3][Ci]
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-            ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
+            ColStats* st = nullptr);
 template <typename T>
 size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -40,7 +40,7 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 // (also the data gradient of a stride-2 conv with the conv weight re-packed [Ci_conv][3][3][Co_conv])
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-             ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
+             ColStats* st = nullptr);
 template <typename T>
 size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -70,30 +70,11 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
                ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
 int conv_c1_fused_rows(int B, int Hi, int Wi);  // partial rows conv_c1_s2 writes with st / bf
 // y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel)
-// The consumer applies its input's train-mode BatchNorm + LeakyReLU(0.01) itself (no bn_act pass): `part`
-// [nparts][2C] statistics rows of the pre-BN map x, folded into `fold`; the consumer writes mean / invstd and the
-// running statistics like bn_stats, and rounds every activation to T as bn_act would have stored it.
-struct BnApply {
-    const double* part;
-    int nparts;
-    int64_t R;
-    float *mean, *invstd, *rmean, *rvar;
-    int64_t* nbt;
-    float momentum, eps;
-    const float *gamma, *beta;
-    Ws fold;
-};
-// the same transform from already-finalized statistics (backward consumers)
-struct BnAct {
-    const float *mean, *invstd, *gamma, *beta;
-};
 template <typename T>
-int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y,
-             const BnApply* ba = nullptr);
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y);
 // dW[m*9+tap] = sum L[b,r,c,m] * Xh[b, 2r-1+kh, 2c-1+kw]   (Xh single channel f32)
 template <typename T>
-int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws,
-             const BnAct* act = nullptr);
+int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws);
 size_t wgrad_c1_ws(int B, int Hl, int Wl, int M);
 
 // ---------------------------------------------------------------- batch norm / activation (kernels.hip)
@@ -110,17 +91,6 @@ size_t fold_ws(int ncols);  // scratch bytes to fold a [rows][ncols] f64 partial
 // Eval-mode statistics from running buffers.
 int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, int C, float eps, float* mean, float* invstd);
 // a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale];  act: 0 lrelu(0.01), 1 relu, 2 none
-// Small train-mode BatchNorm layers (R * C <= 2^21, C <= 512): one launch per direction, each block owning a
-// channel slab over all rows (statistics + apply; backward also writes dgamma / dbeta / dbias (nullable)).
-bool bn_small(int64_t R, int C);
-template <typename T>
-int bn_small_fwd(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean,
-                 float* run_var, int64_t* nbt, float momentum, float eps, const float* gamma, const float* beta,
-                 int act, T* a, int lda);
-template <typename T>
-int bn_small_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean,
-                 const float* invstd, const float* gamma, const float* beta, int act, T* dy, float* dgamma,
-                 float* dbeta, float* dbias);
 // Train-mode BatchNorm + activation with the statistics finalized inside the activation kernel: `part`
 // [nparts][2C] f64 column sums / sums of squares from the producer (nullptr: a moments pass over y into ws
 // first), folded to <= 8 rows; writes mean / invstd and updates the running statistics like bn_stats.
@@ -166,6 +136,12 @@ template <typename T> int relu_bwd(hipStream_t s, T* dy, int lddy, const T* y, i
 template <typename T> int colsum(hipStream_t s, const T* dy, int ld, int rows, int cols, float* db, Ws ws);
 size_t colsum_ws(int rows, int cols);
 // z = mu + eps * exp(0.5 logvar)  (z written as T with row stride ldz)
+// eps ~ N(0,1), element offset + i of the Philox4x32-10 stream `seed` (offset % 4 == 0) -> out[i]
+int randn(hipStream_t s, float* out, int64_t n, uint64_t seed, uint64_t offset);
+// reparam_fwd with eps drawn on the device (the same stream elements as randn) and stored to eps_out
+template <typename T>
+int reparam_rng(hipStream_t s, const float* mu, const float* lv, uint64_t seed, uint64_t offset, int n_rows, int L,
+                float* eps_out, T* z, int ldz);
 template <typename T> int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz);
 // dmu += dz ; dlv += dz * eps * 0.5 exp(0.5 lv)
 template <typename T> int reparam_bwd(hipStream_t s, const T* dz, int lddz, const float* lv, const float* eps, int n_rows, int L, float* dmu, float* dlv);

@@ -78,6 +78,10 @@ class NativeNet:
             shape = (C.c_int64 * 4)()
             L.check(L.lib().hlmc_net_param_info(h, i, name, 256, C.byref(nd), shape))
             self.param_specs.append((name.value.decode(), tuple(shape[k] for k in range(nd.value))))
+        # reparameterisation noise drawn on the device when no eps is passed (hlmc_net_set_rng): the stream is
+        # keyed by torch's current seed, so torch.manual_seed(s) before building a model fixes its noise as it
+        # fixes torch.randn_like's in the reference (src/Convolutional_VAE.py:162-165)
+        L.check(L.lib().hlmc_net_set_rng(h, torch.initial_seed() & 0xFFFFFFFFFFFFFFFF, 0), "hlmc_net_set_rng")
         self.state = None
         self._bound = None
         self._ws = {}
@@ -136,7 +140,8 @@ class _NetFn(torch.autograd.Function):
                                          L.ptr(eps), L.ptr(dropout), L.ptr(out["recon"]), L.ptr(out.get("recon_text")),
                                          L.ptr(out["mu"]), L.ptr(out["logvar"]), L.ptr(out.get("z")), ws.data_ptr()),
                 "hlmc_net_forward")
-        ctx.owner, ctx.ws, ctx.B = owner, ws, B
+        # the engine's backward re-reads audio (the first conv's weight gradient): keep it alive until then
+        ctx.owner, ctx.ws, ctx.B, ctx.audio = owner, ws, B, audio
         ctx.has_text = "recon_text" in out
         ctx.shapes = {k: v.shape for k, v in out.items()}
         outs = [out["recon"], out.get("recon_text"), out["mu"], out["logvar"], out.get("z")]
@@ -165,7 +170,7 @@ class _NetFn(torch.autograd.Function):
                                           L.ptr(d_lv), ctx.ws.data_ptr()), "hlmc_net_backward")
         # autograd reads every gradient right away: no Adam-overlapped tail on this path
         L.check(L.lib().hlmc_net_settle(net.h, L.stream()), "hlmc_net_settle")
-        ctx.ws = None
+        ctx.ws = ctx.audio = None
         return (None, None, None, None, None, None, None, *owner._grad_views)
 
 
@@ -324,11 +329,9 @@ class HybridVAE(_NativeModule):
         return out["recon"], out.get("recon_text")
 
     def forward(self, audio, text=None, eps=None):
-        B = audio.shape[0]
-        if eps is None:
-            eps = torch.randn(B, self.latent_dim, device=audio.device)  # torch.randn_like(std)
+        # eps None: drawn on the device by the engine (its Philox stream), as torch.randn_like(std) in the reference
         ra, rt, mu, lv, _ = self._run(audio.contiguous(), None if self.audio_only else text.contiguous(), None,
-                                      eps.contiguous())
+                                      None if eps is None else eps.contiguous())
         return ra, (None if self.audio_only else rt), mu, lv
 
 
@@ -373,11 +376,8 @@ class ConditionalVAE(_NativeModule):
         return out["recon"], out["recon_text"]
 
     def forward(self, audio, text, condition, eps=None):
-        B = audio.shape[0]
-        if eps is None:
-            eps = torch.randn(B, self.latent_dim, device=audio.device)
         ra, rt, mu, lv, _ = self._run(audio.contiguous(), text.contiguous(), condition.float().contiguous(),
-                                      eps.contiguous())
+                                      None if eps is None else eps.contiguous())
         return ra, rt, mu, lv
 
 
@@ -433,11 +433,9 @@ class VAE(_NativeModule):
 
     def forward(self, x, eps=None, dropout_mask=None):
         B = x.shape[0]
-        if eps is None:
-            eps = torch.randn(B, self.latent_dim, device=x.device)
         if self.training and dropout_mask is None:
             dropout_mask = self.make_dropout_mask(B, x.device)
-        recon, _, mu, lv, z = self._run(x.float().contiguous(), None, None, eps.contiguous(),
+        recon, _, mu, lv, z = self._run(x.float().contiguous(), None, None, None if eps is None else eps.contiguous(),
                                         dropout_mask if self.training else None)
         return recon, mu, lv, z
 

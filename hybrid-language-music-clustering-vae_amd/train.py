@@ -116,7 +116,9 @@ class Trainer:
             self._check_bn_flat()
         c = self._buffers(B)
         out, d = c["out"], c["d"]
-        if eps is None:
+        # eps None: the engine draws the reparameterisation noise on the device (Philox, hlmc_net_set_rng) — except
+        # under graph capture, where the host-side stream offset would freeze into the graph: torch's graph-safe randn
+        if eps is None and self._graph:
             eps = torch.randn(B, self.model.latent_dim, device=self.device)
         if self.kind == "simple" and dropout is None:
             dropout = self.model.make_dropout_mask(B, self.device)

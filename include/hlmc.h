@@ -117,7 +117,10 @@ int64_t hlmc_net_workspace_bytes(const hlmc_net* net, int64_t batch);
 int hlmc_net_bind(hlmc_net* net, float* const* params, float* const* grads, float* const* running,
                   int64_t* const* nbt, void* state);
 /* Forward.  train!=0: BatchNorm batch statistics (running stats updated), dropout mask applied (Simple);
- * eps [batch][latent] is the reparameterisation noise (host/torch generated, like torch.randn_like).
+ * eps [batch][latent] is the reparameterisation noise (torch.randn_like in the reference); eps = NULL draws it on
+ * the device from the net's Philox4x32-10 stream (hlmc_net_set_rng; no host launch), kept for the backward.
+ * in0 is read again by hlmc_net_backward (the first conv's weight gradient): it must stay allocated and unchanged
+ * until then (stream order).
  * hybrid/cvae: in0 = audio [B][1][H][W], in1 = text [B][text_dim], in2 = condition [B][C] (cvae);
  * simple: in0 = x [B][input_dim], dropout = uint8 keep-mask per hidden unit (NULL = no dropout).
  * outputs: recon [B][...], recon_text [B][text_dim] (hybrid with text, cvae), mu, logvar [B][latent],
@@ -125,6 +128,13 @@ int hlmc_net_bind(hlmc_net* net, float* const* params, float* const* grads, floa
 int hlmc_net_forward(hlmc_net* net, void* stream, int64_t batch, int train, const float* in0, const float* in1,
                      const float* in2, const float* eps, const uint8_t* dropout, float* recon, float* recon_text,
                      float* mu, float* logvar, float* z, void* ws);
+/* Device reparameterisation noise (replaces torch.randn_like, src/Convolutional_VAE.py:162-165): the stream is
+ * Philox4x32-10 keyed by `seed`; element g is component g % 4 of the block at counter g / 4, mapped by Box-Muller.
+ * set_rng positions a net's stream (offset % 4 == 0); every forward drawing its own eps advances it by
+ * round4(batch * latent).  hlmc_randn writes elements offset .. offset + n - 1 of stream `seed` to out. */
+int hlmc_net_set_rng(hlmc_net* net, uint64_t seed, uint64_t offset);
+int hlmc_net_get_rng(const hlmc_net* net, uint64_t* seed, uint64_t* offset);
+int hlmc_randn(void* stream, float* out, int64_t n, uint64_t seed, uint64_t offset);
 /* encoder only (latent extraction, src/Convolutional_VAE.py:286-303): mu, logvar */
 int hlmc_net_encode(hlmc_net* net, void* stream, int64_t batch, int train, const float* in0, const float* in1,
                     const float* in2, float* mu, float* logvar, void* ws);

@@ -2,6 +2,8 @@
 
 fp32 path (exact-fp32 MFMA): relative L2 error <= 1e-5.  bf16 path: operands rounded to bf16 on
 both sides, fp32 accumulation; relative L2 error <= 1e-2 (bf16 output rounding ~4e-3)."""
+import ctypes as C
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -293,3 +295,33 @@ def test_wgrad_s2_bench_shapes_bf16(cuda, ws, Hl, Wl, M, C):
     e = rel(dW, ref)
     print(f"wgrad_s2 B={BB} {Hl}x{Wl} M={M} C={C}: rel L2 {e:.2e}")
     assert e < 1e-4
+
+
+def test_device_randn_matches_philox_restatement(cuda):
+    """hlmc_randn (the engine's reparameterisation noise) = oracle/rng_oracle.py's Philox4x32-10 + Box-Muller
+    restatement element for element (float32 libm rounding of log / cos / sin: <= 2e-6), any offset, and N(0, 1)."""
+    from oracle import rng_oracle
+    out = torch.empty(1001, device=cuda)
+    for seed, off in [(0, 0), (42, 0), (2 ** 40 + 7, 4096), (123456789, 1 << 33)]:
+        L.check(L.lib().hlmc_randn(L.stream(), out.data_ptr(), out.numel(), seed, off))
+        ref = torch.from_numpy(rng_oracle.normals(out.numel(), seed, off))
+        err = float((out.cpu() - ref).abs().max())
+        assert err <= 2e-6 * max(1.0, float(ref.abs().max())), (seed, off, err)
+    big = torch.empty(1 << 22, device=cuda)
+    L.check(L.lib().hlmc_randn(L.stream(), big.data_ptr(), big.numel(), 7, 0))
+    m, sd = float(big.mean()), float(big.std())
+    assert abs(m) < 2e-3 and abs(sd - 1) < 2e-3, (m, sd)
+    # the engine draws its forward's eps from the net's stream: simple VAE z = mu + eps * exp(lv / 2)
+    torch.manual_seed(3)
+    vae = hlmc_amd.VAE(370, [128, 64, 32], 32).cuda().eval()
+    seed, off = C.c_uint64(), C.c_uint64()
+    net = vae._native_net()
+    L.check(L.lib().hlmc_net_get_rng(net.h, C.byref(seed), C.byref(off)))
+    assert seed.value == torch.initial_seed() and off.value == 0
+    x = torch.randn(6, 370, device=cuda)
+    with torch.no_grad():
+        _, mu, lv, z = vae(x)
+    eps = torch.from_numpy(rng_oracle.normals(6 * 32, seed.value, 0)).view(6, 32)
+    torch.testing.assert_close(z.cpu(), mu.cpu() + eps * torch.exp(0.5 * lv.cpu()), rtol=1e-5, atol=1e-5)
+    L.check(L.lib().hlmc_net_get_rng(net.h, C.byref(seed), C.byref(off)))
+    assert off.value == 6 * 32

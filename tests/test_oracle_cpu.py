@@ -208,3 +208,15 @@ def test_chroma_oracle_properties():
         assert np.argmax(ch[:, 8:-8].mean(1)) == 9
     ch, tun = SO.chroma_stft(np.zeros(8192, np.float32))
     assert tun == 0.0 and not ch.any()
+
+
+def test_philox_known_answers():
+    """oracle/rng_oracle.py Philox4x32-10 against the Random123 known-answer vectors (kat_vectors: philox4x32_10)."""
+    from oracle.rng_oracle import normals, philox4x32
+    assert philox4x32((0, 0, 0, 0), (0, 0)) == (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)
+    assert philox4x32((0xffffffff,) * 4, (0xffffffff,) * 2) == (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)
+    assert philox4x32((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0)) == (
+        0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)
+    a = normals(4096, seed=1234)
+    assert abs(float(a.mean())) < 0.05 and abs(float(a.std()) - 1) < 0.05
+    np.testing.assert_array_equal(normals(8, seed=1234, offset=4096 - 8), a[-8:])

@@ -596,10 +596,10 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
 
 // ---------------------------------------------------------------- edge convs (one channel side)
 // y[b,oh,ow,co] = bias[co] + sum_{kh,kw} x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + kh*3+kw]
-// One thread per output pixel; the 9*CO weights are read at wave-uniform addresses (scalar loads).
 // y[b, oh, ow, co] = bias[co] + sum_taps x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + tap]  (1 input channel, CO = 32)
 // Four threads per output pixel, each computing 8 channels (one 16-byte store): a wave's store instruction
-// writes 1 KB contiguous; the 9 input taps are re-read by the 4 threads from L1.
+// writes 1 KB contiguous; the 9 input taps are re-read by the 4 threads from L1; each thread's 72 weights are
+// registers, and two pixels' tap loads are in flight per step.
 // MODE 1 (encoder input conv): also the BatchNorm statistics of the stored outputs, one [sum | sum of squares]
 // f64 partial row per block (the col_moments pass it replaces).  MODE 2 (data gradient of the decoder's output
 // convT, which writes the gradient of the last BatchNorm layer's output): also that layer's backward moments
@@ -615,65 +615,81 @@ __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict
                                                          const float* __restrict__ w, const float* __restrict__ bias,
                                                          T* __restrict__ y, FastDiv dWo, FastDiv dHo, C1Fuse fz) {
     constexpr int V = Vec16<T>::N, G = CO / V;  // threads per pixel
-    __shared__ float wsh[CO * 9], bsh[CO];       // per-lane channel groups: LDS broadcast reads, not global
+    constexpr int U = 2;                        // pixels per thread per step: 2 x 9 tap loads in flight
     __shared__ double fred[MODE ? 4 * CO : 1];
-    using Acc = typename std::conditional<MODE == 1, double, float>::type;
-    Acc fa[V], fb[V];
+    // a thread's channel group is fixed (the grid stride is a multiple of G): its 9 x V weights and V biases live in
+    // registers for the whole kernel (no per-pixel LDS weight reads)
+    const int c0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) % G) * V;
+    float wr[V][9], br[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        br[v] = bias ? bias[c0 + v] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) wr[v][k] = w[(c0 + v) * 9 + k];
+    }
+    float fa[V], fb[V];  // per-thread statistics (a handful of pixels) in f32, widened once for the block tree
     float bmu[V], bis[V], bga[V], bbe[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) fa[v] = fb[v] = Acc(0);
-    if constexpr (MODE == 2) {  // a thread's channels are fixed (the grid stride is a multiple of G)
-        const int cf = (int)((blockIdx.x * blockDim.x + threadIdx.x) % G) * V;
-        BnChan::load(fz.mean, cf, bmu);
-        BnChan::load(fz.invstd, cf, bis);
-        BnChan::load(fz.gamma, cf, bga);
-        BnChan::load(fz.beta, cf, bbe);
+    for (int v = 0; v < V; ++v) fa[v] = fb[v] = 0.f;
+    if constexpr (MODE == 2) {
+        BnChan::load(fz.mean, c0, bmu);
+        BnChan::load(fz.invstd, c0, bis);
+        BnChan::load(fz.gamma, c0, bga);
+        BnChan::load(fz.beta, c0, bbe);
     }
-    for (int i = threadIdx.x; i < CO * 9; i += blockDim.x) wsh[i] = w[i];
-    for (int i = threadIdx.x; i < CO; i += blockDim.x) bsh[i] = bias ? bias[i] : 0.f;
-    __syncthreads();
     const int Ho = Hi / 2, Wo = Wi / 2;
     const int nthr = B * Ho * Wo * G;  // < 2^31 (checked by the launcher)
-    for (int t0 = blockIdx.x * blockDim.x + threadIdx.x; t0 < nthr; t0 += gridDim.x * blockDim.x) {
-        const int p = t0 / G, c0 = (t0 - p * G) * V;
-        const int t = (int)dWo.div((uint32_t)p), ow = p - t * Wo;
-        const int b = (int)dHo.div((uint32_t)t), oh = t - b * Ho;
-        float in[9];
+    const int stride = gridDim.x * blockDim.x;
+    for (int tb = blockIdx.x * blockDim.x + threadIdx.x; tb < nthr; tb += U * stride) {
+        float in[U][9];
+        int pix[U];
+        uint4 yraw[U];
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
+        for (int u = 0; u < U; ++u) {  // every load of the U pixels issued before any use
+            const int t0 = tb + u * stride;
+            const bool ok = t0 < nthr;
+            const int p = ok ? t0 / G : 0;
+            pix[u] = ok ? p : -1;
+            const int t = (int)dWo.div((uint32_t)p), ow = p - t * Wo;
+            const int b = (int)dHo.div((uint32_t)t), oh = t - b * Ho;
+            const float* xr = x + ((int64_t)b * Hi + 2 * oh - 1) * Wi + 2 * ow - 1;
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const int ih = 2 * oh - 1 + kh, iw = 2 * ow - 1 + kw;
-                in[kh * 3 + kw] = (ih >= 0 && iw >= 0) ? x[((int64_t)b * Hi + ih) * Wi + iw] : 0.f;  // ih, iw < Hi, Wi
-            }
-        uint4 yraw;
-        if constexpr (MODE == 2) yraw = load16_raw(static_cast<const T*>(fz.ybn) + (int64_t)p * CO + c0);
-        float o[V];
+            for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
-        for (int v = 0; v < V; ++v) {
-            float s = bsh[c0 + v];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) s = fmaf(in[k], wsh[(c0 + v) * 9 + k], s);
-            o[v] = s;
+                for (int kw = 0; kw < 3; ++kw)
+                    in[u][kh * 3 + kw] = (2 * oh - 1 + kh >= 0 && 2 * ow - 1 + kw >= 0) ? xr[kh * Wi + kw] : 0.f;
+            if constexpr (MODE == 2) yraw[u] = load16_raw(static_cast<const T*>(fz.ybn) + (int64_t)p * CO + c0);
         }
-        store16_f32(y + (int64_t)p * CO + c0, o);
-        if constexpr (MODE == 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (pix[u] < 0) break;
+            float o[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                const double q = (double)to_f32<T>(from_f32<T>(o[v]));  // statistics of the stored values
-                fa[v] += q;
-                fb[v] += q * q;
+                float acc = br[v];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) acc = fmaf(in[u][k], wr[v][k], acc);
+                o[v] = acc;
             }
-        } else if constexpr (MODE == 2) {
-            float xb[V];
-            cvt16_f32<T>(yraw, xb);
+            store16_f32(y + (int64_t)pix[u] * CO + c0, o);
+            if constexpr (MODE == 1) {
 #pragma unroll
-            for (int v = 0; v < V; ++v) {
-                const float g = to_f32<T>(from_f32<T>(o[v]));  // the stored gradient
-                const float xh = (xb[v] - bmu[v]) * bis[v];
-                const float dz = g * (xh * bga[v] + bbe[v] > 0.f ? 1.f : 0.01f);
-                fa[v] += dz;
-                fb[v] = fmaf(dz, xh, fb[v]);
+                for (int v = 0; v < V; ++v) {
+                    const float q = to_f32<T>(from_f32<T>(o[v]));  // statistics of the stored values
+                    fa[v] += q;
+                    fb[v] = fmaf(q, q, fb[v]);
+                }
+            } else if constexpr (MODE == 2) {
+                float xb[V];
+                cvt16_f32<T>(yraw[u], xb);
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const float g = to_f32<T>(from_f32<T>(o[v]));  // the stored gradient
+                    const float xh = (xb[v] - bmu[v]) * bis[v];
+                    const float dz = g * (xh * bga[v] + bbe[v] > 0.f ? 1.f : 0.01f);
+                    fa[v] += dz;
+                    fb[v] = fmaf(dz, xh, fb[v]);
+                }
             }
         }
     }
@@ -688,137 +704,139 @@ __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict
 }
 
 // y[b, oh, ow] = bias + sum_ci sum_taps x[b, ih, iw, ci] * w[ci*9 + kh*3 + kw]  (transposed, 1 output channel).
-// (Measured: one thread per output pixel beats one thread per low-res pixel computing the 2 x 2 block, whose
-// long per-accumulator FMA chains leave it latency-bound: 47 vs 61 us at B = 256.)
+// One thread per LOW-RES pixel (r, c) computes its 2 x 2 output block (2r + py, 2c + px): the block reads exactly
+// the 2 x 2 low-res neighbourhood (r..r+1, c..c+1; zero past the image), all of it loaded up front (16 16-byte
+// loads for bf16), and uses each of the 9 taps once: (py, px; dy, dx) -> (kh, kw) with kh = 1 for py = 0, else
+// 0 (dy = 1) / 2 (dy = 0); kw likewise.  Weights sit in LDS as [tap][ci] and are read as float4 broadcasts; each
+// output keeps two accumulators (even / odd channel chunks) to halve its FMA chain.  Stores: two float2 rows.
+// (Supersedes one thread per output pixel, whose per-tap loads waited one round trip each: 47 us at B = 256.)
 template <typename T, int CI>
 __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
-                                                       float* __restrict__ y, FastDiv dWo, FastDiv dHo) {
-    __shared__ float ws[CI * 9];
-    for (int i = threadIdx.x; i < CI * 9; i += blockDim.x) ws[i] = w[i];
+                                                       float* __restrict__ y, FastDiv dWi, FastDiv dHi) {
+    constexpr int V = Vec16<T>::N, NC = CI / V;  // 16-byte chunks per pixel
+    __shared__ __attribute__((aligned(16))) float wt[9 * CI];
+    for (int i = threadIdx.x; i < 9 * CI; i += blockDim.x) {
+        const int tap = i / CI, ci = i - tap * CI;
+        wt[i] = w[ci * 9 + tap];
+    }
     __syncthreads();
     const float b0 = bias ? bias[0] : 0.f;
     const int Ho = 2 * Hi, Wo = 2 * Wi;
-    const int npix = B * Ho * Wo;  // < 2^31 (checked by the launcher)
-    constexpr int V = Vec16<T>::N;
-    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += gridDim.x * blockDim.x) {
-        const int t = (int)dWo.div((uint32_t)p), ow = p - t * Wo;
-        const int b = (int)dHo.div((uint32_t)t), oh = t - b * Ho;
-        int py = oh & 1, px = ow & 1, r = oh >> 1, c = ow >> 1;
-        float s = b0;
-        for (int ty = 0; ty < (py ? 2 : 1); ++ty) {
-            int kh = py ? (ty ? 2 : 0) : 1;
-            int ih = r + ((py && ty == 0) ? 1 : 0);
-            if (ih >= Hi) continue;
-            for (int tx = 0; tx < (px ? 2 : 1); ++tx) {
-                int kw = px ? (tx ? 2 : 0) : 1;
-                int iw = c + ((px && tx == 0) ? 1 : 0);
-                if (iw >= Wi) continue;
-                const T* src = x + (((int64_t)b * Hi + ih) * Wi + iw) * CI;
-                const int tap = kh * 3 + kw;
+    const int nlow = B * Hi * Wi;  // < 2^31 (checked by the launcher)
+    // (out = py * 2 + px, neighbour n = dy * 2 + dx, tap) for the 9 contributions of a 2 x 2 block
+    constexpr int kOut[9] = {0, 1, 1, 2, 2, 3, 3, 3, 3};
+    constexpr int kNb[9] = {0, 0, 1, 0, 2, 0, 1, 2, 3};
+    constexpr int kTap[9] = {4, 5, 3, 7, 1, 8, 6, 2, 0};
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nlow; q += gridDim.x * blockDim.x) {
+        const int t = (int)dWi.div((uint32_t)q), c = q - t * Wi;
+        const int b = (int)dHi.div((uint32_t)t), r = t - b * Hi;
+        const bool okr = r + 1 < Hi, okc = c + 1 < Wi;
+        const T* p00 = x + (int64_t)q * CI;
+        const T* nbp[4] = {p00, okc ? p00 + CI : p00, okr ? p00 + (int64_t)Wi * CI : p00,
+                           (okr && okc) ? p00 + (int64_t)(Wi + 1) * CI : p00};
+        const bool nbok[4] = {true, okc, okr, okr && okc};
+        uint4 raw[4][NC];
 #pragma unroll
-                for (int c0 = 0; c0 < CI; c0 += V) {
-                    float v[V];
-                    load16_f32(src + c0, v);
+        for (int n = 0; n < 4; ++n)
 #pragma unroll
-                    for (int q = 0; q < V; ++q) s = fmaf(v[q], ws[(c0 + q) * 9 + tap], s);
+            for (int j = 0; j < NC; ++j) raw[n][j] = load16_raw(nbp[n] + j * V);
+        float acc[4][2];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) { acc[o][0] = b0; acc[o][1] = 0.f; }
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            float v[4][V];
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+                cvt16_f32<T>(raw[n][j], v[n]);
+#pragma unroll
+                for (int e = 0; e < V; ++e) v[n][e] = nbok[n] ? v[n][e] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const float4* wp = reinterpret_cast<const float4*>(wt + kTap[k] * CI + j * V);
+#pragma unroll
+                for (int e4 = 0; e4 < V / 4; ++e4) {
+                    const float4 wq = wp[e4];
+                    float& a = acc[kOut[k]][j & 1];
+                    a = fmaf(v[kNb[k]][4 * e4 + 0], wq.x, a);
+                    a = fmaf(v[kNb[k]][4 * e4 + 1], wq.y, a);
+                    a = fmaf(v[kNb[k]][4 * e4 + 2], wq.z, a);
+                    a = fmaf(v[kNb[k]][4 * e4 + 3], wq.w, a);
                 }
             }
         }
-        y[p] = s;
+        float* o0 = y + ((int64_t)b * Ho + 2 * r) * Wo + 2 * c;
+        *reinterpret_cast<float2*>(o0) = make_float2(acc[0][0] + acc[0][1], acc[1][0] + acc[1][1]);
+        *reinterpret_cast<float2*>(o0 + Wo) = make_float2(acc[2][0] + acc[2][1], acc[3][0] + acc[3][1]);
     }
 }
 
 // dW[m*9+tap] partials: block = chunk of low-res rows (b,r,c); Xh single-channel high-res [B, 2Hl, 2Wl].
-// Rows are staged in LDS 256 at a time; thread (mg, rg) accumulates a 4(m) x 9(tap) register block over
-// rows rg, rg+32, ... (13 LDS reads per 36 FMAs); the 32 row-groups are combined in a fixed order.
+// Thread (row group rg = tid / 8, channel group cg = tid % 8) accumulates a 4 (m) x 9 (tap) register block over
+// rows k0 + rg, k0 + rg + 32, ... straight from global memory: per row 4 channels of L (8 bytes for bf16; a wave
+// reads 8 whole 64-byte rows) and the row's 9 high-res taps (L1-shared by the 8 channel groups), U rows' loads
+// in flight per step.  The 32 row groups are combined in LDS in a fixed order.  (Supersedes 256-row LDS stages
+// with a barrier each: 45 us at B = 256.)
 template <typename T, int M>
 __global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, int B, int Hl, int Wl,
                                                        const float* __restrict__ Xh, int rows_per_blk,
                                                        float* __restrict__ part, FastDiv dWl, FastDiv dHl) {
-    static_assert(M == 32, "one 8 x 4 channel tiling");
-    constexpr int RC = 256;
-    // one LDS block: [RC][M+1] rows + [RC][9] taps during accumulation, [32][M*9] partials afterwards
-    constexpr int kAcc = RC * (M + 1) + RC * 9, kRed = 32 * M * 9;
-    __shared__ float smem[kAcc > kRed ? kAcc : kRed];
-    float (*Ls)[M + 1] = reinterpret_cast<float (*)[M + 1]>(smem);
-    float (*Hs)[9] = reinterpret_cast<float (*)[9]>(smem + RC * (M + 1));
+    static_assert(M == 32, "8 channel groups of 4");
+    constexpr int U = 4;
+    __shared__ float red[32][M * 9 + 1];
     const int64_t K = (int64_t)B * Hl * Wl;
     const int64_t k0 = (int64_t)blockIdx.x * rows_per_blk, k1 = min(K, k0 + rows_per_blk);
     const int Hh = 2 * Hl, Wh = 2 * Wl;
-    const int mg = threadIdx.x & 7, rg = threadIdx.x >> 3;
+    const int cg = threadIdx.x & 7, rg = threadIdx.x >> 3;
     float acc[4][9];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 9; ++j) acc[i][j] = 0.f;
-    constexpr int V = Vec16<T>::N;
-    constexpr int LPT = RC * (M / V) / 256;  // 16-byte L chunks per thread per row chunk
-    static_assert(RC == 256 && LPT * 256 == RC * (M / V), "one H row and LPT L chunks per thread");
-    // the next row chunk's operands are prefetched into registers while the current one is reduced from LDS
-    uint4 nl[LPT];
-    float nh[9];
-    auto fetch = [&](int64_t kb) {
+    for (int64_t kb = k0 + rg; kb < k1; kb += 32 * U) {
+        float l[U][4], h[U][9];
 #pragma unroll
-        for (int u = 0; u < LPT; ++u) {
-            const int i = threadIdx.x + u * 256, rr = i / (M / V), cg = i % (M / V);
-            const int64_t k = min(kb + rr, k1 - 1);  // clamped (zeroed when stored)
-            nl[u] = load16_raw(L + k * M + cg * V);
+        for (int u = 0; u < U; ++u) {  // every load of the U rows issued before any use
+            const int64_t k = kb + 32 * u;
+            const bool ok = k < k1;
+            const int kk = ok ? (int)k : (int)k0;
+            if constexpr (sizeof(T) == 2) {
+                const uint2 raw = *reinterpret_cast<const uint2*>(L + (int64_t)kk * M + 4 * cg);
+                l[u][0] = __uint_as_float(raw.x << 16);
+                l[u][1] = __uint_as_float(raw.x & 0xffff0000u);
+                l[u][2] = __uint_as_float(raw.y << 16);
+                l[u][3] = __uint_as_float(raw.y & 0xffff0000u);
+            } else {
+                const float4 raw = *reinterpret_cast<const float4*>(L + (int64_t)kk * M + 4 * cg);
+                l[u][0] = raw.x; l[u][1] = raw.y; l[u][2] = raw.z; l[u][3] = raw.w;
+            }
+            const int t = (int)dWl.div((uint32_t)kk), c = kk - t * Wl;
+            const int b = (int)dHl.div((uint32_t)t), r = t - b * Hl;
+            const float* xr = Xh + ((int64_t)b * Hh + 2 * r - 1) * Wh + 2 * c - 1;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int kh = tap / 3, kw = tap % 3;
+                h[u][tap] = (ok && 2 * r - 1 + kh >= 0 && 2 * c - 1 + kw >= 0) ? xr[kh * Wh + kw] : 0.f;
+            }
         }
-        const int64_t kr = kb + threadIdx.x;
-        const int k = (int)min(kr, k1 - 1);
-        const int t = (int)dWl.div((uint32_t)k), c = k - t * Wl;
-        const int b = (int)dHl.div((uint32_t)t), r = t - b * Hl;
-        const float* xr = Xh + ((int64_t)b * Hh + 2 * r - 1) * Wh + 2 * c - 1;
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int ih = 2 * r - 1 + tap / 3, iw = 2 * c - 1 + tap % 3;
-            nh[tap] = (ih >= 0 && iw >= 0) ? xr[(tap / 3) * Wh + tap % 3] : 0.f;
-        }
-    };
-    auto stage = [&](int64_t kb) {
-#pragma unroll
-        for (int u = 0; u < LPT; ++u) {
-            const int i = threadIdx.x + u * 256, rr = i / (M / V), cg = i % (M / V);
-            float v[V];
-            cvt16_f32<T>(nl[u], v);
-            const bool ok = kb + rr < k1;
-#pragma unroll
-            for (int q = 0; q < V; ++q) Ls[rr][cg * V + q] = ok ? v[q] : 0.f;
-        }
-        const bool ok = kb + threadIdx.x < k1;
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) Hs[threadIdx.x][tap] = ok ? nh[tap] : 0.f;
-    };
-    if (k0 < k1) fetch(k0);
-    for (int64_t kb = k0; kb < k1; kb += RC) {
-        stage(kb);
-        __syncthreads();
-        if (kb + RC < k1) fetch(kb + RC);
-        for (int rr = rg; rr < RC; rr += 32) {
-            float l[4], h[9];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) l[i] = Ls[rr][4 * mg + i];
-#pragma unroll
-            for (int j = 0; j < 9; ++j) h[j] = Hs[rr][j];
+        for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 9; ++j) acc[i][j] = fmaf(l[i], h[j], acc[i][j]);
-        }
-        __syncthreads();
+                for (int j = 0; j < 9; ++j) acc[i][j] = fmaf(l[u][i], h[u][j], acc[i][j]);
     }
-    // combine the 32 row-groups: stage [rg][m*9+tap] in LDS (reuses Ls), then fixed-order sums
-    float* red = smem;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 9; ++j) red[rg * (M * 9) + (4 * mg + i) * 9 + j] = acc[i][j];
+        for (int j = 0; j < 9; ++j) red[rg][(4 * cg + i) * 9 + j] = acc[i][j];
     __syncthreads();
     for (int o = threadIdx.x; o < M * 9; o += blockDim.x) {
-        float s = 0.f;
-        for (int g = 0; g < 32; ++g) s += red[g * (M * 9) + o];
-        part[(int64_t)blockIdx.x * M * 9 + o] = s;
+        float v = 0.f;
+        for (int g = 0; g < 32; ++g) v += red[g][o];
+        part[(int64_t)blockIdx.x * (M * 9) + o] = v;
     }
 }
 
@@ -1415,8 +1433,9 @@ int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const flo
     HLMC_CHECK_ARG(Ci == 32, "convT_c1: only Ci == 32");
     int64_t npix = (int64_t)B * 4 * Hi * Wi;
     HLMC_CHECK_ARG(npix < (int64_t)1 << 31, "convT_c1: too many pixels");
-    const FastDiv dW((uint32_t)(2 * Wi)), dH((uint32_t)(2 * Hi));
-    convT_c1_kernel<T, 32><<<grid_for(npix), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH);
+    HLMC_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "convT_c1: alignment");
+    const FastDiv dW((uint32_t)Wi), dH((uint32_t)Hi);
+    convT_c1_kernel<T, 32><<<grid_for(npix / 4, kThreads, 16384), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -206,6 +206,23 @@ struct SubpixelWeight {
 //                (m % 4 == 0, the MFMA C/D row group of a lane); float put(const Quad&, r, n, v) stores
 //                row m+r, column n of v (= accumulator + colbias) and returns the stored value as float.
 //   split-K reduce (per element): set_phase(p); Row row(int m); store(const Row&, int n, float v).
+// 4 consecutive outputs rounded to OutT and stored with one 8-byte (bf16) / 16-byte (f32) store; v <- the stored values
+template <typename OutT>
+__device__ __forceinline__ void store4_round(OutT* p, float (&v)[4]) {
+    if constexpr (sizeof(OutT) == 4) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+        unsigned h[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bf16 t = __float2bfloat16(v[k]);
+            h[k] = *reinterpret_cast<unsigned short*>(&t);
+            v[k] = __uint_as_float(h[k] << 16);
+        }
+        *reinterpret_cast<uint2*>(p) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    }
+}
+
 // Row-major store with bias, activation, optional accumulate:  out[m*ld + n] (+)= act(v + bias[n])
 // act: 0 none, 1 relu
 template <typename OutT>
@@ -231,6 +248,16 @@ struct StoreRM {
         const OutT t = from_f32<OutT>(v);
         *o = t;
         return to_f32<OutT>(t);
+    }
+    // columns n..n+3 of row offset ro in one vector store (v: accumulators + bias; <- the stored values)
+    __device__ void put4(int64_t ro, int n, float (&v)[4]) const {
+        OutT* o = out + ro + n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (act == 1) v[k] = v[k] > 0.f ? v[k] : 0.f;
+            if (accumulate) v[k] += to_f32<OutT>(o[k]);
+        }
+        store4_round<OutT>(o, v);
     }
     // the value store() writes (without accumulate), as float: for the fused column statistics
     __device__ float stored(int n, float v) const {
@@ -281,6 +308,7 @@ struct StoreSubpixel {
         out[ro + n] = t;
         return to_f32<OutT>(t);
     }
+    __device__ void put4(int64_t ro, int n, float (&v)[4]) const { store4_round<OutT>(out + ro + n, v); }
     __device__ float stored(int n, float v) const {
         if (bias) v += bias[n];
         return to_f32<OutT>(from_f32<OutT>(v));
@@ -331,6 +359,9 @@ struct StorePartial {
         ws[ro + n] = v;
         return v;
     }
+    __device__ void put4(int64_t ro, int n, float (&v)[4]) const {
+        *reinterpret_cast<float4*>(ws + ro + n) = make_float4(v[0], v[1], v[2], v[3]);
+    }
 };
 
 // Store one wave's TM x TN grid of 16x16 accumulator tiles through the epilogue (C/D map: col = lane & 15,
@@ -370,6 +401,104 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
     }
 }
 
+// The same for accumulators computed with the operands swapped (mfma(B fragment, A fragment)): acc[i][j] holds the
+// 16 x 16 tile (columns nb + j*16 .., rows mb + i*16 ..) TRANSPOSED, i.e. lane l has columns nb + j*16 + 4*(l >> 4)
+// + 0..3 of row mb + i*16 + (l & 15).  Each lane stores its 4 consecutive columns with one vector store (put4: 8 bytes
+// for bf16) instead of 4 scalar 2-byte stores, so an NHWC output tile costs a quarter of the store instructions.
+// kStatMode 1: per-column sums / sums of squares of the stored values, reduced over the 16 rows of each lane group
+// (xor shuffles) -> cs / cq [j][k] hold the totals of column nb + j*16 + 4*(lane >> 4) + k in every lane.
+template <int TM, int TN, class EP>
+__device__ __forceinline__ void epilogue_tile_t(const EP& ep, const f32x4_t (&acc)[TM][TN], int mb, int nb, int lane,
+                                                int M, int N, double (&cs)[TN][4], double (&cq)[TN][4]) {
+    float bias[TN][4];
+    int n4[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        n4[j] = nb + j * 16 + 4 * (lane >> 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bias[j][k] = n4[j] + k < N ? ep.colbias(n4[j] + k) : 0.f;
+            cs[j][k] = 0.0;
+            cq[j][k] = 0.0;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = mb + i * 16 + (lane & 15);
+        if (m >= M) continue;
+        const int64_t ro = ep.row_off(ep.quad(m), 0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            if (n4[j] >= N) continue;  // N % 4 == 0 (checked by the launcher)
+            float v[4] = {acc[i][j][0] + bias[j][0], acc[i][j][1] + bias[j][1], acc[i][j][2] + bias[j][2],
+                          acc[i][j][3] + bias[j][3]};
+            ep.put4(ro, n4[j], v);
+            if constexpr (EP::kStatMode == 1) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    cs[j][k] += v[k];
+                    cq[j][k] += (double)v[k] * v[k];
+                }
+            }
+        }
+    }
+    if constexpr (EP::kStatMode == 1) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    cs[j][k] += __shfl_xor(cs[j][k], o, 64);
+                    cq[j][k] += __shfl_xor(cq[j][k], o, 64);
+                }
+    }
+}
+
+// A wave's per-column statistics (its rows) into the block scratch sred[(wmi * 2 + {0, 1}) * BN + column] for the
+// column strip wn0 .. wn0 + 16 TN: TR = false from epilogue_tile's per-lane sums (xor over the 4 row groups),
+// TR = true from epilogue_tile_t's already-reduced totals.
+template <bool TR, int TN, int BN>
+__device__ __forceinline__ void stats_to_lds(const double* cs, const double* cq, double* sred, int wmi, int wn0,
+                                             int lane) {
+    if constexpr (TR) {
+        if ((lane & 15) == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    sred[(wmi * 2 + 0) * BN + wn0 + j * 16 + 4 * (lane >> 4) + k] = cs[j * 4 + k];
+                    sred[(wmi * 2 + 1) * BN + wn0 + j * 16 + 4 * (lane >> 4) + k] = cq[j * 4 + k];
+                }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            double a = cs[j], q = cq[j];
+            a += __shfl_xor(a, 16, 64);
+            q += __shfl_xor(q, 16, 64);
+            a += __shfl_xor(a, 32, 64);
+            q += __shfl_xor(q, 32, 64);
+            if (lane < 16) {
+                sred[(wmi * 2 + 0) * BN + wn0 + j * 16 + lane] = a;
+                sred[(wmi * 2 + 1) * BN + wn0 + j * 16 + lane] = q;
+            }
+        }
+    }
+}
+// one MFMA step of a wave's TM x TN tile grid: TR = true swaps the operands (transposed accumulators,
+// epilogue_tile_t), else the row-per-lane-group layout of epilogue_tile
+template <bool TR>
+__device__ __forceinline__ f32x4_t mfma_bf16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+    if constexpr (TR) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <bool TR>
+__device__ __forceinline__ f32x4_t mfma_f32(float a, float b, const f32x4_t& c) {
+    if constexpr (TR) return __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
 // Block coordinates of the NT kernels after the XCD remap: logical id -> (phase fastest, then tile, then
 // K-split), so the phases and N-tiles of one M-tile (which gather the same A rows) run on one XCD.
 #define NT_BLOCK_COORDS()                                                                                  \
@@ -397,7 +526,7 @@ __device__ __forceinline__ int nt_lds_chunk(int row, int c) {
 // ploop > 1: the grid has one y-slice and every block runs all ploop phases of its tile in turn (the sub-pixel
 // phases of one M-tile gather overlapping low-res rows: the later phases find them in L2 instead of every
 // phase's blocks streaming the whole input again).
-template <typename T, int BM, int BN, int WM, int WN, int KCH, class AL, class BL, class EP>
+template <typename T, int BM, int BN, int WM, int WN, int KCH, class AL, class BL, class EP, bool TR = false>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap,
                                                       int ploop) {
     constexpr int V = Vec16<T>::N;
@@ -490,7 +619,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = mfma_bf16<TR>(af[i], bfr[j], acc[i][j]);
             }
         } else {
 #pragma unroll
@@ -510,7 +639,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = mfma_f32<TR>(af[i], bfr[j], acc[i][j]);
             }
         }
     };
@@ -528,27 +657,19 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
             __syncthreads();
         }
     }
-    double cs[TN], cq[TN];
-    epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
+    double cs[TR ? TN * 4 : TN], cq[TR ? TN * 4 : TN];
+    if constexpr (TR)
+        epilogue_tile_t<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N,
+                                *reinterpret_cast<double(*)[TN][4]>(cs), *reinterpret_cast<double(*)[TN][4]>(cq));
+    else
+        epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
     if constexpr (EP::kStatMode != 0) {
-        // per-column sum / sum of squares of the stored values over the block's rows: lane sums over its
-        // 4*TM rows (epilogue_tile), xor-16/32 shuffles over the wave's row groups, then the waves of one
-        // column strip in order
+        // per-column sum / sum of squares of the stored values over the block's rows: the wave's column totals
+        // (stats_to_lds), then the waves of one column strip in order
         constexpr int WAVES_M = BM / WM;
         __shared__ double sred[WAVES_M][2][BN];
         const int wmi = wave / WAVES_N;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            double a = cs[j], q = cq[j];
-            a += __shfl_xor(a, 16, 64);
-            q += __shfl_xor(q, 16, 64);
-            a += __shfl_xor(a, 32, 64);
-            q += __shfl_xor(q, 32, 64);
-            if (lane < 16) {
-                sred[wmi][0][wn0 + j * 16 + lane] = a;
-                sred[wmi][1][wn0 + j * 16 + lane] = q;
-            }
-        }
+        stats_to_lds<TR, TN, BN>(cs, cq, &sred[0][0][0], wmi, wn0, lane);
         __syncthreads();
         const int row = ph * ep.mtiles + tile_m_;
         for (int c = tid; c < BN; c += 256) {
@@ -594,7 +715,7 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
                                      (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, class AL, class BL, class EP>
+template <typename T, int BM, int BN, int WM, int WN, int NS, class AL, class BL, class EP, bool TR = false>
 __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = 8 * V;                       // 128-byte tile rows
@@ -670,7 +791,7 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = mfma_bf16<TR>(af[i], bfr[j], acc[i][j]);
             }
         } else {
 #pragma unroll
@@ -691,30 +812,23 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = mfma_f32<TR>(af[i], bfr[j], acc[i][j]);
             }
         }
     }
-    double cs[TN], cq[TN];
-    epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
+    double cs[TR ? TN * 4 : TN], cq[TR ? TN * 4 : TN];
+    if constexpr (TR)
+        epilogue_tile_t<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N,
+                                *reinterpret_cast<double(*)[TN][4]>(cs), *reinterpret_cast<double(*)[TN][4]>(cq));
+    else
+        epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
     if constexpr (EP::kStatMode != 0) {
         constexpr int WAVES_M = BM / WM;
         static_assert(WAVES_M * 2 * BN * 8 <= NS * STG, "stats scratch fits the staging ring");
         __syncthreads();  // every wave is done with the ring: reuse it for the column-sum scratch
         double* sred = reinterpret_cast<double*>(smem);  // [WAVES_M][2][BN]
         const int wmi = wave / WAVES_N;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            double a = cs[j], q = cq[j];
-            a += __shfl_xor(a, 16, 64);
-            q += __shfl_xor(q, 16, 64);
-            a += __shfl_xor(a, 32, 64);
-            q += __shfl_xor(q, 32, 64);
-            if (lane < 16) {
-                sred[(wmi * 2 + 0) * BN + wn0 + j * 16 + lane] = a;
-                sred[(wmi * 2 + 1) * BN + wn0 + j * 16 + lane] = q;
-            }
-        }
+        stats_to_lds<TR, TN, BN>(cs, cq, sred, wmi, wn0, lane);
         __syncthreads();
         const int prow = phase * ep.mtiles + tile_m_;
         for (int c = tid; c < BN; c += 256) {

@@ -105,27 +105,43 @@ inline bool use_ploop(int phases, int tmn, int pipe, bool with_stats) {
     return mode == 2 || tmn >= min_tiles;
 }
 
-template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class E>
-void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
-                      bool long_k, int pipe) {
+// TR: transposed accumulators + 4-column vector stores (epilogue_tile_t; needs N % 4 == 0 and 4-aligned row
+// strides: the conv / sub-pixel NHWC outputs and their split-K slabs), else the per-element epilogue (linears)
+template <typename T, int BM, int BN, int WM, int WN, bool TR, class AL, class BL, class E>
+void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
+                         bool long_k, int pipe) {
     const int rm = xcd_remap_for_site();
     const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe, E::kStatMode == 1) ? (int)grid.y : 1;
     if (ploop > 1) grid.y = 1;
     HLMC_PROBE_BEGIN(s);
     if (pipe == 3)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (pipe == 4)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (long_k)
-        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     else
-        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     HLMC_PROBE_END(s);
+}
+template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class E>
+void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
+                      bool long_k, int pipe, bool tr) {
+    if (tr) nt_kernel_launch_tr<T, BM, BN, WM, WN, true>(s, grid, al, bl, ep, M, N, ksl, long_k, pipe);
+    else nt_kernel_launch_tr<T, BM, BN, WM, WN, false>(s, grid, al, bl, ep, M, N, ksl, long_k, pipe);
+}
+// HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid)
+inline bool nt_tr_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HLMC_NT_TR");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
 int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
-              ops::ColStats* st = nullptr, bool dma_ok = true) {
+              ops::ColStats* st = nullptr, bool dma_ok = true, bool tr = false) {
     constexpr int BK = gemm_bk<T>();
     const int tmn = cdiv(M, BM) * cdiv(N, BN);
     Plan pl = plan_nt(tmn * phases, Kmax, BK);
@@ -139,13 +155,13 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
         static_cast<EP&>(eps) = ep;
         eps.part = st->part;
         eps.mtiles = cdiv(M, BM);
-        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, eps, M, N, pl.ksl, long_k, pipe);
+        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, eps, M, N, pl.ksl, long_k, pipe, tr);
         HLMC_LAUNCHED();
         st->nparts = phases * cdiv(M, BM);
         return HLMC_OK;
     }
     if (pl.S == 1) {
-        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, ep, M, N, pl.ksl, long_k, pipe);
+        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, ep, M, N, pl.ksl, long_k, pipe, tr);
         HLMC_LAUNCHED();
         return HLMC_OK;
     }
@@ -153,7 +169,7 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "split-K workspace too small");
     StorePartialZ part;
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
-    nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe);
+    nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe, tr);
     HLMC_LAUNCHED();
     int64_t total = (int64_t)phases * M * N;
     int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
@@ -180,11 +196,12 @@ inline int nt_tile(int M, int N, int phases) {
 template <typename T, class AL, class BL, class EP>
 int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
                 ops::ColStats* st = nullptr) {
+    const bool tr = nt_tr_enabled() && N % 4 == 0;  // conv / sub-pixel outputs: NHWC rows of N channels
     switch (nt_tile(M, N, phases)) {
-        case 0: return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true);
-        case 1: return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true);
-        case 2: return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true);
-        default: return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true);
+        case 0: return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, tr);
+        case 1: return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, tr);
+        case 2: return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, tr);
+        default: return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, tr);
     }
 }
 template <typename T>
@@ -397,27 +414,24 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < TN; ++j)  // operands swapped: channels x pixels (epilogue_tile_t)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
             }
         }
-        double cs[TN], cq[TN];
-        epilogue_tile<TM, TN>(ep, acc, t * TP + wm0, n0 + wn0, lane, M, CO, cs, cq);
+        double cs[TN][4], cq[TN][4];
+        epilogue_tile_t<TM, TN>(ep, acc, t * TP + wm0, n0 + wn0, lane, M, CO, cs, cq);
         if constexpr (EP::kStatMode == 1) {
             constexpr int WAVES_M = 4 / WAVES_N;
             __shared__ double sred[WAVES_M][2][COB];
             const int wmi = wave / WAVES_N;
+            if ((lane & 15) == 0) {
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                double a = cs[j], q = cq[j];
-                a += __shfl_xor(a, 16, 64);
-                q += __shfl_xor(q, 16, 64);
-                a += __shfl_xor(a, 32, 64);
-                q += __shfl_xor(q, 32, 64);
-                if (lane < 16) {
-                    sred[wmi][0][wn0 + j * 16 + lane] = a;
-                    sred[wmi][1][wn0 + j * 16 + lane] = q;
-                }
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        sred[wmi][0][wn0 + j * 16 + 4 * (lane >> 4) + k] = cs[j][k];
+                        sred[wmi][1][wn0 + j * 16 + 4 * (lane >> 4) + k] = cq[j][k];
+                    }
             }
             __syncthreads();
             for (int c = tid; c < COB; c += 256) {
@@ -534,28 +548,25 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
 #pragma unroll
                         for (int i = 0; i < TM; ++i)
 #pragma unroll
-                            for (int j = 0; j < TN; ++j)
-                                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                            for (int j = 0; j < TN; ++j)  // operands swapped: channels x pixels (epilogue_tile_t)
+                                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
                     }
                 }
             }
             EP e = ep;
             e.set_phase(ph);
-            double cs[TN], cq[TN];
-            epilogue_tile<TM, TN>(e, acc, t * TP + wm0, n0, lane, M, CO, cs, cq);
+            double cs[TN][4], cq[TN][4];
+            epilogue_tile_t<TM, TN>(e, acc, t * TP + wm0, n0, lane, M, CO, cs, cq);
             if constexpr (EP::kStatMode == 1) {
                 __shared__ double sred[4][2][COB];
+                if ((lane & 15) == 0) {
 #pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    double a = cs[j], q = cq[j];
-                    a += __shfl_xor(a, 16, 64);
-                    q += __shfl_xor(q, 16, 64);
-                    a += __shfl_xor(a, 32, 64);
-                    q += __shfl_xor(q, 32, 64);
-                    if (lane < 16) {
-                        sred[wave][0][j * 16 + lane] = a;
-                        sred[wave][1][j * 16 + lane] = q;
-                    }
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            sred[wave][0][j * 16 + 4 * (lane >> 4) + k] = cs[j][k];
+                            sred[wave][1][j * 16 + 4 * (lane >> 4) + k] = cq[j][k];
+                        }
                 }
                 __syncthreads();
                 const int row = ph * ep.mtiles + t;

@@ -407,9 +407,14 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
 // for bf16) instead of 4 scalar 2-byte stores, so an NHWC output tile costs a quarter of the store instructions.
 // kStatMode 1: per-column sums / sums of squares of the stored values, reduced over the 16 rows of each lane group
 // (xor shuffles) -> cs / cq [j][k] hold the totals of column nb + j*16 + 4*(lane >> 4) + k in every lane.
-template <int TM, int TN, class EP>
+// F32RED: the per-lane sums (<= TM bf16-exact values and their squares) and the 16-lane shuffle tree in f32 (one
+// DPP / swizzle step per value instead of two plus an f64 add), widened to f64 afterwards — for the bf16-only halo
+// kernels; the generic kernels (fp32 parity mode too) keep f64 throughout.
+template <int TM, int TN, class EP, bool F32RED = false>
 __device__ __forceinline__ void epilogue_tile_t(const EP& ep, const f32x4_t (&acc)[TM][TN], int mb, int nb, int lane,
                                                 int M, int N, double (&cs)[TN][4], double (&cq)[TN][4]) {
+    using Acc = typename std::conditional<F32RED, float, double>::type;
+    Acc as[TN][4], aq[TN][4];
     float bias[TN][4];
     int n4[TN];
 #pragma unroll
@@ -418,8 +423,8 @@ __device__ __forceinline__ void epilogue_tile_t(const EP& ep, const f32x4_t (&ac
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             bias[j][k] = n4[j] + k < N ? ep.colbias(n4[j] + k) : 0.f;
-            cs[j][k] = 0.0;
-            cq[j][k] = 0.0;
+            as[j][k] = Acc(0);
+            aq[j][k] = Acc(0);
         }
     }
 #pragma unroll
@@ -436,23 +441,26 @@ __device__ __forceinline__ void epilogue_tile_t(const EP& ep, const f32x4_t (&ac
             if constexpr (EP::kStatMode == 1) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    cs[j][k] += v[k];
-                    cq[j][k] += (double)v[k] * v[k];
+                    as[j][k] += Acc(v[k]);
+                    aq[j][k] += Acc(v[k]) * Acc(v[k]);
                 }
             }
         }
     }
-    if constexpr (EP::kStatMode == 1) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
+        for (int k = 0; k < 4; ++k) {
+            if constexpr (EP::kStatMode == 1) {
 #pragma unroll
                 for (int o = 1; o < 16; o <<= 1) {
-                    cs[j][k] += __shfl_xor(cs[j][k], o, 64);
-                    cq[j][k] += __shfl_xor(cq[j][k], o, 64);
+                    as[j][k] += __shfl_xor(as[j][k], o, 64);
+                    aq[j][k] += __shfl_xor(aq[j][k], o, 64);
                 }
-    }
+            }
+            cs[j][k] = (double)as[j][k];
+            cq[j][k] = (double)aq[j][k];
+        }
 }
 
 // A wave's per-column statistics (its rows) into the block scratch sred[(wmi * 2 + {0, 1}) * BN + column] for the

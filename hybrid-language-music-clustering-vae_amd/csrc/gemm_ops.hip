@@ -124,12 +124,6 @@ void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, c
         gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     HLMC_PROBE_END(s);
 }
-template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class E>
-void nt_kernel_launch(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
-                      bool long_k, int pipe, bool tr) {
-    if (tr) nt_kernel_launch_tr<T, BM, BN, WM, WN, true>(s, grid, al, bl, ep, M, N, ksl, long_k, pipe);
-    else nt_kernel_launch_tr<T, BM, BN, WM, WN, false>(s, grid, al, bl, ep, M, N, ksl, long_k, pipe);
-}
 // HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid)
 inline bool nt_tr_enabled() {
     static const bool on = [] {
@@ -139,9 +133,9 @@ inline bool nt_tr_enabled() {
     return on;
 }
 
-template <typename T, int BM, int BN, int WM, int WN, class AL, class BL, class EP>
+template <typename T, int BM, int BN, int WM, int WN, bool TR, class AL, class BL, class EP>
 int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
-              ops::ColStats* st = nullptr, bool dma_ok = true, bool tr = false) {
+              ops::ColStats* st = nullptr, bool dma_ok = true) {
     constexpr int BK = gemm_bk<T>();
     const int tmn = cdiv(M, BM) * cdiv(N, BN);
     Plan pl = plan_nt(tmn * phases, Kmax, BK);
@@ -155,13 +149,13 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
         static_cast<EP&>(eps) = ep;
         eps.part = st->part;
         eps.mtiles = cdiv(M, BM);
-        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, eps, M, N, pl.ksl, long_k, pipe, tr);
+        nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, eps, M, N, pl.ksl, long_k, pipe);
         HLMC_LAUNCHED();
         st->nparts = phases * cdiv(M, BM);
         return HLMC_OK;
     }
     if (pl.S == 1) {
-        nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, ep, M, N, pl.ksl, long_k, pipe, tr);
+        nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, ep, M, N, pl.ksl, long_k, pipe);
         HLMC_LAUNCHED();
         return HLMC_OK;
     }
@@ -169,7 +163,7 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "split-K workspace too small");
     StorePartialZ part;
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
-    nt_kernel_launch<T, BM, BN, WM, WN>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe, tr);
+    nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe);
     HLMC_LAUNCHED();
     int64_t total = (int64_t)phases * M * N;
     int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
@@ -196,12 +190,18 @@ inline int nt_tile(int M, int N, int phases) {
 template <typename T, class AL, class BL, class EP>
 int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
                 ops::ColStats* st = nullptr) {
-    const bool tr = nt_tr_enabled() && N % 4 == 0;  // conv / sub-pixel outputs: NHWC rows of N channels
+    // conv / sub-pixel outputs are NHWC rows of N (a multiple of 8) channels: transposed-accumulator epilogue
+    if (nt_tr_enabled() && N % 4 == 0) {
+        switch (nt_tile(M, N, phases)) {
+            case 0: return launch_nt<T, 128, 128, 64, 64, true>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+            case 1: return launch_nt<T, 128, 64, 32, 64, true>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+            default: return launch_nt<T, 128, 32, 32, 32, true>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+        }
+    }
     switch (nt_tile(M, N, phases)) {
-        case 0: return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, tr);
-        case 1: return launch_nt<T, 128, 64, 32, 64>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, tr);
-        case 2: return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, tr);
-        default: return launch_nt<T, 128, 32, 32, 32>(s, al, bl, ep, M, N, Kmax, phases, ws, st, true, tr);
+        case 0: return launch_nt<T, 128, 128, 64, 64, false>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+        case 1: return launch_nt<T, 128, 64, 32, 64, false>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
+        default: return launch_nt<T, 128, 32, 32, 32, false>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
     }
 }
 template <typename T>
@@ -219,8 +219,8 @@ size_t dispatch_nt_ws(int M, int N, int Kmax, int phases) {
 template <typename T, class AL, class BL, class EP>
 int dispatch_linear(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int K, Ws ws) {
     // register path: arbitrary ld / K (the DMA path needs 16-byte chunks that never straddle K)
-    if (M >= 1024 && N >= 128) return launch_nt<T, 128, 128, 64, 64>(s, al, bl, ep, M, N, K, 1, ws, nullptr, false);
-    return launch_nt<T, 64, 64, 32, 32>(s, al, bl, ep, M, N, K, 1, ws, nullptr, false);
+    if (M >= 1024 && N >= 128) return launch_nt<T, 128, 128, 64, 64, false>(s, al, bl, ep, M, N, K, 1, ws, nullptr, false);
+    return launch_nt<T, 64, 64, 32, 32, false>(s, al, bl, ep, M, N, K, 1, ws, nullptr, false);
 }
 template <typename T>
 size_t dispatch_linear_ws(int M, int N, int K) {
@@ -334,7 +334,7 @@ inline int log2_exact(int c) { return (c > 0 && (c & (c - 1)) == 0) ? __builtin_
 // Template: CI input channels, COB output channels per block (NSPL blocks share a tile's Co = NSPL * COB), WO
 // output width, ROWS output rows per tile (TP = ROWS * WO pixels), DB: double-buffered halo (else one buffer and
 // an extra barrier).  Shapes: 2 WO * CI / 8 == 256 (one 16-byte chunk per thread per input row).
-template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP>
+template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP, bool TR = true>
 __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
                                                            const bf16* __restrict__ wp, EP ep, int M) {
     constexpr int WI = 2 * WO, HR = 2 * ROWS + 1, HC = WI + 1, PS = CI + 8;  // halo rows / cols / pixel pitch
@@ -414,25 +414,22 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < TN; ++j)  // operands swapped: channels x pixels (epilogue_tile_t)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < TN; ++j)  // TR: operands swapped, channels x pixels (epilogue_tile_t)
+                        acc[i][j] = mfma_bf16<TR>(af[i], bfr[j], acc[i][j]);
             }
         }
-        double cs[TN][4], cq[TN][4];
-        epilogue_tile_t<TM, TN>(ep, acc, t * TP + wm0, n0 + wn0, lane, M, CO, cs, cq);
+        double cs[TR ? TN * 4 : TN], cq[TR ? TN * 4 : TN];
+        if constexpr (TR)
+            epilogue_tile_t<TM, TN, EP, true>(ep, acc, t * TP + wm0, n0 + wn0, lane, M, CO,
+                                              *reinterpret_cast<double(*)[TN][4]>(cs),
+                                              *reinterpret_cast<double(*)[TN][4]>(cq));
+        else
+            epilogue_tile<TM, TN>(ep, acc, t * TP + wm0, n0 + wn0, lane, M, CO, cs, cq);
         if constexpr (EP::kStatMode == 1) {
             constexpr int WAVES_M = 4 / WAVES_N;
             __shared__ double sred[WAVES_M][2][COB];
             const int wmi = wave / WAVES_N;
-            if ((lane & 15) == 0) {
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        sred[wmi][0][wn0 + j * 16 + 4 * (lane >> 4) + k] = cs[j][k];
-                        sred[wmi][1][wn0 + j * 16 + 4 * (lane >> 4) + k] = cq[j][k];
-                    }
-            }
+            stats_to_lds<TR, TN, COB>(cs, cq, &sred[0][0][0], wmi, wn0, lane);
             __syncthreads();
             for (int c = tid; c < COB; c += 256) {
                 double a = 0.0, q = 0.0;
@@ -464,7 +461,7 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
 // 4 phases' taps (1 + 2 + 2 + 4) read their fragments from there.
 // Template: CI input channels, COB output channels per block (NSPL blocks per tile), WI low-res width, ROWS
 // low-res rows per tile (TP = ROWS * WI = 128 pixels), DB: double-buffered halo.  WI * CI / 8 == 256.
-template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP>
+template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP, bool TR = true>
 __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
                                                             const bf16* __restrict__ wp, EP ep, int M) {
     constexpr int HR = ROWS + 1, HC = WI + 1, PS = CI + 8, CPP = CI / 8, TP = ROWS * WI;
@@ -548,26 +545,23 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
 #pragma unroll
                         for (int i = 0; i < TM; ++i)
 #pragma unroll
-                            for (int j = 0; j < TN; ++j)  // operands swapped: channels x pixels (epilogue_tile_t)
-                                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+                            for (int j = 0; j < TN; ++j)  // TR: operands swapped (epilogue_tile_t)
+                                acc[i][j] = mfma_bf16<TR>(af[i], bfr[j], acc[i][j]);
                     }
                 }
             }
             EP e = ep;
             e.set_phase(ph);
-            double cs[TN][4], cq[TN][4];
-            epilogue_tile_t<TM, TN>(e, acc, t * TP + wm0, n0, lane, M, CO, cs, cq);
+            double cs[TR ? TN * 4 : TN], cq[TR ? TN * 4 : TN];
+            if constexpr (TR)
+                epilogue_tile_t<TM, TN, EP, true>(e, acc, t * TP + wm0, n0, lane, M, CO,
+                                                  *reinterpret_cast<double(*)[TN][4]>(cs),
+                                                  *reinterpret_cast<double(*)[TN][4]>(cq));
+            else
+                epilogue_tile<TM, TN>(e, acc, t * TP + wm0, n0, lane, M, CO, cs, cq);
             if constexpr (EP::kStatMode == 1) {
                 __shared__ double sred[4][2][COB];
-                if ((lane & 15) == 0) {
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            sred[wave][0][j * 16 + 4 * (lane >> 4) + k] = cs[j][k];
-                            sred[wave][1][j * 16 + 4 * (lane >> 4) + k] = cq[j][k];
-                        }
-                }
+                stats_to_lds<TR, TN, COB>(cs, cq, &sred[0][0][0], wave, 0, lane);
                 __syncthreads();
                 const int row = ph * ep.mtiles + t;
                 for (int c = tid; c < COB; c += 256) {
@@ -637,12 +631,17 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
+        const bool tr = nt_tr_enabled();
         if (halo && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0)
-            return run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>>,
-                       conv_s2_halo_kernel<32, 64, 1, 32, 4, true, WithStats<StoreRM<T>>>, 128, 1);
+            return tr ? run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, true>,
+                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, WithStats<StoreRM<T>>, true>, 128, 1)
+                      : run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, false>,
+                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, WithStats<StoreRM<T>>, false>, 128, 1);
         if (halo2 && Ci == 64 && Co == 128 && Wi == 32 && Hi % 8 == 0)
-            return run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>>,
-                       conv_s2_halo_kernel<64, 64, 2, 16, 4, false, WithStats<StoreRM<T>>>, 64, 2);
+            return tr ? run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, true>,
+                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, WithStats<StoreRM<T>>, true>, 64, 2)
+                      : run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, false>,
+                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, WithStats<StoreRM<T>>, false>, 64, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
 }
@@ -697,12 +696,17 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
+        const bool tr = nt_tr_enabled();
         if (halo && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0)
-            return run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>>,
-                       subpixel_halo_kernel<64, 32, 1, 32, 4, true, WithStats<StoreSubpixel<T>>>, 1);
+            return tr ? run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, true>,
+                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, WithStats<StoreSubpixel<T>>, true>, 1)
+                      : run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, false>,
+                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, WithStats<StoreSubpixel<T>>, false>, 1);
         if (halo2 && Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0)
-            return run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>>,
-                       subpixel_halo_kernel<128, 32, 2, 16, 8, false, WithStats<StoreSubpixel<T>>>, 2);
+            return tr ? run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>, true>,
+                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, WithStats<StoreSubpixel<T>>, true>, 2)
+                      : run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>, false>,
+                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, WithStats<StoreSubpixel<T>>, false>, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
 }

@@ -610,8 +610,9 @@ struct C1Fuse {
     const void* ybn = nullptr;
     const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
 };
+// (launch bounds: >= 4 waves per SIMD, 3 in MODE 2; unbounded, hipcc hoisted enough to leave one wave per SIMD)
 template <typename T, int CO, int MODE>
-__global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
+__global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
                                                          const float* __restrict__ w, const float* __restrict__ bias,
                                                          T* __restrict__ y, FastDiv dWo, FastDiv dHo, C1Fuse fz) {
     constexpr int V = Vec16<T>::N, G = CO / V;  // threads per pixel
@@ -710,8 +711,10 @@ __global__ __launch_bounds__(256) void conv_c1_s2_kernel(const float* __restrict
 // 0 (dy = 1) / 2 (dy = 0); kw likewise.  Weights sit in LDS as [tap][ci] and are read as float4 broadcasts; each
 // output keeps two accumulators (even / odd channel chunks) to halve its FMA chain.  Stores: two float2 rows.
 // (Supersedes one thread per output pixel, whose per-tap loads waited one round trip each: 47 us at B = 256.)
+// (launch bounds: >= 4 waves per SIMD; unbounded, hipcc hoisted every LDS weight read out of the pixel loop into
+// 450 registers -> one wave per SIMD)
 template <typename T, int CI>
-__global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
+__global__ __launch_bounds__(256, 4) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
                                                        float* __restrict__ y, FastDiv dWi, FastDiv dHi) {
     constexpr int V = Vec16<T>::N, NC = CI / V;  // 16-byte chunks per pixel
@@ -780,7 +783,7 @@ __global__ __launch_bounds__(256) void convT_c1_kernel(const T* __restrict__ x, 
 // in flight per step.  The 32 row groups are combined in LDS in a fixed order.  (Supersedes 256-row LDS stages
 // with a barrier each: 45 us at B = 256.)
 template <typename T, int M>
-__global__ __launch_bounds__(256) void wgrad_c1_kernel(const T* __restrict__ L, int B, int Hl, int Wl,
+__global__ __launch_bounds__(256, 4) void wgrad_c1_kernel(const T* __restrict__ L, int B, int Hl, int Wl,
                                                        const float* __restrict__ Xh, int rows_per_blk,
                                                        float* __restrict__ part, FastDiv dWl, FastDiv dHl) {
     static_assert(M == 32, "8 channel groups of 4");
@@ -1394,8 +1397,9 @@ int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float*
     return HLMC_OK;
 }
 
+// partial rows conv_c1_s2 writes with st / bf: its grid, for either dtype (8 threads per pixel for f32, 4 for bf16)
 int conv_c1_fused_rows(int B, int Hi, int Wi) {
-    return grid_for((int64_t)B * (Hi / 2) * (Wi / 2) * 4, kThreads, kC1FusedBlocks);
+    return grid_for((int64_t)B * (Hi / 2) * (Wi / 2) * 8, kThreads, kC1FusedBlocks);
 }
 
 template <typename T>

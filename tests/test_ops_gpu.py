@@ -257,8 +257,9 @@ def test_conv_s2_bench_shapes_bf16(cuda, ws, Hi, Wi, Ci, Co):
     xd = x.to(cuda).contiguous()
     wp = w.permute(0, 2, 3, 1).contiguous().to(cuda)
     y = torch.empty(BB, Hi // 2, Wi // 2, Co, dtype=torch.bfloat16, device=cuda)
+    bd = b.to(cuda)
     L.check(L.lib().hlmc_op_conv_s2(L.stream(), L.HLMC_BF16, xd.data_ptr(), BB, Hi, Wi, Ci, wp.data_ptr(),
-                                    b.to(cuda).data_ptr(), Co, y.data_ptr(), ws.data_ptr(), WS_BYTES))
+                                    bd.data_ptr(), Co, y.data_ptr(), ws.data_ptr(), WS_BYTES))
     e = rel(y, ref)
     print(f"conv_s2 B={BB} {Hi}x{Wi} {Ci}->{Co}: rel L2 {e:.2e}")
     assert e < 3e-3
@@ -275,8 +276,9 @@ def test_subpixel_bench_shapes_bf16(cuda, ws, Hi, Wi, Ci, Co):
     xd = x.to(cuda).contiguous()
     wp = w.permute(1, 2, 3, 0).contiguous().to(cuda)
     y = torch.empty(BB, 2 * Hi, 2 * Wi, Co, dtype=torch.bfloat16, device=cuda)
+    bd = b.to(cuda)
     L.check(L.lib().hlmc_op_subpixel(L.stream(), L.HLMC_BF16, xd.data_ptr(), BB, Hi, Wi, Ci, wp.data_ptr(),
-                                     b.to(cuda).data_ptr(), Co, y.data_ptr(), ws.data_ptr(), WS_BYTES))
+                                     bd.data_ptr(), Co, y.data_ptr(), ws.data_ptr(), WS_BYTES))
     e = rel(y, ref)
     print(f"subpixel B={BB} {Hi}x{Wi} {Ci}->{Co}: rel L2 {e:.2e}")
     assert e < 3e-3
@@ -290,8 +292,9 @@ def test_wgrad_s2_bench_shapes_bf16(cuda, ws, Hl, Wl, M, C):
     ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (M, C, 3, 3), dy.double().permute(0, 3, 1, 2),
                                       stride=2, padding=1)
     dW = torch.empty(M, C, 3, 3, device=cuda)
-    L.check(L.lib().hlmc_op_wgrad_s2(L.stream(), L.HLMC_BF16, dy.to(cuda).contiguous().data_ptr(), BB, Hl, Wl, M,
-                                     x.to(cuda).contiguous().data_ptr(), C, dW.data_ptr(), ws.data_ptr(), WS_BYTES))
+    dyd, xd = dy.to(cuda).contiguous(), x.to(cuda).contiguous()   # held: a freed temporary's block gets reused
+    L.check(L.lib().hlmc_op_wgrad_s2(L.stream(), L.HLMC_BF16, dyd.data_ptr(), BB, Hl, Wl, M, xd.data_ptr(), C,
+                                     dW.data_ptr(), ws.data_ptr(), WS_BYTES))
     e = rel(dW, ref)
     print(f"wgrad_s2 B={BB} {Hl}x{Wl} M={M} C={C}: rel L2 {e:.2e}")
     assert e < 1e-4

@@ -220,3 +220,21 @@ def test_philox_known_answers():
     a = normals(4096, seed=1234)
     assert abs(float(a.mean())) < 0.05 and abs(float(a.std()) - 1) < 0.05
     np.testing.assert_array_equal(normals(8, seed=1234, offset=4096 - 8), a[-8:])
+
+
+@pytest.mark.parametrize("name", ["hybrid_128x128_td768", "cvae_128x128", "simple_370"])
+def test_oracle_training_chain_reproduces_fixture_latents(name):
+    """The oracle's 3-step train chain (tests/test_models_gpu._oracle_trained: the fixture generator's Adam steps
+    and dropout seeds) then eval-mode encode reproduces the reference classes' fixture eval_mu bit for bit on the
+    generating host — the pin of the latent-extraction contract (src/Convolutional_VAE.py:286-303,
+    src/Conditional_VAE.py:397-402, src/Simple_VAE.py:225-226) the GPU test compares the engine against."""
+    from tests.test_models_gpu import _oracle_trained
+    case = FX.case_by_name(name)
+    ora = _oracle_trained(case)
+    ins, _ = FX.inputs_fn(case)(0)
+    with torch.no_grad():
+        mu = ora.encode(*ins)[0]
+    fx = np.load(f"tests/golden/model_{name}.npz")["eval_mu"]
+    err = float(np.abs(mu.numpy() - fx).max())
+    # bit-exact where the fixtures were generated (this container's CPU); Adam-amplified rounding elsewhere
+    assert err == 0.0 or float(np.linalg.norm(mu.numpy() - fx) / np.linalg.norm(fx)) < 5e-2, err

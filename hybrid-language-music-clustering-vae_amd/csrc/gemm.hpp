@@ -408,8 +408,8 @@ __device__ __forceinline__ void epilogue_tile(const EP& ep, const f32x4_t (&acc)
 // kStatMode 1: per-column sums / sums of squares of the stored values, reduced over the 16 rows of each lane group
 // (xor shuffles) -> cs / cq [j][k] hold the totals of column nb + j*16 + 4*(lane >> 4) + k in every lane.
 // F32RED: the per-lane sums (<= TM bf16-exact values and their squares) and the 16-lane shuffle tree in f32 (one
-// DPP / swizzle step per value instead of two plus an f64 add), widened to f64 afterwards — for the bf16-only halo
-// kernels; the generic kernels (fp32 parity mode too) keep f64 throughout.
+// DPP / swizzle step per value instead of two plus an f64 add), widened to f64 afterwards — bf16 outputs (the
+// throughput mode); fp32 outputs (the parity mode) keep f64 throughout.
 template <int TM, int TN, class EP, bool F32RED = false>
 __device__ __forceinline__ void epilogue_tile_t(const EP& ep, const f32x4_t (&acc)[TM][TN], int mb, int nb, int lane,
                                                 int M, int N, double (&cs)[TN][4], double (&cq)[TN][4]) {
@@ -667,7 +667,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
     }
     double cs[TR ? TN * 4 : TN], cq[TR ? TN * 4 : TN];
     if constexpr (TR)
-        epilogue_tile_t<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N,
+        epilogue_tile_t<TM, TN, EP, sizeof(T) == 2>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N,
                                 *reinterpret_cast<double(*)[TN][4]>(cs), *reinterpret_cast<double(*)[TN][4]>(cq));
     else
         epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);
@@ -826,7 +826,7 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
     }
     double cs[TR ? TN * 4 : TN], cq[TR ? TN * 4 : TN];
     if constexpr (TR)
-        epilogue_tile_t<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N,
+        epilogue_tile_t<TM, TN, EP, sizeof(T) == 2>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N,
                                 *reinterpret_cast<double(*)[TN][4]>(cs), *reinterpret_cast<double(*)[TN][4]>(cq));
     else
         epilogue_tile<TM, TN>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N, cs, cq);

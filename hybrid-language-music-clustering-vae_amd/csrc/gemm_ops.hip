@@ -124,11 +124,22 @@ void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, c
         gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     HLMC_PROBE_END(s);
 }
-// HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid)
+// HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid).  Measured per layer
+// (scripts/bench_gemm.py, round 3): the transposed epilogue takes the split-K / LDS-DMA conv and sub-pixel GEMMs from
+// 28-42 to 22-32 us (the 8 x 8 .. 2 x 2 layers), but makes the LDS halo-tile kernels 4-15 % slower (their stores were
+// not the bound; the swapped fragments cost LDS issue) -> halo kernels keep the per-element epilogue
+// (HLMC_HALO_TR=1 switches them over, A/B aid).
 inline bool nt_tr_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("HLMC_NT_TR");
         return !(e && e[0] == '0');
+    }();
+    return on;
+}
+inline bool halo_tr_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HLMC_HALO_TR");
+        return e && e[0] == '1';
     }();
     return on;
 }
@@ -631,7 +642,7 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
-        const bool tr = nt_tr_enabled();
+        const bool tr = halo_tr_enabled();
         if (halo && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0)
             return tr ? run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, true>,
                             conv_s2_halo_kernel<32, 64, 1, 32, 4, true, WithStats<StoreRM<T>>, true>, 128, 1)
@@ -696,7 +707,7 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
-        const bool tr = nt_tr_enabled();
+        const bool tr = halo_tr_enabled();
         if (halo && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0)
             return tr ? run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, true>,
                             subpixel_halo_kernel<64, 32, 1, 32, 4, true, WithStats<StoreSubpixel<T>>, true>, 1)

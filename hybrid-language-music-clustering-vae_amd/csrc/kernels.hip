@@ -598,8 +598,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
 // y[b,oh,ow,co] = bias[co] + sum_{kh,kw} x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + kh*3+kw]
 // y[b, oh, ow, co] = bias[co] + sum_taps x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + tap]  (1 input channel, CO = 32)
 // Four threads per output pixel, each computing 8 channels (one 16-byte store): a wave's store instruction
-// writes 1 KB contiguous; the 9 input taps are re-read by the 4 threads from L1; each thread's 72 weights are
-// registers, and two pixels' tap loads are in flight per step.
+// writes 1 KB contiguous; the 9 input taps are re-read by the 4 threads from L1.
 // MODE 1 (encoder input conv): also the BatchNorm statistics of the stored outputs, one [sum | sum of squares]
 // f64 partial row per block (the col_moments pass it replaces).  MODE 2 (data gradient of the decoder's output
 // convT, which writes the gradient of the last BatchNorm layer's output): also that layer's backward moments
@@ -610,24 +609,24 @@ struct C1Fuse {
     const void* ybn = nullptr;
     const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
 };
-// (launch bounds: >= 4 waves per SIMD, 3 in MODE 2; unbounded, hipcc hoisted enough to leave one wave per SIMD)
+// Weights in LDS as [tap][CO] (each tap's 8 channels of a thread: two float4 reads), U = 2 pixels' tap loads in flight
+// per step; launch bounds keep >= 4 waves per SIMD (the per-pixel register set is small: no weights in registers).
 template <typename T, int CO, int MODE>
 __global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
-                                                         const float* __restrict__ w, const float* __restrict__ bias,
-                                                         T* __restrict__ y, FastDiv dWo, FastDiv dHo, C1Fuse fz) {
+                                                            const float* __restrict__ w, const float* __restrict__ bias,
+                                                            T* __restrict__ y, FastDiv dWo, FastDiv dHo, C1Fuse fz) {
     constexpr int V = Vec16<T>::N, G = CO / V;  // threads per pixel
-    constexpr int U = 2;                        // pixels per thread per step: 2 x 9 tap loads in flight
+    constexpr int U = 2;                        // pixels per thread per step
+    __shared__ __attribute__((aligned(16))) float wsh[9 * CO];
+    __shared__ __attribute__((aligned(16))) float bsh[CO];
     __shared__ double fred[MODE ? 4 * CO : 1];
-    // a thread's channel group is fixed (the grid stride is a multiple of G): its 9 x V weights and V biases live in
-    // registers for the whole kernel (no per-pixel LDS weight reads)
-    const int c0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) % G) * V;
-    float wr[V][9], br[V];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-        br[v] = bias ? bias[c0 + v] : 0.f;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) wr[v][k] = w[(c0 + v) * 9 + k];
+    for (int i = threadIdx.x; i < 9 * CO; i += blockDim.x) {
+        const int tap = i / CO, c = i - tap * CO;
+        wsh[i] = w[c * 9 + tap];
     }
+    for (int i = threadIdx.x; i < CO; i += blockDim.x) bsh[i] = bias ? bias[i] : 0.f;
+    // a thread's channel group is fixed (the grid stride is a multiple of G)
+    const int c0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) % G) * V;
     float fa[V], fb[V];  // per-thread statistics (a handful of pixels) in f32, widened once for the block tree
     float bmu[V], bis[V], bga[V], bbe[V];
 #pragma unroll
@@ -638,6 +637,7 @@ __global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(cons
         BnChan::load(fz.gamma, c0, bga);
         BnChan::load(fz.beta, c0, bbe);
     }
+    __syncthreads();
     const int Ho = Hi / 2, Wo = Wi / 2;
     const int nthr = B * Ho * Wo * G;  // < 2^31 (checked by the launcher)
     const int stride = gridDim.x * blockDim.x;
@@ -666,11 +666,20 @@ __global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(cons
             if (pix[u] < 0) break;
             float o[V];
 #pragma unroll
-            for (int v = 0; v < V; ++v) {
-                float acc = br[v];
+            for (int v = 0; v < V; v += 4) {
+                const float4 bq = *reinterpret_cast<const float4*>(bsh + c0 + v);
+                o[v] = bq.x; o[v + 1] = bq.y; o[v + 2] = bq.z; o[v + 3] = bq.w;
+            }
 #pragma unroll
-                for (int k = 0; k < 9; ++k) acc = fmaf(in[u][k], wr[v][k], acc);
-                o[v] = acc;
+            for (int k = 0; k < 9; ++k) {
+#pragma unroll
+                for (int v = 0; v < V; v += 4) {
+                    const float4 wq = *reinterpret_cast<const float4*>(wsh + k * CO + c0 + v);
+                    o[v] = fmaf(in[u][k], wq.x, o[v]);
+                    o[v + 1] = fmaf(in[u][k], wq.y, o[v + 1]);
+                    o[v + 2] = fmaf(in[u][k], wq.z, o[v + 2]);
+                    o[v + 3] = fmaf(in[u][k], wq.w, o[v + 3]);
+                }
             }
             store16_f32(y + (int64_t)pix[u] * CO + c0, o);
             if constexpr (MODE == 1) {
@@ -731,7 +740,9 @@ __global__ __launch_bounds__(256, 4) void convT_c1_kernel(const T* __restrict__ 
     constexpr int kOut[9] = {0, 1, 1, 2, 2, 3, 3, 3, 3};
     constexpr int kNb[9] = {0, 0, 1, 0, 2, 0, 1, 2, 3};
     constexpr int kTap[9] = {4, 5, 3, 7, 1, 8, 6, 2, 0};
-    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nlow; q += gridDim.x * blockDim.x) {
+    // one low-res pixel per thread, no grid-stride loop: nothing is loop-invariant for hipcc to hoist into registers
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nlow) {
         const int t = (int)dWi.div((uint32_t)q), c = q - t * Wi;
         const int b = (int)dHi.div((uint32_t)t), r = t - b * Hi;
         const bool okr = r + 1 < Hi, okc = c + 1 < Wi;
@@ -1439,7 +1450,8 @@ int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const flo
     HLMC_CHECK_ARG(npix < (int64_t)1 << 31, "convT_c1: too many pixels");
     HLMC_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "convT_c1: alignment");
     const FastDiv dW((uint32_t)Wi), dH((uint32_t)Hi);
-    convT_c1_kernel<T, 32><<<grid_for(npix / 4, kThreads, 16384), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH);
+    convT_c1_kernel<T, 32><<<(unsigned)((npix / 4 + kThreads - 1) / kThreads), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y,
+                                                                                              dW, dH);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

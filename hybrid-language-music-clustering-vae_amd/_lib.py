@@ -95,8 +95,9 @@ _SIGS = {
     "hlmc_op_subpixel": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_i64]),
     "hlmc_op_wgrad_s2": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_i64]),
     "hlmc_op_linear": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int,
-                               c_int, c_int, c_vp, c_i64]),
-    "hlmc_op_linear_wgrad": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_i64]),
+                               c_int, c_int, c_vp, c_i64, c_vp]),
+    "hlmc_op_linear_wgrad": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                     c_i64]),
     "hlmc_op_conv_c1_s2": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "hlmc_op_convT_c1": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "hlmc_op_wgrad_c1": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_i64]),

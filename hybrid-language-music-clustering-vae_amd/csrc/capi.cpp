@@ -423,23 +423,23 @@ int hlmc_op_wgrad_s2(void* stream, int dtype, const void* Lo, int B, int Hl, int
 }
 int hlmc_op_linear(void* stream, int dtype, const void* x, int ldx, int M, int K, const void* wt, int ldw,
                    const float* bias, int N, void* y, int ldy, int act, int accumulate, int out_f32, void* ws,
-                   int64_t ws_bytes) {
+                   int64_t ws_bytes, const void* relu_ref) {
     Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
     if (dtype == HLMC_BF16 && out_f32)
         return ops::linear<bf16, float>(S(stream), (const bf16*)x, ldx, M, K, (const bf16*)wt, ldw, bias, N, (float*)y,
-                                        ldy, act, accumulate, w);
+                                        ldy, act, accumulate, w, (const float*)relu_ref);
     if (dtype == HLMC_BF16)
         return ops::linear<bf16, bf16>(S(stream), (const bf16*)x, ldx, M, K, (const bf16*)wt, ldw, bias, N, (bf16*)y,
-                                       ldy, act, accumulate, w);
+                                       ldy, act, accumulate, w, (const bf16*)relu_ref);
     return ops::linear<float, float>(S(stream), (const float*)x, ldx, M, K, (const float*)wt, ldw, bias, N, (float*)y,
-                                     ldy, act, accumulate, w);
+                                     ldy, act, accumulate, w, (const float*)relu_ref);
 }
 int hlmc_op_linear_wgrad(void* stream, int dtype, const void* dy, int lddy, const void* x, int ldx, int Mb, int N,
-                         int K, float* dW, void* ws, int64_t ws_bytes) {
+                         int K, float* dW, float* db, void* ws, int64_t ws_bytes) {
     Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
     return DT_DISPATCH(dtype,
-        ops::linear_wgrad<float>(S(stream), (const float*)dy, lddy, (const float*)x, ldx, Mb, N, K, dW, w),
-        ops::linear_wgrad<bf16>(S(stream), (const bf16*)dy, lddy, (const bf16*)x, ldx, Mb, N, K, dW, w));
+        ops::linear_wgrad<float>(S(stream), (const float*)dy, lddy, (const float*)x, ldx, Mb, N, K, dW, db, w),
+        ops::linear_wgrad<bf16>(S(stream), (const bf16*)dy, lddy, (const bf16*)x, ldx, Mb, N, K, dW, db, w));
 }
 int hlmc_op_conv_c1_s2(void* stream, int dtype, const float* x, int B, int Hi, int Wi, const float* w,
                        const float* bias, int Co, void* y) {

@@ -251,14 +251,12 @@ class NetT : public NetBase {
     }
     // weight gradients of the dense layers: on the second stream (HLMC_DENSE_SIDE=1, default) or inline on s
     // (their GEMMs are 5-20 us, about the main-stream bubble a fork's event marker costs)
-    template <class F>
-    int dense_side(hipStream_t s, F&& f) {
+    bool dense_side_on() const {
         static const bool on = [] {
             const char* e = std::getenv("HLMC_DENSE_SIDE");
             return !(e && e[0] == '0');
         }();
-        if (on) return side(s, std::forward<F>(f));
-        return f(s, scratch);
+        return on && use_side;
     }
     // bucket k of the data-parallel all-reduce is final once both streams pass this point
     int mark(hipStream_t s, int k) {
@@ -297,31 +295,21 @@ class NetT : public NetBase {
         need(ops::linear_ws<T>(B, K, N));
         need(ops::linear_ws<T>(B, N, K));
         need(ops::linear_wgrad_ws<T>(B, N, K));
-        need(ops::colsum_ws(B, N));
     }
-    // grads of a linear layer from dy (pre-activation grad): dW, db (weight-gradient stream), optionally dx (+=)
-    int lin_bwd(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int B, int w, int b, T* dx, int lddx, int acc = 0) {
+    // grads of a linear layer from dy (pre-activation grad).  The dense middle of the backward is bound by the
+    // host's launch rate (measured: 40-100 us main-stream gaps per layer, scripts/step_gaps.py), so per layer:
+    // the fork's event first, then dx (+=) on s — the critical path, with the ReLU backward of the layer below
+    // (relu_ref: its post-ReLU output) in the epilogue — then dW and db as ONE weight-gradient GEMM (a ones
+    // column on x gives db) on the weight-gradient stream: 2-3 launches where there were 6-7.
+    int lin_bwd(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int B, int w, int b, T* dx, int lddx,
+                int acc = 0, const T* relu_ref = nullptr) {
         const int N = (int)params[w].shape[0], K = (int)params[w].shape[1];
-        float* gw = G[w];
-        float* gb = b >= 0 ? G[b] : nullptr;
-        HLMC_TRY(dense_side(s, [&](hipStream_t q, Ws sc) {
-            HLMC_TRY(ops::linear_wgrad<T>(q, dy, lddy, x, ldx, B, N, K, gw, sc));
-            if (gb) HLMC_TRY(ops::colsum<T>(q, dy, lddy, B, N, gb, sc));
-            return (int)HLMC_OK;
-        }));
-        if (dx) HLMC_TRY(ops::linear<T, T>(s, dy, lddy, B, N, P1(w), ld1(w), nullptr, K, dx, lddx, 0, acc, scratch));
-        return HLMC_OK;
-    }
-
-    // latent heads: dW = dyT^T x (dyT = T copy of the f32 grad dyF), db = column sums of dyF (weight-gradient stream)
-    int head_wgrad(hipStream_t s, const T* dyT, const float* dyF, int L, const T* x, int ldx, int B, int K, int w, int b) {
-        float* gw = G[w];
-        float* gb = G[b];
-        return dense_side(s, [&](hipStream_t q, Ws sc) {
-            HLMC_TRY(ops::linear_wgrad<T>(q, dyT, L, x, ldx, B, L, K, gw, sc));
-            HLMC_TRY(ops::colsum<float>(q, dyF, L, B, L, gb, sc));
-            return (int)HLMC_OK;
-        });
+        const bool sd = dense_side_on();
+        if (sd) HLMC_TRY(fork(s));
+        if (dx)
+            HLMC_TRY(ops::linear<T, T>(s, dy, lddy, B, N, P1(w), ld1(w), nullptr, K, dx, lddx, 0, acc, scratch, relu_ref));
+        return ops::linear_wgrad<T>(sd ? s2 : s, dy, lddy, x, ldx, B, N, K, G[w], b >= 0 ? G[b] : nullptr,
+                                    sd ? scratch2 : scratch);
     }
 
     struct BnBufs {
@@ -640,7 +628,7 @@ class HybridNet : public NetT<T> {
     // workspace
     size_t flat_, fuse_, tin_, te_y[2], te_a0, h_, mu_, lv_, eps_, z_, d1_, s_, ah_, u_, td_y, td_a, rt_;
     BnBufs te_bb[2], td_bb;
-    size_t gA_, gflat_, gfuse_, gh_, gz_, gd1_, gs_, gah_, gte_, gte1_, gte2_, gtd_, gtd2_, gdmu_, gdlv_, gmuT_, glvT_, grt_;
+    size_t gA_, gflat_, gfuse_, gh_, gz_, gd1_, gs_, gah_, gte_, gte1_, gte2_, gtd_, gtd2_, gmuT_, glvT_, grt_;
     int ldF = 0, ldT = 0, ldFU = 0, ldSP = 0;
 
     HybridNet(int latent, int text_dim, int h, int w) : L(latent), TD(text_dim), H(h), W(w) {
@@ -748,12 +736,9 @@ class HybridNet : public NetT<T> {
         gd1_ = A.take(B * 512 * t);
         gs_ = A.take(B * ldSP * t);
         gah_ = A.take(B * ldF * t);
-        gdmu_ = A.take(B * L * 4);
-        gdlv_ = A.take(B * L * 4);
         gmuT_ = A.take(B * L * t);
         glvT_ = A.take(B * L * t);
         for (int w : {afc_w, fus_w, mu_w, lv_w, di_w, ds_w, adf_w}) this->lin_need((int)B, w);
-        this->need(ops::colsum_ws((int)B, L));
     }
 
     int encode(hipStream_t s, const ForwardArgs& a, int B) {
@@ -831,32 +816,22 @@ class HybridNet : public NetT<T> {
             HLMC_TRY(this->lin_bwd(s, AT(grt_), ldT, AT(td_a), 256, B, td_w[1], td_b[1], AT(gtd_), 256));
             HLMC_TRY(this->bn_bwd(s, AT(gtd_), 256, AT(td_y), B, 256, td_bb, td_g, td_beta, 0, nullptr, 1.f,
                                   AT(gtd2_), td_b[0]));
-            HLMC_TRY(this->lin_bwd(s, AT(gtd2_), 256, AT(s_) + 1024, ldSP, B, td_w[0], -1, AT(gs_) + 1024, ldSP));
+            HLMC_TRY(this->lin_bwd(s, AT(gtd2_), 256, AT(s_) + 1024, ldSP, B, td_w[0], -1, AT(gs_) + 1024, ldSP, 0,
+                                   AT(s_) + 1024));
         }
         // ---- audio decoder
         T* gu = nullptr;
         HLMC_TRY(this->dec_bwd(s, AT(u_), B, a.d_recon, gA, &gu));
         HLMC_TRY(this->mark(s, 0));
-        HLMC_TRY(ops::nhwc_to_flat<T>(s, gu, B, H / 64, W / 64, 512, AT(gah_), ldF));
-        HLMC_TRY(ops::relu_bwd<T>(s, AT(gah_), ldF, AT(ah_), ldF, B, F));
-        HLMC_TRY(this->lin_bwd(s, AT(gah_), ldF, AT(s_), ldSP, B, adf_w, adf_b, AT(gs_), ldSP));
-        HLMC_TRY(ops::relu_bwd<T>(s, AT(gs_), ldSP, AT(s_), ldSP, B, SP));
-        HLMC_TRY(this->lin_bwd(s, AT(gs_), ldSP, AT(d1_), 512, B, ds_w, ds_b, AT(gd1_), 512));
-        HLMC_TRY(ops::relu_bwd<T>(s, AT(gd1_), 512, AT(d1_), 512, B, 512));
+        // (each ReLU backward rides in the epilogue of the GEMM / relayout that writes the gradient)
+        HLMC_TRY(ops::nhwc_to_flat<T>(s, gu, B, H / 64, W / 64, 512, AT(gah_), ldF, AT(ah_)));
+        HLMC_TRY(this->lin_bwd(s, AT(gah_), ldF, AT(s_), ldSP, B, adf_w, adf_b, AT(gs_), ldSP, 0, AT(s_)));
+        HLMC_TRY(this->lin_bwd(s, AT(gs_), ldSP, AT(d1_), 512, B, ds_w, ds_b, AT(gd1_), 512, 0, AT(d1_)));
         HLMC_TRY(this->lin_bwd(s, AT(gd1_), 512, AT(z_), L, B, di_w, di_b, AT(gz_), L));
-        // ---- reparameterisation + heads
-        {
-            const ops::CopySeg cs[2] = {{AF(gdmu_), a.d_mu, (int64_t)B * L}, {AF(gdlv_), a.d_logvar, (int64_t)B * L}};
-            HLMC_TRY(ops::copy_segments(s, cs, 2));
-        }
-        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), L, AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
-        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
-        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
-        HLMC_TRY(this->head_wgrad(s, AT(gmuT_), AF(gdmu_), L, AT(h_), 512, B, 512, mu_w, mu_b));
-        HLMC_TRY(this->head_wgrad(s, AT(glvT_), AF(gdlv_), L, AT(h_), 512, B, 512, lv_w, lv_b));
-        HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, 512, AT(gh_), 512, 0, 0, this->scratch));
-        HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, 512, AT(gh_), 512, 0, 1, this->scratch));
-        HLMC_TRY(ops::relu_bwd<T>(s, AT(gh_), 512, AT(h_), 512, B, 512));
+        // ---- reparameterisation + heads: one pass to the heads' T gradients (the caller's d_mu / d_logvar added)
+        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), L, AF(lv_), AF(eps_), a.d_mu, a.d_logvar, B, L, AT(gmuT_), AT(glvT_)));
+        HLMC_TRY(this->lin_bwd(s, AT(gmuT_), L, AT(h_), 512, B, mu_w, mu_b, AT(gh_), 512, 0));
+        HLMC_TRY(this->lin_bwd(s, AT(glvT_), L, AT(h_), 512, B, lv_w, lv_b, AT(gh_), 512, 1, AT(h_)));
         HLMC_TRY(this->lin_bwd(s, AT(gh_), 512, AT(fuse_), ldFU, B, fus_w, fus_b, AT(gfuse_), ldFU));
         // ---- text encoder
         if (text) {
@@ -895,7 +870,7 @@ class CvaeNet : public NetT<T> {
     int ldF = 0, ldT = 0, ldX = 0, ldZ = 0, ldS = 0;
     size_t tin_, te_y, X_, mu_, lv_, eps_, Z_, S_, u_, td_y, td_a;
     BnBufs te_bb, td_bb;
-    size_t gA_, grt_, gtd_, gt2_, gt3_, gS_, gZ_, gX_, gdmu_, gdlv_, gmuT_, glvT_;
+    size_t gA_, grt_, gtd_, gt2_, gt3_, gS_, gZ_, gX_, gmuT_, glvT_;
 
     CvaeNet(int latent, int text_dim, int ncls, int h, int w) : L(latent), TD(text_dim), C(ncls), H(h), W(w) {
         F = 512 * (H / 64) * (W / 64);
@@ -962,13 +937,10 @@ class CvaeNet : public NetT<T> {
         gS_ = A.take(B * ldS * t);
         gZ_ = A.take(B * ldZ * t);
         gX_ = A.take(B * ldX * t);
-        gdmu_ = A.take(B * L * 4);
-        gdlv_ = A.take(B * L * 4);
         gmuT_ = A.take(B * L * t);
         glvT_ = A.take(B * L * t);
         for (int w_ : {te_w, mu_w, lv_w, dfc_w, td_w[0], td_w[1]}) this->lin_need((int)B, w_);
         this->need(ops::bn_ws(B, 512));
-        this->need(ops::colsum_ws((int)B, ldS));
     }
 
     int encode(hipStream_t s, const ForwardArgs& a, int B) {
@@ -1040,18 +1012,9 @@ class CvaeNet : public NetT<T> {
         // decoder_fc (no activation)
         HLMC_TRY(this->lin_bwd(s, AT(gS_), ldS, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(gZ_), ldZ));
         // reparameterisation
-        {
-            const ops::CopySeg cs[2] = {{AF(gdmu_), a.d_mu, (int64_t)B * L}, {AF(gdlv_), a.d_logvar, (int64_t)B * L}};
-            HLMC_TRY(ops::copy_segments(s, cs, 2));
-        }
-        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gZ_), ldZ, AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
-        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
-        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
-        const int K = F + 256 + C;
-        HLMC_TRY(this->head_wgrad(s, AT(gmuT_), AF(gdmu_), L, AT(X_), ldX, B, K, mu_w, mu_b));
-        HLMC_TRY(this->head_wgrad(s, AT(glvT_), AF(gdlv_), L, AT(X_), ldX, B, K, lv_w, lv_b));
-        HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, K, AT(gX_), ldX, 0, 0, this->scratch));
-        HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, K, AT(gX_), ldX, 0, 1, this->scratch));
+        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gZ_), ldZ, AF(lv_), AF(eps_), a.d_mu, a.d_logvar, B, L, AT(gmuT_), AT(glvT_)));
+        HLMC_TRY(this->lin_bwd(s, AT(gmuT_), L, AT(X_), ldX, B, mu_w, mu_b, AT(gX_), ldX, 0));
+        HLMC_TRY(this->lin_bwd(s, AT(glvT_), L, AT(X_), ldX, B, lv_w, lv_b, AT(gX_), ldX, 1));
         // text encoder
         HLMC_TRY(this->bn_bwd(s, AT(gX_) + F, ldX, AT(te_y), B, 256, te_bb, te_g, te_beta, 0, nullptr, 1.f, AT(gt3_), te_b));
         HLMC_TRY(this->lin_bwd(s, AT(gt3_), 256, AT(tin_), ldT, B, te_w, -1, nullptr, 0));
@@ -1087,7 +1050,7 @@ class SimpleNet : public NetT<T> {
     std::vector<Blk> encb, decb;
     int mu_w, mu_b, lv_w, lv_b, out_w, out_b;
     int ldD = 0;
-    size_t x_, mu_, lv_, eps_, z_, gx1_, gdmu_, gdlv_, gmuT_, glvT_, gz_, grec_, mask_;
+    size_t x_, mu_, lv_, eps_, z_, gx1_, gmuT_, glvT_, gz_, grec_, mask_;
     int64_t mask_total = 0;
 
     SimpleNet(int input_dim, int latent, std::vector<int> hidden) : D(input_dim), L(latent), hid(std::move(hidden)) {
@@ -1160,8 +1123,6 @@ class SimpleNet : public NetT<T> {
         eps_ = A.take(B * L * 4);
         z_ = A.take(B * pad8(L) * t);
         gx1_ = A.take(B * widest * t);
-        gdmu_ = A.take(B * L * 4);
-        gdlv_ = A.take(B * L * 4);
         gmuT_ = A.take(B * L * t);
         glvT_ = A.take(B * L * t);
         gz_ = A.take(B * pad8(L) * t);
@@ -1258,18 +1219,11 @@ class SimpleNet : public NetT<T> {
             const int ldg = i == 0 ? pad8(L) : b.din;
             HLMC_TRY(this->lin_bwd(s, dy, b.dout, xin, ldx, B, b.w, -1, gin, ldg));
         }
-        {
-            const ops::CopySeg cs[2] = {{AF(gdmu_), a.d_mu, (int64_t)B * L}, {AF(gdlv_), a.d_logvar, (int64_t)B * L}};
-            HLMC_TRY(ops::copy_segments(s, cs, 2));
-        }
-        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), pad8(L), AF(lv_), AF(eps_), B, L, AF(gdmu_), AF(gdlv_)));
-        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdmu_), AT(gmuT_), (int64_t)B * L));
-        HLMC_TRY(ops::cast_from_f32<T>(s, AF(gdlv_), AT(glvT_), (int64_t)B * L));
+        HLMC_TRY(ops::reparam_bwd<T>(s, AT(gz_), pad8(L), AF(lv_), AF(eps_), a.d_mu, a.d_logvar, B, L, AT(gmuT_),
+                                     AT(glvT_)));
         const Blk& top = encb.back();
-        HLMC_TRY(this->head_wgrad(s, AT(gmuT_), AF(gdmu_), L, AT(top.a), top.dout, B, top.dout, mu_w, mu_b));
-        HLMC_TRY(this->head_wgrad(s, AT(glvT_), AF(gdlv_), L, AT(top.a), top.dout, B, top.dout, lv_w, lv_b));
-        HLMC_TRY(ops::linear<T, T>(s, AT(gmuT_), L, B, L, this->P1(mu_w), this->ld1(mu_w), nullptr, top.dout, g1, top.dout, 0, 0, this->scratch));
-        HLMC_TRY(ops::linear<T, T>(s, AT(glvT_), L, B, L, this->P1(lv_w), this->ld1(lv_w), nullptr, top.dout, g1, top.dout, 0, 1, this->scratch));
+        HLMC_TRY(this->lin_bwd(s, AT(gmuT_), L, AT(top.a), top.dout, B, mu_w, mu_b, g1, top.dout, 0));
+        HLMC_TRY(this->lin_bwd(s, AT(glvT_), L, AT(top.a), top.dout, B, lv_w, lv_b, g1, top.dout, 1));
         for (int i = (int)encb.size() - 1; i >= 0; --i) {
             const Blk& b = encb[i];
             T* dy = AT(b.dy);

@@ -276,6 +276,39 @@ struct StoreRM {
     }
 };
 
+// StoreRM followed by the ReLU backward mask of the layer below: the stored (accumulated) value is zeroed where
+// relu_ref (that layer's post-ReLU activation, same row stride ld) is not positive.  Replaces a relu_bwd pass over
+// the data gradient (one launch and a read-modify-write of the map per dense layer).
+template <typename OutT>
+struct StoreReluBwd : StoreRM<OutT> {
+    const OutT* relu_ref;
+    __device__ bool live(int64_t e) const { return to_f32<OutT>(relu_ref[e]) > 0.f; }
+    __device__ float put(int64_t ro, int n, float v) const {
+        OutT* o = this->out + ro + n;
+        if (this->accumulate) v += to_f32<OutT>(*o);
+        if (!live(ro + n)) v = 0.f;
+        const OutT t = from_f32<OutT>(v);
+        *o = t;
+        return to_f32<OutT>(t);
+    }
+    __device__ void put4(int64_t ro, int n, float (&v)[4]) const {
+        OutT* o = this->out + ro + n;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (this->accumulate) v[k] += to_f32<OutT>(o[k]);
+            if (!live(ro + n + k)) v[k] = 0.f;
+        }
+        store4_round<OutT>(o, v);
+    }
+    __device__ void store(const typename StoreRM<OutT>::Row& rw, int n, float v) const {
+        if (this->bias) v += this->bias[n];
+        OutT* o = rw.r + n;
+        if (this->accumulate) v += to_f32<OutT>(*o);
+        if (!live(o - this->out)) v = 0.f;
+        *o = from_f32<OutT>(v);
+    }
+};
+
 // Sub-pixel phase store into a high-res NHWC map [B, 2Hi, 2Wi, N]; m = (b, r, c) over the low grid.
 template <typename OutT>
 struct StoreSubpixel {
@@ -892,11 +925,13 @@ struct KRowDense {
     const T* p;
     int ld, Kd, Md;  // rows (k) and columns (m/n)
     bool vec;        // rows 16-byte aligned (ld % V == 0)
+    bool ones;       // a virtual column Md of ones: column Md of the product is the row sum of the other operand
+                     // (a linear layer's bias gradient from its weight-gradient GEMM; register path only)
     struct Col {
         int m;
     };
     __device__ Col prep(int m) const { return Col{m}; }
-    // LDS-DMA path (vec, Md % V == 0): the 16-byte chunk's address or g_zero16 outside the operand
+    // LDS-DMA path (vec, Md % V == 0, no ones column): the 16-byte chunk's address or g_zero16 outside the operand
     __device__ const void* addr(int k, const Col& cl) const {
         return (k < Kd && cl.m < Md) ? static_cast<const void*>(p + (int64_t)k * ld + cl.m) : &g_zero16;
     }
@@ -908,7 +943,8 @@ struct KRowDense {
         if (vec && m + V <= Md) return *reinterpret_cast<const uint4*>(r + m);
         union { uint4 u; T e[V]; } x;
 #pragma unroll
-        for (int i = 0; i < V; ++i) x.e[i] = (m + i < Md) ? r[m + i] : from_f32<T>(0.f);
+        for (int i = 0; i < V; ++i)
+            x.e[i] = (m + i < Md) ? r[m + i] : from_f32<T>((ones && m + i == Md) ? 1.f : 0.f);
         return x.u;
     }
 };

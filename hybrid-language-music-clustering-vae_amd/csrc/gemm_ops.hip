@@ -745,7 +745,7 @@ size_t wgrad_s2_ws(int B, int Hl, int Wl, int M, int C) {
 
 template <typename T, typename OutT>
 int linear(hipStream_t s, const T* x, int ldx, int M, int K, const T* w, int ldw, const float* bias, int N, OutT* y,
-           int ldy, int act, int accumulate, Ws ws) {
+           int ldy, int act, int accumulate, Ws ws, const OutT* relu_ref) {
     constexpr int V = Vec16<T>::N;
     bool vx = (ldx % V == 0) && aligned16(x);
     bool vw = (ldw % V == 0) && aligned16(w);
@@ -753,6 +753,13 @@ int linear(hipStream_t s, const T* x, int ldx, int M, int K, const T* w, int ldw
     DenseLoader<T> bl{w, ldw, N, K, vw};
     StoreRM<OutT> ep{y, bias, ldy, act, accumulate};
     probe::site(probe::kLinear, 2.0 * M * N * K, (double)sizeof(T) * ((double)M * K + (double)N * K) + (double)sizeof(OutT) * M * N);
+    if (relu_ref) {
+        HLMC_CHECK_ARG(act == 0, "linear: a ReLU-backward mask and a forward activation together");
+        StoreReluBwd<OutT> em;
+        static_cast<StoreRM<OutT>&>(em) = ep;
+        em.relu_ref = relu_ref;
+        return dispatch_linear<T>(s, al, bl, em, M, N, K, ws);
+    }
     return dispatch_linear<T>(s, al, bl, ep, M, N, K, ws);
 }
 template <typename T>
@@ -760,18 +767,38 @@ size_t linear_ws(int M, int K, int N) {
     return dispatch_linear_ws<T>(M, N, K);
 }
 
+// Final epilogue of a dense weight gradient whose H operand carries the ones column: C[n][k < K] -> dW[n][k],
+// C[n][K] -> db[n] (the bias gradient, a column sum of dy, from the same GEMM and split-K reduction).
+struct StoreWgradBias {
+    float* dW;
+    float* db;
+    int K;
+    struct Row {
+        float* r;
+        int m;
+    };
+    __device__ void set_phase(int) {}
+    __device__ Row row(int m) const { return Row{dW + (int64_t)m * K, m}; }
+    __device__ void store(const Row& rw, int n, float v) const {
+        if (n < K) rw.r[n] = v;
+        else db[rw.m] = v;
+    }
+};
+
 template <typename T>
-int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int Mb, int N, int K, float* dW, Ws ws) {
+int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int Mb, int N, int K, float* dW, float* db,
+                 Ws ws) {
     constexpr int V = Vec16<T>::N;
-    KRowDense<T> ll{dy, lddy, Mb, N, (lddy % V == 0) && aligned16(dy)};
-    KRowDense<T> hl{x, ldx, Mb, K, (ldx % V == 0) && aligned16(x)};
-    StoreRM<float> ep{dW, nullptr, K, 0, 0};
+    KRowDense<T> ll{dy, lddy, Mb, N, (lddy % V == 0) && aligned16(dy), false};
+    KRowDense<T> hl{x, ldx, Mb, K, (ldx % V == 0) && aligned16(x), db != nullptr};
     probe::site(probe::kLinearWgrad, 2.0 * N * K * Mb, (double)sizeof(T) * ((double)Mb * N + (double)Mb * K) + 4.0 * N * K);
+    if (db) return dispatch_tn<T>(s, ll, hl, StoreWgradBias{dW, db, K}, N, K + 1, Mb, ws);
+    StoreRM<float> ep{dW, nullptr, K, 0, 0};
     return dispatch_tn<T>(s, ll, hl, ep, N, K, Mb, ws);
 }
 template <typename T>
-size_t linear_wgrad_ws(int Mb, int N, int K) {
-    return dispatch_tn_ws<T>(N, K, Mb);
+size_t linear_wgrad_ws(int Mb, int N, int K) {  // with or without the bias column
+    return std::max(dispatch_tn_ws<T>(N, K, Mb), dispatch_tn_ws<T>(N, K + 1, Mb));
 }
 
 #define INST(T)                                                                                                     \
@@ -784,16 +811,16 @@ size_t linear_wgrad_ws(int Mb, int N, int K) {
     template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws);                \
     template size_t wgrad_s2_ws<T>(int, int, int, int, int);                                                       \
     template int linear<T, T>(hipStream_t, const T*, int, int, int, const T*, int, const float*, int, T*, int, int, \
-                              int, Ws);                                                                            \
+                              int, Ws, const T*);                                                                  \
     template size_t linear_ws<T>(int, int, int);                                                                   \
-    template int linear_wgrad<T>(hipStream_t, const T*, int, const T*, int, int, int, int, float*, Ws);            \
+    template int linear_wgrad<T>(hipStream_t, const T*, int, const T*, int, int, int, int, float*, float*, Ws);    \
     template size_t linear_wgrad_ws<T>(int, int, int);
 
 INST(float)
 INST(bf16)
 #undef INST
 template int linear<bf16, float>(hipStream_t, const bf16*, int, int, int, const bf16*, int, const float*, int, float*,
-                                 int, int, int, Ws);
+                                 int, int, int, Ws, const float*);
 
 }  // namespace ops
 }  // namespace hlmc

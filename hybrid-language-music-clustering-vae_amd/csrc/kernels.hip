@@ -884,13 +884,17 @@ __global__ void cast2d_kernel(const TI* __restrict__ x, int ldx, TO* __restrict_
     }
 }
 template <typename T>
-__global__ void nhwc_to_flat_kernel(const T* __restrict__ x, int B, int h, int w, int C, T* __restrict__ y, int ldy) {
+__global__ void nhwc_to_flat_kernel(const T* __restrict__ x, int B, int h, int w, int C, T* __restrict__ y, int ldy,
+                                    const T* __restrict__ relu_ref) {
     const int F = C * h * w;
     int64_t n = (int64_t)B * F;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         int b = (int)(i / F), f = (int)(i % F);
         int c = f / (h * w), hw = f % (h * w);
-        y[(int64_t)b * ldy + f] = x[((int64_t)b * h * w + hw) * C + c];
+        const int64_t o = (int64_t)b * ldy + f;
+        T v = x[((int64_t)b * h * w + hw) * C + c];
+        if (relu_ref && !(to_f32<T>(relu_ref[o]) > 0.f)) v = from_f32<T>(0.f);
+        y[o] = v;
     }
 }
 template <typename T>
@@ -901,14 +905,6 @@ __global__ void flat_to_nhwc_kernel(const T* __restrict__ x, int ldx, int B, int
         int b = (int)(i / F), rem = (int)(i % F);
         int hw = rem / C, c = rem % C;  // i enumerates the NHWC output
         y[i] = x[(int64_t)b * ldx + (int64_t)c * h * w + hw];
-    }
-}
-template <typename T>
-__global__ void relu_bwd_kernel(T* __restrict__ dy, int lddy, const T* __restrict__ y, int ldy, int rows, int cols) {
-    int64_t n = (int64_t)rows * cols;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        int r = (int)(i / cols), c = (int)(i % cols);
-        if (!(to_f32<T>(y[(int64_t)r * ldy + c]) > 0.f)) dy[(int64_t)r * lddy + c] = from_f32<T>(0.f);
     }
 }
 template <typename T>
@@ -983,15 +979,16 @@ __global__ void reparam_rng_kernel(const float* __restrict__ mu, const float* __
 
 template <typename T>
 __global__ void reparam_bwd_kernel(const T* __restrict__ dz, int lddz, const float* __restrict__ lv,
-                                   const float* __restrict__ eps, int n_rows, int L, float* __restrict__ dmu,
-                                   float* __restrict__ dlv) {
+                                   const float* __restrict__ eps, const float* __restrict__ d_mu,
+                                   const float* __restrict__ d_lv, int n_rows, int L, T* __restrict__ gmu,
+                                   T* __restrict__ glv) {
     int64_t n = (int64_t)n_rows * L;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         int r = (int)(i / L), c = (int)(i % L);
         float g = to_f32<T>(dz[(int64_t)r * lddz + c]);
         float sd = expf(0.5f * lv[i]);
-        dmu[i] += g;
-        dlv[i] += g * eps[i] * sd * 0.5f;
+        gmu[i] = from_f32<T>((d_mu ? d_mu[i] : 0.f) + g);
+        glv[i] = from_f32<T>((d_lv ? d_lv[i] : 0.f) + g * eps[i] * sd * 0.5f);
     }
 }
 
@@ -1502,20 +1499,14 @@ int cast2d_from_f32(hipStream_t s, const float* x, int ldx, T* y, int ldy, int r
     return HLMC_OK;
 }
 template <typename T>
-int nhwc_to_flat(hipStream_t s, const T* x, int B, int h, int w, int C, T* y, int ldy) {
-    nhwc_to_flat_kernel<T><<<grid_for((int64_t)B * C * h * w), kThreads, 0, s>>>(x, B, h, w, C, y, ldy);
+int nhwc_to_flat(hipStream_t s, const T* x, int B, int h, int w, int C, T* y, int ldy, const T* relu_ref) {
+    nhwc_to_flat_kernel<T><<<grid_for((int64_t)B * C * h * w), kThreads, 0, s>>>(x, B, h, w, C, y, ldy, relu_ref);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
 template <typename T>
 int flat_to_nhwc(hipStream_t s, const T* x, int ldx, int B, int h, int w, int C, T* y) {
     flat_to_nhwc_kernel<T><<<grid_for((int64_t)B * C * h * w), kThreads, 0, s>>>(x, ldx, B, h, w, C, y);
-    HLMC_LAUNCHED();
-    return HLMC_OK;
-}
-template <typename T>
-int relu_bwd(hipStream_t s, T* dy, int lddy, const T* y, int ldy, int rows, int cols) {
-    relu_bwd_kernel<T><<<grid_for((int64_t)rows * cols), kThreads, 0, s>>>(dy, lddy, y, ldy, rows, cols);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1613,9 +1604,10 @@ int reparam_rng(hipStream_t s, const float* mu, const float* lv, uint64_t seed, 
     return HLMC_OK;
 }
 template <typename T>
-int reparam_bwd(hipStream_t s, const T* dz, int lddz, const float* lv, const float* eps, int n_rows, int L, float* dmu,
-                float* dlv) {
-    reparam_bwd_kernel<T><<<grid_for((int64_t)n_rows * L), kThreads, 0, s>>>(dz, lddz, lv, eps, n_rows, L, dmu, dlv);
+int reparam_bwd(hipStream_t s, const T* dz, int lddz, const float* lv, const float* eps, const float* d_mu,
+                const float* d_lv, int n_rows, int L, T* gmu, T* glv) {
+    reparam_bwd_kernel<T><<<grid_for((int64_t)n_rows * L), kThreads, 0, s>>>(dz, lddz, lv, eps, d_mu, d_lv, n_rows, L,
+                                                                            gmu, glv);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1737,13 +1729,13 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
     template int cast_to_f32<T>(hipStream_t, const T*, float*, int64_t);                                             \
     template int copy2d<T>(hipStream_t, const T*, int, T*, int, int, int);                                           \
     template int cast2d_from_f32<T>(hipStream_t, const float*, int, T*, int, int, int);                              \
-    template int nhwc_to_flat<T>(hipStream_t, const T*, int, int, int, int, T*, int);                                \
+    template int nhwc_to_flat<T>(hipStream_t, const T*, int, int, int, int, T*, int, const T*);                      \
     template int flat_to_nhwc<T>(hipStream_t, const T*, int, int, int, int, int, T*);                                \
-    template int relu_bwd<T>(hipStream_t, T*, int, const T*, int, int, int);                                         \
     template int colsum<T>(hipStream_t, const T*, int, int, int, float*, Ws);                                        \
     template int reparam_fwd<T>(hipStream_t, const float*, const float*, const float*, int, int, T*, int);           \
     template int reparam_rng<T>(hipStream_t, const float*, const float*, uint64_t, uint64_t, int, int, float*, T*, int); \
-    template int reparam_bwd<T>(hipStream_t, const T*, int, const float*, const float*, int, int, float*, float*);   \
+    template int reparam_bwd<T>(hipStream_t, const T*, int, const float*, const float*, const float*, const float*,  \
+                                int, int, T*, T*);                                                                  \
     template int pack<T>(hipStream_t, const AdamJob*, int, int);                                                     \
     template int adam_pack<T>(hipStream_t, const AdamJob*, int, int, AdamArgs, const float*, int);
 

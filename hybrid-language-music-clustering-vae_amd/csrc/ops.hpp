@@ -51,15 +51,19 @@ template <typename T>
 size_t wgrad_s2_ws(int B, int Hl, int Wl, int M, int C);
 
 // y[m*ldy + n] (+)= act(sum_k x[m*ldx+k] * w[n*ldw+k] + bias[n]),  act 0 none / 1 relu
+// relu_ref (nullable, row stride ldy, act == 0): the stored value is zeroed where relu_ref <= 0 — the data gradient
+// of a dense layer with the ReLU backward of the layer below applied in the epilogue (after the accumulate)
 template <typename T, typename OutT>
 int linear(hipStream_t s, const T* x, int ldx, int M, int K, const T* w, int ldw, const float* bias, int N, OutT* y,
-           int ldy, int act, int accumulate, Ws ws);
+           int ldy, int act, int accumulate, Ws ws, const OutT* relu_ref = nullptr);
 template <typename T>
 size_t linear_ws(int M, int K, int N);
 
-// dW[n][k] = sum_b dy[b*lddy+n] * x[b*ldx+k]
+// dW[n][k] = sum_b dy[b*lddy+n] * x[b*ldx+k];  db[n] = sum_b dy[b*lddy+n] (nullable: the same GEMM with a
+// virtual ones column appended to x, so no separate column-sum launches)
 template <typename T>
-int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int Mb, int N, int K, float* dW, Ws ws);
+int linear_wgrad(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int Mb, int N, int K, float* dW, float* db,
+                 Ws ws);
 template <typename T>
 size_t linear_wgrad_ws(int Mb, int N, int K);
 
@@ -128,10 +132,10 @@ template <typename T> int cast_to_f32(hipStream_t s, const T* x, float* y, int64
 template <typename T> int copy2d(hipStream_t s, const T* x, int ldx, T* y, int ldy, int rows, int cols);
 template <typename T> int cast2d_from_f32(hipStream_t s, const float* x, int ldx, T* y, int ldy, int rows, int cols);
 // NHWC [B,h,w,C] <-> flat NCHW [B, C*h*w] (ld = row stride of the flat side)
-template <typename T> int nhwc_to_flat(hipStream_t s, const T* x, int B, int h, int w, int C, T* y, int ldy);
+// relu_ref (nullable, row stride ldy): y zeroed where relu_ref <= 0 (ReLU backward fused into the relayout)
+template <typename T>
+int nhwc_to_flat(hipStream_t s, const T* x, int B, int h, int w, int C, T* y, int ldy, const T* relu_ref = nullptr);
 template <typename T> int flat_to_nhwc(hipStream_t s, const T* x, int ldx, int B, int h, int w, int C, T* y);
-// dy[i] *= (y[i] > 0) for an [rows][cols] slice (relu backward on the stored post-relu output)
-template <typename T> int relu_bwd(hipStream_t s, T* dy, int lddy, const T* y, int ldy, int rows, int cols);
 // db[n] = sum_r dy[r*ld + n]
 template <typename T> int colsum(hipStream_t s, const T* dy, int ld, int rows, int cols, float* db, Ws ws);
 size_t colsum_ws(int rows, int cols);
@@ -143,8 +147,11 @@ template <typename T>
 int reparam_rng(hipStream_t s, const float* mu, const float* lv, uint64_t seed, uint64_t offset, int n_rows, int L,
                 float* eps_out, T* z, int ldz);
 template <typename T> int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz);
-// dmu += dz ; dlv += dz * eps * 0.5 exp(0.5 lv)
-template <typename T> int reparam_bwd(hipStream_t s, const T* dz, int lddz, const float* lv, const float* eps, int n_rows, int L, float* dmu, float* dlv);
+// latent-head gradients in one pass: gmu = d_mu + dz ; glv = d_lv + dz * eps * 0.5 exp(0.5 lv), written as T
+// (the operand of the heads' data / weight gradients); d_mu / d_lv: the caller's loss gradients (nullable: 0)
+template <typename T>
+int reparam_bwd(hipStream_t s, const T* dz, int lddz, const float* lv, const float* eps, const float* d_mu,
+                const float* d_lv, int n_rows, int L, T* gmu, T* glv);
 
 // ---------------------------------------------------------------- loss (kernels.hip)
 // partial sums: out[0] = sum (ra-a)^2, out[1] = sum (rt-t)^2, out[2] = sum(1 + lv - mu^2 - e^lv)  (double)

@@ -284,11 +284,14 @@ int hlmc_op_subpixel(void* stream, int dtype, const void* x, int B, int Hi, int 
                      const float* bias, int Co, void* y, void* ws, int64_t ws_bytes);
 int hlmc_op_wgrad_s2(void* stream, int dtype, const void* L, int B, int Hl, int Wl, int M, const void* Xh, int C,
                      float* dW, void* ws, int64_t ws_bytes);
+/* relu_ref (nullable, row stride ldy, act 0): y zeroed where relu_ref <= 0 after the accumulate (a dense layer's
+ * data gradient with the ReLU backward of the layer below fused into the epilogue). */
 int hlmc_op_linear(void* stream, int dtype, const void* x, int ldx, int M, int K, const void* w, int ldw,
                    const float* bias, int N, void* y, int ldy, int act, int accumulate, int out_f32, void* ws,
-                   int64_t ws_bytes);
+                   int64_t ws_bytes, const void* relu_ref);
+/* db (nullable): the bias gradient sum_b dy[b][n], from the same GEMM (a virtual ones column on x). */
 int hlmc_op_linear_wgrad(void* stream, int dtype, const void* dy, int lddy, const void* x, int ldx, int Mb, int N,
-                         int K, float* dW, void* ws, int64_t ws_bytes);
+                         int K, float* dW, float* db, void* ws, int64_t ws_bytes);
 int hlmc_op_conv_c1_s2(void* stream, int dtype, const float* x, int B, int Hi, int Wi, const float* w,
                        const float* bias, int Co, void* y);
 int hlmc_op_convT_c1(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const float* w,

@@ -137,8 +137,31 @@ def test_linear(cuda, ws, dt, M, K, N, ldx, act, acc):
     y = y0.to(cuda, tdt).contiguous()
     xd, wd, bd = x.to(cuda, tdt).contiguous(), wpad.to(cuda, tdt), b.to(cuda)
     L.check(L.lib().hlmc_op_linear(L.stream(), code, xd.data_ptr(), ldx, M, K, wd.data_ptr(), ldw, bd.data_ptr(), N,
-                                   y.data_ptr(), N, act, acc, 0, ws.data_ptr(), WS_BYTES))
+                                   y.data_ptr(), N, act, acc, 0, ws.data_ptr(), WS_BYTES, None))
     assert rel(y, ref) < tol
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,K,N,acc", [(256, 2048, 1024, 0), (256, 512, 512, 1), (4, 16384, 1024, 0), (3, 64, 40, 1)])
+def test_linear_relu_mask(cuda, ws, dt, M, K, N, acc):
+    """Dense data gradient with the ReLU backward of the layer below in the epilogue (engine.cpp lin_bwd)."""
+    code, tdt, tol = DT[dt]
+    g = torch.Generator().manual_seed(M * 7 + K + N)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    y0 = torch.randn(M, N, generator=g)
+    act = torch.randn(M, N, generator=g).clamp_min(0)  # post-ReLU activation: ~half the entries exactly 0
+    ref = q(x, tdt) @ q(w, tdt).T
+    if acc:
+        ref = ref + q(y0, tdt)
+    ref = torch.where(q(act, tdt) > 0, ref, torch.zeros_like(ref))
+    y = y0.to(cuda, tdt).contiguous()
+    xd, wd, ad = x.to(cuda, tdt).contiguous(), w.to(cuda, tdt).contiguous(), act.to(cuda, tdt).contiguous()
+    L.check(L.lib().hlmc_op_linear(L.stream(), code, xd.data_ptr(), K, M, K, wd.data_ptr(), K, None, N,
+                                   y.data_ptr(), N, 0, acc, 0, ws.data_ptr(), WS_BYTES, ad.data_ptr()))
+    torch.cuda.synchronize()
+    assert rel(y, ref) < tol
+    assert bool((y.float().cpu()[act.to(tdt) <= 0] == 0).all())
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
@@ -151,11 +174,20 @@ def test_linear_wgrad(cuda, ws, dt, Mb, N, K):
     dy = torch.randn(Mb, ldd, generator=g)
     x = torch.randn(Mb, ldx, generator=g)
     ref = q(dy[:, :N], tdt).T @ q(x[:, :K], tdt)
-    dW = torch.empty(N, K, device=cuda)
+    ref_b = q(dy[:, :N], tdt).sum(0)
     dyd, xd = dy.to(cuda, tdt).contiguous(), x.to(cuda, tdt).contiguous()
-    L.check(L.lib().hlmc_op_linear_wgrad(L.stream(), code, dyd.data_ptr(), ldd, xd.data_ptr(), ldx, Mb, N, K,
-                                         dW.data_ptr(), ws.data_ptr(), WS_BYTES))
-    assert rel(dW, ref) < (1e-5 if dt == "fp32" else 5e-3)
+    for with_bias in (False, True):  # the bias gradient through the GEMM's ones column, and without it
+        dW = torch.full((N, K), float("nan"), device=cuda)
+        db = torch.full((N,), float("nan"), device=cuda)
+        L.check(L.lib().hlmc_op_linear_wgrad(L.stream(), code, dyd.data_ptr(), ldd, xd.data_ptr(), ldx, Mb, N, K,
+                                             dW.data_ptr(), db.data_ptr() if with_bias else None, ws.data_ptr(),
+                                             WS_BYTES))
+        torch.cuda.synchronize()
+        assert rel(dW, ref) < (1e-5 if dt == "fp32" else 5e-3)
+        if with_bias:
+            assert rel(db, ref_b) < 1e-5  # dy x 1 is exact in either dtype; f32 accumulation
+        else:
+            assert bool(db.isnan().all())
 
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <functional>
 
 namespace hlmc {
 namespace {
@@ -186,6 +187,7 @@ class NetT : public NetBase {
     // called in backward once every non-late weight gradient has been issued
     int prelate(hipStream_t s) {
         if (!tail_overlap()) return HLMC_OK;
+        HLMC_TRY(flush_side(s));
         HLMC_TRY(fork(s));
         HLMC_HIP(hipEventRecord(prelate_ev, s2));
         return HLMC_OK;
@@ -237,18 +239,56 @@ class NetT : public NetBase {
     }
     int join(hipStream_t s) {
         if (!use_side || !s2) return HLMC_OK;
+        HLMC_TRY(flush_side(s));
         hipEvent_t e = next_ev();
         HLMC_HIP(hipEventRecord(e, s2));
         HLMC_HIP(hipStreamWaitEvent(s, e, 0));
         return HLMC_OK;
     }
-    // run f(stream, scratch) on the weight-gradient stream, ordered after the work issued so far on s
-    template <class F>
-    int side(hipStream_t s, F&& f) {
-        if (!use_side) return f(s, scratch);
-        HLMC_TRY(fork(s));
-        return f(s2, scratch2);
+    // Weight-gradient work queued for the second stream.  A fork (event record on s, wait on s2) costs the main
+    // stream a ~6 us bubble (measured: scripts/step_gaps.py), so queued work is issued in batches behind one
+    // fork: the queue is flushed once it holds `batch` items (and by join / mark / prelate).  Every buffer a
+    // queued op reads is written once per backward, so issuing it later is safe; it only waits longer.
+    using SideFn = std::function<int(hipStream_t, Ws)>;
+    std::vector<SideFn> side_q;
+    int issue_side() {
+        int rc = HLMC_OK;
+        for (auto& f : side_q)
+            if (rc == HLMC_OK) rc = f(s2, scratch2);
+        side_q.clear();
+        return rc;
     }
+    int flush_side(hipStream_t s) {
+        if (side_q.empty()) return HLMC_OK;
+        HLMC_TRY(fork(s));
+        return issue_side();
+    }
+    // queue f(stream, scratch) for the weight-gradient stream (ordered after the work issued so far on s);
+    // inline on s without the second stream
+    int defer_side(hipStream_t s, SideFn f, int batch) {
+        if (!use_side) return f(s, scratch);
+        side_q.push_back(std::move(f));
+        return (int)side_q.size() >= batch ? flush_side(s) : HLMC_OK;
+    }
+    // conv layers / dense layers per fork (HLMC_SIDE_BATCH / HLMC_DENSE_BATCH: measurement aids).  Measured on the
+    // bench step (scripts/gpu_r3_knobs.sh, 3 alternating rounds): conv 1 / dense 1 108.4k, 2 / 1 109.7k, 2 / 2
+    // 110.3k, 3 / 1 108.2k, 6 / 1 104.3k (the weight-gradient stream starts too late), 2 / 9 108.1k
+    static int side_batch() {
+        static const int n = [] {
+            const char* e = std::getenv("HLMC_SIDE_BATCH");
+            return e ? std::max(1, std::atoi(e)) : 2;
+        }();
+        return n;
+    }
+    static int dense_batch() {
+        static const int n = [] {
+            const char* e = std::getenv("HLMC_DENSE_BATCH");
+            return e ? std::max(1, std::atoi(e)) : 2;
+        }();
+        return n;
+    }
+    // run f on the weight-gradient stream now (with everything queued before it)
+    int side(hipStream_t s, SideFn f) { return defer_side(s, std::move(f), 1); }
     // weight gradients of the dense layers: on the second stream (HLMC_DENSE_SIDE=1, default) or inline on s
     // (their GEMMs are 5-20 us, about the main-stream bubble a fork's event marker costs)
     bool dense_side_on() const {
@@ -263,7 +303,8 @@ class NetT : public NetBase {
         if (!this->bucket_sync) return HLMC_OK;
         HLMC_CHECK_ARG(k >= 0 && k < (int)this->bucket_ev.size(), "bucket index");
         if (use_side && k + 1 < (int)this->bucket_ev.size()) {
-            HLMC_TRY(fork(s));
+            if (side_q.empty()) HLMC_TRY(fork(s));
+            else HLMC_TRY(flush_side(s));
             HLMC_HIP(hipEventRecord(this->bucket_ev[k], s2));
         } else {  // the last bucket: the caller has joined the weight-gradient stream
             HLMC_HIP(hipEventRecord(this->bucket_ev[k], s));
@@ -304,12 +345,20 @@ class NetT : public NetBase {
     int lin_bwd(hipStream_t s, const T* dy, int lddy, const T* x, int ldx, int B, int w, int b, T* dx, int lddx,
                 int acc = 0, const T* relu_ref = nullptr) {
         const int N = (int)params[w].shape[0], K = (int)params[w].shape[1];
-        const bool sd = dense_side_on();
-        if (sd) HLMC_TRY(fork(s));
+        float* gw = G[w];
+        float* gb = b >= 0 ? G[b] : nullptr;
+        SideFn wg = [=](hipStream_t q, Ws sc) { return ops::linear_wgrad<T>(q, dy, lddy, x, ldx, B, N, K, gw, gb, sc); };
+        if (!dense_side_on()) {
+            if (dx)
+                HLMC_TRY(ops::linear<T, T>(s, dy, lddy, B, N, P1(w), ld1(w), nullptr, K, dx, lddx, 0, acc, scratch, relu_ref));
+            return wg(s, scratch);
+        }
+        side_q.push_back(std::move(wg));
+        const bool go = (int)side_q.size() >= dense_batch();
+        if (go) HLMC_TRY(fork(s));
         if (dx)
             HLMC_TRY(ops::linear<T, T>(s, dy, lddy, B, N, P1(w), ld1(w), nullptr, K, dx, lddx, 0, acc, scratch, relu_ref));
-        return ops::linear_wgrad<T>(sd ? s2 : s, dy, lddy, x, ldx, B, N, K, G[w], b >= 0 ? G[b] : nullptr,
-                                    sd ? scratch2 : scratch);
+        return go ? issue_side() : HLMC_OK;
     }
 
     struct BnBufs {
@@ -353,7 +402,7 @@ class NetT : public NetBase {
             if (defer_bias)
                 pend_bias = PendingBias{bp, np, C, gb};
             else
-                HLMC_TRY(side(s, [&](hipStream_t q, Ws w2) { return ops::colsum_finalize(q, bp, np, C, gb, w2); }));
+                HLMC_TRY(side(s, [=](hipStream_t q, Ws w2) { return ops::colsum_finalize(q, bp, np, C, gb, w2); }));
         }
         return HLMC_OK;
     }
@@ -364,14 +413,14 @@ class NetT : public NetBase {
     };
     PendingBias pend_bias;
     // f on the weight-gradient stream, after the bias reduction a preceding bn_bwd(defer_bias) left pending
-    template <class F>
-    int side_bias(hipStream_t s, F&& f) {
+    // (queued: flushed every side_batch() layers)
+    int side_bias(hipStream_t s, SideFn f) {
         const PendingBias pb = pend_bias;
         pend_bias = PendingBias{};
-        return side(s, [&](hipStream_t q, Ws sc) {
+        return defer_side(s, [pb, f](hipStream_t q, Ws sc) {
             if (pb.bp) HLMC_TRY(ops::colsum_finalize(q, pb.bp, pb.np, pb.C, pb.gb, sc));
             return f(q, sc);
-        });
+        }, side_batch());
     }
     // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
     static bool tail_on_main() {
@@ -480,10 +529,11 @@ class NetT : public NetBase {
                 if (pb.bp) HLMC_TRY(ops::colsum_finalize(s, pb.bp, pb.np, pb.C, pb.gb, scratch));
                 HLMC_TRY(ops::wgrad_c1<T>(s, dy, B, ho, wo, co, audio, gw, scratch));
             } else if (l == 0) {
-                HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
+                HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
             } else {
                 const T* xin = AT(enc.a[l - 1]);
-                HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
+                HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
+                if (l == 1) HLMC_TRY(flush_side(s));  // nothing queued may wait for the join behind the main tail
                 // grad of layer l-1's activation
                 HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));
             }
@@ -578,7 +628,7 @@ class NetT : public NetBase {
             float* gw = G[dec.w[5]];
             float* gb = G[dec.b[5]];
             const int npix = B * hs[6] * ws_[6];
-            HLMC_TRY(side(s, [&](hipStream_t q, Ws sc) {
+            HLMC_TRY(side(s, [=](hipStream_t q, Ws sc) {
                 HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
                 return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
             }));
@@ -598,7 +648,7 @@ class NetT : public NetBase {
                             &fuse, reinterpret_cast<double*>(ws + dec.bpart[l]), true));
             const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
             float* gw = G[dec.w[l]];
-            HLMC_TRY(side_bias(s, [&](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
+            HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
             HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
             fuse = ops::BnBwdFuse{};  // the stride-2 conv data gradients carry no moments: a separate pass
         }

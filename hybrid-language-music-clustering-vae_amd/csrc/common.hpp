@@ -144,6 +144,98 @@ struct FastDiv {
 };
 
 
+// ------------------------------------------------------------------ exact column-sum accumulators
+// Per-column sums that many blocks of one launch contribute to (BatchNorm batch statistics, backward moments, bias
+// gradients), delivered straight from the producing blocks instead of as per-block f64 rows that a separate fold
+// launch reduces.  Each block's f64 partial v is split into three integer words -- floor(v), the next 32 fraction
+// bits, the 32 after those (bits below 2^-64 truncated; |v| clamped below 2^62) -- and added with no-return agent-scope
+// int64 atomics (performed at the memory side, coherent across the XCDs).  Integer addition is associative, so the
+// totals are bit-identical whatever order the blocks arrive in (deterministic), and exact: the only rounding is the
+// consumer's single conversion back to f64.  Blocks spread their adds over `shards` copies (block id mod shards) so
+// that no address sees more than a few dozen adders.  Layout: [shards][3 words][ncols] int64, zeroed before the
+// producer runs (one memset per pass for all of a pass's accumulators); the consumer sums the shards' words.
+struct XAcc {
+    unsigned long long* p = nullptr;
+    int shards = 0;
+    int ncols = 0;
+    __host__ __device__ bool on() const { return p != nullptr; }
+    static size_t bytes(int shards, int ncols) { return (size_t)shards * 3 * ncols * 8; }
+};
+// shards for a BatchNorm pair table (2C columns): the consumer folds shards x 6C words per block, so fewer shards for
+// wider layers (whose producers also have fewer blocks)
+inline int xacc_shards(int C) { return C >= 512 ? 2 : C >= 256 ? 4 : C >= 128 ? 8 : 16; }
+constexpr int kXAccMaxShards = 16;
+
+__device__ __forceinline__ void xacc_add_shard(const XAcc& x, int shard, int col, double v) {
+    v = fmin(fmax(v, -4.0e18), 4.0e18);
+    const double f = floor(v);
+    const double r1 = (v - f) * 4294967296.0;  // exact: v - floor(v) and power-of-two scales
+    const double g = floor(r1);
+    const double r2 = (r1 - g) * 4294967296.0;
+    unsigned long long* b = x.p + (size_t)shard * 3 * x.ncols + col;
+    atomicAdd(b, (unsigned long long)(long long)f);
+    atomicAdd(b + x.ncols, (unsigned long long)(long long)g);
+    atomicAdd(b + 2 * x.ncols, (unsigned long long)(long long)floor(r2));
+}
+__device__ __forceinline__ void xacc_add(const XAcc& x, int col, double v) {
+    xacc_add_shard(x, (int)(blockIdx.x % (unsigned)x.shards), col, v);
+}
+__device__ __forceinline__ double xacc_value(long long a, long long b, long long c) {
+    return (double)a + ((double)b * 0x1p-32 + (double)c * 0x1p-64);
+}
+// out[c] (LDS, c < ncols) = the accumulator's column totals; every thread of the block calls it (blockDim.x == NT);
+// red: LDS scratch of >= 3 * NT int64 (used when ncols < NT).  Thread (column c, shard group g) issues the loads of
+// all its shards at once (<= 8 shards x 3 words in flight; clamped addresses, masked adds).  Ends with a barrier.
+template <int NT = 256>
+__device__ __forceinline__ void xacc_fold(const XAcc& x, double* out, long long* red) {
+    constexpr int K = 8;  // shards per thread group (shards <= K * G, checked by the launchers via xacc_shards)
+    const int tid = threadIdx.x, n = x.ncols, S = x.shards;
+    const int G = n >= NT ? 1 : NT / n;
+    auto sum = [&](int c, int g, long long& a, long long& b, long long& d) {
+        unsigned long long w0[K], w1[K], w2[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int sh = min(g + k * G, S - 1);
+            const unsigned long long* q = x.p + (size_t)sh * 3 * n + c;
+            w0[k] = q[0];
+            w1[k] = q[n];
+            w2[k] = q[2 * n];
+        }
+        a = b = d = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (g + k * G < S) {
+                a += (long long)w0[k];
+                b += (long long)w1[k];
+                d += (long long)w2[k];
+            }
+    };
+    if (n >= NT) {
+        for (int c = tid; c < n; c += NT) {
+            long long a, b, d;
+            sum(c, 0, a, b, d);
+            out[c] = xacc_value(a, b, d);
+        }
+    } else {
+        const int c = tid % n, g = tid / n;
+        long long a = 0, b = 0, d = 0;
+        if (g < G) sum(c, g, a, b, d);
+        red[tid] = a;
+        red[NT + tid] = b;
+        red[2 * NT + tid] = d;
+        __syncthreads();
+        if (tid < n) {
+            for (int k = 1; k < G; ++k) {
+                a += red[k * n + tid];
+                b += red[NT + k * n + tid];
+                d += red[2 * NT + k * n + tid];
+            }
+            out[tid] = xacc_value(a, b, d);
+        }
+    }
+    __syncthreads();
+}
+
 // wave-level sums (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -134,7 +134,8 @@ class NetT : public NetBase {
     char* ws = nullptr;
     Ws scratch{nullptr, 0};
     Ws scratch2{nullptr, 0};  // split-K / reduction scratch of the weight-gradient stream
-    size_t scratch_off = 0, scratch2_off = 0, scratch_bytes = 0;
+    Ws scratch3{nullptr, 0};  // ... and of the third stream (side3)
+    size_t scratch_off = 0, scratch2_off = 0, scratch3_off = 0, scratch_bytes = 0;
     int64_t planned_B = -1;
     size_t ws_total = 0;
 
@@ -143,17 +144,34 @@ class NetT : public NetBase {
     uint8_t* AU8(size_t off) const { return reinterpret_cast<uint8_t*>(ws + off); }
 
     void need(size_t b) { scratch_bytes = std::max(scratch_bytes, b); }
+    // exact statistics accumulators (common.hpp XAcc): every BatchNorm layer's forward statistics in one region, its
+    // backward moments and bias column sums in the next; zeroed by one memset per train forward (and by backward
+    // when it runs again without a forward in between)
+    size_t xf_total = 0, xb_total = 0, xf_base = 0, xb_base = 0;
+    bool bwd_acc_clean = false;
+    int zero_acc_fwd(hipStream_t s) {
+        if (xf_total + xb_total) HLMC_HIP(hipMemsetAsync(ws + xf_base, 0, xf_total + xb_total, s));
+        bwd_acc_clean = true;
+        return HLMC_OK;
+    }
+    int zero_acc_bwd(hipStream_t s) {
+        if (!bwd_acc_clean && xb_total) HLMC_HIP(hipMemsetAsync(ws + xb_base, 0, xb_total, s));
+        bwd_acc_clean = false;
+        return HLMC_OK;
+    }
 
     virtual void plan(Arena& A, int64_t B) = 0;
     size_t ws_bytes(int64_t B) override {
         if (B != planned_B) {
             Arena A;
             scratch_bytes = 0;
-            bnb_part_bytes = 0;
+            xf_total = xb_total = 0;
             plan(A, B);
             scratch_off = A.take(scratch_bytes + 256);
             scratch2_off = A.take(scratch_bytes + 256);
-            bnb_part_off = A.take(bnb_part_bytes + 256);
+            scratch3_off = A.take(scratch_bytes + 256);
+            xf_base = A.take(xf_total);  // xb directly after xf (one memset covers both: 256-aligned sizes)
+            xb_base = A.take(xb_total);
             ws_total = A.used;
             planned_B = B;
         }
@@ -163,6 +181,7 @@ class NetT : public NetBase {
         ws = reinterpret_cast<char*>(w);
         scratch = Ws{reinterpret_cast<float*>(ws + scratch_off), scratch_bytes + 256};
         scratch2 = Ws{reinterpret_cast<float*>(ws + scratch2_off), scratch_bytes + 256};
+        scratch3 = Ws{reinterpret_cast<float*>(ws + scratch3_off), scratch_bytes + 256};
     }
 
     // ---------------------------------------------------------------- weight-gradient stream
@@ -172,6 +191,10 @@ class NetT : public NetBase {
     // a forked op reads is written once per backward; backward() joins the stream before returning.
     // HLMC_SIDE_STREAM=0 keeps everything on the caller's stream (A/B measurement aid).
     hipStream_t s2 = nullptr;
+    // A third stream for the last, largest weight gradients of backward (the encoder's 32 x 32 / 16 x 16 layers):
+    // on the second stream they queue behind each other at the tail, where that stream is the critical path
+    hipStream_t s3 = nullptr;
+    bool s3_used = false;
     std::vector<hipEvent_t> evs;
     int ev_next = 0;
     bool use_side = true;
@@ -179,6 +202,7 @@ class NetT : public NetBase {
     bool join_pending = false;         // backward left the side stream running (NetBase::overlap_adam)
     ~NetT() override {
         if (s2) (void)hipStreamDestroy(s2);
+        if (s3) (void)hipStreamDestroy(s3);
         for (auto e : evs) (void)hipEventDestroy(e);
         for (auto e : this->bucket_ev) (void)hipEventDestroy(e);
         if (prelate_ev) (void)hipEventDestroy(prelate_ev);
@@ -214,6 +238,7 @@ class NetT : public NetBase {
         use_side = !env_off;
         if (use_side && !s2) {
             HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+            HLMC_HIP(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
             evs.resize(32);
             for (auto& e : evs) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             HLMC_HIP(hipEventCreateWithFlags(&prelate_ev, hipEventDisableTiming));
@@ -243,6 +268,12 @@ class NetT : public NetBase {
         hipEvent_t e = next_ev();
         HLMC_HIP(hipEventRecord(e, s2));
         HLMC_HIP(hipStreamWaitEvent(s, e, 0));
+        if (s3_used) {
+            hipEvent_t e3 = next_ev();
+            HLMC_HIP(hipEventRecord(e3, s3));
+            HLMC_HIP(hipStreamWaitEvent(s, e3, 0));
+            s3_used = false;
+        }
         return HLMC_OK;
     }
     // Weight-gradient work queued for the second stream.  A fork (event record on s, wait on s2) costs the main
@@ -313,15 +344,21 @@ class NetT : public NetBase {
     }
 
     // ---------------------------------------------------------------- reparameterisation
-    // z = mu + eps * exp(0.5 logvar): eps from the caller (copied to eps_keep by the forward's copy_segments) or,
+    // z = mu + eps * exp(0.5 logvar): eps from the caller (copied to eps_keep by the same launch) or,
     // when the caller passes none, drawn on the device from the net's Philox stream (hlmc_net_set_rng) straight
     // into eps_keep (the backward's copy) — no host / torch launch for the noise
+    // mu_out / lv_out (nullable): the caller's latent outputs, written by the same launch
     int reparam(hipStream_t s, const float* eps_in, const float* mu, const float* lv, float* eps_keep, int B, int L,
-                T* z, int ldz) {
-        if (eps_in) return ops::reparam_fwd<T>(s, mu, lv, eps_keep, B, L, z, ldz);
+                T* z, int ldz, float* mu_out, float* lv_out) {
+        if (eps_in) return ops::reparam_fwd<T>(s, mu, lv, eps_in, B, L, z, ldz, mu_out, lv_out, eps_keep);
         const uint64_t off = this->rng_offset;
         this->rng_offset += ((uint64_t)B * L + 3) & ~uint64_t(3);
-        return ops::reparam_rng<T>(s, mu, lv, this->rng_seed, off, B, L, eps_keep, z, ldz);
+        return ops::reparam_rng<T>(s, mu, lv, this->rng_seed, off, B, L, eps_keep, z, ldz, mu_out, lv_out);
+    }
+    // encode only: the latent outputs
+    int latent_out(hipStream_t s, const ForwardArgs& a, const float* mu, const float* lv, int64_t nl) {
+        const ops::CopySeg cs[2] = {{a.mu, mu, nl}, {a.logvar, lv, nl}};
+        return ops::copy_segments(s, cs, 2);
     }
 
     // ---------------------------------------------------------------- layer helpers
@@ -362,53 +399,66 @@ class NetT : public NetBase {
     }
 
     struct BnBufs {
-        size_t mean = 0, inv = 0;
+        size_t mean = 0, inv = 0, sums = 0;
+        size_t xf = 0, xb = 0, xbias = 0;  // offsets in the forward / backward accumulator regions
+        int C = 0;
     };
-    // the part of the main scratch after n f64 partials that start at its base (fold space for their reduction)
-    Ws after_parts(const double* part, size_t n) const {
-        const size_t off = (n * sizeof(double) + 255) & ~(size_t)255;
-        if (reinterpret_cast<const void*>(part) != scratch.p || off >= scratch.bytes) return Ws{nullptr, 0};
-        return Ws{reinterpret_cast<float*>(reinterpret_cast<char*>(scratch.p) + off), scratch.bytes - off};
+    static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+    BnBufs bn_plan(Arena& A, int C) {
+        BnBufs b;
+        b.C = C;
+        b.mean = A.take(C * 4);
+        b.inv = A.take(C * 4);
+        b.sums = A.take(2 * C * 4);
+        b.xf = xf_total;
+        xf_total += al256(ops::bn_acc_bytes(C));
+        b.xb = xb_total;
+        xb_total += al256(ops::bn_acc_bytes(C));
+        b.xbias = xb_total;
+        xb_total += al256(ops::bias_acc_bytes(C));
+        return b;
     }
-    BnBufs bn_plan(Arena& A, int C) { return BnBufs{A.take(C * 4), A.take(C * 4)}; }
-    // st: statistics already emitted by the producing GEMM's epilogue (nparts > 0), else a separate pass
+    XAcc acc_at(size_t off, int C, int ncols) const {
+        return XAcc{reinterpret_cast<unsigned long long*>(ws + off), xacc_shards(C), ncols};
+    }
+    XAcc acc_fwd(const BnBufs& b) const { return acc_at(xf_base + b.xf, b.C, 2 * b.C); }
+    XAcc acc_mom(const BnBufs& b) const { return acc_at(xb_base + b.xb, b.C, 2 * b.C); }
+    XAcc acc_bias(const BnBufs& b) const { return acc_at(xb_base + b.xbias, b.C, b.C); }
+    // st: statistics already delivered by the producing kernel (st->done), else a moments pass first
     int bn_fwd(hipStream_t s, bool train, const T* y, int64_t R, int C, int bn, const BnBufs& bb, int g, int beta, int act,
                const uint8_t* mask, float mscale, T* a, int lda, const ops::ColStats* st = nullptr) {
         float* mean = AF(bb.mean);
         float* inv = AF(bb.inv);
-        if (train && st && st->nparts > 0)  // statistics finalized inside the activation kernel
-            return ops::bn_act_train<T>(s, y, R, C, st->part, st->nparts, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum,
-                                        kBnEps, P[g], P[beta], act, mask, mscale, a, lda,
-                                        after_parts(st->part, (size_t)st->nparts * 2 * C));
-        if (train)
-            return ops::bn_act_train<T>(s, y, R, C, nullptr, 0, mean, inv, RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps,
-                                        P[g], P[beta], act, mask, mscale, a, lda, scratch);
+        if (train)  // statistics finalized inside the activation kernel
+            return ops::bn_act_train<T>(s, y, R, C, acc_fwd(bb), st && st->done, mean, inv, RM[bn], RV[bn], NBT[bn],
+                                        kBnMomentum, kBnEps, P[g], P[beta], act, mask, mscale, a, lda);
         HLMC_TRY(ops::bn_eval_stats(s, RM[bn], RV[bn], C, kBnEps, mean, inv));
         return ops::bn_act<T>(s, y, R, C, mean, inv, P[g], P[beta], act, mask, mscale, a, lda);
     }
-    // fused: moments emitted by the GEMM that wrote da (nullable); bias_part: per-layer buffer of the conv bias
-    // column partials, reduced on the weight-gradient stream (nullable: reduced here)
+    // fused: moments delivered by the kernel that wrote da (nullable); bias_side: the conv bias column sums are
+    // reduced into the gradient on the weight-gradient stream (else here)
     // defer_bias: leave the bias reduction to the next side_bias() call (one fork for it and the layer's weight
     // gradient: every fork puts an event marker on the main stream, measured as a ~10 us bubble)
     int bn_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const BnBufs& bb, int g, int beta,
                int act, const uint8_t* mask, float mscale, T* dy, int bias, const ops::BnBwdFuse* fused = nullptr,
-               double* bias_part = nullptr, bool defer_bias = false) {
-        double* bp = (bias >= 0 && use_side) ? bias_part : nullptr;
+               bool bias_side = false, bool defer_bias = false) {
+        const bool on_side = bias >= 0 && use_side && bias_side;
+        const XAcc bacc = bias >= 0 ? acc_bias(bb) : XAcc{};
         HLMC_TRY(ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask, mscale, dy,
-                                    G[g], G[beta], bias >= 0 ? G[bias] : nullptr, scratch, fused, bp));
-        if (bp) {
+                                    G[g], G[beta], acc_mom(bb), fused, bacc,
+                                    (bias >= 0 && !on_side) ? G[bias] : nullptr, AF(bb.sums)));
+        if (on_side) {
             float* gb = G[bias];
-            const int np = ops::bn_bias_parts(R, C);
             if (defer_bias)
-                pend_bias = PendingBias{bp, np, C, gb};
+                pend_bias = PendingBias{bacc, C, gb};
             else
-                HLMC_TRY(side(s, [=](hipStream_t q, Ws w2) { return ops::colsum_finalize(q, bp, np, C, gb, w2); }));
+                HLMC_TRY(side(s, [=](hipStream_t q, Ws) { return ops::colsum_finalize(q, bacc, C, gb); }));
         }
         return HLMC_OK;
     }
     struct PendingBias {
-        double* bp = nullptr;
-        int np = 0, C = 0;
+        XAcc acc;
+        int C = 0;
         float* gb = nullptr;
     };
     PendingBias pend_bias;
@@ -418,9 +468,30 @@ class NetT : public NetBase {
         const PendingBias pb = pend_bias;
         pend_bias = PendingBias{};
         return defer_side(s, [pb, f](hipStream_t q, Ws sc) {
-            if (pb.bp) HLMC_TRY(ops::colsum_finalize(q, pb.bp, pb.np, pb.C, pb.gb, sc));
+            if (pb.gb) HLMC_TRY(ops::colsum_finalize(q, pb.acc, pb.C, pb.gb));
             return f(q, sc);
         }, side_batch());
+    }
+    // f on the third stream now (after everything issued so far on s), with the pending bias reduction
+    int side3_bias(hipStream_t s, SideFn f) {
+        if (!use_side || !s3) return side_bias(s, std::move(f));
+        const PendingBias pb = pend_bias;
+        pend_bias = PendingBias{};
+        hipEvent_t e = next_ev();
+        HLMC_HIP(hipEventRecord(e, s));
+        HLMC_HIP(hipStreamWaitEvent(s3, e, 0));
+        if (pb.gb) HLMC_TRY(ops::colsum_finalize(s3, pb.acc, pb.C, pb.gb));
+        HLMC_TRY(f(s3, scratch3));
+        s3_used = true;
+        return HLMC_OK;
+    }
+    // encoder layers whose weight gradient goes to the third stream (bit l; HLMC_SIDE3_MASK, default none)
+    static int side3_mask() {
+        static const int m = [] {
+            const char* e = std::getenv("HLMC_SIDE3_MASK");
+            return e ? std::atoi(e) : 0;
+        }();
+        return m;
     }
     // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
     static bool tail_on_main() {
@@ -430,15 +501,13 @@ class NetT : public NetBase {
         }();
         return on;
     }
-    size_t bnb_part_off = 0, bnb_part_bytes = 0;
     ops::BnBwdFuse fuse4{};  // the decoder's last BN layer: moments from the output convT's data gradient
-    void need_bnb(size_t b) { bnb_part_bytes = std::max(bnb_part_bytes, b); }
 
     // ---------------------------------------------------------------- conv encoder (6 x conv-BN-LReLU)
     struct Enc {
         int w[6], b[6], g[6], beta[6], bn[6];
         int H = 0, W = 0;
-        size_t y[6], a[6], dy[6], bpart[6];  // dy: grad wrt the conv output (read by the forked wgrad)
+        size_t y[6], a[6], dy[6];  // dy: grad wrt the conv output (read by the forked wgrad)
         // the caller's input of the last full forward: the first conv's weight gradient reads it in backward (the
         // ABI contract keeps in0 alive and unchanged until then: hlmc.h hlmc_net_forward)
         const float* audio = nullptr;
@@ -466,41 +535,50 @@ class NetT : public NetBase {
                 need(ops::wgrad_s2_ws<T>((int)B, h / 2, w / 2, co, ci));
             } else {
                 need(ops::wgrad_c1_ws((int)B, h / 2, w / 2, co));
-                // the edge conv's fused statistics rows + their fold (bn_act_train reads them from scratch)
-                need((size_t)(ops::conv_c1_fused_rows((int)B, h, w) + 64) * 2 * co * sizeof(double) + 256);
             }
             h /= 2;
             w /= 2;
-            need(ops::col_stats_bytes(B * h * w, 1, co));
             const size_t n = (size_t)B * h * w * co;
             enc.y[l] = A.take(n * sizeof(T));
             enc.a[l] = A.take(n * sizeof(T));
             enc.dy[l] = A.take(n * sizeof(T));
-            enc.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * h * w, co) * co * sizeof(double));
             enc.bb[l] = bn_plan(A, co);
-            need(ops::bn_ws(B * h * w, co));
         }
     }
     size_t enc_max_elems(int64_t B) const { return (size_t)B * (enc.H / 2) * (enc.W / 2) * 32; }
+    // train-mode BatchNorm + LeakyReLU of layer l's output applied by the next conv while it stages its input
+    // (ops::BnInput: the LDS halo-tile kernels) instead of a bn_act pass; the activation is written by that kernel
+    ops::BnInput bn_input(const BnBufs& bb, int bn, int g, int beta, int64_t R, size_t a_off) {
+        return ops::BnInput{acc_fwd(bb), R, AF(bb.mean), AF(bb.inv), RM[bn], RV[bn], NBT[bn], kBnMomentum, kBnEps,
+                            P[g], P[beta], ws + a_off};
+    }
     int enc_fwd(hipStream_t s, bool train, const float* audio_in, int B) {
         int h = enc.H, w = enc.W;
         HLMC_CHECK_ARG(audio_in, "audio input required");
         const float* audio = audio_in;
         enc.audio = audio_in;
+        bool fused_prev = false;  // layer l-1's BatchNorm + activation is applied inside layer l's conv
+        ops::BnInput xin{};
         for (int l = 0; l < 6; ++l) {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             T* y = AT(enc.y[l]);
             // train mode: BN statistics from the producing conv's epilogue
-            ops::ColStats st{train ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
+            ops::ColStats st{train ? acc_fwd(enc.bb[l]) : XAcc{}, false};
             if (l == 0)  // BN statistics from the edge conv itself (no col_moments pass)
                 HLMC_TRY(ops::conv_c1_s2<T>(s, audio, B, h, w, P[enc.w[0]], P[enc.b[0]], co, y, &st));
             else
-                HLMC_TRY(ops::conv_s2<T>(s, AT(enc.a[l - 1]), B, h, w, ci, P0(enc.w[l]), P[enc.b[l]], co, y, scratch,
-                                         &st));
+                HLMC_TRY(ops::conv_s2<T>(s, fused_prev ? AT(enc.y[l - 1]) : AT(enc.a[l - 1]), B, h, w, ci, P0(enc.w[l]),
+                                         P[enc.b[l]], co, y, scratch, &st, fused_prev ? &xin : nullptr));
             h /= 2;
             w /= 2;
-            HLMC_TRY(bn_fwd(s, train, y, (int64_t)B * h * w, co, enc.bn[l], enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f,
-                            AT(enc.a[l]), co, &st));
+            const int64_t R = (int64_t)B * h * w;
+            fused_prev = train && l + 1 < 6 && ops::conv_s2_takes_input_bn<T>(B, h, w, co, ENC_CH[l + 2]);
+            if (fused_prev) {
+                if (!st.done) HLMC_TRY(ops::bn_moments<T>(s, y, R, co, acc_fwd(enc.bb[l])));  // e.g. a split-K producer
+                xin = bn_input(enc.bb[l], enc.bn[l], enc.g[l], enc.beta[l], R, enc.a[l]);
+            } else
+                HLMC_TRY(bn_fwd(s, train, y, R, co, enc.bn[l], enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f,
+                                AT(enc.a[l]), co, &st));
         }
         return HLMC_OK;
     }
@@ -519,20 +597,22 @@ class NetT : public NetBase {
             const int64_t R = (int64_t)B * ho * wo;
             T* dy = AT(enc.dy[l]);
             HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
-                            nullptr, reinterpret_cast<double*>(ws + enc.bpart[l]), true));
+                            nullptr, true, true));
             float* gw = G[enc.w[l]];
             if (l == 0 && tail_on_main()) {
                 // the last weight gradient of backward: on the main stream, which would otherwise only wait for
                 // the weight-gradient stream here (that stream is still reducing layer 1's gradient)
                 const PendingBias pb = pend_bias;
                 pend_bias = PendingBias{};
-                if (pb.bp) HLMC_TRY(ops::colsum_finalize(s, pb.bp, pb.np, pb.C, pb.gb, scratch));
+                if (pb.gb) HLMC_TRY(ops::colsum_finalize(s, pb.acc, pb.C, pb.gb));
                 HLMC_TRY(ops::wgrad_c1<T>(s, dy, B, ho, wo, co, audio, gw, scratch));
             } else if (l == 0) {
                 HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
             } else {
                 const T* xin = AT(enc.a[l - 1]);
-                HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
+                SideFn wg = [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); };
+                if (side3_mask() >> l & 1) HLMC_TRY(side3_bias(s, std::move(wg)));
+                else HLMC_TRY(side_bias(s, std::move(wg)));
                 if (l == 1) HLMC_TRY(flush_side(s));  // nothing queued may wait for the join behind the main tail
                 // grad of layer l-1's activation
                 HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));
@@ -547,7 +627,7 @@ class NetT : public NetBase {
     struct Dec {
         int w[6], b[6], g[5], beta[5], bn[5];
         int h0 = 0, w0 = 0;  // low-res input grid (H/64, W/64)
-        size_t y[5], a[5], dy[5], bpart[5];
+        size_t y[5], a[5], dy[5];
         BnBufs bb[5];
     };
     Dec dec;
@@ -578,15 +658,10 @@ class NetT : public NetBase {
                 dec.y[l] = A.take(n * sizeof(T));
                 dec.a[l] = A.take(n * sizeof(T));
                 dec.dy[l] = A.take(n * sizeof(T));
-                dec.bpart[l] = A.take((size_t)ops::bn_bias_parts(B * 4 * h * w, co) * co * sizeof(double));
                 dec.bb[l] = bn_plan(A, co);
-                need(ops::bn_ws(B * 4 * h * w, co));
-                need(ops::col_stats_bytes(B * h * w, 4, co));
             } else {
                 need(ops::wgrad_c1_ws((int)B, h, w, ci));
                 need(ops::colsum_ws((int)(B * 4 * h * w), 1));
-                // the output convT's data gradient carries layer 4's BN-backward moments (edge conv rows)
-                need_bnb((size_t)ops::conv_c1_fused_rows((int)B, 2 * h, 2 * w) * 2 * ci * sizeof(double));
             }
             h *= 2;
             w *= 2;
@@ -597,15 +672,23 @@ class NetT : public NetBase {
     int dec_fwd(hipStream_t s, bool train, const T* u, int B, float* recon) {
         int h = dec.h0, w = dec.w0;
         const T* x = u;
+        bool fused_prev = false;  // layer l-1's BatchNorm + activation is applied inside layer l's sub-pixel conv
+        ops::BnInput xin{};
         for (int l = 0; l < 6; ++l) {
             const int ci = DEC_CH[l], co = DEC_CH[l + 1];
             if (l < 5) {
                 T* y = AT(dec.y[l]);
                 const int64_t R = (int64_t)B * 4 * h * w;
-                ops::ColStats st{train ? reinterpret_cast<double*>(scratch.p) : nullptr, 0};
-                HLMC_TRY(ops::subpixel<T>(s, x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co, y, scratch, &st));
-                HLMC_TRY(bn_fwd(s, train, y, R, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f,
-                                AT(dec.a[l]), co, &st));
+                ops::ColStats st{train ? acc_fwd(dec.bb[l]) : XAcc{}, false};
+                HLMC_TRY(ops::subpixel<T>(s, fused_prev ? AT(dec.y[l - 1]) : x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co,
+                                          y, scratch, &st, fused_prev ? &xin : nullptr));
+                fused_prev = train && l + 1 < 5 && ops::subpixel_takes_input_bn<T>(B, 2 * h, 2 * w, co, DEC_CH[l + 2]);
+                if (fused_prev) {
+                    if (!st.done) HLMC_TRY(ops::bn_moments<T>(s, y, R, co, acc_fwd(dec.bb[l])));  // split-K producer
+                    xin = bn_input(dec.bb[l], dec.bn[l], dec.g[l], dec.beta[l], R, dec.a[l]);
+                } else
+                    HLMC_TRY(bn_fwd(s, train, y, R, co, dec.bn[l], dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f,
+                                    AT(dec.a[l]), co, &st));
                 x = AT(dec.a[l]);
             } else {
                 HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon));
@@ -634,7 +717,7 @@ class NetT : public NetBase {
             }));
             // layer 4's BN-backward moments come with the edge conv that writes its output gradient
             fuse4 = ops::BnBwdFuse{AT(dec.y[4]), AF(dec.bb[4].mean), AF(dec.bb[4].inv), P[dec.g[4]], P[dec.beta[4]],
-                                   reinterpret_cast<double*>(ws + bnb_part_off), 0};
+                                   acc_mom(dec.bb[4]), false};
             HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA, nullptr,
                                         &fuse4));
         }
@@ -645,7 +728,7 @@ class NetT : public NetBase {
             const int64_t R = (int64_t)B * 4 * hl * wl;
             T* dy = AT(dec.dy[l]);
             HLMC_TRY(bn_bwd(s, gA, co, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f, dy, dec.b[l],
-                            &fuse, reinterpret_cast<double*>(ws + dec.bpart[l]), true));
+                            &fuse, true, true));
             const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
             float* gw = G[dec.w[l]];
             HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
@@ -772,7 +855,6 @@ class HybridNet : public NetT<T> {
             gtd_ = A.take(B * 256 * t);
             gtd2_ = A.take(B * 256 * t);
             grt_ = A.take(B * ldT * t);
-            this->need(ops::bn_ws(B, 256));
             for (int i = 0; i < 2; ++i) this->lin_need((int)B, te_w[i]);
             this->lin_need((int)B, td_w[0]);
             this->lin_need((int)B, td_w[1]);
@@ -820,21 +902,17 @@ class HybridNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
+        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z), src/Convolutional_VAE.py:167-179
             HLMC_CHECK_ARG(a.in0 && a.recon, "z and recon required");
             HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in0, L, AT(z_), L, B, L));
         } else {
             HLMC_TRY(encode(s, a, B));
-            {  // latent outputs (and the eps the backward keeps) in one launch
-                const int64_t nl = (int64_t)B * L;
-                const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
-                                            {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
-                HLMC_TRY(ops::copy_segments(s, cs, 3));
-            }
-            if (a.encode_only) return HLMC_OK;
+            if (a.encode_only) return this->latent_out(s, a, AF(mu_), AF(lv_), (int64_t)B * L);
             HLMC_CHECK_ARG(a.recon, "recon required");
-            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), L));
+            // z, the kept eps and the caller's mu / logvar outputs in one launch
+            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), L, a.mu, a.logvar));
         }
         HLMC_TRY(this->template lin_fwd<T>(s, AT(z_), L, B, di_w, di_b, AT(d1_), 512, 1));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(d1_), 512, B, ds_w, ds_b, AT(s_), ldSP, 1));
@@ -858,6 +936,7 @@ class HybridNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
         HLMC_TRY(this->settle(s));
+        HLMC_TRY(this->zero_acc_bwd(s));
         T* gA = AT(gA_);
         // ---- text decoder
         if (text) {
@@ -990,7 +1069,6 @@ class CvaeNet : public NetT<T> {
         gmuT_ = A.take(B * L * t);
         glvT_ = A.take(B * L * t);
         for (int w_ : {te_w, mu_w, lv_w, dfc_w, td_w[0], td_w[1]}) this->lin_need((int)B, w_);
-        this->need(ops::bn_ws(B, 512));
     }
 
     int encode(hipStream_t s, const ForwardArgs& a, int B) {
@@ -1014,21 +1092,17 @@ class CvaeNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
+        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z, condition), src/Conditional_VAE.py:206-225
             HLMC_CHECK_ARG(a.in0 && a.in2 && a.recon && a.recon_text, "z / condition / recon / recon_text required");
             HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in0, L, AT(Z_), ldZ, B, L));
         } else {
             HLMC_TRY(encode(s, a, B));
-            {  // latent outputs (and the eps the backward keeps) in one launch
-                const int64_t nl = (int64_t)B * L;
-                const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
-                                            {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
-                HLMC_TRY(ops::copy_segments(s, cs, 3));
-            }
-            if (a.encode_only) return HLMC_OK;
+            if (a.encode_only) return this->latent_out(s, a, AF(mu_), AF(lv_), (int64_t)B * L);
             HLMC_CHECK_ARG(a.recon && a.recon_text, "recon / recon_text required");
-            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(Z_), ldZ));
+            // z, the kept eps and the caller's mu / logvar outputs in one launch
+            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(Z_), ldZ, a.mu, a.logvar));
         }
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in2, C, AT(Z_) + L, ldZ, B, C));
         HLMC_TRY(this->template lin_fwd<T>(s, AT(Z_), ldZ, B, dfc_w, dfc_b, AT(S_), ldS, 0));
@@ -1048,6 +1122,7 @@ class CvaeNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
         HLMC_TRY(this->settle(s));
+        HLMC_TRY(this->zero_acc_bwd(s));
         T* gA = AT(gA_);
         // text decoder
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon_text, TD, AT(grt_), ldT, B, TD));
@@ -1164,7 +1239,6 @@ class SimpleNet : public NetT<T> {
                 moff += B * b.dout;
                 widest = std::max(widest, pad8(b.dout));
                 this->lin_need((int)B, b.w);
-                this->need(ops::bn_ws(B, b.dout));
             }
         mask_total = moff;
         mask_ = A.take((size_t)moff);
@@ -1213,6 +1287,7 @@ class SimpleNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
+        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z), src/Simple_VAE.py:95-96 (decoder blocks' dropout from the same mask layout)
             HLMC_CHECK_ARG(a.in0 && a.recon, "z and recon required");
@@ -1224,15 +1299,10 @@ class SimpleNet : public NetT<T> {
             HLMC_TRY(ops::cast2d_from_f32<T>(s, a.in0, L, AT(z_), pad8(L), B, L));
         } else {
             HLMC_TRY(encode(s, a, B));
-            {  // latent outputs (and the eps the backward keeps) in one launch
-                const int64_t nl = (int64_t)B * L;
-                const ops::CopySeg cs[3] = {{a.mu, AF(mu_), nl}, {a.logvar, AF(lv_), nl},
-                                            {a.encode_only ? nullptr : AF(eps_), a.eps, nl}};
-                HLMC_TRY(ops::copy_segments(s, cs, 3));
-            }
-            if (a.encode_only) return HLMC_OK;
+            if (a.encode_only) return this->latent_out(s, a, AF(mu_), AF(lv_), (int64_t)B * L);
             HLMC_CHECK_ARG(a.recon, "recon required");
-            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), pad8(L)));
+            // z, the kept eps and the caller's mu / logvar outputs in one launch
+            HLMC_TRY(this->reparam(s, a.eps, AF(mu_), AF(lv_), AF(eps_), B, L, AT(z_), pad8(L), a.mu, a.logvar));
             if (a.z) HLMC_TRY(ops::reparam_fwd<float>(s, AF(mu_), AF(lv_), AF(eps_), B, L, a.z, L));
         }
         const T* x = AT(z_);
@@ -1255,6 +1325,7 @@ class SimpleNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->side_init());
         HLMC_TRY(this->settle(s));
+        HLMC_TRY(this->zero_acc_bwd(s));
         T* g1 = AT(gx1_);
         HLMC_TRY(ops::cast2d_from_f32<T>(s, a.d_recon, D, AT(grec_), ldD, B, D));
         const Blk& last = decb.back();

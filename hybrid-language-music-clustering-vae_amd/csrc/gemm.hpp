@@ -359,14 +359,13 @@ struct StoreSubpixel {
     }
 };
 
-// Any epilogue plus fused per-column statistics of the stored values (BatchNorm batch statistics):
-// block (phase, m-tile) writes part[(phase * mtiles + mtile) * 2N + n] = sum, [... + N + n] = sum of squares
-// (f64, fixed-order reduction) over its rows — the [nparts][2C] layout bn_finalize reduces.
+// Any epilogue plus fused per-column statistics of the stored values (BatchNorm batch statistics): each block's
+// column sums (f64, fixed-order reduction over its rows) go to the exact accumulator `acc` (2N columns: sum n,
+// sum of squares N + n; common.hpp XAcc) -- the consumer reads the totals, no fold launch.
 template <class Base>
 struct WithStats : Base {
     static constexpr int kStatMode = 1;
-    double* part;
-    int mtiles;
+    XAcc acc;
 };
 
 // Split-K partial slab: ws[((phase * S + split) * M + m) * N + n]
@@ -712,7 +711,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
         const int wmi = wave / WAVES_N;
         stats_to_lds<TR, TN, BN>(cs, cq, &sred[0][0][0], wmi, wn0, lane);
         __syncthreads();
-        const int row = ph * ep.mtiles + tile_m_;
+        const int shard = (int)((blockIdx.x + gridDim.x * blockIdx.y) % (unsigned)ep.acc.shards);
         for (int c = tid; c < BN; c += 256) {
             const int n = n0 + c;
             if (n >= N) continue;
@@ -722,8 +721,8 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
                 a += sred[w][0][c];
                 q += sred[w][1][c];
             }
-            ep.part[(int64_t)row * 2 * N + n] = a;
-            ep.part[(int64_t)row * 2 * N + N + n] = q;
+            xacc_add_shard(ep.acc, shard, n, a);
+            xacc_add_shard(ep.acc, shard, N + n, q);
         }
     }
     if (ph + 1 < ph1) __syncthreads();  // the next phase's LDS fills / statistics scratch
@@ -871,7 +870,7 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
         const int wmi = wave / WAVES_N;
         stats_to_lds<TR, TN, BN>(cs, cq, sred, wmi, wn0, lane);
         __syncthreads();
-        const int prow = phase * ep.mtiles + tile_m_;
+        const int shard = (int)((blockIdx.x + gridDim.x * blockIdx.y) % (unsigned)ep.acc.shards);
         for (int c = tid; c < BN; c += 256) {
             const int n = n0 + c;
             if (n >= N) continue;
@@ -881,8 +880,8 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
                 a += sred[(w * 2 + 0) * BN + c];
                 q += sred[(w * 2 + 1) * BN + c];
             }
-            ep.part[(int64_t)prow * 2 * N + n] = a;
-            ep.part[(int64_t)prow * 2 * N + N + n] = q;
+            xacc_add_shard(ep.acc, shard, n, a);
+            xacc_add_shard(ep.acc, shard, N + n, q);
         }
     }
 }
@@ -914,6 +913,82 @@ __global__ void splitk_reduce_kernel(const float* ws, EP ep, int M, int N, int S
         EP e = ep;
         e.set_phase(ph);
         e.store(e.row(m), n, s);
+    }
+}
+
+// The same reduction for a launch whose output feeds a train-mode BatchNorm: each block owns a contiguous range of
+// output rows (phase-major, all N columns) and also delivers the column sums / sums of squares of the values it
+// stored to `acc` (2N columns, common.hpp XAcc) -- no separate moments pass over the output.  Thread (column
+// c = tid % N, row group g = tid / N) for N <= 256 (N divides 256), else columns tid, tid + 256, ...
+template <class EP>
+__global__ __launch_bounds__(256) void splitk_reduce_stats_kernel(const float* ws, EP ep, int M, int N, int S,
+                                                                  int phases, int rows_per_blk, XAcc acc) {
+    __shared__ double red[2][256];
+    const int tid = threadIdx.x;
+    const int64_t rows = (int64_t)phases * M, st = (int64_t)M * N;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
+    const int G = N <= 256 ? 256 / N : 1;
+    const int cstep = N <= 256 ? N : 256;
+    for (int c0 = N <= 256 ? tid % N : tid; c0 < N; c0 += cstep) {
+        double a = 0.0, q = 0.0;
+        const int g = N <= 256 ? tid / N : 0;
+        constexpr int U = 4;  // rows in flight per thread (each summed over the S slabs in k order, as above)
+        for (int64_t rb = r0 + g; rb < r1; rb += U * G) {
+            const float* p[U];
+            float s[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = min(rb + u * G, r1 - 1);  // clamped: in bounds, skipped below
+                const int ph = (int)(r / M), m = (int)(r - (int64_t)ph * M);
+                p[u] = ws + ((int64_t)ph * S * M + m) * N + c0;
+                s[u] = 0.f;
+            }
+            int k = 0;
+            for (; k + 2 <= S; k += 2) {
+                float x0[U], x1[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    x0[u] = p[u][k * st];
+                    x1[u] = p[u][(k + 1) * st];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    s[u] += x0[u];
+                    s[u] += x1[u];
+                }
+            }
+            if (k < S)
+#pragma unroll
+                for (int u = 0; u < U; ++u) s[u] += p[u][k * st];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = rb + u * G;
+                if (r >= r1) break;
+                const int ph = (int)(r / M), m = (int)(r - (int64_t)ph * M);
+                EP e = ep;
+                e.set_phase(ph);
+                e.store(e.row(m), c0, s[u]);
+                const float v = e.stored(c0, s[u]);
+                a += v;
+                q += (double)v * v;
+            }
+        }
+        if (G > 1) {
+            red[0][tid] = a;
+            red[1][tid] = q;
+            __syncthreads();
+            if (tid < N) {
+                for (int k = 1; k < G; ++k) {
+                    a += red[0][k * N + tid];
+                    q += red[1][k * N + tid];
+                }
+                xacc_add(acc, c0, a);
+                xacc_add(acc, N + c0, q);
+            }
+        } else {
+            xacc_add(acc, c0, a);
+            xacc_add(acc, N + c0, q);
+        }
     }
 }
 

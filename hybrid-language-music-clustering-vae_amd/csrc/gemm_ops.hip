@@ -154,15 +154,15 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     // register path: short reductions keep the 4-chunk K-step (more co-resident blocks), long ones 8 chunks
     const bool long_k = Kmax >= 1024;
     const int pipe = (dma_ok && BN >= 32 && BM >= 64) ? nt_pipe_select(pl.ksl, pl.S, tmn * phases * pl.S) : 0;
-    if (st) st->nparts = 0;
-    if (pl.S == 1 && st && st->part) {  // single pass: the epilogue also emits the column statistics
+    const bool stats = st && st->acc.on();
+    if (st) st->done = false;
+    if (pl.S == 1 && stats) {  // single pass: the epilogue also emits the column statistics
         WithStats<EP> eps;
         static_cast<EP&>(eps) = ep;
-        eps.part = st->part;
-        eps.mtiles = cdiv(M, BM);
+        eps.acc = st->acc;
         nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, eps, M, N, pl.ksl, long_k, pipe);
         HLMC_LAUNCHED();
-        st->nparts = phases * cdiv(M, BM);
+        st->done = true;
         return HLMC_OK;
     }
     if (pl.S == 1) {
@@ -176,6 +176,19 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
     nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe);
     HLMC_LAUNCHED();
+    static const bool red_stats = [] {  // HLMC_SPLITK_STATS=1: the reduction also delivers the statistics (A/B aid)
+        const char* e = std::getenv("HLMC_SPLITK_STATS");
+        return e && e[0] == '1';
+    }();
+    if (red_stats && stats && (N > 256 ? N % 256 == 0 : 256 % N == 0)) {
+        const int64_t rows = (int64_t)phases * M;
+        const int G = N <= 256 ? 256 / N : 1;
+        const int64_t rpb = (std::max<int64_t>(1, (rows + 255) / 256) + G - 1) / G * G;  // <= 256 blocks
+        splitk_reduce_stats_kernel<EP><<<cdiv(rows, rpb), 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases, (int)rpb, st->acc);
+        HLMC_LAUNCHED();
+        st->done = true;
+        return HLMC_OK;
+    }
     int64_t total = (int64_t)phases * M * N;
     int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
     splitk_reduce_kernel<EP><<<blocks, 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases);
@@ -335,6 +348,71 @@ size_t dispatch_tn_ws(int M, int N, int K) {
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline int log2_exact(int c) { return (c > 0 && (c & (c - 1)) == 0) ? __builtin_ctz(c) : -1; }
 
+// ---- train-mode BatchNorm + LeakyReLU(0.01) of a halo kernel's INPUT, applied while its rows are staged (XIN):
+// the input pointer is the pre-BN map y of the layer below; the block folds that layer's statistics accumulator
+// in its prologue (bn_act_train's consumer-side finalize, same arithmetic; block 0 stores mean / invstd / running
+// statistics), transforms each staged 16-byte chunk (8 channels) in registers, and writes the activation a of the
+// rows its tile owns (every input row exactly once over the grid, by the first channel-split block) for the weight
+// gradient that reads it later.  Rows outside the image stay zero (padding).
+struct BnIn {
+    XAcc acc;                       // 2C columns
+    int64_t R;                      // rows of the normalised map
+    float *mean, *invstd, *rmean, *rvar;
+    int64_t* nbt;
+    float momentum, eps;
+    const float *gamma, *beta;
+    bf16* a_out;
+};
+template <int CI>
+struct BnInLds {  // prologue scratch + per-channel parameters (LDS)
+    double tot[2 * CI];
+    long long red[3 * 256];
+    float prm[4 * CI];  // mean | invstd | gamma | beta
+};
+template <int CI>
+__device__ __forceinline__ void bn_in_prologue(const BnIn& f, BnInLds<CI>& L) {
+    xacc_fold(f.acc, L.tot, L.red);
+    for (int c = threadIdx.x; c < CI; c += 256) {
+        const double m = L.tot[c] / (double)f.R;
+        double var = L.tot[CI + c] / (double)f.R - m * m;
+        if (var < 0.0) var = 0.0;
+        const float mf = (float)m, inv = (float)(1.0 / sqrt(var + (double)f.eps));
+        L.prm[c] = mf;
+        L.prm[CI + c] = inv;
+        L.prm[2 * CI + c] = f.gamma[c];
+        L.prm[3 * CI + c] = f.beta[c];
+        if (blockIdx.x == 0) {
+            f.mean[c] = mf;
+            f.invstd[c] = inv;
+            if (f.rmean) {
+                const double unb = f.R > 1 ? var * (double)f.R / (double)(f.R - 1) : var;
+                f.rmean[c] = (float)((1.0 - f.momentum) * f.rmean[c] + f.momentum * m);
+                f.rvar[c] = (float)((1.0 - f.momentum) * f.rvar[c] + f.momentum * unb);
+            }
+            if (c == 0 && f.nbt) f.nbt[0] += 1;
+        }
+    }
+    __syncthreads();
+}
+// lrelu((x - mean) * invstd * gamma + beta) of 8 bf16 channels (the thread's parameters in registers)
+__device__ __forceinline__ uint4 bn_in_apply(uint4 v, const float (&pr)[4][8]) {
+    float x[8];
+    cvt16_f32<bf16>(v, x);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float z = (x[k] - pr[0][k]) * pr[1][k] * pr[2][k] + pr[3][k];
+        x[k] = z > 0.f ? z : 0.01f * z;
+    }
+    uint4 o;
+    unsigned* w = reinterpret_cast<unsigned*>(&o);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        bf16 lo = __float2bfloat16(x[2 * i]), hi = __float2bfloat16(x[2 * i + 1]);
+        w[i] = (unsigned)(*reinterpret_cast<unsigned short*>(&lo)) | ((unsigned)(*reinterpret_cast<unsigned short*>(&hi)) << 16);
+    }
+    return o;
+}
+
 // ---- stride-2 3x3 conv over LDS halo tiles (HLMC_CONV_HALO=0 disables): Ci = 32, Wo = 32, bf16, Co = CO.
 // Measured (scripts/bench_gemm.py): the 64x64x32 -> 64 conv and the matching decoder data gradient 46.3 / 44.1 ->
 // 36.7 / 34.2 us; bench A/B 106.4k vs 105.0k clips/s (3 alternating rounds).
@@ -345,9 +423,9 @@ inline int log2_exact(int c) { return (c > 0 && (c & (c - 1)) == 0) ? __builtin_
 // Template: CI input channels, COB output channels per block (NSPL blocks share a tile's Co = NSPL * COB), WO
 // output width, ROWS output rows per tile (TP = ROWS * WO pixels), DB: double-buffered halo (else one buffer and
 // an extra barrier).  Shapes: 2 WO * CI / 8 == 256 (one 16-byte chunk per thread per input row).
-template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP, bool TR = true>
+template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP, bool TR = true, bool XIN = false>
 __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
-                                                           const bf16* __restrict__ wp, EP ep, int M) {
+                                                           const bf16* __restrict__ wp, EP ep, int M, BnIn xin) {
     constexpr int WI = 2 * WO, HR = 2 * ROWS + 1, HC = WI + 1, PS = CI + 8;  // halo rows / cols / pixel pitch
     constexpr int TP = ROWS * WO, CPP = CI / 8;                             // tile pixels, chunks per pixel
     static_assert(WI * CPP == 256 && (COB == 64 || COB == 32), "halo chunk map / wave tiling");
@@ -374,14 +452,27 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
         *reinterpret_cast<uint4*>(&Hs[(bufr / HR) * HS + ((bufr % HR) * HC) * PS + q * 8]) = make_uint4(0, 0, 0, 0);
     }
     uint4 hr[HR];  // HR rows x 256 chunks / 256 threads
+    auto row_off = [&](int b, int ih) { return (((int64_t)b * Hi + ih) * WI + tid / CPP) * CI + (tid % CPP) * 8; };
     auto load_rows = [&](int t) {
         const int b = t / tpi, oh0 = (t - b * tpi) * ROWS;
 #pragma unroll
         for (int u = 0; u < HR; ++u) {
             const int ih = 2 * oh0 - 1 + u;
-            hr[u] = ih >= 0 ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * WI + tid / CPP) * CI +
-                                                             (tid % CPP) * 8)
-                            : make_uint4(0, 0, 0, 0);
+            hr[u] = ih >= 0 ? *reinterpret_cast<const uint4*>(x + row_off(b, ih)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    float pr[XIN ? 4 : 1][8];  // XIN: this thread's 8 channels' BatchNorm parameters
+    // XIN: the rows of tile t become activations (in range: all but row -1); rows 2 oh0 .. are this tile's to write
+    auto xform_rows = [&](int t) {
+        if constexpr (XIN) {
+            const int b = t / tpi, oh0 = (t - b * tpi) * ROWS;
+#pragma unroll
+            for (int u = 0; u < HR; ++u) {
+                const int ih = 2 * oh0 - 1 + u;
+                if (ih < 0) continue;
+                hr[u] = bn_in_apply(hr[u], pr);
+                if (u > 0 && nh == 0) *reinterpret_cast<uint4*>(xin.a_out + row_off(b, ih)) = hr[u];
+            }
         }
     };
     auto store_rows = [&](int buf) {
@@ -390,12 +481,26 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
             *reinterpret_cast<uint4*>(&Hs[buf * HS + (u * HC + tid / CPP + 1) * PS + (tid % CPP) * 8]) = hr[u];
     };
     int t = blockIdx.x / NSPL, buf = 0;
+    if (t < ntiles) load_rows(t);  // in flight during the statistics prologue
+    if constexpr (XIN) {
+        __shared__ BnInLds<CI> bl;
+        bn_in_prologue<CI>(xin, bl);
+        const int c0 = (tid % CPP) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            pr[0][k] = bl.prm[c0 + k];
+            pr[1][k] = bl.prm[CI + c0 + k];
+            pr[2][k] = bl.prm[2 * CI + c0 + k];
+            pr[3][k] = bl.prm[3 * CI + c0 + k];
+        }
+    }
     if (t < ntiles) {
-        load_rows(t);
+        xform_rows(t);
         store_rows(0);
     }
     __syncthreads();
     const int g8 = (lane >> 4) * 8;
+    double run_a = 0.0, run_q = 0.0;  // statistics (kStatMode 1): thread c < COB, column n0 + c
     for (; t < ntiles; t += bstep) {
         const int tn = t + bstep;
         if (tn < ntiles) load_rows(tn);  // in flight during this tile's MFMAs and stores
@@ -442,25 +547,33 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
             const int wmi = wave / WAVES_N;
             stats_to_lds<TR, TN, COB>(cs, cq, &sred[0][0][0], wmi, wn0, lane);
             __syncthreads();
-            for (int c = tid; c < COB; c += 256) {
-                double a = 0.0, q = 0.0;
+            if (tid < COB) {  // this block's running column sums over its tiles (tile order: deterministic)
 #pragma unroll
                 for (int w = 0; w < WAVES_M; ++w) {
-                    a += sred[w][0][c];
-                    q += sred[w][1][c];
+                    run_a += sred[w][0][tid];
+                    run_q += sred[w][1][tid];
                 }
-                ep.part[(int64_t)t * 2 * CO + n0 + c] = a;
-                ep.part[(int64_t)t * 2 * CO + CO + n0 + c] = q;
             }
         }
         if constexpr (DB) {
-            if (tn < ntiles) store_rows(buf ^ 1);
+            if (tn < ntiles) {
+                xform_rows(tn);
+                store_rows(buf ^ 1);
+            }
             __syncthreads();
             buf ^= 1;
         } else {
+            if (tn < ntiles) xform_rows(tn);
             __syncthreads();  // every wave is done with this tile's halo (and the statistics scratch)
             if (tn < ntiles) store_rows(0);
             __syncthreads();
+        }
+    }
+    if constexpr (EP::kStatMode == 1) {
+        if (tid < COB) {
+            const int shard = (int)(blockIdx.x % (unsigned)ep.acc.shards);
+            xacc_add_shard(ep.acc, shard, n0 + tid, run_a);
+            xacc_add_shard(ep.acc, shard, CO + n0 + tid, run_q);
         }
     }
 }
@@ -472,9 +585,9 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
 // 4 phases' taps (1 + 2 + 2 + 4) read their fragments from there.
 // Template: CI input channels, COB output channels per block (NSPL blocks per tile), WI low-res width, ROWS
 // low-res rows per tile (TP = ROWS * WI = 128 pixels), DB: double-buffered halo.  WI * CI / 8 == 256.
-template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP, bool TR = true>
+template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP, bool TR = true, bool XIN = false>
 __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
-                                                            const bf16* __restrict__ wp, EP ep, int M) {
+                                                            const bf16* __restrict__ wp, EP ep, int M, BnIn xin) {
     constexpr int HR = ROWS + 1, HC = WI + 1, PS = CI + 8, CPP = CI / 8, TP = ROWS * WI;
     static_assert(WI * CPP == 256 && TP == 128 && (COB == 32 || COB == 16), "halo chunk map / wave tiling");
     constexpr int KP = 9 * CI + 8;                        // weight row: fragment rows on distinct 16-byte slots
@@ -497,14 +610,27 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
         *reinterpret_cast<uint4*>(&Hs[(bufr / HR) * HS + ((bufr % HR) * HC + WI) * PS + q * 8]) = make_uint4(0, 0, 0, 0);
     }
     uint4 hr[HR];  // HR rows x 256 chunks / 256 threads
+    auto row_off = [&](int b, int ih) { return (((int64_t)b * Hi + ih) * WI + tid / CPP) * CI + (tid % CPP) * 8; };
     auto load_rows = [&](int t) {
         const int b = t / tpi, r0 = (t - b * tpi) * ROWS;
 #pragma unroll
         for (int u = 0; u < HR; ++u) {
             const int ih = r0 + u;
-            hr[u] = ih < Hi ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * Hi + ih) * WI + tid / CPP) * CI +
-                                                             (tid % CPP) * 8)
-                            : make_uint4(0, 0, 0, 0);
+            hr[u] = ih < Hi ? *reinterpret_cast<const uint4*>(x + row_off(b, ih)) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    float pr[XIN ? 4 : 1][8];  // XIN: this thread's 8 channels' BatchNorm parameters
+    // XIN: the rows of tile t inside the image become activations; rows r0 .. r0 + ROWS - 1 are this tile's to write
+    auto xform_rows = [&](int t) {
+        if constexpr (XIN) {
+            const int b = t / tpi, r0 = (t - b * tpi) * ROWS;
+#pragma unroll
+            for (int u = 0; u < HR; ++u) {
+                const int ih = r0 + u;
+                if (ih >= Hi) continue;
+                hr[u] = bn_in_apply(hr[u], pr);
+                if (u < ROWS && nh == 0) *reinterpret_cast<uint4*>(xin.a_out + row_off(b, ih)) = hr[u];
+            }
         }
     };
     auto store_rows = [&](int buf) {
@@ -513,12 +639,26 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
             *reinterpret_cast<uint4*>(&Hs[buf * HS + (u * HC + tid / CPP) * PS + (tid % CPP) * 8]) = hr[u];
     };
     int t = blockIdx.x / NSPL, buf = 0;
+    if (t < ntiles) load_rows(t);  // in flight during the statistics prologue
+    if constexpr (XIN) {
+        __shared__ BnInLds<CI> bl;
+        bn_in_prologue<CI>(xin, bl);
+        const int c0 = (tid % CPP) * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            pr[0][k] = bl.prm[c0 + k];
+            pr[1][k] = bl.prm[CI + c0 + k];
+            pr[2][k] = bl.prm[2 * CI + c0 + k];
+            pr[3][k] = bl.prm[3 * CI + c0 + k];
+        }
+    }
     if (t < ntiles) {
-        load_rows(t);
+        xform_rows(t);
         store_rows(0);
     }
     __syncthreads();
     const int g8 = (lane >> 4) * 8;
+    double run_a = 0.0, run_q = 0.0;  // statistics (kStatMode 1): thread c < COB, column n0 + c
     for (; t < ntiles; t += bstep) {
         const int tn = t + bstep;
         if (tn < ntiles) load_rows(tn);
@@ -574,24 +714,32 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
                 __shared__ double sred[4][2][COB];
                 stats_to_lds<TR, TN, COB>(cs, cq, &sred[0][0][0], wave, 0, lane);
                 __syncthreads();
-                const int row = ph * ep.mtiles + t;
-                for (int c = tid; c < COB; c += 256) {
-                    ep.part[(int64_t)row * 2 * CO + n0 + c] =
-                        (sred[0][0][c] + sred[1][0][c]) + (sred[2][0][c] + sred[3][0][c]);
-                    ep.part[(int64_t)row * 2 * CO + CO + n0 + c] =
-                        (sred[0][1][c] + sred[1][1][c]) + (sred[2][1][c] + sred[3][1][c]);
+                if (tid < COB) {  // running column sums over this block's (tile, phase) pairs, in order
+                    run_a += (sred[0][0][tid] + sred[1][0][tid]) + (sred[2][0][tid] + sred[3][0][tid]);
+                    run_q += (sred[0][1][tid] + sred[1][1][tid]) + (sred[2][1][tid] + sred[3][1][tid]);
                 }
                 __syncthreads();  // sred is reused by the next phase
             }
         }
         if constexpr (DB) {
-            if (tn < ntiles) store_rows(buf ^ 1);
+            if (tn < ntiles) {
+                xform_rows(tn);
+                store_rows(buf ^ 1);
+            }
             __syncthreads();
             buf ^= 1;
         } else {
+            if (tn < ntiles) xform_rows(tn);
             __syncthreads();  // every wave is done with this tile's halo
             if (tn < ntiles) store_rows(0);
             __syncthreads();
+        }
+    }
+    if constexpr (EP::kStatMode == 1) {
+        if (tid < COB) {
+            const int shard = (int)(blockIdx.x % (unsigned)ep.acc.shards);
+            xacc_add_shard(ep.acc, shard, n0 + tid, run_a);
+            xacc_add_shard(ep.acc, shard, CO + n0 + tid, run_q);
         }
     }
 }
@@ -600,9 +748,52 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
 
 namespace ops {
 
+static BnIn bn_in_of(const BnInput* xi) {
+    BnIn b{};
+    if (!xi) return b;
+    b.acc = xi->acc; b.R = xi->R; b.mean = xi->mean; b.invstd = xi->invstd; b.rmean = xi->rmean; b.rvar = xi->rvar;
+    b.nbt = xi->nbt; b.momentum = xi->momentum; b.eps = xi->eps; b.gamma = xi->gamma; b.beta = xi->beta;
+    b.a_out = static_cast<bf16*>(xi->a_out);
+    return b;
+}
+static bool conv_halo_shape(int Ci, int Co, int Wi, int Hi, int& which) {
+    which = (Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0) ? 1 : (Ci == 64 && Co == 128 && Wi == 32 && Hi % 8 == 0) ? 2 : 0;
+    return which != 0;
+}
+static bool subpixel_halo_shape(int Ci, int Co, int Wi, int Hi, int& which) {
+    which = (Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0) ? 1 : (Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0) ? 2 : 0;
+    return which != 0;
+}
+inline bool bn_in_enabled() {  // HLMC_BN_IN=0: input BatchNorm stays a bn_act pass (A/B aid)
+    static const bool on = [] {
+        const char* e = std::getenv("HLMC_BN_IN");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+template <typename T>
+bool conv_s2_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co) {
+    (void)B;
+    int w;
+    return std::is_same<T, bf16>::value && bn_in_enabled() && conv_halo_shape(Ci, Co, Wi, Hi, w) &&
+           !(w == 1 && std::getenv("HLMC_CONV_HALO") && std::getenv("HLMC_CONV_HALO")[0] == '0') &&
+           !(w == 2 && std::getenv("HLMC_CONV_HALO2") && std::getenv("HLMC_CONV_HALO2")[0] == '0');
+}
+template <typename T>
+bool subpixel_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co) {
+    (void)B;
+    int w;
+    return std::is_same<T, bf16>::value && bn_in_enabled() && subpixel_halo_shape(Ci, Co, Wi, Hi, w) &&
+           !(w == 1 && std::getenv("HLMC_SP_HALO") && std::getenv("HLMC_SP_HALO")[0] == '0') &&
+           !(w == 2 && std::getenv("HLMC_SP_HALO2") && std::getenv("HLMC_SP_HALO2")[0] == '0');
+}
+
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-            ColStats* st) {
+            ColStats* st, const BnInput* xin) {
+    HLMC_CHECK_ARG(!xin || conv_s2_takes_input_bn<T>(B, Hi, Wi, Ci, Co), "conv_s2: input BatchNorm needs a halo shape");
+    if (xin) HLMC_CHECK_ARG(xin->acc.p && xin->acc.ncols == 2 * Ci && xin->a_out && st && st->acc.on(),
+                            "conv_s2: input BatchNorm arguments");
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(Hi % 2 == 0 && Wi % 2 == 0 && Ci % V == 0, "conv_s2: need even H/W and Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "conv_s2: 16-byte alignment");
@@ -623,42 +814,43 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
         }();
         // (CI, Co, Wi): (32, 64, 64) 128-pixel tiles, double-buffered halo; (64, 128, 32) two 64-channel halves per
         // 64-pixel tile, one halo buffer (the weights take half the LDS)
-        auto run = [&](auto kern_plain, auto kern_stats, int tp, int nspl) -> int {
+        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int tp, int nspl) -> int {
             const int ntiles = M / tp;  // whole output rows: tiles stay inside an image
             const int grid = std::min(ntiles * nspl, 256);
             HLMC_PROBE_BEGIN(s);
-            if (st && st->part) {
+            if (st && st->acc.on()) {
                 WithStats<StoreRM<T>> eps;
                 static_cast<StoreRM<T>&>(eps) = ep;
-                eps.part = st->part;
-                eps.mtiles = ntiles;
-                kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M);
-                st->nparts = ntiles;
+                eps.acc = st->acc;
+                if (xin) kern_xin<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, bn_in_of(xin));
+                else kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, BnIn{});
+                st->done = true;
             } else {
-                if (st) st->nparts = 0;
-                kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M);
+                if (st) st->done = false;
+                kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{});
             }
             HLMC_PROBE_END(s);
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
         const bool tr = halo_tr_enabled();
+        using StRM = WithStats<StoreRM<T>>;  // XIN variants: per-element epilogue (TR = false)
         if (halo && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0)
             return tr ? run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, true>,
-                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, WithStats<StoreRM<T>>, true>, 128, 1)
+                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, true>,
+                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false, true>, 128, 1)
                       : run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, false>,
-                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, WithStats<StoreRM<T>>, false>, 128, 1);
+                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false>,
+                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false, true>, 128, 1);
         if (halo2 && Ci == 64 && Co == 128 && Wi == 32 && Hi % 8 == 0)
             return tr ? run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, true>,
-                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, WithStats<StoreRM<T>>, true>, 64, 2)
+                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, true>,
+                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false, true>, 64, 2)
                       : run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, false>,
-                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, WithStats<StoreRM<T>>, false>, 64, 2);
+                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false>,
+                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false, true>, 64, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
-}
-// partial rows (phases x 64-row tiles, the smallest BM) | fold scratch for their reduction
-size_t col_stats_bytes(int64_t M, int phases, int C) {
-    return (((size_t)phases * cdiv((int)M, 64) * 2 * C * sizeof(double) + 255) & ~(size_t)255) + fold_ws(2 * C);
 }
 
 template <typename T>
@@ -668,7 +860,10 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {
 
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-             ColStats* st) {
+             ColStats* st, const BnInput* xin) {
+    HLMC_CHECK_ARG(!xin || subpixel_takes_input_bn<T>(B, Hi, Wi, Ci, Co), "subpixel: input BatchNorm needs a halo shape");
+    if (xin) HLMC_CHECK_ARG(xin->acc.p && xin->acc.ncols == 2 * Ci && xin->a_out && st && st->acc.on(),
+                            "subpixel: input BatchNorm arguments");
     constexpr int V = Vec16<T>::N;
     HLMC_CHECK_ARG(Ci % V == 0, "subpixel: Ci % 8 (bf16) / 4 (f32)");
     HLMC_CHECK_ARG(aligned16(x) && aligned16(wp), "subpixel: 16-byte alignment");
@@ -688,36 +883,41 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
             const char* e = std::getenv("HLMC_SP_HALO2");
             return !(e && e[0] == '0');
         }();
-        auto run = [&](auto kern_plain, auto kern_stats, int nspl) -> int {
+        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int nspl) -> int {
             const int ntiles = M / 128;  // 128 low-res pixels (whole rows) per tile, inside one image
             const int grid = std::min(ntiles * nspl, 256);
             HLMC_PROBE_BEGIN(s);
-            if (st && st->part) {
+            if (st && st->acc.on()) {
                 WithStats<StoreSubpixel<T>> eps;
                 static_cast<StoreSubpixel<T>&>(eps) = ep;
-                eps.part = st->part;
-                eps.mtiles = ntiles;
-                kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M);
-                st->nparts = 4 * ntiles;
+                eps.acc = st->acc;
+                if (xin) kern_xin<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, bn_in_of(xin));
+                else kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, BnIn{});
+                st->done = true;
             } else {
-                if (st) st->nparts = 0;
-                kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M);
+                if (st) st->done = false;
+                kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{});
             }
             HLMC_PROBE_END(s);
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
         const bool tr = halo_tr_enabled();
+        using StSP = WithStats<StoreSubpixel<T>>;  // XIN variants: per-element epilogue (TR = false)
         if (halo && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0)
             return tr ? run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, true>,
-                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, WithStats<StoreSubpixel<T>>, true>, 1)
+                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, true>,
+                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false, true>, 1)
                       : run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, false>,
-                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, WithStats<StoreSubpixel<T>>, false>, 1);
+                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false>,
+                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false, true>, 1);
         if (halo2 && Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0)
             return tr ? run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>, true>,
-                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, WithStats<StoreSubpixel<T>>, true>, 2)
+                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, true>,
+                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2)
                       : run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>, false>,
-                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, WithStats<StoreSubpixel<T>>, false>, 2);
+                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false>,
+                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
 }
@@ -803,10 +1003,12 @@ size_t linear_wgrad_ws(int Mb, int N, int K) {  // with or without the bias colu
 
 #define INST(T)                                                                                                     \
     template int conv_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,         \
-                            ColStats*);                                                                              \
+                            ColStats*, const BnInput*);                                                  \
+    template bool conv_s2_takes_input_bn<T>(int, int, int, int, int);                                              \
+    template bool subpixel_takes_input_bn<T>(int, int, int, int, int);                                             \
     template size_t conv_s2_ws<T>(int, int, int, int, int);                                                        \
     template int subpixel<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,        \
-                             ColStats*);                                                                             \
+                             ColStats*, const BnInput*);                                                                             \
     template size_t subpixel_ws<T>(int, int, int, int, int);                                                       \
     template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws);                \
     template size_t wgrad_s2_ws<T>(int, int, int, int, int);                                                       \

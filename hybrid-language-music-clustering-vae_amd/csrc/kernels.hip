@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -13,7 +14,7 @@ namespace hlmc {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kC1FusedBlocks = 4096;  // grid of the statistics-fused edge conv (partial rows it writes)
+constexpr int kC1FusedBlocks = 1024;  // grid of the statistics-fused edge conv (accumulator contributions)
 
 inline int grid_for(int64_t n, int per_block = kThreads, int cap = 8192) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(cap, (n + per_block - 1) / per_block));
@@ -46,9 +47,9 @@ __device__ __forceinline__ float act_grad(float z, int act) {
 // Column sums of per-thread V-channel accumulators across a 256-thread block whose thread t covers row
 // rr = t / tpr, channel group cg = t % tpr (tpr = C / V, a power of two dividing 256).  Fixed order:
 // xor-shuffle tree inside each wavefront over the lanes sharing cg, then the (<= 4) wave / row slots in LDS.
-// out[c] for c < C.  lds: >= 256 * V doubles.
+// The block's column totals go to the exact accumulator acc, columns coff + c (c < C).  lds: >= 256 * V doubles.
 template <int V>
-__device__ __forceinline__ void block_colsum(double (&a)[V], int tpr, int C, double* lds, double* out) {
+__device__ __forceinline__ void block_colsum(double (&a)[V], int tpr, int C, double* lds, const XAcc& acc, int coff) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     int slot, cg, nslot;
     bool valid;
@@ -67,7 +68,7 @@ __device__ __forceinline__ void block_colsum(double (&a)[V], int tpr, int C, dou
     for (int c = tid; c < C; c += 256) {
         double x = 0.0;
         for (int k = 0; k < nslot; ++k) x += lds[k * C + c];
-        out[c] = x;
+        xacc_add(acc, coff + c, x);
     }
 }
 
@@ -89,7 +90,7 @@ __device__ __forceinline__ double block_sum_partials(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------- BN statistics
-// Partial column sums: part[blk][0..C) = sum y, part[blk][C..2C) = sum y^2 (double).
+// Column sums into the exact accumulator acc (2C columns): [0..C) = sum y, [C..2C) = sum y^2.
 // Column-streaming kernels over a row-major [R][C] map: thread = (row lane rr, column group cg of V channels);
 // a block pass covers rpp = 256 / (C/V) consecutive rows (one contiguous 4 KB span); each thread keeps its
 // V channels' parameters in registers and has kU rows in flight.
@@ -98,7 +99,7 @@ constexpr int kUb = 2;  // backward (two operands per row, the next step's rows 
 
 template <typename T>
 __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ y, int64_t R, int C, int64_t rows_per_blk,
-                                                          double* __restrict__ part) {
+                                                          XAcc acc) {
     constexpr int V = Vec16<T>::N;
     __shared__ double s1[2048], s2[2048];
     const int tpr = C / V;                 // threads per row
@@ -123,76 +124,23 @@ __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ 
             for (int v = 0; v < V; ++v) { a[v] += x[v]; b[v] += (double)x[v] * x[v]; }
         }
     }
-    block_colsum<V>(a, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C);
-    block_colsum<V>(b, tpr, C, s2, part + (int64_t)blockIdx.x * 2 * C + C);
+    block_colsum<V>(a, tpr, C, s1, acc, 0);
+    block_colsum<V>(b, tpr, C, s2, acc, C);
 }
 
-// ---------------------------------------------------------------- partial-row reductions
-// Partials are [rows][ncols] f64 tables (one row per producing block / GEMM tile).  Large tables are first
-// folded to <= kFoldRows rows by parts_fold_kernel (grid: 64-column slabs x row chunks, lanes = columns so
-// every wave reads 512 contiguous bytes); the finalizers then reduce <= a few hundred rows with 16 waves per
-// 64 columns.  Both passes use fixed partitions and fixed combine orders (deterministic).
-constexpr int kFoldRows = 64;      // max rows a fold leaves (one load round per wave in the finalizers)
-constexpr int kFoldMin = 64;       // fold tables with more rows than this
-__global__ __launch_bounds__(256) void parts_fold_kernel(const double* __restrict__ part, int nrows, int ncols, int rp,
-                                                         double* __restrict__ out) {
-    __shared__ double red[4][64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + lane;
-    const int r0 = blockIdx.y * rp, r1 = min(nrows, r0 + rp);
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0, a5 = 0.0, a6 = 0.0, a7 = 0.0;
-    if (c < ncols) {
-        const double* p = part + c;
-        int r = r0 + w;
-        for (; r + 28 < r1; r += 32) {  // 8 row loads in flight per lane
-            a0 += p[(int64_t)r * ncols];
-            a1 += p[(int64_t)(r + 4) * ncols];
-            a2 += p[(int64_t)(r + 8) * ncols];
-            a3 += p[(int64_t)(r + 12) * ncols];
-            a4 += p[(int64_t)(r + 16) * ncols];
-            a5 += p[(int64_t)(r + 20) * ncols];
-            a6 += p[(int64_t)(r + 24) * ncols];
-            a7 += p[(int64_t)(r + 28) * ncols];
-        }
-        for (; r < r1; r += 4) a0 += p[(int64_t)r * ncols];
-    }
-    red[w][lane] = ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7));
-    __syncthreads();
-    if (w == 0 && c < ncols) out[(int64_t)blockIdx.y * ncols + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-}
-// sum over rows of column col of a [nrows][stride] table: 16 waves x 4 accumulators, LDS combine (1024 threads)
-__device__ __forceinline__ double fold_column(const double* __restrict__ p, int nrows, int64_t stride, int col, bool ok,
-                                              double (*sh)[64]) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    if (ok) {
-        int r = w;
-        for (; r + 48 < nrows; r += 64) {
-            a0 += p[(int64_t)r * stride + col];
-            a1 += p[(int64_t)(r + 16) * stride + col];
-            a2 += p[(int64_t)(r + 32) * stride + col];
-            a3 += p[(int64_t)(r + 48) * stride + col];
-        }
-        for (; r < nrows; r += 16) a0 += p[(int64_t)r * stride + col];
-    }
-    sh[w][lane] = (a0 + a1) + (a2 + a3);
-    __syncthreads();
-    double x = 0.0;
-    for (int k = 0; k < 16; ++k) x += sh[k][lane];
-    __syncthreads();
-    return x;
-}
-
-// mean / invstd / running statistics from [nblk][2C] partials (sum | sum of squares); grid ceil(C / 64) x 1024
-__global__ __launch_bounds__(1024) void bn_finalize_kernel(const double* __restrict__ part, int nblk, int C, int64_t R,
-                                                           float* mean, float* invstd, float* rmean, float* rvar,
-                                                           int64_t* nbt, float momentum, float eps) {
-    __shared__ double sh[16][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const bool ok = c < C;
-    const double s = fold_column(part, nblk, 2 * C, c, ok, sh);
-    const double q = fold_column(part, nblk, 2 * C, C + c, ok, sh);
-    if (threadIdx.x >= 64 || !ok) return;
+// ---------------------------------------------------------------- statistics finalize
+// mean / invstd / running statistics from the exact accumulator (2C columns: sum | sum of squares); one thread per
+// channel, grid ceil(C / 64) x 64 (the C > 512 layers, whose consumers do not finalize themselves)
+__global__ __launch_bounds__(64) void bn_finalize_kernel(XAcc acc, int C, int64_t R, float* mean, float* invstd,
+                                                         float* rmean, float* rvar, int64_t* nbt, float momentum,
+                                                         float eps) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= C) return;
+    long long w[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    for (int sh = 0; sh < acc.shards; ++sh)
+        for (int k = 0; k < 2; ++k)
+            for (int j = 0; j < 3; ++j) w[k][j] += (long long)acc.p[((size_t)sh * 3 + j) * acc.ncols + k * C + c];
+    const double s = xacc_value(w[0][0], w[0][1], w[0][2]), q = xacc_value(w[1][0], w[1][1], w[1][2]);
     if (c == 0 && nbt) nbt[0] += 1;
     const double m = s / (double)R;
     double var = q / (double)R - m * m;
@@ -214,89 +162,64 @@ __global__ void bn_eval_kernel(const float* rmean, const float* rvar, int C, flo
 }
 
 // Consumer-side BatchNorm finalize: the streaming kernel that needs the per-channel statistics (bn_act: mean /
-// invstd; bn_bwd_apply: sum dz / sum dz*xhat) folds the <= kFinRows-row [rows][2C] f64 partial table itself,
-// in a fixed row order, into LDS -- instead of a separate one-block-per-64-channels finalize launch (every
-// such launch costs >= 5 us on the critical path).  Every block computes the same values in the same order;
-// block 0 also stores the ones later kernels read (mean / invstd and the running statistics; dgamma / dbeta).
-constexpr int kFinRows = 8;       // rows one thread folds
-// rows a consumer folds itself: channels C <= 256 spread every channel over 256 / C threads (row groups)
-inline int fin_max_rows(int C) { return kFinRows * (C <= 256 ? 256 / C : 1); }
+// invstd; bn_bwd_apply: sum dz / sum dz*xhat) reads the totals from the producer's exact accumulator itself
+// (xacc_fold: shards x 6C int64 words) -- no finalize launch (every one costs >= 5 us on the critical path).
+// Every block computes the same values; block 0 also stores the ones later kernels read (mean / invstd and the
+// running statistics; dgamma / dbeta).
+constexpr int kFinMaxC = 512;  // channels a consumer finalizes itself (LDS: 2 x 512 floats + 2 x 512 doubles)
 struct BnFin {
-    const double* part = nullptr;  // [rows][2C]
-    int rows = 0;
+    XAcc acc;                      // 2C columns
     int64_t R = 0;                 // rows of the normalised map (forward)
     float *mean = nullptr, *invstd = nullptr, *rmean = nullptr, *rvar = nullptr;  // forward outputs (block 0)
     int64_t* nbt = nullptr;
     float momentum = 0.f, eps = 0.f;
     float *dgamma = nullptr, *dbeta = nullptr;  // backward outputs (block 0)
 };
-// x0[c] / x1[c] (LDS, c < C <= 512) = the two folded columns c and C + c; fwd: -> mean / invstd (+ running stats).
-// C <= 256: thread (c = t % C, g = t / C) sums rows g, g + G, ... (G = 256 / C), then the G group sums are added
-// in group order; C > 256: each thread folds channels t and t + 256 alone.  red: >= 512 doubles of LDS.
+// The per-channel values from the totals tot (LDS, 2C doubles): fwd mean / invstd, bwd sum dz / sum dz*xhat
 template <bool kFwd>
-__device__ __forceinline__ void bn_fin_prologue(const BnFin& f, int C, float* x0, float* x1, double* red) {
-    const int tid = threadIdx.x;
-    const int G = C <= 256 ? kThreads / C : 1;
-    auto fold = [&](int c, int g, double& s, double& q) {
-        double ps[kFinRows], pq[kFinRows];
-#pragma unroll
-        for (int i = 0; i < kFinRows; ++i) {  // every row load issued before the adds
-            const int r = g + i * G;
-            ps[i] = r < f.rows ? f.part[(int64_t)r * 2 * C + c] : 0.0;
-            pq[i] = r < f.rows ? f.part[(int64_t)r * 2 * C + C + c] : 0.0;
-        }
-        s = 0.0;
-        q = 0.0;
-#pragma unroll
-        for (int i = 0; i < kFinRows; ++i) { s += ps[i]; q += pq[i]; }
-    };
-    auto finish = [&](int c, double s, double q) {
-        if constexpr (kFwd) {
-            const double m = s / (double)f.R;
-            double var = q / (double)f.R - m * m;
-            if (var < 0.0) var = 0.0;
-            const float mf = (float)m, inv = (float)(1.0 / sqrt(var + (double)f.eps));
-            x0[c] = mf;
-            x1[c] = inv;
-            if (blockIdx.x == 0) {
-                f.mean[c] = mf;
-                f.invstd[c] = inv;
+__device__ __forceinline__ void bn_fin_values(const BnFin& f, const double* tot, int C, int c, float& x0, float& x1,
+                                              double* var_out = nullptr) {
+    const double s = tot[c], q = tot[C + c];
+    if constexpr (kFwd) {
+        const double m = s / (double)f.R;
+        double var = q / (double)f.R - m * m;
+        if (var < 0.0) var = 0.0;
+        x0 = (float)m;
+        x1 = (float)(1.0 / sqrt(var + (double)f.eps));
+        if (var_out) *var_out = var;
+    } else {
+        x0 = (float)s;
+        x1 = (float)q;
+    }
+}
+// x0[c] / x1[c] (LDS floats, c < C) <- the per-channel values from the accumulator's totals (tot: LDS >= 2C
+// doubles; red: LDS >= 3 * 256 int64, may not overlap tot); block 0 stores the finalized per-channel outputs.
+// Ends with a barrier.
+template <bool kFwd>
+__device__ __forceinline__ void bn_fin_prologue(const BnFin& f, int C, double* tot, long long* red, float* x0s,
+                                                float* x1s) {
+    xacc_fold(f.acc, tot, red);
+    for (int c = threadIdx.x; c < C; c += kThreads) {
+        float x0, x1;
+        double var = 0.0;
+        bn_fin_values<kFwd>(f, tot, C, c, x0, x1, &var);
+        x0s[c] = x0;
+        x1s[c] = x1;
+        if (blockIdx.x == 0) {
+            if constexpr (kFwd) {
+                f.mean[c] = x0;
+                f.invstd[c] = x1;
                 if (f.rmean) {
+                    const double m = tot[c] / (double)f.R;
                     const double unb = f.R > 1 ? var * (double)f.R / (double)(f.R - 1) : var;
                     f.rmean[c] = (float)((1.0 - f.momentum) * f.rmean[c] + f.momentum * m);
                     f.rvar[c] = (float)((1.0 - f.momentum) * f.rvar[c] + f.momentum * unb);
                 }
                 if (c == 0 && f.nbt) f.nbt[0] += 1;
+            } else {
+                f.dbeta[c] = x0;
+                f.dgamma[c] = x1;
             }
-        } else {
-            x0[c] = (float)s;
-            x1[c] = (float)q;
-            if (blockIdx.x == 0) {
-                f.dbeta[c] = (float)s;
-                f.dgamma[c] = (float)q;
-            }
-        }
-    };
-    if (C <= 256) {
-        const int c = tid % C, g = tid / C;
-        double s, q;
-        fold(c, g, s, q);
-        red[g * C + c] = s;
-        red[kThreads + g * C + c] = q;
-        __syncthreads();
-        if (tid < C) {
-            double ss = 0.0, qq = 0.0;
-            for (int k = 0; k < G; ++k) {
-                ss += red[k * C + tid];
-                qq += red[kThreads + k * C + tid];
-            }
-            finish(tid, ss, qq);
-        }
-    } else {
-        for (int c = tid; c < C; c += kThreads) {
-            double s, q;
-            fold(c, 0, s, q);
-            finish(c, s, q);
         }
     }
     __syncthreads();
@@ -319,8 +242,8 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ y, in
                                                      int act, const uint8_t* __restrict__ mask, float mscale,
                                                      T* __restrict__ a, int lda, BnFin fin) {
     constexpr int V = Vec16<T>::N;
-    __shared__ float fin_sh[kFin ? 1024 : 1];
-    __shared__ double fin_red[kFin ? 2 * kThreads : 1];
+    __shared__ double fin_sh[kFin ? 2 * kFinMaxC + 3 * kThreads : 1];  // totals | fold scratch
+    __shared__ float fin_x[kFin ? 2 * kFinMaxC : 1];                     // mean | invstd
     const int tpr = C / V, rpp = kThreads / tpr;
     const int tid = threadIdx.x, cg = tid % tpr, rr = tid / tpr;
     const int c0 = cg * V;
@@ -334,9 +257,10 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ y, in
     if (rfirst < R) load_rows(rfirst);  // the first pass's rows are in flight during the finalize prologue
     float mu[V], is[V], ga[V], be[V];
     if constexpr (kFin) {
-        bn_fin_prologue<true>(fin, C, fin_sh, fin_sh + 512, fin_red);
-        BnChan::load(fin_sh, c0, mu);
-        BnChan::load(fin_sh + 512, c0, is);
+        bn_fin_prologue<true>(fin, C, fin_sh, reinterpret_cast<long long*>(fin_sh + 2 * kFinMaxC), fin_x,
+                              fin_x + kFinMaxC);
+        BnChan::load(fin_x, c0, mu);
+        BnChan::load(fin_x + kFinMaxC, c0, is);
     } else {
         BnChan::load(mean, c0, mu);
         BnChan::load(invstd, c0, is);
@@ -371,7 +295,7 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, int act,
                                                              const uint8_t* __restrict__ mask, float mscale,
-                                                             int64_t rows_per_blk, double* __restrict__ part) {
+                                                             int64_t rows_per_blk, XAcc acc) {
     constexpr int V = Vec16<T>::N;
     __shared__ double s1[2048];
     const int tpr = C / V, rpp = kThreads / tpr;
@@ -425,20 +349,27 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
     double da_[V], db_[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) { da_[v] = a[v]; db_[v] = b[v]; }
-    block_colsum<V>(da_, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C);
+    block_colsum<V>(da_, tpr, C, s1, acc, 0);
     __syncthreads();   // s1 reused
-    block_colsum<V>(db_, tpr, C, s1, part + (int64_t)blockIdx.x * 2 * C + C);
+    block_colsum<V>(db_, tpr, C, s1, acc, C);
 }
 
-// backward partials [nblk][2C]: sum dz (-> dbeta), sum dz*xhat (-> dgamma); grid ceil(C / 64) x 1024
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nblk, int C,
-                                                               float* dgamma, float* dbeta, float* sums_f) {
-    __shared__ double sh[16][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const bool ok = c < C;
-    const double s = fold_column(part, nblk, 2 * C, c, ok, sh);
-    const double q = fold_column(part, nblk, 2 * C, C + c, ok, sh);
-    if (threadIdx.x >= 64 || !ok) return;
+// column c of an exact accumulator, summed over its shards
+__device__ __forceinline__ double xacc_column(const XAcc& acc, int c) {
+    long long a = 0, b = 0, d = 0;
+    for (int sh = 0; sh < acc.shards; ++sh) {
+        const unsigned long long* q = acc.p + (size_t)sh * 3 * acc.ncols + c;
+        a += (long long)q[0];
+        b += (long long)q[acc.ncols];
+        d += (long long)q[2 * acc.ncols];
+    }
+    return xacc_value(a, b, d);
+}
+// backward moments (2C columns): sum dz (-> dbeta), sum dz*xhat (-> dgamma); grid ceil(C / 64) x 64 (C > 512)
+__global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(XAcc acc, int C, float* dgamma, float* dbeta, float* sums_f) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= C) return;
+    const double s = xacc_column(acc, c), q = xacc_column(acc, C + c);
     dbeta[c] = (float)s;
     dgamma[c] = (float)q;
     sums_f[c] = (float)s;
@@ -456,7 +387,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ beta, int act,
                                                            const uint8_t* __restrict__ mask, float mscale,
                                                            const float* __restrict__ sums, T* __restrict__ dy,
-                                                           int64_t rows_per_blk, double* __restrict__ part, BnFin fin) {
+                                                           int64_t rows_per_blk, XAcc bias_acc, BnFin fin) {
     constexpr int V = Vec16<T>::N;
     __shared__ double s1[2048];
     const int tpr = C / V, rpp = kThreads / tpr;
@@ -483,10 +414,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     };
     if (r0 + rr < r1) fetch(r0 + rr);  // in flight during the finalize prologue
     if constexpr (kFin) {
-        float* fsh = reinterpret_cast<float*>(s1 + 2 * kThreads);  // s1 is free until the closing block_colsum
-        bn_fin_prologue<false>(fin, C, fsh, fsh + 512, s1);
-        BnChan::load(fsh, c0, s0);
-        BnChan::load(fsh + 512, c0, sx);
+        // s1 is free until the closing block_colsum: totals in [0, 2C), the 2C sums as floats from 1024 (C
+        // doubles), fold scratch after them (only used when 2C < 256: ends below 1024 + 64 + 768)
+        float* xs = reinterpret_cast<float*>(s1 + 2 * kFinMaxC);
+        bn_fin_prologue<false>(fin, C, s1, reinterpret_cast<long long*>(s1 + 2 * kFinMaxC + C), xs, xs + C);
+        BnChan::load(xs, c0, s0);
+        BnChan::load(xs + C, c0, sx);
         __syncthreads();  // every thread has its sums before block_colsum reuses s1
     } else {
         BnChan::load(sums, c0, s0);
@@ -519,14 +452,43 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
             for (int v = 0; v < V; ++v) a[v] += to_f32<T>(from_f32<T>(o[v]));
         }
     }
-    double ad[V];
+    if (bias_acc.on()) {
+        double ad[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) ad[v] = a[v];
-    block_colsum<V>(ad, tpr, C, s1, part + (int64_t)blockIdx.x * C);
+        for (int v = 0; v < V; ++v) ad[v] = a[v];
+        block_colsum<V>(ad, tpr, C, s1, bias_acc, 0);
+    }
 }
 
+// out[c] = column c of an exact accumulator (bias gradients); grid ceil(C / 64) x 64
+__global__ __launch_bounds__(64) void xacc_to_f32_kernel(XAcc acc, int C, float* out) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c < C) out[c] = (float)xacc_column(acc, c);
+}
 
-// out[c] = sum_k part[k][c] over [nblk][C] partials; grid ceil(C / 64) x 1024
+// sum over rows of column col of a [nrows][stride] table: 16 waves x 4 accumulators, LDS combine (1024 threads)
+__device__ __forceinline__ double fold_column(const double* __restrict__ p, int nrows, int64_t stride, int col, bool ok,
+                                              double (*sh)[64]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    if (ok) {
+        int r = w;
+        for (; r + 48 < nrows; r += 64) {
+            a0 += p[(int64_t)r * stride + col];
+            a1 += p[(int64_t)(r + 16) * stride + col];
+            a2 += p[(int64_t)(r + 32) * stride + col];
+            a3 += p[(int64_t)(r + 48) * stride + col];
+        }
+        for (; r < nrows; r += 16) a0 += p[(int64_t)r * stride + col];
+    }
+    sh[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    double x = 0.0;
+    for (int k = 0; k < 16; ++k) x += sh[k][lane];
+    __syncthreads();
+    return x;
+}
+// out[c] = sum_k part[k][c] over [nblk][C] partials (the generic colsum); grid ceil(C / 64) x 1024
 __global__ __launch_bounds__(1024) void colsum_finalize_kernel(const double* __restrict__ part, int nblk, int C,
                                                                float* out) {
     __shared__ double sh[16][64];
@@ -546,35 +508,6 @@ __global__ __launch_bounds__(1024) void colsum_finalize_kernel(const double* __r
         HLMC_PROBE_END(s);                                \
     } while (0)
 
-// Fold a [nrows][ncols] partial table into scratch when it is large; returns the table the finalizers read.
-size_t fold_bytes(int ncols) { return (size_t)kFoldRows * ncols * sizeof(double); }
-struct Folded {
-    const double* p;
-    int rows;
-};
-Folded fold_parts(hipStream_t s, const double* part, int nrows, int ncols, Ws ws) {
-    if (nrows <= kFoldMin || !ws.p || ws.bytes < fold_bytes(ncols)) return Folded{part, nrows};
-    int G = std::min(kFoldRows, cdiv(nrows, 64));  // >= 64 rows per fold block: one 4-load round per wave
-    const int rp = cdiv(nrows, G);
-    G = cdiv(nrows, rp);
-    double* out = reinterpret_cast<double*>(ws.p);
-    HLMC_BN_PROBED(s, 8.0 * ((double)nrows + G) * ncols,
-                   (parts_fold_kernel<<<dim3(cdiv(ncols, 64), G), 256, 0, s>>>(part, nrows, ncols, rp, out)));
-    return Folded{out, G};
-}
-// Fold to at most maxrows rows (a consumer-side finalize reads <= fin_max_rows(C) rows); tables already that
-// short are returned as they are unless `copy` (the consumer overwrites the table).
-Folded fold_parts_to(hipStream_t s, const double* part, int nrows, int ncols, Ws ws, int maxrows, bool copy = false) {
-    if (nrows <= maxrows && !copy) return Folded{part, nrows};
-    if (!ws.p || ws.bytes < (size_t)maxrows * ncols * sizeof(double)) return Folded{nullptr, 0};
-    int G = maxrows;
-    const int rp = cdiv(nrows, G);
-    G = cdiv(nrows, rp);
-    double* out = reinterpret_cast<double*>(ws.p);
-    HLMC_BN_PROBED(s, 8.0 * ((double)nrows + G) * ncols,
-                   (parts_fold_kernel<<<dim3(cdiv(ncols, 64), G), 256, 0, s>>>(part, nrows, ncols, rp, out)));
-    return Folded{out, G};
-}
 inline unsigned fin_grid(int C) { return (unsigned)cdiv(C, 64); }
 
 // generic column sum for arbitrary ld/cols (bias grads): block = (row chunk, 64-column slab);
@@ -599,13 +532,13 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const T* __restrict
 // y[b, oh, ow, co] = bias[co] + sum_taps x[b, 2oh-1+kh, 2ow-1+kw] * w[co*9 + tap]  (1 input channel, CO = 32)
 // Four threads per output pixel, each computing 8 channels (one 16-byte store): a wave's store instruction
 // writes 1 KB contiguous; the 9 input taps are re-read by the 4 threads from L1.
-// MODE 1 (encoder input conv): also the BatchNorm statistics of the stored outputs, one [sum | sum of squares]
-// f64 partial row per block (the col_moments pass it replaces).  MODE 2 (data gradient of the decoder's output
+// MODE 1 (encoder input conv): also the BatchNorm statistics of the stored outputs, [sum | sum of squares] into an
+// exact accumulator (the col_moments pass it replaces).  MODE 2 (data gradient of the decoder's output
 // convT, which writes the gradient of the last BatchNorm layer's output): also that layer's backward moments
-// [sum dz | sum dz * xhat] (bn_bwd_moments_kernel's partial rows), with ybn / mean / invstd / gamma / beta of
-// the layer (LeakyReLU 0.01).  Both: per-thread accumulators over the grid-stride pixels, block_colsum rows.
+// [sum dz | sum dz * xhat] (what bn_bwd_moments_kernel accumulates), with ybn / mean / invstd / gamma / beta of
+// the layer (LeakyReLU 0.01).  Both: per-thread accumulators over the grid-stride pixels, block_colsum per block.
 struct C1Fuse {
-    double* part = nullptr;
+    XAcc acc;  // 2 CO columns
     const void* ybn = nullptr;
     const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
 };
@@ -707,9 +640,9 @@ __global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(cons
         double da_[V], db_[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) { da_[v] = fa[v]; db_[v] = fb[v]; }
-        block_colsum<V>(da_, G, CO, fred, fz.part + (int64_t)blockIdx.x * 2 * CO);
+        block_colsum<V>(da_, G, CO, fred, fz.acc, 0);
         __syncthreads();
-        block_colsum<V>(db_, G, CO, fred, fz.part + (int64_t)blockIdx.x * 2 * CO + CO);
+        block_colsum<V>(db_, G, CO, fred, fz.acc, CO);
     }
 }
 
@@ -907,14 +840,26 @@ __global__ void flat_to_nhwc_kernel(const T* __restrict__ x, int ldx, int B, int
         y[i] = x[(int64_t)b * ldx + (int64_t)c * h * w + hw];
     }
 }
+// optional copies a reparameterisation launch also writes: the caller's mu / logvar outputs and (host-supplied eps)
+// the eps the backward keeps -- one launch instead of a copy launch plus the reparameterisation
+struct LatentOut {
+    float* mu = nullptr;
+    float* lv = nullptr;
+    float* eps = nullptr;
+};
 template <typename T>
 __global__ void reparam_fwd_kernel(const float* __restrict__ mu, const float* __restrict__ lv,
-                                   const float* __restrict__ eps, int n_rows, int L, T* __restrict__ z, int ldz) {
+                                   const float* __restrict__ eps, int n_rows, int L, T* __restrict__ z, int ldz,
+                                   LatentOut lo) {
     int64_t n = (int64_t)n_rows * L;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         int r = (int)(i / L), c = (int)(i % L);
-        float sd = expf(0.5f * lv[i]);
-        z[(int64_t)r * ldz + c] = from_f32<T>(mu[i] + eps[i] * sd);
+        const float m = mu[i], l = lv[i], e = eps[i];
+        float sd = expf(0.5f * l);
+        z[(int64_t)r * ldz + c] = from_f32<T>(m + e * sd);
+        if (lo.mu) lo.mu[i] = m;
+        if (lo.lv) lo.lv[i] = l;
+        if (lo.eps) lo.eps[i] = e;
     }
 }
 // ---------------------------------------------------------------- reparameterisation noise (Philox4x32-10)
@@ -961,7 +906,7 @@ __global__ void randn_kernel(float* __restrict__ out, int64_t n, uint64_t seed, 
 template <typename T>
 __global__ void reparam_rng_kernel(const float* __restrict__ mu, const float* __restrict__ lv, uint64_t seed,
                                    uint64_t offset, int n_rows, int L, float* __restrict__ eps_out, T* __restrict__ z,
-                                   int ldz) {
+                                   int ldz, LatentOut lo) {
     const int64_t n = (int64_t)n_rows * L, groups = (n + 3) / 4;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < groups; t += (int64_t)gridDim.x * blockDim.x) {
         float v[4];
@@ -971,8 +916,11 @@ __global__ void reparam_rng_kernel(const float* __restrict__ mu, const float* __
             const int64_t i = 4 * t + j;
             if (i >= n) break;
             const int r = (int)(i / L), c = (int)(i - (int64_t)r * L);
+            const float m = mu[i], l = lv[i];
             eps_out[i] = v[j];
-            z[(int64_t)r * ldz + c] = from_f32<T>(mu[i] + v[j] * expf(0.5f * lv[i]));
+            z[(int64_t)r * ldz + c] = from_f32<T>(m + v[j] * expf(0.5f * l));
+            if (lo.mu) lo.mu[i] = m;
+            if (lo.lv) lo.lv[i] = l;
         }
     }
 }
@@ -1130,6 +1078,27 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamBatch bt, AdamCoef c) {
 // Adam update, keeps the new values in LDS (row stride 32*taps+1: conflict-free for both read-outs) and
 // writes each (i0, tap) segment of P0 and each (i1, tap) segment of P1 as 32 consecutive elements.
 // Unpacked tensors (BatchNorm affine, biases) are 4096-element chunks of the same launch.
+// Tile edge of a packed job: conv weights (taps 9) 32 x 32 x 9, linear weights (taps 1) 64 x 64 (4096 elements:
+// 16 per thread, every float4 of p / g / m / v in flight at once; 128-byte pack segments)
+__host__ __device__ inline int adam_tile_edge(int taps) { return taps == 1 ? 64 : 32; }
+// the tile's P0 [d0][taps][ld0] and P1 [d1][taps][ld1] segments from the updated values in LDS (row stride RS)
+template <typename T>
+__device__ __forceinline__ void pack_tile_out(const ops::AdamJob& jb, const float* tile, int RS, int TS, int t0, int t1,
+                                              int n0, int n1) {
+    const int taps = jb.taps, sh = TS == 64 ? 6 : 5;
+    T* p0 = (T*)jb.p0;
+    T* p1 = (T*)jb.p1;
+    if (p0)
+        for (int e = threadIdx.x; e < n0 * taps * TS; e += 256) {
+            const int q = e & (TS - 1), at = e >> sh, a = at / taps, tap = at - a * taps;
+            if (q < n1) p0[((int64_t)(t0 + a) * taps + tap) * jb.ld0 + t1 + q] = from_f32<T>(tile[a * RS + q * taps + tap]);
+        }
+    if (p1)
+        for (int e = threadIdx.x; e < n1 * taps * TS; e += 256) {
+            const int q = e & (TS - 1), ct = e >> sh, cc = ct / taps, tap = ct - cc * taps;
+            if (q < n0) p1[((int64_t)(t1 + cc) * taps + tap) * jb.ld1 + t0 + q] = from_f32<T>(tile[q * RS + cc * taps + tap]);
+        }
+}
 template <typename T>
 // cdev (nullable): coefficients read from device memory (graph replays: the host refreshes them per step)
 // tile_base: first tile of this launch (a launch may cover a contiguous tile range of the job list)
@@ -1149,19 +1118,19 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(const ops::AdamJob* __re
         for (int64_t i = base + threadIdx.x; i < end; i += 256) adam_elem(jb.p, jb.g, jb.m, jb.v, i, c);
         return;
     }
-    const int taps = jb.taps;
+    const int taps = jb.taps, TS = adam_tile_edge(taps);
     const int tt0 = tl / jb.nt1, tt1 = tl - tt0 * jb.nt1;
-    const int t0 = tt0 * 32, t1 = tt1 * 32;
-    const int n0 = min(32, jb.d0 - t0), n1 = min(32, jb.d1 - t1);
-    const int RS = 32 * taps + 1;
-    __shared__ float tile[32 * (32 * 9 + 1)];
+    const int t0 = tt0 * TS, t1 = tt1 * TS;
+    const int n0 = min(TS, jb.d0 - t0), n1 = min(TS, jb.d1 - t1);
+    const int RS = TS * taps + 1;
+    __shared__ float tile[32 * (32 * 9 + 1)];  // >= 64 x 65 as well
     const int rowlen = n1 * taps;
     const int64_t row0 = ((int64_t)t0 * jb.d1 + t1) * taps;  // element offset of the tile's first row
     const auto al16 = [&](const float* q) { return ((reinterpret_cast<uintptr_t>(q + row0)) & 15) == 0; };
     if ((rowlen & 3) == 0 && ((jb.d1 * taps) & 3) == 0 && al16(jb.p) && al16(jb.g) && al16(jb.m) && al16(jb.v)) {
         // 16-byte rows: every thread has U float4 of each of p / g / m / v in flight before the updates
         // (the per-element path below waits on each element's four loads in turn: 3.7 TB/s for the whole step)
-        constexpr int U = 3;
+        constexpr int U = 4;
         const int rl4 = rowlen >> 2, total4 = n0 * rl4;
         for (int e0 = threadIdx.x; e0 < total4; e0 += 256 * U) {
             float4 pp[U], gg[U], mm[U], vv[U];
@@ -1205,18 +1174,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(const ops::AdamJob* __re
         }
     }
     __syncthreads();
-    T* p0 = (T*)jb.p0;
-    T* p1 = (T*)jb.p1;
-    if (p0)
-        for (int e = threadIdx.x; e < n0 * taps * 32; e += 256) {
-            const int q = e & 31, at = e >> 5, a = at / taps, tap = at - a * taps;
-            if (q < n1) p0[((int64_t)(t0 + a) * taps + tap) * jb.ld0 + t1 + q] = from_f32<T>(tile[a * RS + q * taps + tap]);
-        }
-    if (p1)
-        for (int e = threadIdx.x; e < n1 * taps * 32; e += 256) {
-            const int q = e & 31, ct = e >> 5, cc = ct / taps, tap = ct - cc * taps;
-            if (q < n0) p1[((int64_t)(t1 + cc) * taps + tap) * jb.ld1 + t0 + q] = from_f32<T>(tile[q * RS + cc * taps + tap]);
-        }
+    pack_tile_out<T>(jb, tile, RS, TS, t0, t1, n0, n1);
 }
 
 // packing alone (forward of a model whose weights were changed outside the engine)
@@ -1231,11 +1189,11 @@ __global__ __launch_bounds__(256) void pack_kernel(const ops::AdamJob* __restric
     const ops::AdamJob jb = jobs[lo];
     if (jb.taps == 0) return;
     const int tl = bid - jb.tile0;
-    const int taps = jb.taps;
+    const int taps = jb.taps, TS = adam_tile_edge(taps);
     const int tt0 = tl / jb.nt1, tt1 = tl - tt0 * jb.nt1;
-    const int t0 = tt0 * 32, t1 = tt1 * 32;
-    const int n0 = min(32, jb.d0 - t0), n1 = min(32, jb.d1 - t1);
-    const int RS = 32 * taps + 1;
+    const int t0 = tt0 * TS, t1 = tt1 * TS;
+    const int n0 = min(TS, jb.d0 - t0), n1 = min(TS, jb.d1 - t1);
+    const int RS = TS * taps + 1;
     __shared__ float tile[32 * (32 * 9 + 1)];
     const int rowlen = n1 * taps;
     {
@@ -1248,18 +1206,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const ops::AdamJob* __restric
         }
     }
     __syncthreads();
-    T* p0 = (T*)jb.p0;
-    T* p1 = (T*)jb.p1;
-    if (p0)
-        for (int e = threadIdx.x; e < n0 * taps * 32; e += 256) {
-            const int q = e & 31, at = e >> 5, a = at / taps, tap = at - a * taps;
-            if (q < n1) p0[((int64_t)(t0 + a) * taps + tap) * jb.ld0 + t1 + q] = from_f32<T>(tile[a * RS + q * taps + tap]);
-        }
-    if (p1)
-        for (int e = threadIdx.x; e < n1 * taps * 32; e += 256) {
-            const int q = e & 31, ct = e >> 5, cc = ct / taps, tap = ct - cc * taps;
-            if (q < n0) p1[((int64_t)(t1 + cc) * taps + tap) * jb.ld1 + t0 + q] = from_f32<T>(tile[q * RS + cc * taps + tap]);
-        }
+    pack_tile_out<T>(jb, tile, RS, TS, t0, t1, n0, n1);
 }
 
 }  // namespace
@@ -1267,15 +1214,9 @@ __global__ __launch_bounds__(256) void pack_kernel(const ops::AdamJob* __restric
 // ============================================================================ launchers
 namespace ops {
 
-size_t fold_ws(int ncols) { return fold_bytes(ncols); }
-// [nblk][2C] f64 partials | sums 2C f32 | fold scratch
-static size_t bn_fold_off(int64_t R, int C) {
-    return ((size_t)bn_blocks(R, C) * 2 * C * sizeof(double) + 2 * C * sizeof(float) + 255) & ~(size_t)255;
-}
-size_t bn_ws(int64_t R, int C) { return bn_fold_off(R, C) + fold_ws(2 * C); }
-static Ws ws_from(Ws ws, size_t off) {
-    return off < ws.bytes ? Ws{reinterpret_cast<float*>(reinterpret_cast<char*>(ws.p) + off), ws.bytes - off} : Ws{nullptr, 0};
-}
+// the accumulator a layer's statistics use (xacc_shards(C) copies of 2C columns)
+size_t bn_acc_bytes(int C) { return XAcc::bytes(xacc_shards(C), 2 * C); }
+size_t bias_acc_bytes(int C) { return XAcc::bytes(xacc_shards(C), C); }
 
 template <typename T>
 static int check_bn_shape(int C) {
@@ -1283,32 +1224,31 @@ static int check_bn_shape(int C) {
     HLMC_CHECK_ARG(C % V == 0 && C / V <= 256 && 256 % (C / V) == 0, "BatchNorm channel count unsupported");
     return HLMC_OK;
 }
+static int check_acc(const XAcc& a, int ncols) {
+    HLMC_CHECK_ARG(a.p && a.ncols == ncols && a.shards >= 1 && a.shards <= kXAccMaxShards, "statistics accumulator");
+    return HLMC_OK;
+}
 
 template <typename T>
 int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean, float* run_var,
-             int64_t* nbt, float momentum, float eps, Ws ws) {
+             int64_t* nbt, float momentum, float eps, XAcc acc) {
     HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_TRY(check_acc(acc, 2 * C));
     const int nblk = bn_blocks(R, C);
-    HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
-    double* part = reinterpret_cast<double*>(ws.p);
-    HLMC_BN_PROBED(s, (double)sizeof(T) * R * C + 16.0 * nblk * C,
-                   (col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), part)));
+    HLMC_BN_PROBED(s, (double)sizeof(T) * R * C,
+                   (col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), acc)));
     HLMC_LAUNCHED();
-    const Folded f = fold_parts(s, part, nblk, 2 * C, ws_from(ws, bn_fold_off(R, C)));
-    HLMC_BN_PROBED(s, 16.0 * f.rows * C,
-                   (bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, R, mean, invstd, run_mean, run_var,
-                                                                    nbt, momentum, eps)));
+    bn_finalize_kernel<<<fin_grid(C), 64, 0, s>>>(acc, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
 
-int bn_stats_from_parts(hipStream_t s, const double* part, int nparts, int64_t R, int C, float* mean, float* invstd,
-                        float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, Ws fold) {
-    HLMC_CHECK_ARG(part && nparts > 0 && R > 0, "bn_stats_from_parts arguments");
-    const Folded f = fold_parts(s, part, nparts, 2 * C, fold);
-    HLMC_BN_PROBED(s, 16.0 * f.rows * C,
-                   (bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, R, mean, invstd, run_mean, run_var,
-                                                                    nbt, momentum, eps)));
+template <typename T>
+int bn_moments(hipStream_t s, const T* y, int64_t R, int C, XAcc acc) {
+    HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_TRY(check_acc(acc, 2 * C));
+    HLMC_BN_PROBED(s, (double)sizeof(T) * R * C,
+                   (col_moments_kernel<T><<<bn_blocks(R, C), kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), acc)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1338,39 +1278,29 @@ int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const
 }
 
 template <typename T>
-int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, const double* part, int nparts, float* mean, float* invstd,
+int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, XAcc acc, bool have_stats, float* mean, float* invstd,
                  float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, const float* gamma,
-                 const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda, Ws ws) {
+                 const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda) {
     HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_TRY(check_acc(acc, 2 * C));
     HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act: output row stride must be a multiple of 16 bytes");
-    Ws fw = ws;
-    if (!part) {  // no statistics from the producer: a moments pass into ws first
-        const int nblk = bn_blocks(R, C);
-        HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
-        double* p = reinterpret_cast<double*>(ws.p);
-        HLMC_BN_PROBED(s, (double)sizeof(T) * R * C + 16.0 * nblk * C,
-                       (col_moments_kernel<T><<<nblk, kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), p)));
+    if (!have_stats) {  // no statistics from the producer: a moments pass into the (zeroed) accumulator first
+        HLMC_BN_PROBED(s, (double)sizeof(T) * R * C,
+                       (col_moments_kernel<T><<<bn_blocks(R, C), kThreads, 0, s>>>(y, R, C, bn_rows_per_blk(R, C), acc)));
         HLMC_LAUNCHED();
-        part = p;
-        nparts = nblk;
-        fw = ws_from(ws, bn_fold_off(R, C));
     }
-    Folded f = C <= 512 ? fold_parts_to(s, part, nparts, 2 * C, fw, fin_max_rows(C)) : Folded{nullptr, 0};
-    if (!f.p) {  // wide channels / no fold space: separate finalize
-        const Folded f2 = fold_parts(s, part, nparts, 2 * C, fw);
-        HLMC_BN_PROBED(s, 16.0 * f2.rows * C,
-                       (bn_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f2.p, f2.rows, C, R, mean, invstd, run_mean,
-                                                                        run_var, nbt, momentum, eps)));
+    if (C > kFinMaxC) {  // wide channels: a separate finalize
+        bn_finalize_kernel<<<fin_grid(C), 64, 0, s>>>(acc, C, R, mean, invstd, run_mean, run_var, nbt, momentum, eps);
         HLMC_LAUNCHED();
         return bn_act<T>(s, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, a, lda);
     }
     BnFin fin;
-    fin.part = f.p; fin.rows = f.rows; fin.R = R;
+    fin.acc = acc; fin.R = R;
     fin.mean = mean; fin.invstd = invstd; fin.rmean = run_mean; fin.rvar = run_var; fin.nbt = nbt;
     fin.momentum = momentum; fin.eps = eps;
     const int rpp = kThreads / (C / Vec16<T>::N);
     const unsigned g = grid_for(R, rpp * kU);
-    const double by = 2.0 * sizeof(T) * R * C + 16.0 * f.rows * C;
+    const double by = 2.0 * sizeof(T) * R * C;
     if (mask)
         HLMC_BN_PROBED(s, by, (bn_act_kernel<T, true, true><<<g, kThreads, 0, s>>>(y, R, C, mean, invstd, gamma, beta, act,
                                                                                   mask, mscale, a, lda, fin)));
@@ -1384,76 +1314,50 @@ int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, const double* part
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
-               float* dbeta, float* dbias, Ws ws, const BnBwdFuse* fused, double* bias_part) {
+               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums) {
     HLMC_TRY(check_bn_shape<T>(C));
+    HLMC_TRY(check_acc(mom, 2 * C));
+    if (bias_acc.on()) HLMC_TRY(check_acc(bias_acc, C));
+    HLMC_CHECK_ARG(!dbias || bias_acc.on(), "bn_act_bwd: dbias needs its accumulator");
     HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act_bwd: grad row stride must be a multiple of 16 bytes");
     const int nblk = bn_blocks(R, C);
-    HLMC_CHECK_ARG(ws.bytes >= bn_ws(R, C), "bn workspace");
     const int64_t rpb = bn_rows_per_blk(R, C);
-    double* part = reinterpret_cast<double*>(ws.p);
-    float* sums = reinterpret_cast<float*>(part + (size_t)nblk * 2 * C);
-    const Ws fw = ws_from(ws, bn_fold_off(R, C));
-    Folded fin{nullptr, 0};
-    if (fused && fused->nparts > 0) {  // moments came with the producing GEMM's epilogue
-        HLMC_CHECK_ARG(lda == C && !mask && act == 0, "bn_act_bwd: fused moments need a dense lrelu layer");
-        fin = C <= 512 ? fold_parts_to(s, fused->part, fused->nparts, 2 * C, fw, fin_max_rows(C),
-                                       bias_part == nullptr)
-                       : Folded{nullptr, 0};
-        if (!fin.p) {
-            const Folded f = fold_parts(s, fused->part, fused->nparts, 2 * C, fw);
-            HLMC_BN_PROBED(s, 16.0 * f.rows * C,
-                           (bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums)));
-            HLMC_LAUNCHED();
-        }
+    if (fused && fused->done) {  // moments came with the producer of da
+        HLMC_CHECK_ARG(fused->acc.p == mom.p && lda == C && !mask && act == 0,
+                       "bn_act_bwd: fused moments need a dense lrelu layer and its accumulator");
     } else {
         auto k = mask ? bn_bwd_moments_kernel<T, true> : bn_bwd_moments_kernel<T, false>;
-        HLMC_BN_PROBED(s, 2.0 * sizeof(T) * R * C + 16.0 * nblk * C,
+        HLMC_BN_PROBED(s, 2.0 * sizeof(T) * R * C,
                        (k<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb,
-                                                    part)));
+                                                    mom)));
         HLMC_LAUNCHED();
-        // the apply kernel folds the (<= fin_max_rows(C)-row) table itself: no finalize launch
-        // (without bias_part the apply kernel writes its bias partials over `part`: fold into fw even when short)
-        fin = C <= 512 ? fold_parts_to(s, part, nblk, 2 * C, fw, fin_max_rows(C), bias_part == nullptr)
-                       : Folded{nullptr, 0};
-        if (!fin.p) {
-            const Folded f = fold_parts(s, part, nblk, 2 * C, fw);
-            HLMC_BN_PROBED(s, 16.0 * f.rows * C,
-                           (bn_bwd_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dgamma, dbeta, sums)));
-            HLMC_LAUNCHED();
-        }
     }
-    double* bpart = bias_part ? bias_part : part;
+    const bool fin_here = C <= kFinMaxC;  // the apply kernel finalizes the moments itself: no finalize launch
     BnFin bf;
-    if (fin.p) {
-        bf.part = fin.p; bf.rows = fin.rows; bf.dgamma = dgamma; bf.dbeta = dbeta;
-    }
-    HLMC_CHECK_ARG(!fin.p || fin.p != bpart, "bn_act_bwd: the folded table aliases the bias partials");
-    auto ka = mask ? (fin.p ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
-                   : (fin.p ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
-    HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C + 8.0 * nblk * C,
-                   (ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
-                                                 dy, rpb, bpart, bf)));
-    HLMC_LAUNCHED();
-    if (dbias && !bias_part) {
-        const Folded f = fold_parts(s, part, nblk, C, fw);
-        HLMC_BN_PROBED(s, 8.0 * f.rows * C, (colsum_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, dbias)));
+    if (fin_here) {
+        bf.acc = mom; bf.dgamma = dgamma; bf.dbeta = dbeta;
+    } else {
+        HLMC_CHECK_ARG(sums, "bn_act_bwd: C > 512 needs 2C floats of sums scratch");
+        bn_bwd_finalize_kernel<<<fin_grid(C), 64, 0, s>>>(mom, C, dgamma, dbeta, sums);
         HLMC_LAUNCHED();
     }
+    auto ka = mask ? (fin_here ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
+                   : (fin_here ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
+    HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C,
+                   (ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
+                                                 dy, rpb, bias_acc, bf)));
+    HLMC_LAUNCHED();
+    if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
     return HLMC_OK;
 }
-int bn_bias_parts(int64_t R, int C) { return bn_blocks(R, C); }
-int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out, Ws fold) {
-    HLMC_CHECK_ARG(part && out && nparts > 0 && C > 0, "colsum_finalize: bad arguments");
-    const Folded f = fold_parts(s, part, nparts, C, fold);
-    HLMC_BN_PROBED(s, 8.0 * f.rows * C, (colsum_finalize_kernel<<<fin_grid(C), 1024, 0, s>>>(f.p, f.rows, C, out)));
+int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out) {
+    HLMC_CHECK_ARG(out && C > 0, "colsum_finalize: bad arguments");
+    HLMC_TRY(check_acc(acc, C));
+    HLMC_BN_PROBED(s, 24.0 * acc.shards * C, (xacc_to_f32_kernel<<<fin_grid(C), 64, 0, s>>>(acc, C, out)));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
 
-// partial rows conv_c1_s2 writes with st / bf: its grid, for either dtype (8 threads per pixel for f32, 4 for bf16)
-int conv_c1_fused_rows(int B, int Hi, int Wi) {
-    return grid_for((int64_t)B * (Hi / 2) * (Wi / 2) * 8, kThreads, kC1FusedBlocks);
-}
 
 template <typename T>
 int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y,
@@ -1463,20 +1367,22 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
     HLMC_CHECK_ARG(nthr < (int64_t)1 << 31, "conv_c1_s2: too many pixels");
     const FastDiv dW((uint32_t)(Wi / 2)), dH((uint32_t)(Hi / 2));
     C1Fuse fz;
-    if (st) st->nparts = 0;
-    if (bf) bf->nparts = 0;
-    if (st && st->part) {
-        // fewer, longer-running blocks: one partial row each (the fold reads them)
+    if (st) st->done = false;
+    if (bf) bf->done = false;
+    if (st && st->acc.on()) {
+        // fewer, longer-running blocks: one accumulator contribution each
+        HLMC_TRY(check_acc(st->acc, 2 * Co));
         const int g = grid_for(nthr, kThreads, kC1FusedBlocks);
-        fz.part = st->part;
+        fz.acc = st->acc;
         conv_c1_s2_kernel<T, 32, 1><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
-        st->nparts = g;
-    } else if (bf && bf->part) {
+        st->done = true;
+    } else if (bf && bf->acc.on()) {
+        HLMC_TRY(check_acc(bf->acc, 2 * Co));
         const int g = grid_for(nthr, kThreads, kC1FusedBlocks);
-        fz.part = bf->part;
+        fz.acc = bf->acc;
         fz.ybn = bf->y; fz.mean = bf->mean; fz.invstd = bf->invstd; fz.gamma = bf->gamma; fz.beta = bf->beta;
         conv_c1_s2_kernel<T, 32, 2><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
-        bf->nparts = g;
+        bf->done = true;
     } else {
         conv_c1_s2_kernel<T, 32, 0><<<grid_for(nthr, kThreads, 16384), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH,
                                                                                         fz);
@@ -1627,8 +1533,11 @@ int copy_segments(hipStream_t s, const CopySeg* segs, int nseg) {
 }
 
 template <typename T>
-int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz) {
-    reparam_fwd_kernel<T><<<grid_for((int64_t)n_rows * L), kThreads, 0, s>>>(mu, lv, eps, n_rows, L, z, ldz);
+int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz,
+                float* mu_out, float* lv_out, float* eps_keep) {
+    LatentOut lo;
+    lo.mu = mu_out; lo.lv = lv_out; lo.eps = eps_keep;
+    reparam_fwd_kernel<T><<<grid_for((int64_t)n_rows * L), kThreads, 0, s>>>(mu, lv, eps, n_rows, L, z, ldz, lo);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1641,10 +1550,12 @@ int randn(hipStream_t s, float* out, int64_t n, uint64_t seed, uint64_t offset) 
 }
 template <typename T>
 int reparam_rng(hipStream_t s, const float* mu, const float* lv, uint64_t seed, uint64_t offset, int n_rows, int L,
-                float* eps_out, T* z, int ldz) {
+                float* eps_out, T* z, int ldz, float* mu_out, float* lv_out) {
     HLMC_CHECK_ARG(offset % 4 == 0, "reparam_rng: offset must be a multiple of 4");
+    LatentOut lo;
+    lo.mu = mu_out; lo.lv = lv_out;
     reparam_rng_kernel<T><<<grid_for(((int64_t)n_rows * L + 3) / 4), kThreads, 0, s>>>(mu, lv, seed, offset, n_rows, L,
-                                                                                       eps_out, z, ldz);
+                                                                                       eps_out, z, ldz, lo);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1727,8 +1638,9 @@ int adam_job_tiles(AdamJob& j) {
         j.nt1 = 0;
         return (int)((j.n + 4095) / 4096);
     }
-    j.nt1 = (j.d1 + 31) / 32;
-    return ((j.d0 + 31) / 32) * j.nt1;
+    const int TS = adam_tile_edge(j.taps);
+    j.nt1 = (j.d1 + TS - 1) / TS;
+    return ((j.d0 + TS - 1) / TS) * j.nt1;
 }
 
 void adam_coef_host(const AdamArgs& a, float* out6) {
@@ -1757,15 +1669,16 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
 
 #define INST(T)                                                                                                      \
     template int bn_stats<T>(hipStream_t, const T*, int64_t, int, float*, float*, float*, float*, int64_t*, float,     \
-                             float, Ws);                                                                              \
+                             float, XAcc);                                                                            \
+    template int bn_moments<T>(hipStream_t, const T*, int64_t, int, XAcc);                                             \
     template int bn_act<T>(hipStream_t, const T*, int64_t, int, const float*, const float*, const float*, const float*, \
                            int, const uint8_t*, float, T*, int);                                                      \
-    template int bn_act_train<T>(hipStream_t, const T*, int64_t, int, const double*, int, float*, float*, float*,    \
+    template int bn_act_train<T>(hipStream_t, const T*, int64_t, int, XAcc, bool, float*, float*, float*,            \
                                  float*, int64_t*, float, float, const float*, const float*, int, const uint8_t*, float, \
-                                 T*, int, Ws);                                                                       \
+                                 T*, int);                                                                           \
     template int bn_act_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,          \
-                               const float*, const float*, int, const uint8_t*, float, T*, float*, float*, float*, Ws, \
-                               const BnBwdFuse*, double*);                                                           \
+                               const float*, const float*, int, const uint8_t*, float, T*, float*, float*, XAcc,      \
+                               const BnBwdFuse*, XAcc, float*, float*);                                              \
     template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*,        \
                                ColStats*, BnBwdFuse*);                                                               \
     template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);         \
@@ -1777,8 +1690,10 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
     template int nhwc_to_flat<T>(hipStream_t, const T*, int, int, int, int, T*, int, const T*);                      \
     template int flat_to_nhwc<T>(hipStream_t, const T*, int, int, int, int, int, T*);                                \
     template int colsum<T>(hipStream_t, const T*, int, int, int, float*, Ws);                                        \
-    template int reparam_fwd<T>(hipStream_t, const float*, const float*, const float*, int, int, T*, int);           \
-    template int reparam_rng<T>(hipStream_t, const float*, const float*, uint64_t, uint64_t, int, int, float*, T*, int); \
+    template int reparam_fwd<T>(hipStream_t, const float*, const float*, const float*, int, int, T*, int, float*,     \
+                                float*, float*);                                                                     \
+    template int reparam_rng<T>(hipStream_t, const float*, const float*, uint64_t, uint64_t, int, int, float*, T*, int, \
+                                float*, float*);                                                                     \
     template int reparam_bwd<T>(hipStream_t, const T*, int, const float*, const float*, const float*, const float*,  \
                                 int, int, T*, T*);                                                                  \
     template int pack<T>(hipStream_t, const AdamJob*, int, int);                                                     \

@@ -13,26 +13,44 @@ struct Ws {  // split-K / reduction scratch handed down by the caller
 namespace ops {
 
 // ---------------------------------------------------------------- GEMM-shaped (gemm_ops.hip)
-// Optional fused BatchNorm statistics of a conv output: when the launch is single-pass the epilogue writes
-// nparts rows of [sum(C) | sum of squares(C)] f64 partials to part (else nparts = 0: compute them separately).
+// Optional fused BatchNorm statistics of a conv output: the producer adds [sum(C) | sum of squares(C)] of the
+// values it stores to acc (a zeroed exact accumulator of 2C columns, common.hpp XAcc) and sets done; done = false:
+// the caller computes them separately (into the same accumulator).
 struct ColStats {
-    double* part;
-    int nparts;
+    XAcc acc;
+    bool done;
 };
-size_t col_stats_bytes(int64_t M, int phases, int C);  // bytes of part for M output rows x phases
 // Fused BatchNorm(+LeakyReLU 0.01) backward moments of a data-gradient producer's output da (conv_c1_s2 as the
 // output convT's data gradient): y / mean / invstd / gamma / beta of the BN layer whose output gradient it
-// writes; part receives nparts rows of [sum dz | sum dz*xhat] (nparts = 0: compute them separately).
+// writes; acc (2C columns, zeroed) receives [sum dz | sum dz*xhat] and done is set (else computed separately).
 struct BnBwdFuse {
     const void* y;
     const float *mean, *invstd, *gamma, *beta;
-    double* part;
-    int nparts;
+    XAcc acc;
+    bool done;
 };
 // y[B, Hi/2, Wi/2, Co] = conv3x3_s2_p1(x[B,Hi,Wi,Ci]) + bias ; wp packed [Co][3][3][Ci]
+// Train-mode BatchNorm + LeakyReLU(0.01) of a conv's input applied while an LDS halo-tile kernel stages it: x is
+// then the layer-below pre-BN map y, acc its statistics (2 Ci columns, delivered by its producer); the kernel
+// writes mean / invstd / running statistics like bn_act_train and the activation a_out (Ci channels, x's layout)
+// for the weight gradient that reads it.  Only where *_takes_input_bn says so (bf16 halo shapes, train mode).
+struct BnInput {
+    XAcc acc;
+    int64_t R;
+    float *mean, *invstd, *rmean, *rvar;
+    int64_t* nbt;
+    float momentum, eps;
+    const float *gamma, *beta;
+    void* a_out;
+};
+template <typename T>
+bool conv_s2_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co);
+template <typename T>
+bool subpixel_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co);
+// xin (nullable): BnInput (train-mode BatchNorm of the input applied while staging; needs st)
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-            ColStats* st = nullptr);
+            ColStats* st = nullptr, const BnInput* xin = nullptr);
 template <typename T>
 size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -40,7 +58,7 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 // (also the data gradient of a stride-2 conv with the conv weight re-packed [Ci_conv][3][3][Co_conv])
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-             ColStats* st = nullptr);
+             ColStats* st = nullptr, const BnInput* xin = nullptr);
 template <typename T>
 size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -72,7 +90,6 @@ size_t linear_wgrad_ws(int Mb, int N, int K);
 template <typename T>
 int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y,
                ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
-int conv_c1_fused_rows(int B, int Hi, int Wi);  // partial rows conv_c1_s2 writes with st / bf
 // y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel)
 template <typename T>
 int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y);
@@ -82,40 +99,43 @@ int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const floa
 size_t wgrad_c1_ws(int B, int Hl, int Wl, int M);
 
 // ---------------------------------------------------------------- batch norm / activation (kernels.hip)
-// Train-mode statistics over R rows of an [R][C] map; writes mean / invstd and updates running stats.
+// Statistics travel through exact accumulators (common.hpp XAcc): the caller owns them and zeroes them before the
+// producer runs; bn_acc_bytes(C) per BatchNorm pair table (2C columns), bias_acc_bytes(C) per bias column sum.
+size_t bn_acc_bytes(int C);
+size_t bias_acc_bytes(int C);
+// Train-mode statistics over R rows of an [R][C] map (a moments pass into acc); writes mean / invstd and updates
+// running stats.
 template <typename T>
 int bn_stats(hipStream_t s, const T* y, int64_t R, int C, float* mean, float* invstd, float* run_mean, float* run_var,
-             int64_t* nbt, float momentum, float eps, Ws ws);
-size_t bn_ws(int64_t R, int C);
-// Train-mode statistics from nparts fused partial rows ([nparts][2C] f64, ColStats) over R rows.
-// fold: scratch (>= fold_ws(2C) bytes, not overlapping part) for folding large partial tables; may be empty.
-int bn_stats_from_parts(hipStream_t s, const double* part, int nparts, int64_t R, int C, float* mean, float* invstd,
-                        float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, Ws fold);
-size_t fold_ws(int ncols);  // scratch bytes to fold a [rows][ncols] f64 partial table
+             int64_t* nbt, float momentum, float eps, XAcc acc);
+// Column sums / sums of squares of an [R][C] map into the (zeroed) accumulator acc (2C columns): the statistics a
+// consumer finalizes itself when the producer could not deliver them
+template <typename T>
+int bn_moments(hipStream_t s, const T* y, int64_t R, int C, XAcc acc);
 // Eval-mode statistics from running buffers.
 int bn_eval_stats(hipStream_t s, const float* run_mean, const float* run_var, int C, float eps, float* mean, float* invstd);
 // a = act(gamma*(y-mean)*invstd + beta) [* mask * mscale];  act: 0 lrelu(0.01), 1 relu, 2 none
-// Train-mode BatchNorm + activation with the statistics finalized inside the activation kernel: `part`
-// [nparts][2C] f64 column sums / sums of squares from the producer (nullptr: a moments pass over y into ws
-// first), folded to <= 8 rows; writes mean / invstd and updates the running statistics like bn_stats.
+// Train-mode BatchNorm + activation with the statistics finalized inside the activation kernel (C <= 512): the
+// column totals come from acc (have_stats: delivered by the producer; else a moments pass into acc first);
+// writes mean / invstd and updates the running statistics like bn_stats.
 template <typename T>
-int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, const double* part, int nparts, float* mean, float* invstd,
+int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, XAcc acc, bool have_stats, float* mean, float* invstd,
                  float* run_mean, float* run_var, int64_t* nbt, float momentum, float eps, const float* gamma,
-                 const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda, Ws ws);
+                 const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda);
 template <typename T>
 int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const float* invstd, const float* gamma,
            const float* beta, int act, const uint8_t* mask, float mscale, T* a, int lda);
-// backward through act+BN: dy from da (ld lda); dgamma, dbeta, dbias(sum of dy; nullable).
-// fused (nullable): moments already emitted by the producing GEMM (BnBwdFuse with nparts > 0) -> no moments pass.
-// bias_part (nullable): write the dbias column partials there (bn_bias_parts(R) rows of C) and leave their
-// reduction to the caller (colsum_finalize) instead of reducing into dbias here.
+// backward through act+BN: dy from da (ld lda); dgamma, dbeta.  mom: zeroed accumulator of the moments (2C
+// columns; fused->done: the producer of da already delivered them there).  bias_acc (may be off): the column sums
+// of dy (the conv bias gradient) are added there; dbias (nullable, needs bias_acc): also reduce them into dbias
+// here (else the caller runs colsum_finalize, e.g. on the weight-gradient stream).  sums: 2C floats of scratch,
+// needed for C > 512 only.
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
-               float* dbeta, float* dbias, Ws ws, const BnBwdFuse* fused = nullptr, double* bias_part = nullptr);
-int bn_bias_parts(int64_t R, int C);  // partial rows of bn_act_bwd's bias column sums
-// out[c] = sum_k part[k * C + c], k < nparts (fixed order, f64); fold: scratch >= fold_ws(C) bytes (may be empty)
-int colsum_finalize(hipStream_t s, const double* part, int nparts, int C, float* out, Ws fold);
+               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums);
+// out[c] = total of column c of acc (C columns)
+int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out);
 
 // ---------------------------------------------------------------- misc elementwise (kernels.hip)
 // Up to 4 float copies in one launch (segments with null dst or src are skipped): the small per-step copies
@@ -142,11 +162,15 @@ size_t colsum_ws(int rows, int cols);
 // z = mu + eps * exp(0.5 logvar)  (z written as T with row stride ldz)
 // eps ~ N(0,1), element offset + i of the Philox4x32-10 stream `seed` (offset % 4 == 0) -> out[i]
 int randn(hipStream_t s, float* out, int64_t n, uint64_t seed, uint64_t offset);
-// reparam_fwd with eps drawn on the device (the same stream elements as randn) and stored to eps_out
+// reparam_fwd with eps drawn on the device (the same stream elements as randn) and stored to eps_out; mu_out /
+// lv_out (nullable): copies of mu / lv written by the same launch (the caller's latent outputs)
 template <typename T>
 int reparam_rng(hipStream_t s, const float* mu, const float* lv, uint64_t seed, uint64_t offset, int n_rows, int L,
-                float* eps_out, T* z, int ldz);
-template <typename T> int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz);
+                float* eps_out, T* z, int ldz, float* mu_out = nullptr, float* lv_out = nullptr);
+// mu_out / lv_out / eps_keep (nullable): copies of mu / lv / eps written by the same launch
+template <typename T>
+int reparam_fwd(hipStream_t s, const float* mu, const float* lv, const float* eps, int n_rows, int L, T* z, int ldz,
+                float* mu_out = nullptr, float* lv_out = nullptr, float* eps_keep = nullptr);
 // latent-head gradients in one pass: gmu = d_mu + dz ; glv = d_lv + dz * eps * 0.5 exp(0.5 lv), written as T
 // (the operand of the heads' data / weight gradients); d_mu / d_lv: the caller's loss gradients (nullable: 0)
 template <typename T>

@@ -5,10 +5,10 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-BASE=$R/hybrid-language-music-clustering-vae_amd/libhlmc_base.so
+BASE=${BASE:-$R/hybrid-language-music-clustering-vae_amd/libhlmc_base.so}
 N=${1:-3}
 TESTS=${TESTS:-"tests/test_ops_gpu.py tests/test_models_gpu.py tests/test_bench_parity_gpu.py tests/test_e2e_gpu.py"}
-timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q -rf --timeout 200 --timeout-method thread > gpurun_out/lib_tests.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q -rf --timeout 200 --timeout-method thread > gpurun_out/lib_tests.log 2>&1; rc=$?
 echo "tests rc=$rc"; grep -E "passed|failed|Error" gpurun_out/lib_tests.log | tail -3
 [ $rc -eq 0 ] || exit $rc
 for i in $(seq 1 $N); do

@@ -9,6 +9,11 @@ buffer broadcast, Adam waiting on the comm stream — must leave both ranks with
   * identical parameters, equal to torch.optim.Adam applied to that reduced gradient;
   * identical BatchNorm running statistics equal to rank 0's (DDP broadcast_buffers), i.e. the oracle's
     statistics after rank 0's shard.
+Over STEPS consecutive steps (a fresh batch per rank and step): every step's forward on every rank starts from
+rank 0's post-previous-step statistics (the broadcast overlapping the next forward), so after step k both ranks
+hold the oracle chain's statistics — rank 0's shard run through the chain's parameters from rank 0's step-(k-1)
+statistics — and the step-k reduced gradient equals the oracle's shard sum at the chain parameters (which are
+torch Adam applied to the reduced gradients of steps 0..k-1).
 RCCL itself is covered by the 1-rank NCCL test in test_trainer_gpu.py."""
 import os
 import tempfile
@@ -21,10 +26,11 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 WORLD = 2
 B = 4
+STEPS = 3
 
 
-def _batch(rank):
-    g = torch.Generator().manual_seed(100 + rank)
+def _batch(rank, step=0):
+    g = torch.Generator().manual_seed(100 + rank + 10 * step)
     return torch.randn(B, 1, 128, 128, generator=g), torch.randn(B, 128, generator=g)
 
 
@@ -40,34 +46,40 @@ def _worker(rank, port, outdir, grad_dtype):
     m = hlmc_amd.HybridVAE(128, 768, (128, 128), audio_only=True).cuda()
     tr = hlmc_amd.Trainer(m, lr=1e-4, distributed=True, grad_dtype=grad_dtype)
     assert tr._comm is not None and len(tr.buckets) == 4 and tr.broadcast_buffers
-    audio, eps = _batch(rank)
-    tr.step(audio.cuda(), None, eps=eps.cuda())
-    torch.cuda.synchronize()
-    torch.save({"grad": tr.gflat.detach().cpu().clone(),
-                "params": {n: p.detach().cpu() for n, p in m.named_parameters()},
-                "buffers": {n: b.detach().cpu().clone() for n, b in m.named_buffers()}},
-               os.path.join(outdir, f"rank{rank}.pt"))
+    steps = []
+    for k in range(STEPS):
+        audio, eps = _batch(rank, k)
+        tr.step(audio.cuda(), None, eps=eps.cuda())
+        torch.cuda.synchronize()
+        steps.append({"grad": tr.gflat.detach().cpu().clone(),
+                      "params": {n: p.detach().cpu().clone() for n, p in m.named_parameters()},
+                      "buffers": {n: b.detach().cpu().clone() for n, b in m.named_buffers()}})
+    torch.save(steps, os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _oracle_shards():
-    """Per-shard gradients of the oracle model, their sum, and rank 0's BN statistics after its forward."""
+def _oracle_shards(params, buffers, step):
+    """Per-shard gradients of the oracle model at the given parameters / BN buffers (every rank's forward starts from
+    the same broadcast statistics), their sum, and rank 0's BN statistics after its forward."""
     from oracle import models_oracle as OM
     total, buf0 = None, None
     for rank in range(WORLD):
         torch.manual_seed(42)
         ora = OM.HybridVAE(128, 768, (128, 128), audio_only=True)
-        audio, eps = _batch(rank)
+        with torch.no_grad():
+            for n, p in ora.named_parameters():
+                p.copy_(params[n])
+            for n, b in ora.named_buffers():
+                b.copy_(buffers[n])
+        audio, eps = _batch(rank, step)
         out = ora(audio, None, eps=eps)
         OM.loss_function(out[0], audio, None, None, out[2], out[3])[0].backward()
         g = torch.cat([p.grad.reshape(-1) for p in ora.parameters()])
         total = g if total is None else total + g
         if rank == 0:
             buf0 = {n: b.clone() for n, b in ora.named_buffers()}
-            names = [n for n, _ in ora.named_parameters()]
-            shapes = [p.shape for p in ora.parameters()]
-    return total, buf0, names, shapes
+    return total, buf0
 
 
 def _bn_fed_bias(name):
@@ -85,42 +97,49 @@ def test_dp_two_ranks_match_oracle(cuda, grad_dtype):
         port = 29700 + (os.getpid() % 500) + (0 if grad_dtype == torch.float32 else 500)
         mp.spawn(_worker, args=(port, outdir, grad_dtype), nprocs=WORLD, join=True)
         res = [torch.load(os.path.join(outdir, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
-    # ranks agree bit for bit
-    assert torch.equal(res[0]["grad"], res[1]["grad"])
-    for n in res[0]["params"]:
-        assert torch.equal(res[0]["params"][n], res[1]["params"][n]), f"ranks diverged at {n}"
-    for n in res[0]["buffers"]:
-        assert torch.equal(res[0]["buffers"][n], res[1]["buffers"][n]), f"BN buffer {n} differs across ranks"
-    # reduced gradient = oracle per-shard SUM
-    ref, buf0, names, shapes = _oracle_shards()
-    got = res[0]["grad"]
-    offs, o = [], 0
-    for s in shapes:
-        offs.append((o, o + s.numel()))
-        o += s.numel()
-    keep = torch.ones_like(ref, dtype=torch.bool)
-    for name, (a, b) in zip(names, offs):
-        if _bn_fed_bias(name):
-            keep[a:b] = False
-            wa, wb = offs[names.index(name[:-4] + "weight")]
-            assert float((got[a:b] - ref[a:b]).abs().max()) <= 1e-3 * float(ref[wa:wb].abs().max()) + 1e-5, name
-    tol = 1e-3 if grad_dtype == torch.float32 else 2e-2
-    err = float((got[keep] - ref[keep]).norm() / ref[keep].norm())
-    print(f"DP gradient vs oracle shard sum ({grad_dtype}): rel L2 {err:.2e}")
-    assert err <= tol
-    # parameters = torch Adam on the reduced gradient
-    torch.manual_seed(42)
     from oracle import models_oracle as OM
-    init = OM.HybridVAE(128, 768, (128, 128), audio_only=True)
-    ps = [p.detach().clone().requires_grad_(True) for p in init.parameters()]
-    for p, (a, b) in zip(ps, offs):
-        p.grad = got[a:b].view_as(p).clone()
-    torch.optim.Adam(ps, lr=1e-4).step()
-    for name, p in zip(names, ps):
-        torch.testing.assert_close(res[0]["params"][name], p.detach(), rtol=1e-6, atol=1e-7, msg=name)
-    # running statistics = rank 0's (DDP broadcast_buffers)
-    for n, b in buf0.items():
-        if b.dtype.is_floating_point:
-            assert float((res[1]["buffers"][n] - b).norm() / max(float(b.norm()), 1e-30)) < 1e-4, n
-        else:
-            assert torch.equal(res[1]["buffers"][n], b), n
+    torch.manual_seed(42)
+    chain = OM.HybridVAE(128, 768, (128, 128), audio_only=True)
+    names = [n for n, _ in chain.named_parameters()]
+    shapes = [p.shape for p in chain.parameters()]
+    offs, o = [], 0
+    for sh in shapes:
+        offs.append((o, o + sh.numel()))
+        o += sh.numel()
+    ps = [p.detach().clone().requires_grad_(True) for p in chain.parameters()]
+    opt = torch.optim.Adam(ps, lr=1e-4)
+    bufs = {n: b.detach().clone() for n, b in chain.named_buffers()}
+    tol = 1e-3 if grad_dtype == torch.float32 else 2e-2
+    for k in range(STEPS):
+        r0, r1 = res[0][k], res[1][k]
+        # ranks agree bit for bit
+        assert torch.equal(r0["grad"], r1["grad"]), k
+        for n in r0["params"]:
+            assert torch.equal(r0["params"][n], r1["params"][n]), f"step {k}: ranks diverged at {n}"
+        for n in r0["buffers"]:
+            assert torch.equal(r0["buffers"][n], r1["buffers"][n]), f"step {k}: BN buffer {n} differs across ranks"
+        # reduced gradient = oracle per-shard SUM at the chain's parameters and broadcast statistics
+        ref, buf0 = _oracle_shards({n: p.detach() for n, p in zip(names, ps)}, bufs, k)
+        got = r0["grad"]
+        keep = torch.ones_like(ref, dtype=torch.bool)
+        for name, (a, b) in zip(names, offs):
+            if _bn_fed_bias(name):
+                keep[a:b] = False
+                wa, wb = offs[names.index(name[:-4] + "weight")]
+                assert float((got[a:b] - ref[a:b]).abs().max()) <= 1e-3 * float(ref[wa:wb].abs().max()) + 1e-5, name
+        err = float((got[keep] - ref[keep]).norm() / ref[keep].norm())
+        print(f"step {k}: DP gradient vs oracle shard sum ({grad_dtype}): rel L2 {err:.2e}")
+        assert err <= tol, k
+        # parameters = torch Adam on the reduced gradient (the chain continues from them)
+        for p, (a, b) in zip(ps, offs):
+            p.grad = got[a:b].view_as(p).clone()
+        opt.step()
+        for name, p in zip(names, ps):
+            torch.testing.assert_close(r0["params"][name], p.detach(), rtol=1e-6, atol=1e-7, msg=f"step {k}: {name}")
+        # running statistics = rank 0's after its forward from the broadcast statistics (DDP broadcast_buffers)
+        for n, b in buf0.items():
+            if b.dtype.is_floating_point:
+                assert float((r1["buffers"][n] - b).norm() / max(float(b.norm()), 1e-30)) < 1e-4, (k, n)
+            else:
+                assert torch.equal(r1["buffers"][n], b), (k, n)
+        bufs = buf0

@@ -354,6 +354,14 @@ def test_bf16_mode_tracks_fp32(cuda):
     gm = torch.cat([p.grad.reshape(-1).cpu() for p in ours.parameters()])
     go = torch.cat([p.grad.reshape(-1) for p in ora.parameters()])
     assert rel(gm, go) < 0.15
+    # every BatchNorm layer's running statistics (the statistics path of each layer: producer epilogue, split-K
+    # moments pass, consumer-side finalize or the next halo kernel's input staging) track the oracle's
+    bo = dict(ora.named_buffers())
+    for n, b in ours.named_buffers():
+        if b.dtype.is_floating_point:
+            assert rel(b.detach(), bo[n]) < 5e-2, n
+        else:
+            assert torch.equal(b.detach().cpu(), bo[n]), n
 
 
 @pytest.mark.parametrize("train", [True, False], ids=["train", "eval"])

@@ -190,11 +190,13 @@ def test_linear_wgrad(cuda, ws, dt, Mb, N, K):
             assert bool(db.isnan().all())
 
 
+# the bench's 128 x 128 clip and a 128 x 1024 mel row band besides the small case
+@pytest.mark.parametrize("shape", [(3, 16, 32), (2, 128, 128), (2, 32, 64), (1, 16, 1024)])
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
-def test_edge_convs(cuda, ws, dt):
+def test_edge_convs(cuda, ws, dt, shape):
     code, tdt, tol = DT[dt]
     g = torch.Generator().manual_seed(9)
-    B, H, W = 3, 16, 32
+    B, H, W = shape
     img = torch.randn(B, H, W, generator=g)
     w1 = torch.randn(32, 1, 3, 3, generator=g) / 3
     b1 = torch.randn(32, generator=g)

@@ -54,23 +54,21 @@ def synthetic_pcm(batch, n, seed, device):
 
 
 class MelStage:
-    """PCM -> mel dB [B,128,128] -> z-score -> audio tensor [B,1,128,128] (f32) for the VAE."""
+    """PCM -> mel dB [B,128,128] -> z-score -> audio tensor [B,1,128,128] (f32) for the VAE: the STFT/mel kernel,
+    then one dB pass with the fitted StandardScaler's transform fused in (hlmc_mel_db_zscore)."""
 
     def __init__(self, batch, device, scaler):
         self.plan = hlmc_amd.features._plan(SR, NFFT, HOP, NMEL)
         self.B = batch
-        self.mel = torch.empty(batch, NMEL, FRAMES, device=device)
         self.audio = torch.empty(batch, 1, NMEL, FRAMES, device=device)
         self.ws = torch.empty(int(L.lib().hlmc_mel_workspace(self.plan, batch, N_SAMPLES)), dtype=torch.uint8,
                               device=device)
         self.scaler = scaler
 
     def __call__(self, pcm):
-        L.check(L.lib().hlmc_mel_db(self.plan, L.stream(), pcm.data_ptr(), self.B, N_SAMPLES, FRAMES, 1e-10, 80.0,
-                                    self.mel.data_ptr(), self.ws.data_ptr()))
-        L.check(L.lib().hlmc_zscore_apply(L.stream(), self.mel.data_ptr(), self.B, NMEL * FRAMES,
-                                          self.scaler.mean_d.data_ptr(), self.scaler.scale_d.data_ptr(), L.HLMC_F32,
-                                          self.audio.data_ptr()))
+        L.check(L.lib().hlmc_mel_db_zscore(self.plan, L.stream(), pcm.data_ptr(), self.B, N_SAMPLES, FRAMES, 1e-10,
+                                           80.0, self.scaler.mean_d.data_ptr(), self.scaler.scale_d.data_ptr(),
+                                           L.HLMC_F32, self.audio.data_ptr(), self.ws.data_ptr()))
         return self.audio
 
 

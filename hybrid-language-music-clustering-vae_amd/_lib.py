@@ -31,6 +31,8 @@ _SIGS = {
     "hlmc_mel_workspace": (c_i64, [c_vp, c_i64, c_i64]),
     "hlmc_melspectrogram": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "hlmc_mel_db": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_f32, c_vp, c_vp]),
+    "hlmc_mel_db_zscore": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_f32, c_f32, c_vp, c_vp, c_int, c_vp,
+                                   c_vp]),
     "hlmc_power_to_db": (c_int, [c_vp, c_vp, c_i64, c_i64, c_int, c_f32, c_f32, c_f32, c_vp, c_vp]),
     "hlmc_mfcc": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_vp]),
     "hlmc_spectral_shape": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i64, c_f64, c_vp]),

@@ -119,6 +119,12 @@ int hlmc_mel_db(const hlmc_mel_plan* p, void* stream, const float* pcm, int64_t 
     HLMC_CHECK_ARG(p && t_keep > 0, "bad arguments");
     return feat::mel_db(p->impl, S(stream), pcm, B, n, t_keep, amin, top_db, out, ws);
 }
+int hlmc_mel_db_zscore(const hlmc_mel_plan* p, void* stream, const float* pcm, int64_t B, int64_t n, int64_t t_keep,
+                       float amin, float top_db, const double* mean, const double* scale, int out_dtype, void* out,
+                       void* ws) {
+    HLMC_CHECK_ARG(p, "plan is NULL");
+    return feat::mel_db_zscore(p->impl, S(stream), pcm, B, n, t_keep, amin, top_db, mean, scale, out_dtype, out, ws);
+}
 int hlmc_power_to_db(void* stream, const float* S_, int64_t B, int64_t per, int ref_max, float ref_value, float amin,
                      float top_db, float* out, void* ws) {
     return feat::power_to_db(S(stream), S_, B, per, ref_max, ref_value, amin, top_db, out, ws);

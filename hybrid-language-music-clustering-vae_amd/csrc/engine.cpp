@@ -134,8 +134,7 @@ class NetT : public NetBase {
     char* ws = nullptr;
     Ws scratch{nullptr, 0};
     Ws scratch2{nullptr, 0};  // split-K / reduction scratch of the weight-gradient stream
-    Ws scratch3{nullptr, 0};  // ... and of the third stream (side3)
-    size_t scratch_off = 0, scratch2_off = 0, scratch3_off = 0, scratch_bytes = 0;
+    size_t scratch_off = 0, scratch2_off = 0, scratch_bytes = 0;
     int64_t planned_B = -1;
     size_t ws_total = 0;
 
@@ -169,7 +168,6 @@ class NetT : public NetBase {
             plan(A, B);
             scratch_off = A.take(scratch_bytes + 256);
             scratch2_off = A.take(scratch_bytes + 256);
-            scratch3_off = A.take(scratch_bytes + 256);
             xf_base = A.take(xf_total);  // xb directly after xf (one memset covers both: 256-aligned sizes)
             xb_base = A.take(xb_total);
             ws_total = A.used;
@@ -181,7 +179,6 @@ class NetT : public NetBase {
         ws = reinterpret_cast<char*>(w);
         scratch = Ws{reinterpret_cast<float*>(ws + scratch_off), scratch_bytes + 256};
         scratch2 = Ws{reinterpret_cast<float*>(ws + scratch2_off), scratch_bytes + 256};
-        scratch3 = Ws{reinterpret_cast<float*>(ws + scratch3_off), scratch_bytes + 256};
     }
 
     // ---------------------------------------------------------------- weight-gradient stream
@@ -191,10 +188,6 @@ class NetT : public NetBase {
     // a forked op reads is written once per backward; backward() joins the stream before returning.
     // HLMC_SIDE_STREAM=0 keeps everything on the caller's stream (A/B measurement aid).
     hipStream_t s2 = nullptr;
-    // A third stream for the last, largest weight gradients of backward (the encoder's 32 x 32 / 16 x 16 layers):
-    // on the second stream they queue behind each other at the tail, where that stream is the critical path
-    hipStream_t s3 = nullptr;
-    bool s3_used = false;
     std::vector<hipEvent_t> evs;
     int ev_next = 0;
     bool use_side = true;
@@ -202,7 +195,6 @@ class NetT : public NetBase {
     bool join_pending = false;         // backward left the side stream running (NetBase::overlap_adam)
     ~NetT() override {
         if (s2) (void)hipStreamDestroy(s2);
-        if (s3) (void)hipStreamDestroy(s3);
         for (auto e : evs) (void)hipEventDestroy(e);
         for (auto e : this->bucket_ev) (void)hipEventDestroy(e);
         if (prelate_ev) (void)hipEventDestroy(prelate_ev);
@@ -238,7 +230,6 @@ class NetT : public NetBase {
         use_side = !env_off;
         if (use_side && !s2) {
             HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-            HLMC_HIP(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
             evs.resize(32);
             for (auto& e : evs) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             HLMC_HIP(hipEventCreateWithFlags(&prelate_ev, hipEventDisableTiming));
@@ -268,12 +259,6 @@ class NetT : public NetBase {
         hipEvent_t e = next_ev();
         HLMC_HIP(hipEventRecord(e, s2));
         HLMC_HIP(hipStreamWaitEvent(s, e, 0));
-        if (s3_used) {
-            hipEvent_t e3 = next_ev();
-            HLMC_HIP(hipEventRecord(e3, s3));
-            HLMC_HIP(hipStreamWaitEvent(s, e3, 0));
-            s3_used = false;
-        }
         return HLMC_OK;
     }
     // Weight-gradient work queued for the second stream.  A fork (event record on s, wait on s2) costs the main
@@ -472,27 +457,6 @@ class NetT : public NetBase {
             return f(q, sc);
         }, side_batch());
     }
-    // f on the third stream now (after everything issued so far on s), with the pending bias reduction
-    int side3_bias(hipStream_t s, SideFn f) {
-        if (!use_side || !s3) return side_bias(s, std::move(f));
-        const PendingBias pb = pend_bias;
-        pend_bias = PendingBias{};
-        hipEvent_t e = next_ev();
-        HLMC_HIP(hipEventRecord(e, s));
-        HLMC_HIP(hipStreamWaitEvent(s3, e, 0));
-        if (pb.gb) HLMC_TRY(ops::colsum_finalize(s3, pb.acc, pb.C, pb.gb));
-        HLMC_TRY(f(s3, scratch3));
-        s3_used = true;
-        return HLMC_OK;
-    }
-    // encoder layers whose weight gradient goes to the third stream (bit l; HLMC_SIDE3_MASK, default none)
-    static int side3_mask() {
-        static const int m = [] {
-            const char* e = std::getenv("HLMC_SIDE3_MASK");
-            return e ? std::atoi(e) : 0;
-        }();
-        return m;
-    }
     // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
     static bool tail_on_main() {
         static const bool on = [] {
@@ -610,9 +574,7 @@ class NetT : public NetBase {
                 HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
             } else {
                 const T* xin = AT(enc.a[l - 1]);
-                SideFn wg = [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); };
-                if (side3_mask() >> l & 1) HLMC_TRY(side3_bias(s, std::move(wg)));
-                else HLMC_TRY(side_bias(s, std::move(wg)));
+                HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
                 if (l == 1) HLMC_TRY(flush_side(s));  // nothing queued may wait for the join behind the main tail
                 // grad of layer l-1's activation
                 HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));

@@ -543,6 +543,57 @@ __global__ void power_to_db_kernel(const float* __restrict__ S, int B, int rows,
     }
 }
 
+// extract_mel_spectrogram's dB pass (ref = clip max, top_db floor, crop / pad with the clip minimum) with, when ZS,
+// StandardScaler.transform fused in (column = position within the clip; the same float32 / float64 steps as
+// power_to_db_kernel followed by zscore_kernel, so the output is bit-identical to that pair).  Four consecutive
+// frames per thread (t_keep % 4 == 0): one 16-byte (f32) / 8-byte (bf16) store.
+template <bool ZS, typename OutT>
+__global__ __launch_bounds__(256) void mel_db_kernel(const float* __restrict__ S, int B, int rows, int T, int t_keep,
+                                                     const unsigned* __restrict__ clip_max,
+                                                     const unsigned* __restrict__ clip_min, float amin, float top_db,
+                                                     const double* __restrict__ mean, const double* __restrict__ scale,
+                                                     OutT* __restrict__ out) {
+    const int q4 = t_keep >> 2;
+    const int64_t n4 = (int64_t)B * rows * q4;
+    for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i4 < n4; i4 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t br = i4 / q4;
+        const int t0 = (int)(i4 - br * q4) * 4;
+        const int b = (int)(br / rows);
+        const float smax = __uint_as_float(clip_max[b]);
+        const float ref_db = db_of(smax, amin);
+        const float floor_db = db_of(smax, amin) - ref_db - top_db;
+        const float pad = db_of(__uint_as_float(clip_min[b]), amin) - ref_db;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = t0 + j;
+            v[j] = t < T ? db_of(S[br * T + t], amin) - ref_db : pad;
+            if (top_db >= 0.f) v[j] = fmaxf(v[j], floor_db);
+        }
+        if constexpr (ZS) {
+            const int64_t c = (br - (int64_t)b * rows) * t_keep + t0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float a = (float)((double)v[j] - mean[c + j]);
+                v[j] = (float)((double)a / scale[c + j]);
+            }
+        }
+        OutT* o = out + br * t_keep + t0;
+        if constexpr (sizeof(OutT) == 4) {
+            *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+            unsigned w[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                bf16 lo = __float2bfloat16(v[2 * j]), hi = __float2bfloat16(v[2 * j + 1]);
+                w[j] = (unsigned)(*reinterpret_cast<unsigned short*>(&lo)) |
+                       ((unsigned)(*reinterpret_cast<unsigned short*>(&hi)) << 16);
+            }
+            *reinterpret_cast<uint2*>(o) = make_uint2(w[0], w[1]);
+        }
+    }
+}
+
 // MFCC: dB (ref 1.0, top_db) then DCT-II ortho over the mel axis: out[b][k][t] = sum_m D[k][m] db[b][m][t]
 __global__ __launch_bounds__(256) void mfcc_kernel(const float* __restrict__ S, int n_mels, int T,
                                                    const unsigned* __restrict__ clip_max, const float* __restrict__ D,
@@ -917,7 +968,36 @@ int mel_db(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int
     unsigned* cmin = reinterpret_cast<unsigned*>(w + sb + ((B * 4 + 255) & ~int64_t(255)));
     HLMC_TRY(mel_power(p, s, pcm, B, n, S, cmax, cmin));
     const int64_t tot = B * p->n_mels * t_keep;
-    power_to_db_kernel<<<gridn(tot), 256, 0, s>>>(S, (int)B, p->n_mels, T, (int)t_keep, cmax, cmin, 1, 1.f, amin, top_db, out);
+    if (t_keep % 4 == 0 && ((uintptr_t)out & 15) == 0)
+        mel_db_kernel<false, float><<<gridn(tot / 4), 256, 0, s>>>(S, (int)B, p->n_mels, T, (int)t_keep, cmax, cmin,
+                                                                   amin, top_db, nullptr, nullptr, out);
+    else
+        power_to_db_kernel<<<gridn(tot), 256, 0, s>>>(S, (int)B, p->n_mels, T, (int)t_keep, cmax, cmin, 1, 1.f, amin,
+                                                       top_db, out);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+int mel_db_zscore(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, int64_t t_keep,
+                  float amin, float top_db, const double* mean, const double* scale, int dtype, void* out, void* ws) {
+    HLMC_CHECK_ARG(ws && mean && scale && out, "bad mel_db_zscore arguments");
+    HLMC_CHECK_ARG(t_keep > 0 && t_keep % 4 == 0, "t_keep must be a positive multiple of 4");
+    HLMC_CHECK_ARG(dtype == HLMC_F32 || dtype == HLMC_BF16, "out dtype f32 or bf16");
+    HLMC_CHECK_ARG(((uintptr_t)out & (dtype == HLMC_F32 ? 15 : 7)) == 0, "out must be 16-byte (f32) / 8-byte (bf16) aligned");
+    const int T = (int)frames(p, n);
+    char* w = reinterpret_cast<char*>(ws);
+    float* S = reinterpret_cast<float*>(w);
+    const int64_t sb = (B * p->n_mels * T * 4 + 255) & ~int64_t(255);
+    unsigned* cmax = reinterpret_cast<unsigned*>(w + sb);
+    unsigned* cmin = reinterpret_cast<unsigned*>(w + sb + ((B * 4 + 255) & ~int64_t(255)));
+    HLMC_TRY(mel_power(p, s, pcm, B, n, S, cmax, cmin));
+    const unsigned g = gridn(B * p->n_mels * t_keep / 4);
+    if (dtype == HLMC_BF16)
+        mel_db_kernel<true, bf16><<<g, 256, 0, s>>>(S, (int)B, p->n_mels, T, (int)t_keep, cmax, cmin, amin, top_db,
+                                                    mean, scale, reinterpret_cast<bf16*>(out));
+    else
+        mel_db_kernel<true, float><<<g, 256, 0, s>>>(S, (int)B, p->n_mels, T, (int)t_keep, cmax, cmin, amin, top_db,
+                                                     mean, scale, reinterpret_cast<float*>(out));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

@@ -34,6 +34,8 @@ int64_t workspace(const MelPlanImpl* p, int64_t B, int64_t n);
 int melspectrogram(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, float* out, void* ws);
 int mel_db(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, int64_t t_keep, float amin,
            float top_db, float* out, void* ws);
+int mel_db_zscore(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, int64_t t_keep,
+                  float amin, float top_db, const double* mean, const double* scale, int dtype, void* out, void* ws);
 int mfcc(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, int n_mfcc, const float* dct,
          float amin, float top_db, float* out, void* ws);
 int power_to_db(hipStream_t s, const float* S, int64_t B, int64_t per, int ref_max, float ref_value, float amin,

@@ -916,79 +916,74 @@ __global__ void splitk_reduce_kernel(const float* ws, EP ep, int M, int N, int S
     }
 }
 
-// The same reduction for a launch whose output feeds a train-mode BatchNorm: each block owns a contiguous range of
-// output rows (phase-major, all N columns) and also delivers the column sums / sums of squares of the values it
-// stored to `acc` (2N columns, common.hpp XAcc) -- no separate moments pass over the output.  Thread (column
-// c = tid % N, row group g = tid / N) for N <= 256 (N divides 256), else columns tid, tid + 256, ...
-template <class EP>
+// The same reduction for a launch whose output feeds a train-mode BatchNorm: block = a tile of 4 * RU output rows
+// (phase-major) x 64 columns; it also delivers the column sums / sums of squares of the values it stored to `acc`
+// (2N columns, common.hpp XAcc) -- no separate moments pass over the output.  Thread (column tid % 64, row group
+// tid / 64) owns rows g, g + 4, ...; every row is loaded before the adds (two slabs at a time, k ascending: the sums
+// equal splitk_reduce_kernel's).  Tall tiles keep the accumulator adds per output element low (6 per column per
+// tile: measured, 16-row tiles were atomic-bound at 3x the plain reduce's time).  Needs N % 64 == 0 and
+// phases * S * M * N < 2^31 (32-bit offsets).
+template <class EP, int RU>
 __global__ __launch_bounds__(256) void splitk_reduce_stats_kernel(const float* ws, EP ep, int M, int N, int S,
-                                                                  int phases, int rows_per_blk, XAcc acc) {
+                                                                  int phases, XAcc acc) {
     __shared__ double red[2][256];
-    const int tid = threadIdx.x;
-    const int64_t rows = (int64_t)phases * M, st = (int64_t)M * N;
-    const int64_t r0 = (int64_t)blockIdx.x * rows_per_blk, r1 = min(rows, r0 + rows_per_blk);
-    const int G = N <= 256 ? 256 / N : 1;
-    const int cstep = N <= 256 ? N : 256;
-    for (int c0 = N <= 256 ? tid % N : tid; c0 < N; c0 += cstep) {
-        double a = 0.0, q = 0.0;
-        const int g = N <= 256 ? tid / N : 0;
-        constexpr int U = 4;  // rows in flight per thread (each summed over the S slabs in k order, as above)
-        for (int64_t rb = r0 + g; rb < r1; rb += U * G) {
-            const float* p[U];
-            float s[U];
+    const int tid = threadIdx.x, c = tid & 63, g = tid >> 6;
+    const int ntc = N >> 6;
+    const int tr = (int)(blockIdx.x / (unsigned)ntc);
+    const int col = ((int)blockIdx.x - tr * ntc) * 64 + c;
+    const int rows = phases * M;
+    const unsigned st = (unsigned)M * (unsigned)N;
+    const int r0 = tr * 4 * RU + g;
+    unsigned off[RU];
+    float s[RU];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t r = min(rb + u * G, r1 - 1);  // clamped: in bounds, skipped below
-                const int ph = (int)(r / M), m = (int)(r - (int64_t)ph * M);
-                p[u] = ws + ((int64_t)ph * S * M + m) * N + c0;
-                s[u] = 0.f;
-            }
-            int k = 0;
-            for (; k + 2 <= S; k += 2) {
-                float x0[U], x1[U];
+    for (int u = 0; u < RU; ++u) {
+        const int r = min(r0 + 4 * u, rows - 1);  // clamped: in bounds, skipped below
+        const int ph = r / M, m = r - ph * M;
+        off[u] = ((unsigned)(ph * S) * (unsigned)M + (unsigned)m) * (unsigned)N + (unsigned)col;
+        s[u] = 0.f;
+    }
+    int k = 0;
+    for (; k + 2 <= S; k += 2) {
+        float x0[RU], x1[RU];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    x0[u] = p[u][k * st];
-                    x1[u] = p[u][(k + 1) * st];
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    s[u] += x0[u];
-                    s[u] += x1[u];
-                }
-            }
-            if (k < S)
-#pragma unroll
-                for (int u = 0; u < U; ++u) s[u] += p[u][k * st];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t r = rb + u * G;
-                if (r >= r1) break;
-                const int ph = (int)(r / M), m = (int)(r - (int64_t)ph * M);
-                EP e = ep;
-                e.set_phase(ph);
-                e.store(e.row(m), c0, s[u]);
-                const float v = e.stored(c0, s[u]);
-                a += v;
-                q += (double)v * v;
-            }
+        for (int u = 0; u < RU; ++u) {
+            x0[u] = ws[off[u] + (unsigned)k * st];
+            x1[u] = ws[off[u] + (unsigned)(k + 1) * st];
         }
-        if (G > 1) {
-            red[0][tid] = a;
-            red[1][tid] = q;
-            __syncthreads();
-            if (tid < N) {
-                for (int k = 1; k < G; ++k) {
-                    a += red[0][k * N + tid];
-                    q += red[1][k * N + tid];
-                }
-                xacc_add(acc, c0, a);
-                xacc_add(acc, N + c0, q);
-            }
-        } else {
-            xacc_add(acc, c0, a);
-            xacc_add(acc, N + c0, q);
+#pragma unroll
+        for (int u = 0; u < RU; ++u) {
+            s[u] += x0[u];
+            s[u] += x1[u];
         }
+    }
+    if (k < S)
+#pragma unroll
+        for (int u = 0; u < RU; ++u) s[u] += ws[off[u] + (unsigned)k * st];
+    double a = 0.0, q = 0.0;
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+        const int r = r0 + 4 * u;
+        if (r >= rows) break;
+        const int ph = r / M, m = r - ph * M;
+        EP e = ep;
+        e.set_phase(ph);
+        e.store(e.row(m), col, s[u]);
+        const float v = e.stored(col, s[u]);
+        a += v;
+        q += (double)v * v;
+    }
+    red[0][tid] = a;
+    red[1][tid] = q;
+    __syncthreads();
+    if (tid < 64) {
+#pragma unroll
+        for (int j = 1; j < 4; ++j) {
+            a += red[0][j * 64 + tid];
+            q += red[1][j * 64 + tid];
+        }
+        xacc_add(acc, col, a);
+        xacc_add(acc, N + col, q);
     }
 }
 

@@ -176,15 +176,20 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
     nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe);
     HLMC_LAUNCHED();
-    static const bool red_stats = [] {  // HLMC_SPLITK_STATS=1: the reduction also delivers the statistics (A/B aid)
+    static const bool red_stats = [] {  // HLMC_SPLITK_STATS=0: statistics from a separate moments pass (A/B aid)
         const char* e = std::getenv("HLMC_SPLITK_STATS");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
-    if (red_stats && stats && (N > 256 ? N % 256 == 0 : 256 % N == 0)) {
-        const int64_t rows = (int64_t)phases * M;
-        const int G = N <= 256 ? 256 / N : 1;
-        const int64_t rpb = (std::max<int64_t>(1, (rows + 255) / 256) + G - 1) / G * G;  // <= 256 blocks
-        splitk_reduce_stats_kernel<EP><<<cdiv(rows, rpb), 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases, (int)rpb, st->acc);
+    if (red_stats && stats && N % 64 == 0 && (double)phases * pl.S * M * N < 2147483648.0) {  // the reduce delivers them
+        const int rows = phases * M, ntc = N / 64;
+        // the tallest tile (fewest accumulator adds) that still gives >= 1024 blocks (A/B: 128 / 256 / 512 / 1024)
+        const int RU = cdiv(rows, 128) * ntc >= 1024 ? 32 : cdiv(rows, 64) * ntc >= 1024 ? 16 : 8;
+        const unsigned nb = (unsigned)(cdiv(rows, 4 * RU) * ntc);
+        switch (RU) {
+            case 32: splitk_reduce_stats_kernel<EP, 32><<<nb, 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases, st->acc); break;
+            case 16: splitk_reduce_stats_kernel<EP, 16><<<nb, 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases, st->acc); break;
+            default: splitk_reduce_stats_kernel<EP, 8><<<nb, 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases, st->acc); break;
+        }
         HLMC_LAUNCHED();
         st->done = true;
         return HLMC_OK;

@@ -94,18 +94,29 @@ def power_to_db(S, ref=1.0, amin=1e-10, top_db=80.0):
 
 
 def extract_mel_spectrogram(audio, sr=22050, n_mels=128, n_fft=2048, hop_length=512, fixed_time_steps=None,
-                            amin=1e-10, top_db=80.0):
+                            amin=1e-10, top_db=80.0, scaler=None, out_dtype=torch.float32):
     """src/1_preprocessing_advanced.py:97-114 (fixed_time_steps=1024) / src/1_preprocessing.py:48-58 (None).
 
     dB reference = maximum over ALL frames of the clip, then crop (or pad with the clip minimum) to
-    fixed_time_steps frames.  Batched: audio [B, n] -> [B, n_mels, T']."""
+    fixed_time_steps frames.  Batched: audio [B, n] -> [B, n_mels, T'].
+    scaler: a fitted StandardScaler over the flattened [n_mels * T'] mel (src/1_preprocessing_advanced.py:376-379);
+    its transform is applied inside the dB pass (hlmc_mel_db_zscore, T' % 4 == 0), output in out_dtype."""
     x, was_np, sq = _to_dev(audio)
     p = _plan(sr, n_fft, hop_length, n_mels)
     B, n = x.shape
     T = int(L.lib().hlmc_mel_frames(p, n))
     keep = T if fixed_time_steps is None else int(fixed_time_steps)
-    out = torch.empty(B, n_mels, keep, device=x.device)
     ws = torch.empty(int(L.lib().hlmc_mel_workspace(p, B, n)), dtype=torch.uint8, device=x.device)
+    if scaler is not None:
+        if scaler.mean_d.numel() != n_mels * keep:
+            raise ValueError(f"scaler fitted on {scaler.mean_d.numel()} columns, mel has {n_mels * keep}")
+        out = torch.empty(B, n_mels, keep, device=x.device, dtype=out_dtype)
+        L.check(L.lib().hlmc_mel_db_zscore(p, L.stream(), x.data_ptr(), B, n, keep, float(amin), float(top_db),
+                                           scaler.mean_d.data_ptr(), scaler.scale_d.data_ptr(),
+                                           L.HLMC_BF16 if out_dtype == torch.bfloat16 else L.HLMC_F32,
+                                           out.data_ptr(), ws.data_ptr()), "hlmc_mel_db_zscore")
+        return _ret(out, was_np, sq)
+    out = torch.empty(B, n_mels, keep, device=x.device)
     L.check(L.lib().hlmc_mel_db(p, L.stream(), x.data_ptr(), B, n, keep, float(amin), float(top_db),
                                 out.data_ptr(), ws.data_ptr()), "hlmc_mel_db")
     return _ret(out, was_np, sq)

@@ -53,6 +53,13 @@ int hlmc_melspectrogram(const hlmc_mel_plan* plan, void* stream, const float* pc
  * -> keep the first t_keep frames (pad with the clip minimum if t_keep > T). out [batch][n_mels][t_keep] */
 int hlmc_mel_db(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
                 int64_t t_keep, float amin, float top_db, float* out, void* ws);
+/* hlmc_mel_db followed by StandardScaler.transform (hlmc_zscore_apply with cols = n_mels * t_keep) in the same
+ * dB pass: the fitted mel scaler applied to freshly extracted clips (src/1_preprocessing_advanced.py:97-114, then
+ * the transform half of mel_scaler.fit_transform at :376-379 on the flattened mel).  Bit-identical to that pair.
+ * t_keep % 4 == 0; out [batch][n_mels][t_keep] f32 (16-byte aligned) or bf16 (8-byte aligned). */
+int hlmc_mel_db_zscore(const hlmc_mel_plan* plan, void* stream, const float* pcm, int64_t batch, int64_t n_samples,
+                       int64_t t_keep, float amin, float top_db, const double* mean, const double* scale,
+                       int out_dtype, void* out, void* ws);
 /* librosa.power_to_db on a [batch][per_clip] array: ref_max!=0 -> ref = per-clip max, else ref_value
  * (ws: >= 8*batch bytes) */
 int hlmc_power_to_db(void* stream, const float* S, int64_t batch, int64_t per_clip, int ref_max, float ref_value,

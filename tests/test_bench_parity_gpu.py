@@ -1,6 +1,6 @@
 """Parity of the EXACT benchmarked configuration (bench.py, BASELINE config[1]): 256 clips of synthetic PCM
-(bench.synthetic_pcm, generated on the GPU as the bench does) -> bench.MelStage (HIP mel-dB 128x128 + the
-HIP StandardScaler z-score) -> audio-only HybridVAE 128x128 -> one fused Trainer.step (forward, ELBO sums,
+(bench.synthetic_pcm, generated on the GPU as the bench does) -> bench.MelStage (HIP mel-dB 128x128 with the
+HIP StandardScaler z-score fused into the dB pass) -> audio-only HybridVAE 128x128 -> one fused Trainer.step (forward, ELBO sums,
 backward, Adam), the B = 256 GEMM plans (split-K factors, sub-pixel tiles, LDS-DMA variants) the bench
 times.  Compared with the oracle chain: oracle/mel_oracle.py (numpy librosa restatement) for the mel stage,
 oracle/models_oracle.py (pinned bit-exact to the AST-loaded reference classes) for the step, seed-42
@@ -45,13 +45,15 @@ def _hip_chain(dtype, workload="audio"):
     scaler = hlmc_amd.StandardScaler().fit(calib.reshape(B, -1))
     stage = bench.MelStage(B, dev, scaler)
     x = stage(pcm)
+    # the fused dB + z-score pass is bit-identical to hlmc_mel_db followed by hlmc_zscore_apply
+    assert torch.equal(x.reshape(B, -1), scaler.transform(calib.reshape(B, -1)))
     model, trainer, text, cond = bench.build_workload(workload, dtype, B, dev, 1)
     eps = torch.randn(B, LATENT[workload], generator=torch.Generator().manual_seed(1))
     init = [p.detach().cpu().clone() for p in model.parameters()]
     sums = trainer.step(x, text, cond, eps=eps.to(dev))
     out = trainer._cache[B]["out"]
     torch.cuda.synchronize()
-    return dict(pcm=pcm.cpu().numpy(), mel=stage.mel.cpu().numpy(), x=x.detach().cpu().clone(), eps=eps,
+    return dict(pcm=pcm.cpu().numpy(), mel=calib.cpu().numpy(), x=x.detach().cpu().clone(), eps=eps,
                 text=None if text is None else text.cpu(), cond=None if cond is None else cond.cpu(),
                 loss=trainer.loss_tuple(sums), mu=out["mu"].cpu(), logvar=out["logvar"].cpu(),
                 recon=out["recon"].cpu(), recon_text=out["recon_text"].cpu() if "recon_text" in out else None,

@@ -35,6 +35,31 @@ def test_mel_db(cuda, n_samples, keep):
     assert np.abs(got - ref)[hi].max() < 2e-3
 
 
+@pytest.mark.parametrize("n_samples,keep", [(65024, 128), (22050 * 3, 256), (661500, 1024)])
+def test_mel_db_zscore_fused_bitexact(cuda, n_samples, keep):
+    """hlmc_mel_db_zscore (the scaler's transform inside the dB pass, the bench's mel stage) is bit-identical to
+    extract_mel_spectrogram followed by StandardScaler.transform; pad (T < keep) and crop (T > keep) cases."""
+    y = torch.from_numpy(MO.synthetic_pcm(3, n_samples, seed=5)).cuda()
+    mel = hlmc_amd.extract_mel_spectrogram(y, fixed_time_steps=keep)
+    sc = hlmc_amd.StandardScaler().fit(mel.reshape(3, -1))
+    for dt in (torch.float32, torch.bfloat16):
+        fused = hlmc_amd.extract_mel_spectrogram(y, fixed_time_steps=keep, scaler=sc, out_dtype=dt)
+        two = sc.transform(mel.reshape(3, -1), out_dtype=dt).reshape(fused.shape)
+        assert fused.dtype == dt and torch.equal(fused, two), dt
+    with pytest.raises(RuntimeError):
+        hlmc_amd.extract_mel_spectrogram(y[:, :65024 - 512], fixed_time_steps=126,
+                                         scaler=hlmc_amd.StandardScaler().fit(torch.zeros(2, 128 * 126).cuda()))
+
+
+def test_mel_db_vector_and_scalar_paths_agree(cuda):
+    """The 4-frame vector dB kernel (keep % 4 == 0) and the scalar one (otherwise) give identical frames."""
+    y = MO.synthetic_pcm(2, 22050 * 3, seed=9)   # T = 130 frames
+    a = hlmc_amd.extract_mel_spectrogram(y, fixed_time_steps=130)
+    b = hlmc_amd.extract_mel_spectrogram(y, fixed_time_steps=132)
+    assert np.array_equal(a, b[:, :, :130])
+    assert np.array_equal(b[:, :, 130], b[:, :, 131])   # padded with the clip minimum
+
+
 def test_mel_db_golden(cuda):
     fx = np.load("tests/golden/features.npz")
     y = MO.synthetic_pcm(2, 65024, seed=7)

@@ -259,6 +259,19 @@ struct StoreRM {
         }
         store4_round<OutT>(o, v);
     }
+    // put / put4 without the accumulate read (kernels whose output is never accumulated into: no global loads)
+    __device__ float put_na(int64_t ro, int n, float v) const {
+        if (act == 1) v = v > 0.f ? v : 0.f;
+        const OutT t = from_f32<OutT>(v);
+        out[ro + n] = t;
+        return to_f32<OutT>(t);
+    }
+    __device__ void put4_na(int64_t ro, int n, float (&v)[4]) const {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (act == 1) v[k] = v[k] > 0.f ? v[k] : 0.f;
+        store4_round<OutT>(out + ro + n, v);
+    }
     // the value store() writes (without accumulate), as float: for the fused column statistics
     __device__ float stored(int n, float v) const {
         if (bias) v += bias[n];
@@ -342,6 +355,8 @@ struct StoreSubpixel {
         return to_f32<OutT>(t);
     }
     __device__ void put4(int64_t ro, int n, float (&v)[4]) const { store4_round<OutT>(out + ro + n, v); }
+    __device__ float put_na(int64_t ro, int n, float v) const { return put(ro, n, v); }
+    __device__ void put4_na(int64_t ro, int n, float (&v)[4]) const { put4(ro, n, v); }
     __device__ float stored(int n, float v) const {
         if (bias) v += bias[n];
         return to_f32<OutT>(from_f32<OutT>(v));

@@ -34,6 +34,8 @@ __device__ __forceinline__ int xcd_logical_block(int lin, int total) {
 
 // 16 zero bytes: the source of every out-of-range / padding chunk of the LDS-DMA (global_load_lds) loaders
 static __device__ __attribute__((aligned(16))) uint4 g_zero16 = {0u, 0u, 0u, 0u};
+// a 16-byte chunk whose first element is 1 (the ones column of a weight-gradient operand)
+template <typename T> __device__ __attribute__((aligned(16))) uint4 g_one16 = {sizeof(T) == 2 ? 0x3F80u : 0x3F800000u, 0u, 0u, 0u};
 
 // ============================================================================ A / B loaders (NT)
 // Loader contract: set_phase(p); int K() const;
@@ -1020,6 +1022,16 @@ struct KRowDense {
     __device__ const void* addr(int k, const Col& cl) const {
         return (k < Kd && cl.m < Md) ? static_cast<const void*>(p + (int64_t)k * ld + cl.m) : &g_zero16;
     }
+    // branch-free path (vec_ok: 16-byte rows, Md % V == 0): one 16-byte load from a selected address -- the chunk,
+    // g_zero16 outside the operand, g_one16 for the ones column's chunk.  (The per-element fallback inside the
+    // K loop made the compiler wait for every outstanding load at its join: the loads issued one at a time.)
+    __host__ bool vec_ok() const { return vec && Md % Vec16<T>::N == 0; }
+    __device__ uint4 vload(int k, const Col& cl) const {
+        const void* a = (k < Kd && cl.m < Md) ? static_cast<const void*>(p + (int64_t)k * ld + cl.m)
+                        : (k < Kd && ones && cl.m == Md) ? static_cast<const void*>(&g_one16<T>)
+                                                         : static_cast<const void*>(&g_zero16);
+        return *reinterpret_cast<const uint4*>(a);
+    }
     __device__ uint4 load(int k, const Col& cl) const {
         constexpr int V = Vec16<T>::N;
         const int m = cl.m;
@@ -1062,6 +1074,8 @@ struct KRowConvS2 {
         const int64_t pix = ((int64_t)b * 2 * Hl + 2 * r - 1) * (2 * Wl) + 2 * c - 1;
         return x + pix * C + cl.off;
     }
+    __host__ bool vec_ok() const { return true; }
+    __device__ uint4 vload(int k, const Col& cl) const { return *reinterpret_cast<const uint4*>(addr(k, cl)); }
     __device__ uint4 load(int k, const Col& cl) const {
         if (k >= Kd || !cl.ok) return make_uint4(0, 0, 0, 0);
         const uint32_t t = dW.div((uint32_t)k);
@@ -1085,7 +1099,7 @@ __device__ __forceinline__ int tn_swz(int row) {
 
 // Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_grouped_kernel).
 // One K-step of global loads in flight in one register set, double-buffered LDS images.
-template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL>
+template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, bool VEC = false>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len,
                                                       int remap) {
     constexpr int V = Vec16<T>::N;
@@ -1138,12 +1152,12 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) rg.a[i] = ll.load(k0 + c / ACPR, acol[i]);
+            if (c < ACH) rg.a[i] = VEC ? ll.vload(k0 + c / ACPR, acol[i]) : ll.load(k0 + c / ACPR, acol[i]);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) rg.b[i] = hl.load(k0 + c / BCPR, bcol[i]);
+            if (c < BCH) rg.b[i] = VEC ? hl.vload(k0 + c / BCPR, bcol[i]) : hl.load(k0 + c / BCPR, bcol[i]);
         }
     };
     auto lstore = [&](const Regs& rg, int buf) {

@@ -300,10 +300,18 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
     HLMC_PROBE_BEGIN(s);
     // the 64-deep K-step for splits of >= 1024 rows (measured: 490.9 vs 450.9 us for the 9 conv layers when
     // every split took it), the 32-deep one below
-    if (pl.ksl >= kTnKch8Min)
-        gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-    else
-        gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    static const bool vec_env = [] {  // HLMC_TN_VEC=0: the per-element loader path everywhere (A/B aid)
+        const char* e = std::getenv("HLMC_TN_VEC");
+        return !(e && e[0] == '0');
+    }();
+    const bool vec = vec_env && ll.vec_ok() && hl.vec_ok();
+    if (pl.ksl >= kTnKch8Min) {
+        if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, true><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        else gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    } else {
+        if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, true><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        else gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    }
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     reduce_splits(s, ws.p, ep, M, N, pl.S);

@@ -64,10 +64,13 @@ struct DenseLoader {  // X[m * ld + k], m < M, k < K
     __device__ const void* addr(const Row& rw, const Ctx& cx) const {  // DMA path: Kd % V == 0, 16-byte rows
         return (rw.r && cx.k < Kd) ? static_cast<const void*>(rw.r + cx.k) : static_cast<const void*>(&g_zero16);
     }
+    // whole-chunk operand (Kd % V == 0, aligned rows: every conv weight): the kernel takes the unconditional
+    // load from addr() for all its chunks (one uniform branch around the whole K-step's loads: a per-chunk branch
+    // makes hipcc wait for every outstanding load at its join)
+    __host__ __device__ bool vec_ok() const { return vec && (Kd % Vec16<T>::N) == 0; }
     __device__ uint4 load(const Row& rw, const Ctx& cx) const {
         constexpr int V = Vec16<T>::N;
         const int k = cx.k;
-        // whole-chunk operand (Kd % V == 0, aligned rows: every conv weight): unconditional load, no tail path
         if (vec && (Kd % V) == 0) return *reinterpret_cast<const uint4*>(addr(rw, cx));
         if (!rw.r) return make_uint4(0, 0, 0, 0);
         if (vec && k + V <= Kd) return *reinterpret_cast<const uint4*>(rw.r + k);
@@ -110,6 +113,7 @@ struct ConvS2Loader {
         const int kh = tap / 3, kw = tap - kh * 3;
         return Ctx{((int64_t)kh * Wi + kw) * C + ci, 1 | (kh == 0 ? 2 : 0) | (kw == 0 ? 4 : 0) | (tap >= 9 ? 8 : 0)};
     }
+    __host__ __device__ bool vec_ok() const { return true; }
     // unconditional load from a selected address (no branch around the load: hipcc would wait per chunk)
     __device__ uint4 load(const Row& rw, const Ctx& cx) const { return *reinterpret_cast<const uint4*>(addr(rw, cx)); }
     __device__ const void* addr(const Row& rw, const Ctx& cx) const {
@@ -160,6 +164,7 @@ struct SubpixelLoader {
         const int dr = sp_delta(py, ty), dc = sp_delta(px, tx);
         return Ctx{((int64_t)dr * Wi + dc) * C + ci, 1 | (dr ? 2 : 0) | (dc ? 4 : 0) | (k >= Kd ? 8 : 0)};
     }
+    __host__ __device__ bool vec_ok() const { return true; }
     // unconditional load from a selected address (no branch around the load: hipcc would wait per chunk)
     __device__ uint4 load(const Row& rw, const Ctx& cx) const { return *reinterpret_cast<const uint4*>(addr(rw, cx)); }
     __device__ const void* addr(const Row& rw, const Ctx& cx) const {
@@ -195,6 +200,7 @@ struct SubpixelWeight {
         const int ty = ntx == 2 ? (tt >> 1) : tt, tx = ntx == 2 ? (tt & 1) : 0;
         return Ctx{(sp_kidx(py, ty) * 3 + sp_kidx(px, tx)) * C + ci};
     }
+    __host__ __device__ bool vec_ok() const { return true; }
     __device__ uint4 load(const Row& rw, const Ctx& cx) const { return *reinterpret_cast<const uint4*>(addr(rw, cx)); }
     __device__ const void* addr(const Row& rw, const Ctx& cx) const {
         if (!rw.r || cx.off < 0) return &g_zero16;
@@ -625,9 +631,23 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
     Regs r0;  // staging set: one K-step of global loads in flight (measured: a second set, two steps in
               // flight, was 1.2-1.6x slower on every short-K layer — lower occupancy)
     const int kc = (tid % KCH) * V;  // this thread's chunk column (256 % KCH == 0: the same for every i)
+    const bool vec = al.vec_ok() && bl.vec_ok();  // uniform: every chunk from addr() (DenseLoader::vec_ok)
     auto gload = [&](Regs& rg, int k0) {
         const typename AL::Ctx ax = al.ctx(k0 + kc);
         const typename BL::Ctx bx = bl.ctx(k0 + kc);
+        if (vec) {
+#pragma unroll
+            for (int i = 0; i < AR; ++i) {
+                int c = tid + i * 256;
+                if (ACH % 256 == 0 || c < ACH) rg.a[i] = *reinterpret_cast<const uint4*>(al.addr(arow[i], ax));
+            }
+#pragma unroll
+            for (int i = 0; i < BR; ++i) {
+                int c = tid + i * 256;
+                if (BCH % 256 == 0 || c < BCH) rg.b[i] = *reinterpret_cast<const uint4*>(bl.addr(brow[i], bx));
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;

@@ -42,6 +42,9 @@ __device__ __forceinline__ float act_grad(float z, int act) {
     if (act == 1) return z > 0.f ? 1.f : 0.f;
     return 1.f;
 }
+// ACT >= 0: the activation fixed at compile time (0 = LeakyReLU 0.01, the conv layers'), else the runtime `act`
+template <int ACT>
+__device__ __forceinline__ float act_grad_t(float z, int act) { return act_grad(z, ACT >= 0 ? ACT : act); }
 
 
 // Column sums of per-thread V-channel accumulators across a 256-thread block whose thread t covers row
@@ -288,7 +291,10 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const T* __restrict__ y, in
 }
 
 // backward partial sums: part[blk][0..C) = sum dz, [C..2C) = sum dz*xhat
-template <typename T, bool kMask>
+// Rows past the block's range are clamped (always-valid addresses) and masked out of the sums, so every load is
+// unconditional: a conditional prefetch leaves hipcc unable to count the loads younger than the ones it waits for
+// at the top of the next step, and it waits for all of them (measured in the halo and GEMM loops).
+template <typename T, bool kMask, int ACT = -1>
 __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
                                                              int64_t R, int C, const float* __restrict__ mean,
                                                              const float* __restrict__ invstd,
@@ -322,16 +328,16 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
             ng[u] = load16_raw(da + rc * lda + c0);
         }
     };
-    if (r0 + rr < r1) fetch(r0 + rr);
+    fetch(r0 + rr);
     for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
         uint4 rx[kUb], rg[kUb];
 #pragma unroll
         for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
-        if (r + kUb * rpp < r1) fetch(r + kUb * rpp);
+        fetch(r + kUb * rpp);
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t ru = r + u * rpp;
-            if (ru >= r1) break;
+            const bool valid = ru < r1;
             float x[1][V], g[1][V];
             cvt16_f32<T>(rx[u], x[0]);
             cvt16_f32<T>(rg[u], g[0]);
@@ -339,8 +345,9 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
             for (int v = 0; v < V; ++v) {
                 float xh = (x[0][v] - mu[v]) * is[v];
                 float z = xh * ga[v] + be[v];
-                float dz = g[0][v] * act_grad(z, act);
-                if constexpr (kMask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
+                float dz = g[0][v] * act_grad_t<ACT>(z, act);
+                if constexpr (kMask) dz = (valid && mask[ru * C + c0 + v]) ? dz * mscale : 0.f;
+                dz = valid ? dz : 0.f;
                 a[v] += dz;
                 b[v] = fmaf(dz, xh, b[v]);
             }
@@ -379,7 +386,8 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(XAcc acc, int C, fl
 // dy = gamma*invstd*(dz - sum_dz/R - xhat*sum_dzxh/R); also column partial sums of dy (bias grad)
 // kFin: sum dz / sum dz*xhat folded here from the moments' partial table (bn_fin_prologue; block 0 stores
 // dgamma / dbeta) instead of read from `sums`
-template <typename T, bool kMask, bool kFin>
+// (unconditional clamped loads and stores: bn_bwd_moments_kernel; a clamped row's store rewrites the same value)
+template <typename T, bool kMask, bool kFin, int ACT = -1>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
                                                            int64_t R, int C, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -412,7 +420,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
             ng[u] = load16_raw(da + rc * lda + c0);
         }
     };
-    if (r0 + rr < r1) fetch(r0 + rr);  // in flight during the finalize prologue
+    fetch(r0 + rr);  // in flight during the finalize prologue
     if constexpr (kFin) {
         // s1 is free until the closing block_colsum: totals in [0, 2C), the 2C sums as floats from 1024 (C
         // doubles), fold scratch after them (only used when 2C < 256: ends below 1024 + 64 + 768)
@@ -429,11 +437,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
         uint4 rx[kUb], rg[kUb];
 #pragma unroll
         for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
-        if (r + kUb * rpp < r1) fetch(r + kUb * rpp);
+        fetch(r + kUb * rpp);
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t ru = r + u * rpp;
-            if (ru >= r1) break;
+            const bool valid = ru < r1;
+            const int64_t rc = valid ? ru : r1 - 1;  // the row whose inputs rx / rg hold (fetch clamps the same way)
             float x[1][V], g[1][V];
             cvt16_f32<T>(rx[u], x[0]);
             cvt16_f32<T>(rg[u], g[0]);
@@ -442,14 +451,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
             for (int v = 0; v < V; ++v) {
                 float xh = (x[0][v] - mu[v]) * is[v];
                 float z = xh * ga[v] + be[v];
-                float dz = g[0][v] * act_grad(z, act);
-                if constexpr (kMask) dz = mask[ru * C + c0 + v] ? dz * mscale : 0.f;
+                float dz = g[0][v] * act_grad_t<ACT>(z, act);
+                if constexpr (kMask) dz = mask[rc * C + c0 + v] ? dz * mscale : 0.f;
                 o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
             }
-            store16_f32(dy + ru * C + c0, o);
-            // the bias grad is the sum of the dy actually stored (rounded to T)
+            store16_f32(dy + rc * C + c0, o);
+            // the bias grad is the sum of the dy actually stored (rounded to T), each row once
 #pragma unroll
-            for (int v = 0; v < V; ++v) a[v] += to_f32<T>(from_f32<T>(o[v]));
+            for (int v = 0; v < V; ++v) a[v] += valid ? to_f32<T>(from_f32<T>(o[v])) : 0.f;
         }
     }
     if (bias_acc.on()) {
@@ -1326,7 +1335,8 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
         HLMC_CHECK_ARG(fused->acc.p == mom.p && lda == C && !mask && act == 0,
                        "bn_act_bwd: fused moments need a dense lrelu layer and its accumulator");
     } else {
-        auto k = mask ? bn_bwd_moments_kernel<T, true> : bn_bwd_moments_kernel<T, false>;
+        auto k = mask ? bn_bwd_moments_kernel<T, true> : act == 0 ? bn_bwd_moments_kernel<T, false, 0>
+                                                                  : bn_bwd_moments_kernel<T, false>;
         HLMC_BN_PROBED(s, 2.0 * sizeof(T) * R * C,
                        (k<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, rpb,
                                                     mom)));
@@ -1342,7 +1352,8 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
         HLMC_LAUNCHED();
     }
     auto ka = mask ? (fin_here ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
-                   : (fin_here ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
+              : act == 0 ? (fin_here ? bn_bwd_apply_kernel<T, false, true, 0> : bn_bwd_apply_kernel<T, false, false, 0>)
+                         : (fin_here ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
     HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C,
                    (ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
                                                  dy, rpb, bias_acc, bf)));

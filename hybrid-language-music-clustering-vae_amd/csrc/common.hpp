@@ -183,6 +183,17 @@ __device__ __forceinline__ void xacc_add(const XAcc& x, int col, double v) {
 __device__ __forceinline__ double xacc_value(long long a, long long b, long long c) {
     return (double)a + ((double)b * 0x1p-32 + (double)c * 0x1p-64);
 }
+// column c of an exact accumulator, summed over its shards (one thread)
+__device__ __forceinline__ double xacc_column(const XAcc& acc, int c) {
+    long long a = 0, b = 0, d = 0;
+    for (int sh = 0; sh < acc.shards; ++sh) {
+        const unsigned long long* q = acc.p + (size_t)sh * 3 * acc.ncols + c;
+        a += (long long)q[0];
+        b += (long long)q[acc.ncols];
+        d += (long long)q[2 * acc.ncols];
+    }
+    return xacc_value(a, b, d);
+}
 // out[c] (LDS, c < ncols) = the accumulator's column totals; every thread of the block calls it (blockDim.x == NT);
 // red: LDS scratch of >= 3 * NT int64 (used when ncols < NT).  Thread (column c, shard group g) issues the loads of
 // all its shards at once (<= 8 shards x 3 words in flight; clamped addresses, masked adds).  Ends with a barrier.

@@ -447,6 +447,11 @@ class NetT : public NetBase {
         float* gb = nullptr;
     };
     PendingBias pend_bias;
+    PendingBias take_bias() {
+        const PendingBias pb = pend_bias;
+        pend_bias = PendingBias{};
+        return pb;
+    }
     // f on the weight-gradient stream, after the bias reduction a preceding bn_bwd(defer_bias) left pending
     // (queued: flushed every side_batch() layers)
     int side_bias(hipStream_t s, SideFn f) {
@@ -574,7 +579,10 @@ class NetT : public NetBase {
                 HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_c1<T>(q, dy, B, ho, wo, co, audio, gw, sc); }));
             } else {
                 const T* xin = AT(enc.a[l - 1]);
-                HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc); }));
+                const PendingBias pb = take_bias();  // written by the weight gradient's reduce launch
+                HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) {
+                    return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc, pb.acc, pb.gb);
+                }));
                 if (l == 1) HLMC_TRY(flush_side(s));  // nothing queued may wait for the join behind the main tail
                 // grad of layer l-1's activation
                 HLMC_TRY(ops::subpixel<T>(s, dy, B, ho, wo, co, P1(enc.w[l]), nullptr, ci, gA, scratch));
@@ -693,7 +701,10 @@ class NetT : public NetBase {
                             &fuse, true, true));
             const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
             float* gw = G[dec.w[l]];
-            HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) { return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc); }));
+            const PendingBias pb = take_bias();  // written by the weight gradient's reduce launch
+            HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) {
+                return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc, pb.acc, pb.gb);
+            }));
             HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
             fuse = ops::BnBwdFuse{};  // the stride-2 conv data gradients carry no moments: a separate pass
         }

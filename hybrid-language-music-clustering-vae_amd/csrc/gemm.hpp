@@ -1290,9 +1290,16 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
 // the G group sums are added in group order.  Fixed order => deterministic; G = 1 is the plain split-order sum.
 // Deep split counts (the 16-262k-row weight gradients split 50-170 ways over 3-18 tiles) are latency chains
 // otherwise: one thread per output walking S slabs waits S / 4 memory round trips.
+// an epilogue's optional side task (E::extra(), e.g. StoreWgradConv's bias gradient), run once per reduce launch
+template <class E>
+__device__ __forceinline__ auto ep_extra(const E& e, int) -> decltype(e.extra(), void()) { e.extra(); }
+template <class E>
+__device__ __forceinline__ void ep_extra(const E&, long) {}
+
 template <int G, class EP>
 __global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(const float* __restrict__ ws, EP ep, int M, int N,
                                                                     int S) {
+    ep_extra(ep, 0);
     constexpr int OPB = 256 / G;
     __shared__ float part[G][OPB];
     const int o = threadIdx.x % OPB, g = threadIdx.x / OPB;

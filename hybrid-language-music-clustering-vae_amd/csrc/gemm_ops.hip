@@ -262,6 +262,14 @@ size_t dispatch_linear_ws(int M, int N, int K) {
 struct StoreWgradConv {
     float* dW;
     int C;
+    // the layer's bias gradient (column totals of its exact accumulator) written by the reduce launch's first block
+    // (splitk_reduce_grouped_kernel: ep_extra) instead of a separate launch on the weight-gradient stream
+    XAcc bacc;
+    float* gb = nullptr;
+    __device__ void extra() const {
+        if (gb && blockIdx.x == 0)
+            for (int c = threadIdx.x; c < bacc.ncols; c += blockDim.x) gb[c] = (float)xacc_column(bacc, c);
+    }
     struct Row {
         float* r;
     };
@@ -976,13 +984,15 @@ size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co) {
 }
 
 template <typename T>
-int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* Xh, int C, float* dW, Ws ws) {
+int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* Xh, int C, float* dW, Ws ws,
+             XAcc bias_acc, float* dbias) {
     constexpr int V = Vec16<T>::N;
+    HLMC_CHECK_ARG(!dbias || bias_acc.on(), "wgrad_s2: a bias gradient needs its accumulator");
     HLMC_CHECK_ARG(M % V == 0 && C % V == 0, "wgrad_s2: channel counts must be multiples of the vector width");
     const int K = B * Hl * Wl, N = 9 * C;
     KRowDense<T> ll{L, M, K, M, aligned16(L)};
     KRowConvS2<T> hl{Xh, Hl, Wl, C, K, FastDiv((uint32_t)Wl), FastDiv((uint32_t)Hl)};
-    StoreWgradConv ep{dW, C};
+    StoreWgradConv ep{dW, C, bias_acc, dbias};
     probe::site(probe::kWgradS2, 2.0 * M * N * K,
                 (double)sizeof(T) * ((double)K * M + 4.0 * K * C) + 4.0 * M * N);
     return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
@@ -1059,7 +1069,7 @@ size_t linear_wgrad_ws(int Mb, int N, int K) {  // with or without the bias colu
     template int subpixel<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,        \
                              ColStats*, const BnInput*);                                                                             \
     template size_t subpixel_ws<T>(int, int, int, int, int);                                                       \
-    template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws);                \
+    template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws, XAcc, float*);  \
     template size_t wgrad_s2_ws<T>(int, int, int, int, int);                                                       \
     template int linear<T, T>(hipStream_t, const T*, int, int, int, const T*, int, const float*, int, T*, int, int, \
                               int, Ws, const T*);                                                                  \

@@ -361,17 +361,6 @@ __global__ __launch_bounds__(256) void bn_bwd_moments_kernel(const T* __restrict
     block_colsum<V>(db_, tpr, C, s1, acc, C);
 }
 
-// column c of an exact accumulator, summed over its shards
-__device__ __forceinline__ double xacc_column(const XAcc& acc, int c) {
-    long long a = 0, b = 0, d = 0;
-    for (int sh = 0; sh < acc.shards; ++sh) {
-        const unsigned long long* q = acc.p + (size_t)sh * 3 * acc.ncols + c;
-        a += (long long)q[0];
-        b += (long long)q[acc.ncols];
-        d += (long long)q[2 * acc.ncols];
-    }
-    return xacc_value(a, b, d);
-}
 // backward moments (2C columns): sum dz (-> dbeta), sum dz*xhat (-> dgamma); grid ceil(C / 64) x 64 (C > 512)
 __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(XAcc acc, int C, float* dgamma, float* dbeta, float* sums_f) {
     const int c = blockIdx.x * 64 + threadIdx.x;

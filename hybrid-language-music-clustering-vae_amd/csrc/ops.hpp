@@ -64,7 +64,8 @@ size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co);
 
 // dW[M][C][3][3] = sum_{b,r,c} L[b,r,c,m] * Xh[b, 2r-1+kh, 2c-1+kw, ci]   (L low-res [B,Hl,Wl,M], Xh [B,2Hl,2Wl,C])
 template <typename T>
-int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* Xh, int C, float* dW, Ws ws);
+int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* Xh, int C, float* dW, Ws ws,
+             XAcc bias_acc = XAcc{}, float* dbias = nullptr);  // dbias: the layer's bias gradient from bias_acc
 template <typename T>
 size_t wgrad_s2_ws(int B, int Hl, int Wl, int M, int C);
 

@@ -544,7 +544,12 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
     }
     __syncthreads();
     const int g8 = (lane >> 4) * 8;
-    double run_a = 0.0, run_q = 0.0;  // statistics (kStatMode 1): thread c < COB, column n0 + c
+    // statistics (kStatMode 1): each lane's column sums over all its tiles in registers, reduced across the block
+    // once at the end (a per-tile LDS reduction cost two barriers per tile)
+    constexpr int NS = TR ? TN * 4 : TN;
+    double run_s[NS], run_q[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) run_s[j] = run_q[j] = 0.0;
     constexpr int WAVES_M = 4 / WAVES_N;
     __shared__ double sred[EP::kStatMode == 1 ? WAVES_M : 1][2][COB];
     for (; t < ntiles; t += bstep) {
@@ -593,15 +598,10 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
         else
             epilogue_tile<TM, TN>(hep, acc, t * TP + wm0, n0 + wn0, lane, M, CO, cs, cq);
         if constexpr (EP::kStatMode == 1) {
-            const int wmi = wave / WAVES_N;
-            stats_to_lds<TR, TN, COB>(cs, cq, &sred[0][0][0], wmi, wn0, lane);
-            __syncthreads();
-            if (tid < COB) {  // this block's running column sums over its tiles (tile order: deterministic)
 #pragma unroll
-                for (int w = 0; w < WAVES_M; ++w) {
-                    run_a += sred[w][0][tid];
-                    run_q += sred[w][1][tid];
-                }
+            for (int j = 0; j < NS; ++j) {
+                run_s[j] += cs[j];
+                run_q[j] += cq[j];
             }
         }
         if constexpr (DB) {
@@ -619,10 +619,18 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
         }
     }
     if constexpr (EP::kStatMode == 1) {
+        stats_to_lds<TR, TN, COB>(run_s, run_q, &sred[0][0][0], wave / WAVES_N, wn0, lane);
+        __syncthreads();
         if (tid < COB) {
+            double a = 0.0, q = 0.0;
+#pragma unroll
+            for (int w = 0; w < WAVES_M; ++w) {
+                a += sred[w][0][tid];
+                q += sred[w][1][tid];
+            }
             const int shard = (int)(blockIdx.x % (unsigned)ep.acc.shards);
-            xacc_add_shard(ep.acc, shard, n0 + tid, run_a);
-            xacc_add_shard(ep.acc, shard, CO + n0 + tid, run_q);
+            xacc_add_shard(ep.acc, shard, n0 + tid, a);
+            xacc_add_shard(ep.acc, shard, CO + n0 + tid, q);
         }
     }
 }
@@ -711,7 +719,12 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
     }
     __syncthreads();
     const int g8 = (lane >> 4) * 8;
-    double run_a = 0.0, run_q = 0.0;  // statistics (kStatMode 1): thread c < COB, column n0 + c
+    // statistics (kStatMode 1): per-lane column sums over all tiles and phases in registers, one block reduction
+    // at the end (conv_s2_halo_kernel; per phase it cost two barriers, eight per tile)
+    constexpr int NS = TR ? TN * 4 : TN;
+    double run_s[NS], run_q[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) run_s[j] = run_q[j] = 0.0;
     __shared__ double sred[EP::kStatMode == 1 ? 4 : 1][2][COB];
     for (; t < ntiles; t += bstep) {
         const int tn = t + bstep;
@@ -769,13 +782,11 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
             else
                 epilogue_tile<TM, TN>(e, acc, t * TP + wm0, n0, lane, M, CO, cs, cq);
             if constexpr (EP::kStatMode == 1) {
-                stats_to_lds<TR, TN, COB>(cs, cq, &sred[0][0][0], wave, 0, lane);
-                __syncthreads();
-                if (tid < COB) {  // running column sums over this block's (tile, phase) pairs, in order
-                    run_a += (sred[0][0][tid] + sred[1][0][tid]) + (sred[2][0][tid] + sred[3][0][tid]);
-                    run_q += (sred[0][1][tid] + sred[1][1][tid]) + (sred[2][1][tid] + sred[3][1][tid]);
+#pragma unroll
+                for (int j = 0; j < NS; ++j) {
+                    run_s[j] += cs[j];
+                    run_q[j] += cq[j];
                 }
-                __syncthreads();  // sred is reused by the next phase
             }
         }
         if constexpr (DB) {
@@ -793,10 +804,14 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
         }
     }
     if constexpr (EP::kStatMode == 1) {
+        stats_to_lds<TR, TN, COB>(run_s, run_q, &sred[0][0][0], wave, 0, lane);
+        __syncthreads();
         if (tid < COB) {
+            const double a = (sred[0][0][tid] + sred[1][0][tid]) + (sred[2][0][tid] + sred[3][0][tid]);
+            const double q = (sred[0][1][tid] + sred[1][1][tid]) + (sred[2][1][tid] + sred[3][1][tid]);
             const int shard = (int)(blockIdx.x % (unsigned)ep.acc.shards);
-            xacc_add_shard(ep.acc, shard, n0 + tid, run_a);
-            xacc_add_shard(ep.acc, shard, CO + n0 + tid, run_q);
+            xacc_add_shard(ep.acc, shard, n0 + tid, a);
+            xacc_add_shard(ep.acc, shard, CO + n0 + tid, q);
         }
     }
 }

@@ -25,9 +25,17 @@ inline int grid_for(int64_t n, int per_block = kThreads, int cap = 8192) {
 // the former 1024-block cap left the wide-channel layers with 16-64 blocks, latency-bound at 5-20% of HBM.)
 // <= 1024 blocks (about 4 per CU); each range is a multiple of 8192 / C rows (one 4-row-per-thread step for bf16)
 // and the backward kernels prefetch the next step's rows into registers while reducing the current one.
+inline int bn_block_target() {
+    static const int t = [] {
+        const char* e = std::getenv("HLMC_BN_BLOCKS");
+        return e ? std::max(64, std::atoi(e)) : 1024;
+    }();
+    return t;
+}
 inline int64_t bn_rows_per_blk(int64_t R, int C) {
     const int64_t step = std::max(1, 8192 / C);
-    const int64_t want = std::max<int64_t>(1, (R + 1023) / 1024);
+    const int64_t tb = bn_block_target();
+    const int64_t want = std::max<int64_t>(1, (R + tb - 1) / tb);
     return (want + step - 1) / step * step;
 }
 inline int bn_blocks(int64_t R, int C) { return (int)((R + bn_rows_per_blk(R, C) - 1) / bn_rows_per_blk(R, C)); }
@@ -98,7 +106,7 @@ __device__ __forceinline__ double block_sum_partials(const double* __restrict__ 
 // a block pass covers rpp = 256 / (C/V) consecutive rows (one contiguous 4 KB span); each thread keeps its
 // V channels' parameters in registers and has kU rows in flight.
 constexpr int kU = 4;   // rows in flight, forward streaming kernels
-constexpr int kUb = 2;  // backward (two operands per row, the next step's rows prefetched as well)
+constexpr int kUb = 2;  // backward (two operands per row, the next step's rows prefetched as well; 4 measured -0.6%)
 
 template <typename T>
 __global__ __launch_bounds__(256) void col_moments_kernel(const T* __restrict__ y, int64_t R, int C, int64_t rows_per_blk,

@@ -8,7 +8,9 @@ with fp32 accumulation and fp32 master weights; for N > 1 ranks the flat fp32 gr
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload audio|hybrid|cvae] [--dtype bf16|fp32]
                     [--grad-dtype bf16|fp32] [--no-cpu-baseline] [--no-roofline] [--no-extras] [--graph]
-N > 1 is launched by torch.distributed.run (one process per GPU); rank 0 prints ONE JSON line.
+N > 1 runs one process per GPU under torch.distributed.run; `python bench.py --gpus N` outside torchrun starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child process (nothing touches the GPU in the
+parent), relays rank 0's JSON line and exits with the child's status.  Rank 0 prints ONE JSON line.
 Besides the headline (BASELINE config[1]), the default run times three more workloads on the same mel stage and
 reports them under "extras" (never as `value`): the headline in fp32 (the parity precision), the hybrid ConvVAE
 with 384-d lyrics (config[2]) and the genre-conditioned ConditionalVAE (config[3]), each bs=256 per GPU; the
@@ -205,9 +207,12 @@ def time_e2e(device, dist, world, n_clips, grad_dtype):
         t = torch.tensor([el], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    src = r["stages_s"].get("pcm_source", 0.0)
     return {"workload": "config[4] end to end: 30 s PCM -> mel-dB -> scaler -> HybridVAE 128x1024 bf16 train (1 epoch) "
                         "-> eval latents -> KMeans(10, n_init=10)",
             "n_clips": n_clips, "value": round(n_clips / el, 2), "unit": "clips/s", "seconds": round(el, 3),
+            # the synthetic PCM generation (torch, stands in for WAV decoding, which is out of scope) excluded
+            "value_excl_pcm_source": round(n_clips / max(1e-9, el - src), 2),
             "stages_s_rank0": {k: round(v, 4) for k, v in r["stages_s"].items()}, "train_steps": r["train_steps"],
             "final_loss": r["final_loss"], "kmeans_n_iter": int(r["kmeans_n_iter"])}
 
@@ -238,17 +243,20 @@ def kind_roofline(kind, st):
 
 
 def pmc_traffic(kind):
-    """HBM bytes per launch of this kind and its counter-based MFMA busy fraction from the committed rocprofv3
-    PMC summary (scripts/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes, per the gfx950 correction of
-    MI355X_MICROARCH.md; SQ_VALU_MFMA_BUSY_CYCLES over the dispatch's SIMD-cycles), or None."""
+    """The committed rocprofv3 summary of this kind (profiles/pmc_traffic.json, scripts/pmc_traffic.py): HBM bytes
+    per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes, per the gfx950 correction of MI355X_MICROARCH.md), the
+    counter-based MFMA busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over the dispatch's SIMD-cycles) and the kernel-trace
+    average launch duration in us; {} when absent."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d["kinds"][PROBE_KINDS[kind][0]]
-        return e.get("hbm_bytes_per_launch"), e.get("mfma_busy"), d.get("source")
+        e = dict(d["kinds"][PROBE_KINDS[kind][0]])
+        e["source"] = d.get("source")
+        e["file"] = d.get("file", "profiles/pmc_traffic.json")
+        return e
     except (OSError, KeyError, ValueError):
-        return None, None, None
+        return {}
 
 
 def host_cpu_share():
@@ -313,6 +321,32 @@ def cpu_baseline(batch=256, steps=5, warmup=2):
                       f"{warmup} warm-up steps ({dt:.1f} s: mel {t_mel:.1f} s, VAE {t_vae:.1f} s)"}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def relaunch_under_torchrun(n):
+    """`--gpus N > 1` outside torch.distributed.run: run this same command line as N ranks in a child
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1).  Called before any GPU or libhlmc use,
+    so the parent never initialises the device; the child is a subprocess, never an exec.  Rank 0's JSON line is
+    relayed to stdout, everything else the ranks print goes to stderr.  Returns the child's exit status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HLMC_BENCH_SELF_LAUNCHED="1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    for line in proc.stdout:
+        if line.startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return proc.wait()
+
+
 PROBE_STEPS = int(os.environ.get("HLMC_PROBE_STEPS", "3"))  # timed steps whose dominant-kernel launches are timed
 PCM_BATCHES = 5
 
@@ -328,20 +362,20 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default=None,
-                    help="gradient all-reduce wire for N > 1 (default bf16: half the xGMI bytes, DESIGN.md §7; the "
-                         "fp32 master gradient is what Adam reads either way)")
+    ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="fp32",
+                    help="gradient all-reduce wire for N > 1 (default fp32, the reference's numerics; bf16 halves the "
+                         "xGMI bytes and is reported as the labelled `headline_bf16_wire` extra, DESIGN.md §7)")
     ap.add_argument("--e2e-clips", type=int, default=20000, help="clips of the config[4] end-to-end extra line")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (N = 1 only; measured 12%% slower on ROCm 7: the graph "
                          "executor serialises the weight-gradient stream's branch, see DESIGN.md)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_under_torchrun(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus > 1 and world == 1:
-        raise SystemExit("--gpus N>1: launch with python -m torch.distributed.run --nproc-per-node N bench.py ...")
     # one rank per GPU; HLMC_DIST_BACKEND=gloo (with ranks sharing a device) rehearses the N > 1 control flow
     # (barriers, max-over-ranks timing, bucketed all-reduce) on a one-GPU box
     backend = os.environ.get("HLMC_DIST_BACKEND", "nccl")
@@ -368,7 +402,7 @@ def main():
     calib = hlmc_amd.extract_mel_spectrogram(pcm, fixed_time_steps=FRAMES)
     scaler = hlmc_amd.StandardScaler().fit(calib.reshape(B, -1))
     mel = MelStage(B, device, scaler)
-    gd = args.grad_dtype or ("bf16" if world > 1 else "fp32")
+    gd = args.grad_dtype
     grad_dtype = torch.bfloat16 if gd == "bf16" else torch.float32
     model, trainer, text, cond = build_workload(args.workload, args.dtype, B, device, world, grad_dtype=grad_dtype)
     nstep = [0]
@@ -456,6 +490,10 @@ def main():
         for key, (wl, dt) in {"audio_fp32": ("audio", "fp32"), "hybrid_td384_bf16": ("hybrid", "bf16"),
                               "cvae_bf16": ("cvae", "bf16")}.items():
             extras[key] = time_workload(wl, dt, B, device, world, mel, pcms, dist, grad_dtype=grad_dtype)
+        if world > 1:  # the headline on the half-width gradient wire (convert + all-reduce + copy back on the comm stream)
+            extras["headline_bf16_wire"] = dict(time_workload("audio", "bf16", B, device, world, mel, pcms, dist,
+                                                              steps=args.steps, warmup=args.warmup,
+                                                              grad_dtype=torch.bfloat16), grad_wire="bf16")
         extras["kmeans_n100k_k10"] = time_kmeans(device, dist, world, rank)
         extras["config4_e2e_n20k"] = time_e2e(device, dist, world, args.e2e_clips, grad_dtype)
 
@@ -473,7 +511,11 @@ def main():
                                       ": PCM[256,65024] -> HIP mel-dB 128x128 -> z-score -> VAE fwd+bwd+Adam",
                           "per_gpu_batch": B, "global_batch": B * world, "mel": "128x128", "params": n_params,
                           "parallelism": f"dp{world}",
-                          **({"backend": backend, "grad_wire": gd} if world > 1 else {}),
+                          "world_size": dist.get_world_size() if dist else 1,
+                          "backend": backend if dist else None, "grad_wire": gd if dist else None,
+                          "launch": ("self-launched torch.distributed.run child" if
+                                     os.environ.get("HLMC_BENCH_SELF_LAUNCHED") == "1" else
+                                     "torch.distributed.run" if dist else "single process"),
                           "pcm_batches": f"{PCM_BATCHES} distinct batches in rotation "
                                          f"({PCM_BATCHES * B * N_SAMPLES * 4 / 1e6:.0f} MB)",
                           "final_loss": round(loss, 3),
@@ -482,10 +524,19 @@ def main():
                                              if flops_clip else None)}}
         if live is not None:
             roof = kind_roofline(dominant, live)
-            traffic, mfma_busy, src = pmc_traffic(dominant)
-            roof["traffic"] = traffic
-            roof["mfma_busy"] = mfma_busy
-            roof["traffic_source"] = src
+            pmc = pmc_traffic(dominant)
+            roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+            roof["mfma_busy"] = pmc.get("mfma_busy")
+            roof["traffic_source"] = pmc.get("source")
+            # the same rate from the committed rocprofv3 kernel-trace average (no event pairs, no live probe):
+            # reproducible from profiles/ alone.  The live figure above includes the other stream's contention.
+            tavg = pmc.get("trace_avg_us")
+            if tavg:
+                work = roof["flops_per_launch"] if roof["bound"] == "mfma" else roof["bytes_per_launch"]
+                ach_t = work / (tavg * 1e-6) / (1e12 if roof["bound"] == "mfma" else 1e9)
+                roof["trace"] = {"avg_us_per_launch": tavg, "launches": pmc.get("trace_dispatches"),
+                                 "achieved": round(ach_t, 2), "frac": round(ach_t / roof["peak"], 4),
+                                 "file": pmc.get("file")}
             roof["timing"] = (f"HIP events around each launch on its stream, inside the timed region "
                               + (f"(event nodes of the step graph; the {live['launches']} launches of the last "
                                  f"of {args.steps} replays)" if graphed else

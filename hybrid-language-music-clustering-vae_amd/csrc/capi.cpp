@@ -464,4 +464,48 @@ int hlmc_op_wgrad_c1(void* stream, int dtype, const void* Lo, int B, int Hl, int
                        ops::wgrad_c1<bf16>(S(stream), (const bf16*)Lo, B, Hl, Wl, M, Xh, dW, w));
 }
 
+// LDS halo-tile forward (conv_s2 / subpixel, bf16) with the train-mode epilogue statistics and, when gamma is given,
+// the layer below's BatchNorm + LeakyReLU(0.01) applied while the input is staged (the engine's BnInput path):
+// x is then the pre-BN map, whose exact statistics this entry first accumulates with the moments pass the engine's
+// producers would have delivered.  out_sums[2 Co] = (sum y | sum y^2) over the stored bf16 outputs.
+static size_t halo_acc_off(int Ci) { return (XAcc::bytes(xacc_shards(Ci), 2 * Ci) + 255) & ~(size_t)255; }
+int64_t hlmc_op_halo_workspace(int Ci, int Co) {
+    return (int64_t)(halo_acc_off(Ci) + XAcc::bytes(xacc_shards(Co), 2 * Co));
+}
+int hlmc_op_halo_fwd(void* stream, int kind, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
+                     const float* bias, int Co, void* y, double* out_sums, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum, float eps,
+                     float* mean_out, float* invstd_out, void* a_out, void* ws, int64_t ws_bytes) {
+    HLMC_CHECK_ARG(kind == 0 || kind == 1, "hlmc_op_halo_fwd: kind 0 (conv_s2) or 1 (subpixel)");
+    HLMC_CHECK_ARG(out_sums && ws && ws_bytes >= hlmc_op_halo_workspace(Ci, Co), "hlmc_op_halo_fwd: workspace / out_sums");
+    const bool xin = gamma != nullptr;
+    HLMC_CHECK_ARG(kind == 0 ? ops::conv_s2_takes_input_bn<bf16>(B, Hi, Wi, Ci, Co)
+                             : ops::subpixel_takes_input_bn<bf16>(B, Hi, Wi, Ci, Co),
+                   "hlmc_op_halo_fwd: not an LDS halo-tile shape");
+    if (xin) HLMC_CHECK_ARG(beta && mean_out && invstd_out && a_out, "hlmc_op_halo_fwd: input BatchNorm arguments");
+    hipStream_t s = S(stream);
+    unsigned char* w = static_cast<unsigned char*>(ws);
+    XAcc ain{reinterpret_cast<unsigned long long*>(w), xacc_shards(Ci), 2 * Ci};
+    XAcc aout{reinterpret_cast<unsigned long long*>(w + halo_acc_off(Ci)), xacc_shards(Co), 2 * Co};
+    HLMC_HIP(hipMemsetAsync(ws, 0, (size_t)hlmc_op_halo_workspace(Ci, Co), s));
+    const int64_t R = (int64_t)B * Hi * Wi;
+    ops::BnInput bi{};
+    if (xin) {
+        HLMC_TRY(ops::bn_moments<bf16>(s, (const bf16*)x, R, Ci, ain));
+        bi.acc = ain; bi.R = R; bi.mean = mean_out; bi.invstd = invstd_out; bi.rmean = running_mean;
+        bi.rvar = running_var; bi.nbt = num_batches_tracked; bi.momentum = momentum; bi.eps = eps; bi.gamma = gamma;
+        bi.beta = beta; bi.a_out = a_out;
+    }
+    ops::ColStats st{aout, false};
+    Ws none{nullptr, 0};
+    if (kind == 0)
+        HLMC_TRY(ops::conv_s2<bf16>(s, (const bf16*)x, B, Hi, Wi, Ci, (const bf16*)wp, bias, Co, (bf16*)y, none, &st,
+                                    xin ? &bi : nullptr));
+    else
+        HLMC_TRY(ops::subpixel<bf16>(s, (const bf16*)x, B, Hi, Wi, Ci, (const bf16*)wp, bias, Co, (bf16*)y, none, &st,
+                                     xin ? &bi : nullptr));
+    HLMC_CHECK_ARG(st.done, "hlmc_op_halo_fwd: statistics not delivered by the halo kernel");
+    return ops::colsum_to_f64(s, aout, 2 * Co, out_sums);
+}
+
 }  // extern "C"

@@ -127,19 +127,11 @@ void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, c
 // HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid).  Measured per layer
 // (scripts/bench_gemm.py, round 3): the transposed epilogue takes the split-K / LDS-DMA conv and sub-pixel GEMMs from
 // 28-42 to 22-32 us (the 8 x 8 .. 2 x 2 layers), but makes the LDS halo-tile kernels 4-15 % slower (their stores were
-// not the bound; the swapped fragments cost LDS issue) -> halo kernels keep the per-element epilogue
-// (HLMC_HALO_TR=1 switches them over, A/B aid).
+// not the bound; the swapped fragments cost LDS issue) -> halo kernels keep the per-element epilogue.
 inline bool nt_tr_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("HLMC_NT_TR");
         return !(e && e[0] == '0');
-    }();
-    return on;
-}
-inline bool halo_tr_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HLMC_HALO_TR");
-        return e && e[0] == '1';
     }();
     return on;
 }
@@ -836,28 +828,34 @@ static bool subpixel_halo_shape(int Ci, int Co, int Wi, int Hi, int& which) {
     which = (Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0) ? 1 : (Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0) ? 2 : 0;
     return which != 0;
 }
-inline bool bn_in_enabled() {  // HLMC_BN_IN=0: input BatchNorm stays a bn_act pass (A/B aid)
-    static const bool on = [] {
-        const char* e = std::getenv("HLMC_BN_IN");
-        return !(e && e[0] == '0');
-    }();
+// environment switches read once per process (A/B aids; every one defaults on)
+static bool env_on(const char* name) {
+    const char* e = std::getenv(name);
+    return !(e && e[0] == '0');
+}
+inline bool bn_in_enabled() {  // HLMC_BN_IN=0: input BatchNorm stays a bn_act pass
+    static const bool on = env_on("HLMC_BN_IN");
     return on;
+}
+inline bool conv_halo_on(int which) {  // HLMC_CONV_HALO=0 / HLMC_CONV_HALO2=0: that shape on the gather GEMM
+    static const bool h1 = env_on("HLMC_CONV_HALO"), h2 = env_on("HLMC_CONV_HALO2");
+    return which == 1 ? h1 : which == 2 ? h2 : false;
+}
+inline bool sp_halo_on(int which) {  // HLMC_SP_HALO=0 / HLMC_SP_HALO2=0
+    static const bool h1 = env_on("HLMC_SP_HALO"), h2 = env_on("HLMC_SP_HALO2");
+    return which == 1 ? h1 : which == 2 ? h2 : false;
 }
 template <typename T>
 bool conv_s2_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co) {
     (void)B;
     int w;
-    return std::is_same<T, bf16>::value && bn_in_enabled() && conv_halo_shape(Ci, Co, Wi, Hi, w) &&
-           !(w == 1 && std::getenv("HLMC_CONV_HALO") && std::getenv("HLMC_CONV_HALO")[0] == '0') &&
-           !(w == 2 && std::getenv("HLMC_CONV_HALO2") && std::getenv("HLMC_CONV_HALO2")[0] == '0');
+    return std::is_same<T, bf16>::value && bn_in_enabled() && conv_halo_shape(Ci, Co, Wi, Hi, w) && conv_halo_on(w);
 }
 template <typename T>
 bool subpixel_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co) {
     (void)B;
     int w;
-    return std::is_same<T, bf16>::value && bn_in_enabled() && subpixel_halo_shape(Ci, Co, Wi, Hi, w) &&
-           !(w == 1 && std::getenv("HLMC_SP_HALO") && std::getenv("HLMC_SP_HALO")[0] == '0') &&
-           !(w == 2 && std::getenv("HLMC_SP_HALO2") && std::getenv("HLMC_SP_HALO2")[0] == '0');
+    return std::is_same<T, bf16>::value && bn_in_enabled() && subpixel_halo_shape(Ci, Co, Wi, Hi, w) && sp_halo_on(w);
 }
 
 template <typename T>
@@ -876,14 +874,8 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     probe::site(probe::kConvS2, 2.0 * M * Co * K,
                 (double)sizeof(T) * ((double)B * Hi * Wi * Ci + (double)Co * K + (double)M * Co));
     if constexpr (std::is_same<T, bf16>::value) {
-        static const bool halo = [] {
-            const char* e = std::getenv("HLMC_CONV_HALO");
-            return !(e && e[0] == '0');
-        }();
-        static const bool halo2 = [] {  // HLMC_CONV_HALO2=0: the 32x32x64 -> 128 layers on the gather GEMM (A/B)
-            const char* e = std::getenv("HLMC_CONV_HALO2");
-            return !(e && e[0] == '0');
-        }();
+        int which;
+        conv_halo_shape(Ci, Co, Wi, Hi, which);
         // (CI, Co, Wi): (32, 64, 64) 128-pixel tiles, double-buffered halo; (64, 128, 32) two 64-channel halves per
         // 64-pixel tile, one halo buffer (the weights take half the LDS)
         auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int tp, int nspl) -> int {
@@ -905,22 +897,15 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
-        const bool tr = halo_tr_enabled();
-        using StRM = WithStats<StoreRM<T>>;  // XIN variants: per-element epilogue (TR = false)
-        if (halo && Ci == 32 && Co == 64 && Wi == 64 && Hi % 8 == 0)
-            return tr ? run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, true>,
-                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, true>,
-                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false, true>, 128, 1)
-                      : run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, false>,
-                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false>,
-                            conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false, true>, 128, 1);
-        if (halo2 && Ci == 64 && Co == 128 && Wi == 32 && Hi % 8 == 0)
-            return tr ? run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, true>,
-                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, true>,
-                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false, true>, 64, 2)
-                      : run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, false>,
-                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false>,
-                            conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false, true>, 64, 2);
+        using StRM = WithStats<StoreRM<T>>;  // per-element epilogue (TR = false), see nt_tr_enabled
+        if (which == 1 && conv_halo_on(1))
+            return run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, false>,
+                       conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false>,
+                       conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false, true>, 128, 1);
+        if (which == 2 && conv_halo_on(2))
+            return run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, false>,
+                       conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false>,
+                       conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false, true>, 64, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
 }
@@ -947,14 +932,8 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
     probe::site(probe::kSubpixel, 2.0 * M * Co * 9.0 * Ci,
                 (double)sizeof(T) * ((double)M * Ci + 9.0 * Ci * Co + 4.0 * M * Co));
     if constexpr (std::is_same<T, bf16>::value) {
-        static const bool halo = [] {
-            const char* e = std::getenv("HLMC_SP_HALO");
-            return !(e && e[0] == '0');
-        }();
-        static const bool halo2 = [] {  // HLMC_SP_HALO2=0: the 16x16x128 -> 64 layers on the gather GEMM (A/B)
-            const char* e = std::getenv("HLMC_SP_HALO2");
-            return !(e && e[0] == '0');
-        }();
+        int which;
+        subpixel_halo_shape(Ci, Co, Wi, Hi, which);
         auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int nspl) -> int {
             const int ntiles = M / 128;  // 128 low-res pixels (whole rows) per tile, inside one image
             const int grid = std::min(ntiles * nspl, 256);
@@ -974,22 +953,15 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
-        const bool tr = halo_tr_enabled();
-        using StSP = WithStats<StoreSubpixel<T>>;  // XIN variants: per-element epilogue (TR = false)
-        if (halo && Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0)
-            return tr ? run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, true>,
-                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, true>,
-                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false, true>, 1)
-                      : run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, false>,
-                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false>,
-                            subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false, true>, 1);
-        if (halo2 && Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0)
-            return tr ? run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>, true>,
-                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, true>,
-                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2)
-                      : run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>, false>,
-                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false>,
-                            subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2);
+        using StSP = WithStats<StoreSubpixel<T>>;  // per-element epilogue (TR = false), see nt_tr_enabled
+        if (which == 1 && sp_halo_on(1))
+            return run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, false>,
+                       subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false>,
+                       subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false, true>, 1);
+        if (which == 2 && sp_halo_on(2))
+            return run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>, false>,
+                       subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false>,
+                       subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
 }

@@ -471,6 +471,10 @@ __global__ __launch_bounds__(64) void xacc_to_f32_kernel(XAcc acc, int C, float*
     const int c = blockIdx.x * 64 + threadIdx.x;
     if (c < C) out[c] = (float)xacc_column(acc, c);
 }
+__global__ __launch_bounds__(64) void xacc_to_f64_kernel(XAcc acc, int C, double* out) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c < C) out[c] = xacc_column(acc, c);
+}
 
 // sum over rows of column col of a [nrows][stride] table: 16 waves x 4 accumulators, LDS combine (1024 threads)
 __device__ __forceinline__ double fold_column(const double* __restrict__ p, int nrows, int64_t stride, int col, bool ok,
@@ -1356,6 +1360,13 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
                                                  dy, rpb, bias_acc, bf)));
     HLMC_LAUNCHED();
     if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
+    return HLMC_OK;
+}
+int colsum_to_f64(hipStream_t s, XAcc acc, int C, double* out) {
+    HLMC_CHECK_ARG(out && C > 0, "colsum_to_f64: bad arguments");
+    HLMC_TRY(check_acc(acc, C));
+    xacc_to_f64_kernel<<<fin_grid(C), 64, 0, s>>>(acc, C, out);
+    HLMC_LAUNCHED();
     return HLMC_OK;
 }
 int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out) {

@@ -137,6 +137,8 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
                float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums);
 // out[c] = total of column c of acc (C columns)
 int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out);
+// out[c] (f64) = column c of an exact accumulator (the op-level statistics entry)
+int colsum_to_f64(hipStream_t s, XAcc acc, int C, double* out);
 
 // ---------------------------------------------------------------- misc elementwise (kernels.hip)
 // Up to 4 float copies in one launch (segments with null dst or src are skipped): the small per-step copies

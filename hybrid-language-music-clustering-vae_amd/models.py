@@ -235,8 +235,24 @@ class _NativeModule(nn.Module):
         self._bn_flat = flat
         return flat
 
+    def get_rng_state(self):
+        """(seed, offset) of the engine's Philox reparameterisation-noise stream (drawn when forward gets no eps).
+        Not part of state_dict (whose keys stay the reference's); Trainer.state_dict carries it for resume."""
+        seed, off = C.c_uint64(), C.c_uint64()
+        L.check(L.lib().hlmc_net_get_rng(self._native_net().h, C.byref(seed), C.byref(off)), "hlmc_net_get_rng")
+        return int(seed.value), int(off.value)
+
+    def set_rng_state(self, state):
+        seed, off = state
+        L.check(L.lib().hlmc_net_set_rng(self._native_net().h, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                         int(off) & 0xFFFFFFFFFFFFFFFF), "hlmc_net_set_rng")
+
     def _run(self, audio, text=None, cond=None, eps=None, dropout=None):
         L.require_cuda(audio, text, cond, eps, dropout)
+        if eps is None and audio.is_cuda and torch.cuda.is_current_stream_capturing():
+            # under torch.cuda.graph capture the engine's host-side Philox offset would freeze into the graph (every
+            # replay the same noise): draw it with torch's graph-safe generator instead, as Trainer does
+            eps = torch.randn(audio.shape[0], self.latent_dim, device=audio.device)
         train = self.training
         return _NetFn.apply(self, train, audio, text, cond, eps, dropout, *self._params())
 

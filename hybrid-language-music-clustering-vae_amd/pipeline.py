@@ -94,7 +94,9 @@ def run_pipeline(n_clips, batch=256, epochs=1, text_dim=768, latent_dim=128, com
 
     pcm_fn(i, b) -> [b, 661500] float32 device PCM of clips i..i+b (default: synthetic_clips seeded per batch);
     lyrics: [n_clips, text_dim] lyric embeddings (default: seeded N(0, 1/text_dim), on the device);
-    eps_fn(step, b) -> reparameterisation noise (default torch.randn, as the reference's randn_like);
+    eps_fn(step, b) -> reparameterisation noise (default None: the engine draws it on the device from its Philox
+    stream, as the reference's randn_like; under process_group each rank's stream is keyed by its rank, see
+    Trainer);
     order_fn(epoch) -> clip order of that epoch over the rank's shard (local indices; default a seeded
     torch.randperm: DataLoader(shuffle=True)).
 

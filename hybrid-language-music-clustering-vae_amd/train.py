@@ -67,6 +67,15 @@ class Trainer:
         self.buckets = self._bucket_ranges()
         self._comm = None
         self._fwd_done = None
+        if self.distributed:
+            # per-rank reparameterisation noise: every rank builds its model after the same torch.manual_seed, so
+            # the engine's Philox streams start equal; rank r > 0 re-keys its seed (rank 0 keeps the single-process
+            # stream), so the ranks' clips get independent eps as separate torch.randn_like draws would
+            import torch.distributed as dist
+            rank = dist.get_rank(process_group) if process_group is not None else dist.get_rank()
+            if rank:
+                seed, off = model.get_rng_state()
+                model.set_rng_state(((seed + rank * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF, off))
         if self.distributed and dev.type == "cuda":
             self._fwd_done = torch.cuda.Event()
             L.check(L.lib().hlmc_net_set_bucket_sync(self.net.h, 1), "hlmc_net_set_bucket_sync")
@@ -103,6 +112,18 @@ class Trainer:
                 coef = torch.tensor([2.0, 2.0 * self.text_weight, self.beta], device=dev)
             self._cache[B] = dict(out=out, d=d, ws=ws, lws=lws, sums=sums, coef=coef, n=(na, nt, nl))
         return self._cache[B]
+
+    def state_dict(self):
+        """Optimizer + noise state for checkpoint / resume (the model's own state_dict holds the parameters and
+        BatchNorm buffers): Adam step count and moments, and the engine's Philox (seed, offset)."""
+        return {"step": self.step_count, "exp_avg": self.m.detach().clone(), "exp_avg_sq": self.v.detach().clone(),
+                "rng": self.model.get_rng_state()}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.m.copy_(sd["exp_avg"])
+        self.v.copy_(sd["exp_avg_sq"])
+        self.model.set_rng_state(sd["rng"])
 
     def step(self, in0, in1=None, in2=None, eps=None, dropout=None, before_adam=None):
         """One optimisation step on a batch; returns device float64 sums (sum sq audio err, sum sq text err,

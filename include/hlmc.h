@@ -305,6 +305,21 @@ int hlmc_op_convT_c1(void* stream, int dtype, const void* x, int B, int Hi, int 
                      const float* bias, float* y);
 int hlmc_op_wgrad_c1(void* stream, int dtype, const void* L, int B, int Hl, int Wl, int M, const float* Xh,
                      float* dW, void* ws, int64_t ws_bytes);
+/* The train-mode forward of the LDS halo-tile conv (kind 0: conv_s2) / sub-pixel conv (kind 1: subpixel), bf16, at
+ * the shapes where hlmc_net_forward runs them (conv Ci 32 -> Co 64 at Wi 64, Ci 64 -> 128 at Wi 32; sub-pixel
+ * Ci 64 -> 32 at Wi 32, Ci 128 -> 64 at Wi 16), as the engine launches them:
+ *   - out_sums (device f64 [2 Co]) = (sum_rows y | sum_rows y^2) of the stored bf16 output, from the epilogue's exact
+ *     statistics accumulator (the next BatchNorm's batch statistics; src/Convolutional_VAE.py:80-100, 124-139);
+ *   - gamma != NULL: x is the PRE-BatchNorm map of the layer below; its train-mode BatchNorm2d (batch statistics,
+ *     biased variance, eps) + LeakyReLU(0.01) is applied while the input is staged.  mean_out / invstd_out [Ci]
+ *     receive the batch statistics, running_mean / running_var / num_batches_tracked (nullable) are updated as
+ *     torch does (momentum, unbiased variance), a_out [B,Hi,Wi,Ci] bf16 receives the activation.
+ * ws: hlmc_op_halo_workspace(Ci, Co) bytes.  Returns an error for any other shape. */
+int64_t hlmc_op_halo_workspace(int Ci, int Co);
+int hlmc_op_halo_fwd(void* stream, int kind, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
+                     const float* bias, int Co, void* y, double* out_sums, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum, float eps,
+                     float* mean_out, float* invstd_out, void* a_out, void* ws, int64_t ws_bytes);
 
 #ifdef __cplusplus
 }

@@ -362,3 +362,95 @@ def test_device_randn_matches_philox_restatement(cuda):
     torch.testing.assert_close(z.cpu(), mu.cpu() + eps * torch.exp(0.5 * lv.cpu()), rtol=1e-5, atol=1e-5)
     L.check(L.lib().hlmc_net_get_rng(net.h, C.byref(seed), C.byref(off)))
     assert off.value == 6 * 32
+
+
+# The four LDS halo-tile shapes of the B = 256 bench step, through hlmc_op_halo_fwd: the train-mode forward as the
+# engine launches it — epilogue statistics accumulated per lane over all of a persistent block's tiles (8 tiles per
+# block at these shapes) and, with bn_in, the layer below's BatchNorm + LeakyReLU applied while the input is staged
+# (BnInput; src/Convolutional_VAE.py:80-100 encoder, :124-139 decoder).  Checked:
+#   * output vs CPU float32 conv of the bf16 operands (the kernel's own activation a_out as input): rel L2 <= 3e-3;
+#   * out_sums vs the float64 sums of the kernel's own bf16 output: rel <= 1e-9 (exact accumulator, f64 order only);
+#   * bn_in: batch mean / invstd vs float64 statistics of the input <= 1e-6 rel; running statistics as torch's
+#     BatchNorm2d(momentum 0.1) updates them; num_batches_tracked 1; a_out = bf16(LeakyReLU((x - mean) * invstd *
+#     gamma + beta)) within one bf16 ulp, <= 0.1 % of elements off by that ulp (fp32 contraction order).
+HALO = [(0, 64, 64, 32, 64), (0, 32, 32, 64, 128), (1, 32, 32, 64, 32), (1, 16, 16, 128, 64)]
+
+
+@pytest.mark.parametrize("bn_in", [False, True], ids=["stats", "bn_in+stats"])
+@pytest.mark.parametrize("kind,Hi,Wi,Ci,Co", HALO)
+def test_halo_fwd_bn_stats_bench_shapes(cuda, kind, Hi, Wi, Ci, Co, bn_in):
+    g = torch.Generator().manual_seed(kind * 100 + Hi + Ci + int(bn_in))
+    shift, scale = torch.randn(Ci, generator=g) * 0.5, torch.rand(Ci, generator=g) + 0.5
+    yin = (torch.randn(BB, Hi, Wi, Ci, generator=g) * scale + shift).to(torch.bfloat16)
+    if kind == 0:
+        w = (torch.randn(Co, Ci, 3, 3, generator=g) / (3 * Ci ** 0.5)).to(torch.bfloat16)
+        wp = w.permute(0, 2, 3, 1).contiguous()
+        oshape = (BB, Hi // 2, Wi // 2, Co)
+    else:
+        w = (torch.randn(Ci, Co, 3, 3, generator=g) / (3 * Ci ** 0.5)).to(torch.bfloat16)
+        wp = w.permute(1, 2, 3, 0).contiguous()
+        oshape = (BB, 2 * Hi, 2 * Wi, Co)
+    b = torch.randn(Co, generator=g) * 0.1
+    gamma, beta = 1 + 0.1 * torch.randn(Ci, generator=g), 0.1 * torch.randn(Ci, generator=g)
+    rm0, rv0 = 0.1 * torch.randn(Ci, generator=g), 1 + 0.1 * torch.rand(Ci, generator=g)
+    d = {k: v.to(cuda).contiguous() for k, v in dict(yin=yin, wp=wp, b=b, gamma=gamma, beta=beta, rm=rm0.clone(),
+                                                     rv=rv0.clone()).items()}
+    nbt = torch.zeros(1, dtype=torch.int64, device=cuda)
+    mean_o, inv_o = torch.empty(Ci, device=cuda), torch.empty(Ci, device=cuda)
+    a_out = torch.empty(BB, Hi, Wi, Ci, dtype=torch.bfloat16, device=cuda)
+    y = torch.empty(*oshape, dtype=torch.bfloat16, device=cuda)
+    sums = torch.empty(2 * Co, dtype=torch.float64, device=cuda)
+    wsb = int(L.lib().hlmc_op_halo_workspace(Ci, Co))
+    hws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+    P = L.ptr
+    L.check(L.lib().hlmc_op_halo_fwd(L.stream(), kind, P(d["yin"]), BB, Hi, Wi, Ci, P(d["wp"]), P(d["b"]), Co, P(y),
+                                     P(sums), P(d["gamma"]) if bn_in else None, P(d["beta"]) if bn_in else None,
+                                     P(d["rm"]), P(d["rv"]), P(nbt), 0.1, 1e-5, P(mean_o), P(inv_o), P(a_out),
+                                     P(hws), wsb), "hlmc_op_halo_fwd")
+    torch.cuda.synchronize()
+    inp = yin
+    if bn_in:
+        y64 = yin.double().reshape(-1, Ci)
+        m64, v64 = y64.mean(0), y64.var(0, unbiased=False)
+        e_mean = float(((mean_o.cpu().double() - m64).abs() / (v64.sqrt())).max())
+        e_inv = float(((inv_o.cpu().double() - 1 / (v64 + 1e-5).sqrt()).abs() * (v64 + 1e-5).sqrt()).max())
+        assert e_mean < 1e-6 and e_inv < 1e-6, (e_mean, e_inv)
+        n = y64.shape[0]
+        torch.testing.assert_close(d["rm"].cpu().double(), 0.9 * rm0.double() + 0.1 * m64, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(d["rv"].cpu().double(), 0.9 * rv0.double() + 0.1 * v64 * n / (n - 1), rtol=1e-6,
+                                   atol=1e-7)
+        assert int(nbt.item()) == 1
+        z = (yin.float() - mean_o.cpu()) * inv_o.cpu() * gamma + beta
+        a_ref = torch.nn.functional.leaky_relu(z, 0.01).to(torch.bfloat16)
+        got = a_out.cpu()
+        diff = (got.float() - a_ref.float()).abs()
+        ulp = a_ref.float().abs().clamp_min(1e-30) * 2.0 ** -7
+        frac_off = float((diff > 0).float().mean())
+        print(f"halo bn_in {Hi}x{Wi} {Ci}->{Co}: mean {e_mean:.1e} invstd {e_inv:.1e}, a_out off-by-ulp {frac_off:.1e}")
+        assert bool((diff <= ulp).all()) and frac_off <= 1e-3
+        inp = got
+    else:
+        assert torch.equal(d["rm"].cpu(), rm0) and int(nbt.item()) == 0   # untouched without gamma
+    x = inp.float().permute(0, 3, 1, 2)
+    if kind == 0:
+        ref = F.conv2d(x, w.float(), b, stride=2, padding=1)
+    else:
+        ref = F.conv_transpose2d(x, w.float(), b, stride=2, padding=1, output_padding=1)
+    ref = ref.permute(0, 2, 3, 1)
+    e = rel(y, ref)
+    yo = y.cpu().double().reshape(-1, Co)
+    s_ref = torch.cat([yo.sum(0), (yo * yo).sum(0)])
+    e_s = float(((sums.cpu() - s_ref).abs() / s_ref.abs().clamp_min(1e-300)).max())
+    # the first moment can cancel: bound it by the sum of |y| instead
+    e_s1 = float(((sums.cpu()[:Co] - s_ref[:Co]).abs() / yo.abs().sum(0)).max())
+    e_s2 = float(((sums.cpu()[Co:] - s_ref[Co:]).abs() / s_ref[Co:]).max())
+    print(f"halo kind {kind} {Hi}x{Wi} {Ci}->{Co} bn_in={bn_in}: rel L2 {e:.2e}, stats {e_s1:.1e} / {e_s2:.1e}")
+    assert e < 3e-3 and e_s1 < 1e-9 and e_s2 < 1e-9
+
+
+def test_halo_fwd_rejects_other_shapes(cuda):
+    ws_ = torch.empty(1 << 20, dtype=torch.uint8, device=cuda)
+    st = L.lib().hlmc_op_halo_fwd(L.stream(), 0, ws_.data_ptr(), 4, 8, 8, 256, ws_.data_ptr(), None, 512,
+                                  ws_.data_ptr(), ws_.data_ptr(), None, None, None, None, None, 0.1, 1e-5, None, None,
+                                  None, ws_.data_ptr(), 1 << 20)
+    assert st != 0 and b"halo" in L.lib().hlmc_last_error()

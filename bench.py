@@ -548,7 +548,7 @@ def main():
             rec["roofline"] = roof
         if extras:
             rec["extras"] = extras
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the host cores' baseline: rank 0 at N = 1 only
             rec["cpu_baseline"] = cpu_baseline()
         print(json.dumps(rec), flush=True)
     if dist:

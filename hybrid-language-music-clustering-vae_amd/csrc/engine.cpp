@@ -147,10 +147,18 @@ class NetT : public NetBase {
     // backward moments and bias column sums in the next; zeroed by one memset per train forward (and by backward
     // when it runs again without a forward in between)
     size_t xf_total = 0, xb_total = 0, xf_base = 0, xb_base = 0;
+    // split-K arrival counters of the in-launch combine (gemm.hpp SplitFix), kFixCnt per stream, directly after the
+    // accumulators: zeroed with them (train) or alone (other forwards); every combining block resets its own
+    static constexpr int kFixCnt = 4096;
+    size_t cnt_base = 0;
     bool bwd_acc_clean = false;
     int zero_acc_fwd(hipStream_t s) {
-        if (xf_total + xb_total) HLMC_HIP(hipMemsetAsync(ws + xf_base, 0, xf_total + xb_total, s));
+        HLMC_HIP(hipMemsetAsync(ws + xf_base, 0, cnt_base + 2 * kFixCnt * 4 - xf_base, s));
         bwd_acc_clean = true;
+        return HLMC_OK;
+    }
+    int zero_fix_counters(hipStream_t s) {
+        HLMC_HIP(hipMemsetAsync(ws + cnt_base, 0, 2 * kFixCnt * 4, s));
         return HLMC_OK;
     }
     int zero_acc_bwd(hipStream_t s) {
@@ -168,8 +176,9 @@ class NetT : public NetBase {
             plan(A, B);
             scratch_off = A.take(scratch_bytes + 256);
             scratch2_off = A.take(scratch_bytes + 256);
-            xf_base = A.take(xf_total);  // xb directly after xf (one memset covers both: 256-aligned sizes)
+            xf_base = A.take(xf_total);  // xb and the counters directly after xf (one memset: 256-aligned sizes)
             xb_base = A.take(xb_total);
+            cnt_base = A.take(2 * kFixCnt * 4);
             ws_total = A.used;
             planned_B = B;
         }
@@ -177,8 +186,9 @@ class NetT : public NetBase {
     }
     void set_ws(void* w) {
         ws = reinterpret_cast<char*>(w);
-        scratch = Ws{reinterpret_cast<float*>(ws + scratch_off), scratch_bytes + 256};
-        scratch2 = Ws{reinterpret_cast<float*>(ws + scratch2_off), scratch_bytes + 256};
+        unsigned* cnt = reinterpret_cast<unsigned*>(ws + cnt_base);
+        scratch = Ws{reinterpret_cast<float*>(ws + scratch_off), scratch_bytes + 256, cnt, kFixCnt};
+        scratch2 = Ws{reinterpret_cast<float*>(ws + scratch2_off), scratch_bytes + 256, cnt + kFixCnt, kFixCnt};
     }
 
     // ---------------------------------------------------------------- weight-gradient stream
@@ -875,7 +885,7 @@ class HybridNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
+        HLMC_TRY(a.train ? this->zero_acc_fwd(s) : this->zero_fix_counters(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z), src/Convolutional_VAE.py:167-179
             HLMC_CHECK_ARG(a.in0 && a.recon, "z and recon required");
@@ -1065,7 +1075,7 @@ class CvaeNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
+        HLMC_TRY(a.train ? this->zero_acc_fwd(s) : this->zero_fix_counters(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z, condition), src/Conditional_VAE.py:206-225
             HLMC_CHECK_ARG(a.in0 && a.in2 && a.recon && a.recon_text, "z / condition / recon / recon_text required");
@@ -1260,7 +1270,7 @@ class SimpleNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
+        HLMC_TRY(a.train ? this->zero_acc_fwd(s) : this->zero_fix_counters(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z), src/Simple_VAE.py:95-96 (decoder blocks' dropout from the same mask layout)
             HLMC_CHECK_ARG(a.in0 && a.recon, "z and recon required");

@@ -109,20 +109,28 @@ inline bool use_ploop(int phases, int tmn, int pipe, bool with_stats) {
 // strides: the conv / sub-pixel NHWC outputs and their split-K slabs), else the per-element epilogue (linears)
 template <typename T, int BM, int BN, int WM, int WN, bool TR, class AL, class BL, class E>
 void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
-                         bool long_k, int pipe) {
+                         bool long_k, int pipe, SplitFix fx = SplitFix{}) {
     const int rm = xcd_remap_for_site();
-    const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe, E::kStatMode == 1) ? (int)grid.y : 1;
+    const int ploop = (fx.S <= 1 && use_ploop((int)grid.y, (int)grid.x, pipe, E::kStatMode == 1)) ? (int)grid.y : 1;
     if (ploop > 1) grid.y = 1;
     HLMC_PROBE_BEGIN(s);
     if (pipe == 3)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, fx);
     else if (pipe == 4)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, fx);
     else if (long_k)
-        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop, fx);
     else
-        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop, fx);
     HLMC_PROBE_END(s);
+}
+// HLMC_SPLITK_FIX=0: split-K launches keep the separate reduce launch (A/B measurement aid)
+inline bool splitk_fix_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("HLMC_SPLITK_FIX");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 // HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid).  Measured per layer
 // (scripts/bench_gemm.py, round 3): the transposed epilogue takes the split-K / LDS-DMA conv and sub-pixel GEMMs from
@@ -164,6 +172,22 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     }
     size_t need = (size_t)phases * pl.S * M * N * sizeof(float);
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "split-K workspace too small");
+    if (splitk_fix_enabled() && ws.cnt && (int64_t)tmn * phases <= ws.ncnt && need < 0x80000000ull) {
+        // in-launch combine (gemm.hpp SplitFix): the tile's last block reduces the slabs and runs the final epilogue
+        const SplitFix fx{ws.p, ws.cnt, (unsigned)need, pl.S};
+        if (stats) {
+            WithStats<EP> eps;
+            static_cast<EP&>(eps) = ep;
+            eps.acc = st->acc;
+            nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, eps, M, N, pl.ksl, long_k, pipe, fx);
+            HLMC_LAUNCHED();
+            st->done = true;
+            return HLMC_OK;
+        }
+        nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, ep, M, N, pl.ksl, long_k, pipe, fx);
+        HLMC_LAUNCHED();
+        return HLMC_OK;
+    }
     StorePartialZ part;
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
     nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe);

@@ -8,6 +8,10 @@ namespace hlmc {
 struct Ws {  // split-K / reduction scratch handed down by the caller
     float* p;
     size_t bytes;
+    // in-launch split-K combine (gemm.hpp SplitFix): ncnt arrival counters, zero on entry to every launch that uses
+    // them (each combining block resets its own); nullptr = a separate reduce launch
+    unsigned* cnt = nullptr;
+    int ncnt = 0;
 };
 
 namespace ops {

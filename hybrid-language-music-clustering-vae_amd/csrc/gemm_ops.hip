@@ -124,13 +124,16 @@ void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, c
         gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop, fx);
     HLMC_PROBE_END(s);
 }
-// HLMC_SPLITK_FIX=0: split-K launches keep the separate reduce launch (A/B measurement aid)
-inline bool splitk_fix_enabled() {
-    static const bool on = [] {
+// In-launch split-K combine (gemm.hpp SplitFix) where S x tile bytes <= HLMC_SPLITK_FIX KiB; default 0 = never.
+// Measured (round 4, bench_gemm.py and 3 alternating bench rounds): 128 x 128 tiles at S = 4 (256 KiB) +3 us and at
+// S = 15 (960 KiB) +20 us per layer against the separate reduce launch (the combining block reads the partials
+// serially); step 122.1k / 122.8k / 122.4k clips/s at 128 / 64 / 256 KiB against 123.4k with the reduce launches.
+inline int splitk_fix_max_kib() {
+    static const int kib = [] {
         const char* e = std::getenv("HLMC_SPLITK_FIX");
-        return !(e && e[0] == '0');
+        return e ? std::atoi(e) : 0;
     }();
-    return on;
+    return kib;
 }
 // HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid).  Measured per layer
 // (scripts/bench_gemm.py, round 3): the transposed epilogue takes the split-K / LDS-DMA conv and sub-pixel GEMMs from
@@ -172,7 +175,8 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     }
     size_t need = (size_t)phases * pl.S * M * N * sizeof(float);
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "split-K workspace too small");
-    if (splitk_fix_enabled() && ws.cnt && (int64_t)tmn * phases <= ws.ncnt && need < 0x80000000ull) {
+    if (ws.cnt && (int64_t)pl.S * BM * BN * 4 <= (int64_t)splitk_fix_max_kib() * 1024 &&
+        (int64_t)tmn * phases <= ws.ncnt && need < 0x80000000ull) {
         // in-launch combine (gemm.hpp SplitFix): the tile's last block reduces the slabs and runs the final epilogue
         const SplitFix fx{ws.p, ws.cnt, (unsigned)need, pl.S};
         if (stats) {
@@ -832,6 +836,112 @@ __global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restri
     }
 }
 
+
+// ---- weight gradient of a stride-2 3x3 conv over LDS halo tiles (the 32 / 64-channel layers whose reductions run
+// over 65k-262k pixels): dW[m][ci][tap] = sum_{b,r,c} L[b,r,c,m] Xh[b, 2r-1+kh, 2c-1+kw, ci] (zero outside Xh).
+// A persistent block owns tiles of ROWS low-res rows x WL columns (TP = 128 pixels = the tile's K) and keeps its
+// whole M x 9C partial in registers over all its tiles: per tile it stages L's rows [TP][M] and Xh's halo rows
+// [2 ROWS + 1][2 WL + 1][C] (column 0 = input column -1, zero) in LDS once, and reads both MFMA operands with
+// transposed LDS reads (ds_read_b64_tr_b16: pixels are the k dimension) -- no im2col gather, no per-K-step slab.
+// The next tile's rows are loaded into registers during the MFMAs.  Each block writes one fp32 partial slab
+// ws[blockIdx.x][m][tap * C + ci]; reduce_splits sums them in block order (deterministic) into the torch layout.
+// Waves: 2 (M halves) x 2 (N halves of 9 x 16 columns).
+template <int M, int C, int WL, int ROWS>
+__global__ __launch_bounds__(256) void wgrad_halo_kernel(const bf16* __restrict__ L, const bf16* __restrict__ Xh, int Hl,
+                                                         int ntiles, float* __restrict__ ws) {
+    constexpr int TP = ROWS * WL, N = 9 * C, HR = 2 * ROWS + 1, HC = 2 * WL + 1;
+    constexpr int PSL = M + 8, PSX = C + 8;     // LDS pixel pitches (bf16): 144 / 80 bytes
+    constexpr int CPX = C / 8, CPL = M / 8;     // 16-byte chunks per pixel
+    constexpr int LCH = TP * CPL / 256;         // L chunks per thread per tile
+    static_assert(2 * WL * CPX == 256 && TP == 128 && WL == 32 && LCH * 256 == TP * CPL, "halo chunk maps");
+    static_assert(M == 64 && N % 32 == 0, "2 x 2 waves of 32 rows x N / 2 columns");
+    constexpr int NB = N / 32;                  // 16-column blocks per wave (9 for C = 32)
+    __shared__ __attribute__((aligned(16))) bf16 Ls[TP * PSL];
+    __shared__ __attribute__((aligned(16))) bf16 Xs[HR * HC * PSX];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int tpi = Hl / ROWS;
+    const int Hh = 2 * Hl, Wh = 2 * WL;
+    for (int c = tid; c < HR * CPX; c += 256) {  // input column -1: zero for every tile
+        const int u = c / CPX, q = c - u * CPX;
+        *reinterpret_cast<uint4*>(&Xs[(u * HC) * PSX + q * 8]) = make_uint4(0, 0, 0, 0);
+    }
+    uint4 xr[HR], lr[LCH];
+    const int xcol = tid / CPX, xq = tid % CPX;
+    auto load = [&](int t) {  // unconditional (row -1 clamped to row 0, zeroed when staged)
+        const int b = t / tpi, r0 = (t - b * tpi) * ROWS;
+#pragma unroll
+        for (int u = 0; u < HR; ++u) {
+            const int ih = 2 * r0 - 1 + u;
+            xr[u] = *reinterpret_cast<const uint4*>(Xh + (((int64_t)b * Hh + (ih < 0 ? 0 : ih)) * Wh + xcol) * C + xq * 8);
+        }
+        const bf16* lt = L + ((int64_t)b * Hl + r0) * WL * M;  // the tile's TP x M block is contiguous
+#pragma unroll
+        for (int i = 0; i < LCH; ++i) lr[i] = *reinterpret_cast<const uint4*>(lt + (int64_t)(tid + 256 * i) * 8);
+    };
+    auto stage = [&](int t) {
+        const bool top = (t % tpi) == 0;
+#pragma unroll
+        for (int u = 0; u < HR; ++u)
+            *reinterpret_cast<uint4*>(&Xs[(u * HC + xcol + 1) * PSX + xq * 8]) = (u == 0 && top) ? make_uint4(0, 0, 0, 0) : xr[u];
+#pragma unroll
+        for (int i = 0; i < LCH; ++i) {
+            const int c = tid + 256 * i, px = c / CPL, q = c - px * CPL;
+            *reinterpret_cast<uint4*>(&Ls[px * PSL + q * 8]) = lr[i];
+        }
+    };
+    f32x4_t acc[2][NB];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    int t = blockIdx.x;
+    if (t < ntiles) {
+        load(t);
+        stage(t);
+    }
+    __syncthreads();
+    for (; t < ntiles; t += gridDim.x) {
+        load(min(t + (int)gridDim.x, ntiles - 1));  // next tile in flight during the MFMAs (unconditional)
+#pragma unroll
+        for (int ks = 0; ks < ROWS; ++ks) {  // one low-res row (32 pixels) per 32-deep K-step
+            bf16x8_t af[2], bfr[NB];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const bf16* a = Ls + (32 * ks + 8 * g + q) * PSL + wm * 32 + i * 16 + 4 * p;
+                const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)a);
+                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(a + 4 * PSL));
+                af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+                const int n0 = (wn * NB + j) * 16, tap = n0 / C, ci0 = n0 % C, kh = tap / 3, kw = tap % 3;
+                // pixel (row ks, column 8 g + q) -> halo (2 ks + kh, 2 (8 g + q) + kw); the hi half is 4 columns on
+                const bf16* x = Xs + ((2 * ks + kh) * HC + 2 * (8 * g + q) + kw) * PSX + ci0 + 4 * p;
+                const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)x);
+                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(x + 8 * PSX));
+                bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < NB; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();  // every wave is done with this tile's images
+        if (t + (int)gridDim.x < ntiles) stage(t + (int)gridDim.x);
+        __syncthreads();
+    }
+    float* slab = ws + (int64_t)blockIdx.x * M * N;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                slab[(int64_t)(wm * 32 + i * 16 + 4 * g + r) * N + (wn * NB + j) * 16 + li] = acc[i][j][r];
+}
 }  // namespace
 
 namespace ops {
@@ -868,6 +978,20 @@ inline bool conv_halo_on(int which) {  // HLMC_CONV_HALO=0 / HLMC_CONV_HALO2=0: 
 inline bool sp_halo_on(int which) {  // HLMC_SP_HALO=0 / HLMC_SP_HALO2=0
     static const bool h1 = env_on("HLMC_SP_HALO"), h2 = env_on("HLMC_SP_HALO2");
     return which == 1 ? h1 : which == 2 ? h2 : false;
+}
+// the LDS halo-tile weight gradient (wgrad_halo_kernel): the 32 x 32 low-res, M = 64, C = 32 shape (encoder layer 2,
+// the decoder's layer-4 transposed conv).  HLMC_WGRAD_HALO=0: the split-K TN GEMM (A/B aid); HLMC_WGRAD_HALO_BLOCKS:
+// persistent grid size (default 256)
+inline bool wgrad_halo_shape(int Hl, int Wl, int M, int C) {
+    static const bool on = env_on("HLMC_WGRAD_HALO");
+    return on && Wl == 32 && M == 64 && C == 32 && Hl % 4 == 0;
+}
+inline int wgrad_halo_blocks() {
+    static const int n = [] {
+        const char* e = std::getenv("HLMC_WGRAD_HALO_BLOCKS");
+        return e ? std::max(8, std::atoi(e)) : 256;
+    }();
+    return n;
 }
 template <typename T>
 bool conv_s2_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co) {
@@ -1006,11 +1130,28 @@ int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* X
     StoreWgradConv ep{dW, C, bias_acc, dbias};
     probe::site(probe::kWgradS2, 2.0 * M * N * K,
                 (double)sizeof(T) * ((double)K * M + 4.0 * K * C) + 4.0 * M * N);
+    if constexpr (std::is_same<T, bf16>::value) {
+        if (wgrad_halo_shape(Hl, Wl, M, C)) {
+            const int ntiles = B * Hl / 4, grid = std::min(ntiles, wgrad_halo_blocks());
+            HLMC_CHECK_ARG(ws.p && ws.bytes >= (size_t)grid * M * N * sizeof(float), "wgrad workspace too small");
+            HLMC_CHECK_ARG(aligned16(L) && aligned16(Xh), "wgrad_s2: 16-byte alignment");
+            HLMC_PROBE_BEGIN(s);
+            wgrad_halo_kernel<64, 32, 32, 4><<<grid, 256, 0, s>>>(L, Xh, Hl, ntiles, ws.p);
+            HLMC_PROBE_END(s);
+            HLMC_LAUNCHED();
+            reduce_splits(s, ws.p, ep, M, N, grid);
+            HLMC_LAUNCHED();
+            return HLMC_OK;
+        }
+    }
     return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
 }
 template <typename T>
 size_t wgrad_s2_ws(int B, int Hl, int Wl, int M, int C) {
-    return dispatch_tn_ws<T>(M, 9 * C, B * Hl * Wl);
+    size_t w = dispatch_tn_ws<T>(M, 9 * C, B * Hl * Wl);
+    if (std::is_same<T, bf16>::value && wgrad_halo_shape(Hl, Wl, M, C))
+        w = std::max(w, (size_t)std::min(B * Hl / 4, wgrad_halo_blocks()) * M * 9 * C * sizeof(float));
+    return w;
 }
 
 template <typename T, typename OutT>

@@ -80,9 +80,12 @@ def test_subpixel_convT(cuda, ws, dt, B, Hi, Wi, Ci, Co):
 
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 @pytest.mark.parametrize("B,Hl,Wl,M,C", [(2, 8, 8, 64, 32), (2, 4, 4, 128, 64), (2, 2, 2, 512, 256),
-                                        (3, 1, 1, 512, 512), (2, 16, 16, 32, 64), (4, 2, 8, 256, 128)])
+                                        (3, 1, 1, 512, 512), (2, 16, 16, 32, 64), (4, 2, 8, 256, 128),
+                                        (3, 8, 32, 64, 32), (1, 32, 32, 64, 32)])
 def test_wgrad_s2_conv(cuda, ws, dt, B, Hl, Wl, M, C):
-    """Conv2d weight gradient: L = dY (low-res, M=Co), Xh = X (high-res, C=Ci)."""
+    """Conv2d weight gradient: L = dY (low-res, M=Co), Xh = X (high-res, C=Ci).  (The Wl = 32, M = 64, C = 32 shapes
+    run the LDS halo-tile weight gradient in bf16: 6 / 8 tiles, fewer than the persistent grid; the B = 256 bench
+    shape is test_wgrad_s2_bench_shapes_bf16.)"""
     code, tdt, tol = DT[dt]
     g = torch.Generator().manual_seed(M + C + B)
     dy = torch.randn(B, Hl, Wl, M, generator=g)

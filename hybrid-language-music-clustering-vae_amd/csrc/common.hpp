@@ -166,13 +166,20 @@ struct XAcc {
 inline int xacc_shards(int C) { return C >= 512 ? 2 : C >= 256 ? 4 : C >= 128 ? 8 : 16; }
 constexpr int kXAccMaxShards = 16;
 
+// A non-finite partial (NaN, inf, or beyond the +-4e18 range the integer word holds) sets bit 63 of the shard's
+// third word instead (sticky: that word's adds total < 2^48, so no add reaches bit 63); the readers below return NaN
+// for such a column, as torch's statistics of a diverged run would be, instead of finite garbage.
+constexpr unsigned long long kXAccBad = 1ull << 63;
 __device__ __forceinline__ void xacc_add_shard(const XAcc& x, int shard, int col, double v) {
-    v = fmin(fmax(v, -4.0e18), 4.0e18);
+    unsigned long long* b = x.p + (size_t)shard * 3 * x.ncols + col;
+    if (!(fabs(v) <= 4.0e18)) {
+        atomicOr(b + 2 * x.ncols, kXAccBad);
+        return;
+    }
     const double f = floor(v);
     const double r1 = (v - f) * 4294967296.0;  // exact: v - floor(v) and power-of-two scales
     const double g = floor(r1);
     const double r2 = (r1 - g) * 4294967296.0;
-    unsigned long long* b = x.p + (size_t)shard * 3 * x.ncols + col;
     atomicAdd(b, (unsigned long long)(long long)f);
     atomicAdd(b + x.ncols, (unsigned long long)(long long)g);
     atomicAdd(b + 2 * x.ncols, (unsigned long long)(long long)floor(r2));
@@ -186,13 +193,15 @@ __device__ __forceinline__ double xacc_value(long long a, long long b, long long
 // column c of an exact accumulator, summed over its shards (one thread)
 __device__ __forceinline__ double xacc_column(const XAcc& acc, int c) {
     long long a = 0, b = 0, d = 0;
+    unsigned long long bad = 0;
     for (int sh = 0; sh < acc.shards; ++sh) {
         const unsigned long long* q = acc.p + (size_t)sh * 3 * acc.ncols + c;
         a += (long long)q[0];
         b += (long long)q[acc.ncols];
-        d += (long long)q[2 * acc.ncols];
+        bad |= q[2 * acc.ncols] & kXAccBad;
+        d += (long long)(q[2 * acc.ncols] & ~kXAccBad);
     }
-    return xacc_value(a, b, d);
+    return bad ? __builtin_nan("") : xacc_value(a, b, d);
 }
 // out[c] (LDS, c < ncols) = the accumulator's column totals; every thread of the block calls it (blockDim.x == NT);
 // red: LDS scratch of >= 3 * NT int64 (used when ncols < NT).  Thread (column c, shard group g) issues the loads of
@@ -202,6 +211,8 @@ __device__ __forceinline__ void xacc_fold(const XAcc& x, double* out, long long*
     constexpr int K = 8;  // shards per thread group (shards <= K * G, checked by the launchers via xacc_shards)
     const int tid = threadIdx.x, n = x.ncols, S = x.shards;
     const int G = n >= NT ? 1 : NT / n;
+    // the third word's bad bit (xacc_add_shard) rides along as bit 63 of the group's d total: the d words' adds total
+    // < 2^48, so the masked sum never reaches it and OR-ing the flags back in keeps it
     auto sum = [&](int c, int g, long long& a, long long& b, long long& d) {
         unsigned long long w0[K], w1[K], w2[K];
 #pragma unroll
@@ -213,19 +224,25 @@ __device__ __forceinline__ void xacc_fold(const XAcc& x, double* out, long long*
             w2[k] = q[2 * n];
         }
         a = b = d = 0;
+        unsigned long long bad = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (g + k * G < S) {
                 a += (long long)w0[k];
                 b += (long long)w1[k];
-                d += (long long)w2[k];
+                bad |= w2[k] & kXAccBad;
+                d += (long long)(w2[k] & ~kXAccBad);
             }
+        d = (long long)((unsigned long long)d | bad);
+    };
+    auto value = [](long long a, long long b, long long d) {
+        return ((unsigned long long)d & kXAccBad) ? __builtin_nan("") : xacc_value(a, b, d);
     };
     if (n >= NT) {
         for (int c = tid; c < n; c += NT) {
             long long a, b, d;
             sum(c, 0, a, b, d);
-            out[c] = xacc_value(a, b, d);
+            out[c] = value(a, b, d);
         }
     } else {
         const int c = tid % n, g = tid / n;
@@ -236,12 +253,16 @@ __device__ __forceinline__ void xacc_fold(const XAcc& x, double* out, long long*
         red[2 * NT + tid] = d;
         __syncthreads();
         if (tid < n) {
+            unsigned long long bad = (unsigned long long)d & kXAccBad;
+            d = (long long)((unsigned long long)d & ~kXAccBad);
             for (int k = 1; k < G; ++k) {
                 a += red[k * n + tid];
                 b += red[NT + k * n + tid];
-                d += red[2 * NT + k * n + tid];
+                const unsigned long long dk = (unsigned long long)red[2 * NT + k * n + tid];
+                bad |= dk & kXAccBad;
+                d += (long long)(dk & ~kXAccBad);
             }
-            out[tid] = xacc_value(a, b, d);
+            out[tid] = bad ? __builtin_nan("") : xacc_value(a, b, d);
         }
     }
     __syncthreads();

@@ -850,7 +850,10 @@ template <int M, int C, int WL, int ROWS>
 __global__ __launch_bounds__(256) void wgrad_halo_kernel(const bf16* __restrict__ L, const bf16* __restrict__ Xh, int Hl,
                                                          int ntiles, float* __restrict__ ws) {
     constexpr int TP = ROWS * WL, N = 9 * C, HR = 2 * ROWS + 1, HC = 2 * WL + 1;
-    constexpr int PSL = M + 8, PSX = C + 8;     // LDS pixel pitches (bf16): 144 / 80 bytes
+    // LDS pixel pitches (bf16): 160 / 80 bytes.  A transposed read (one 32-lane half) takes 8 rows of 32 bytes: with
+    // the k-order below those are 8 consecutive L pixels (160-byte pitch) or 8 Xh pixels 2 apart (160 bytes): bank
+    // offsets 40 c mod 64 -> 8 disjoint 8-bank spans, conflict-free
+    constexpr int PSL = M + 16, PSX = C + 8;
     constexpr int CPX = C / 8, CPL = M / 8;     // 16-byte chunks per pixel
     constexpr int LCH = TP * CPL / 256;         // L chunks per thread per tile
     static_assert(2 * WL * CPX == 256 && TP == 128 && WL == 32 && LCH * 256 == TP * CPL, "halo chunk maps");
@@ -896,6 +899,10 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(const bf16* __restrict_
 #pragma unroll
         for (int j = 0; j < NB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+    // k-order of a 32-pixel K-step (any bijection serves both operands): lane group g's k = 8 g + j holds pixel
+    // column 16 (g >> 1) + 8 (j >> 2) + 4 (g & 1) + (j & 3), so each 32-lane half's lo / hi read covers 8
+    // consecutive pixels
+    const int cc = 16 * (g >> 1) + 4 * (g & 1) + q;  // lo rows; hi rows are cc + 8
     int t = blockIdx.x;
     if (t < ntiles) {
         load(t);
@@ -909,18 +916,18 @@ __global__ __launch_bounds__(256) void wgrad_halo_kernel(const bf16* __restrict_
             bf16x8_t af[2], bfr[NB];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const bf16* a = Ls + (32 * ks + 8 * g + q) * PSL + wm * 32 + i * 16 + 4 * p;
+                const bf16* a = Ls + (32 * ks + cc) * PSL + wm * 32 + i * 16 + 4 * p;
                 const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)a);
-                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(a + 4 * PSL));
+                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(a + 8 * PSL));
                 af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             }
 #pragma unroll
             for (int j = 0; j < NB; ++j) {
                 const int n0 = (wn * NB + j) * 16, tap = n0 / C, ci0 = n0 % C, kh = tap / 3, kw = tap % 3;
-                // pixel (row ks, column 8 g + q) -> halo (2 ks + kh, 2 (8 g + q) + kw); the hi half is 4 columns on
-                const bf16* x = Xs + ((2 * ks + kh) * HC + 2 * (8 * g + q) + kw) * PSX + ci0 + 4 * p;
+                // pixel (row ks, column cc) -> halo (2 ks + kh, 2 cc + kw); the hi rows are 8 pixels = 16 columns on
+                const bf16* x = Xs + ((2 * ks + kh) * HC + 2 * cc + kw) * PSX + ci0 + 4 * p;
                 const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)x);
-                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(x + 8 * PSX));
+                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(x + 16 * PSX));
                 bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
             }
 #pragma unroll

@@ -457,3 +457,34 @@ def test_halo_fwd_rejects_other_shapes(cuda):
                                   ws_.data_ptr(), ws_.data_ptr(), None, None, None, None, None, 0.1, 1e-5, None, None,
                                   None, ws_.data_ptr(), 1 << 20)
     assert st != 0 and b"halo" in L.lib().hlmc_last_error()
+
+
+def test_halo_fwd_nan_propagates(cuda):
+    """A non-finite value reaching the exact statistics accumulators comes out as NaN (torch's BatchNorm of a diverged
+    run), not as finite garbage: one NaN in channel 3 of the pre-BN input -> that channel's batch mean / invstd /
+    running statistics NaN, every other input channel finite; the conv outputs next to it are NaN in every channel,
+    so every output column sum is NaN."""
+    B, Hi, Wi, Ci, Co = 2, 64, 64, 32, 64
+    g = torch.Generator().manual_seed(11)
+    yin = torch.randn(B, Hi, Wi, Ci, generator=g)
+    yin[1, 10, 20, 3] = float("nan")
+    yin = yin.to(torch.bfloat16).to(cuda)
+    wp = (torch.randn(Co, 3, 3, Ci, generator=g) / 30).to(torch.bfloat16).to(cuda)
+    gamma, beta = torch.ones(Ci, device=cuda), torch.zeros(Ci, device=cuda)
+    rm, rv = torch.zeros(Ci, device=cuda), torch.ones(Ci, device=cuda)
+    nbt = torch.zeros(1, dtype=torch.int64, device=cuda)
+    mean_o, inv_o = torch.empty(Ci, device=cuda), torch.empty(Ci, device=cuda)
+    a_out = torch.empty(B, Hi, Wi, Ci, dtype=torch.bfloat16, device=cuda)
+    y = torch.empty(B, Hi // 2, Wi // 2, Co, dtype=torch.bfloat16, device=cuda)
+    sums = torch.empty(2 * Co, dtype=torch.float64, device=cuda)
+    wsb = int(L.lib().hlmc_op_halo_workspace(Ci, Co))
+    hws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+    P = L.ptr
+    L.check(L.lib().hlmc_op_halo_fwd(L.stream(), 0, P(yin), B, Hi, Wi, Ci, P(wp), None, Co, P(y), P(sums), P(gamma),
+                                     P(beta), P(rm), P(rv), P(nbt), 0.1, 1e-5, P(mean_o), P(inv_o), P(a_out), P(hws), wsb))
+    torch.cuda.synchronize()
+    m = mean_o.cpu()
+    assert torch.isnan(m[3]) and torch.isnan(inv_o.cpu()[3]) and torch.isnan(rm.cpu()[3]) and torch.isnan(rv.cpu()[3])
+    others = torch.arange(Ci) != 3
+    assert torch.isfinite(m[others]).all() and torch.isfinite(rm.cpu()[others]).all()
+    assert torch.isnan(sums.cpu()).all()

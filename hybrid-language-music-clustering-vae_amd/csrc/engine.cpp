@@ -436,12 +436,12 @@ class NetT : public NetBase {
     // gradient: every fork puts an event marker on the main stream, measured as a ~10 us bubble)
     int bn_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const BnBufs& bb, int g, int beta,
                int act, const uint8_t* mask, float mscale, T* dy, int bias, const ops::BnBwdFuse* fused = nullptr,
-               bool bias_side = false, bool defer_bias = false) {
+               bool bias_side = false, bool defer_bias = false, const ops::Wc1Grad* wg = nullptr) {
         const bool on_side = bias >= 0 && use_side && bias_side;
         const XAcc bacc = bias >= 0 ? acc_bias(bb) : XAcc{};
         HLMC_TRY(ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask, mscale, dy,
                                     G[g], G[beta], acc_mom(bb), fused, bacc,
-                                    (bias >= 0 && !on_side) ? G[bias] : nullptr, AF(bb.sums)));
+                                    (bias >= 0 && !on_side) ? G[bias] : nullptr, AF(bb.sums), wg));
         if (on_side) {
             float* gb = G[bias];
             if (defer_bias)
@@ -471,6 +471,14 @@ class NetT : public NetBase {
             if (pb.gb) HLMC_TRY(ops::colsum_finalize(q, pb.acc, pb.C, pb.gb));
             return f(q, sc);
         }, side_batch());
+    }
+    // HLMC_WC1_FUSE=0: the encoder's first-layer weight gradient as its own launch reading the stored dy (A/B aid)
+    static bool wc1_fused() {
+        static const bool on = [] {
+            const char* e = std::getenv("HLMC_WC1_FUSE");
+            return !(e && e[0] == '0');
+        }();
+        return on;
     }
     // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
     static bool tail_on_main() {
@@ -514,6 +522,7 @@ class NetT : public NetBase {
                 need(ops::wgrad_s2_ws<T>((int)B, h / 2, w / 2, co, ci));
             } else {
                 need(ops::wgrad_c1_ws((int)B, h / 2, w / 2, co));
+                need((size_t)ops::bn_wc1_part_floats((int64_t)B * (h / 2) * (w / 2), co) * sizeof(float));
             }
             h /= 2;
             w /= 2;
@@ -575,9 +584,19 @@ class NetT : public NetBase {
             const int ho = hs[l + 1], wo = ws_[l + 1];
             const int64_t R = (int64_t)B * ho * wo;
             T* dy = AT(enc.dy[l]);
+            float* gw = G[enc.w[l]];
+            if (l == 0 && wc1_fused()) {
+                // the first conv's weight gradient inside its BatchNorm backward (ops::Wc1Grad): dy is never stored
+                ops::Wc1Grad wg;
+                wg.x = audio; wg.B = B; wg.Hl = ho; wg.Wl = wo; wg.dW = gw;
+                wg.part = scratch.p;
+                wg.part_floats = (int64_t)(scratch.bytes / sizeof(float));
+                HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy,
+                                enc.b[l], nullptr, false, false, &wg));  // (bias gradient finalized in there)
+                continue;
+            }
             HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
                             nullptr, true, true));
-            float* gw = G[enc.w[l]];
             if (l == 0 && tail_on_main()) {
                 // the last weight gradient of backward: on the main stream, which would otherwise only wait for
                 // the weight-gradient stream here (that stream is still reducing layer 1's gradient)

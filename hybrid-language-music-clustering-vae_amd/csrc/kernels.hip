@@ -384,7 +384,17 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(XAcc acc, int C, fl
 // kFin: sum dz / sum dz*xhat folded here from the moments' partial table (bn_fin_prologue; block 0 stores
 // dgamma / dbeta) instead of read from `sums`
 // (unconditional clamped loads and stores: bn_bwd_moments_kernel; a clamped row's store rewrites the same value)
-template <typename T, bool kMask, bool kFin, int ACT = -1>
+// kWc1 (the encoder's first BatchNorm layer, whose dy feeds only the single-channel input conv's weight gradient):
+// instead of storing dy, each thread accumulates that gradient's products dy[row][c] * x[tap of row] (the 9 f32 input
+// taps of the row's output pixel, prefetched with the row) and the block writes its [C x 9] partial to
+// wc.part[blockIdx.x] -- the wgrad_c1 launch and one write + read of dy are gone.
+struct Wc1 {
+    const float* x = nullptr;  // [B, 2 Hl, 2 Wl] single-channel input of the conv
+    int Hl = 0, Wl = 0;         // conv output (= this BatchNorm layer's) height / width
+    FastDiv dWl, dHl;
+    float* part = nullptr;      // [gridDim.x][C * 9] (co-major, tap minor: the torch [co][1][kh][kw] order)
+};
+template <typename T, bool kMask, bool kFin, int ACT = -1, bool kWc1 = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
                                                            int64_t R, int C, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -392,7 +402,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ beta, int act,
                                                            const uint8_t* __restrict__ mask, float mscale,
                                                            const float* __restrict__ sums, T* __restrict__ dy,
-                                                           int64_t rows_per_blk, XAcc bias_acc, BnFin fin) {
+                                                           int64_t rows_per_blk, XAcc bias_acc, BnFin fin, Wc1 wc) {
     constexpr int V = Vec16<T>::N;
     __shared__ double s1[2048];
     const int tpr = C / V, rpp = kThreads / tpr;
@@ -409,12 +419,35 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
     for (int v = 0; v < V; ++v) a[v] = 0.f;
     uint4 nx[kUb], ng[kUb];  // next step's rows (clamped, always in-bounds)
+    constexpr int NT = kWc1 ? 9 : 1;
+    float nt[kUb][NT];       // kWc1: the next rows' input taps (zero outside the image: the conv's padding)
+    float wacc[kWc1 ? V : 1][NT];
+#pragma unroll
+    for (int v = 0; v < (kWc1 ? V : 1); ++v)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) wacc[v][t] = 0.f;
     auto fetch = [&](int64_t rb) {
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t rc = min(rb + u * rpp, r1 - 1);
             nx[u] = load16_raw(y + rc * C + c0);
             ng[u] = load16_raw(da + rc * lda + c0);
+            if constexpr (kWc1) {
+                const int q = (int)rc;  // rows < 2^31 (checked by the launcher)
+                const int t = (int)wc.dWl.div((uint32_t)q), ow = q - t * wc.Wl;
+                const int b = (int)wc.dHl.div((uint32_t)t), oh = t - b * wc.Hl;
+                const int Wi = 2 * wc.Wl;
+                const float* xr = wc.x + ((int64_t)b * 2 * wc.Hl + 2 * oh - 1) * Wi + 2 * ow - 1;
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+                        const bool in = 2 * oh - 1 + kh >= 0 && 2 * ow - 1 + kw >= 0;
+                        const float* p = in ? xr + kh * Wi + kw : wc.x;  // clamped address, zeroed below
+                        const float xv = *p;
+                        nt[u][kh * 3 + kw] = in ? xv : 0.f;
+                    }
+            }
         }
     };
     fetch(r0 + rr);  // in flight during the finalize prologue
@@ -432,8 +465,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     }
     for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
         uint4 rx[kUb], rg[kUb];
+        float tx[kUb][NT];
 #pragma unroll
-        for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
+        for (int u = 0; u < kUb; ++u) {
+            rx[u] = nx[u];
+            rg[u] = ng[u];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) tx[u][t] = nt[u][t];
+        }
         fetch(r + kUb * rpp);
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
@@ -452,11 +491,41 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                 if constexpr (kMask) dz = mask[rc * C + c0 + v] ? dz * mscale : 0.f;
                 o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
             }
-            store16_f32(dy + rc * C + c0, o);
+            if constexpr (!kWc1) store16_f32(dy + rc * C + c0, o);
             // the bias grad is the sum of the dy actually stored (rounded to T), each row once
 #pragma unroll
-            for (int v = 0; v < V; ++v) a[v] += valid ? to_f32<T>(from_f32<T>(o[v])) : 0.f;
+            for (int v = 0; v < V; ++v) {
+                const float d = valid ? to_f32<T>(from_f32<T>(o[v])) : 0.f;
+                a[v] += d;
+                if constexpr (kWc1) {
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) wacc[v][t] = fmaf(d, tx[u][t], wacc[v][t]);
+                }
+            }
         }
+    }
+    if constexpr (kWc1) {
+        // the block's [C][9] partial: the tpr-strided lanes of one channel group (lane % tpr) summed by xor shuffles,
+        // the waves in order through LDS (s1 as floats, before the bias block_colsum reuses it)
+        float* red = reinterpret_cast<float*>(s1);  // [4 waves][C * 9]
+        const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                float w = wacc[v][t];
+                for (int o = tpr; o < 64; o <<= 1) w += __shfl_xor(w, o, 64);
+                wacc[v][t] = w;
+            }
+        if (lane < tpr)
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) red[wave * C * 9 + (c0 + v) * 9 + t] = wacc[v][t];
+        __syncthreads();
+        for (int i = tid; i < C * 9; i += kThreads)
+            wc.part[(int64_t)blockIdx.x * C * 9 + i] = (red[i] + red[C * 9 + i]) + (red[2 * C * 9 + i] + red[3 * C * 9 + i]);
+        __syncthreads();  // s1 reused below
     }
     if (bias_acc.on()) {
         double ad[V];
@@ -1324,7 +1393,8 @@ int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, XAcc acc, bool hav
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
-               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums) {
+               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums,
+               const Wc1Grad* wg) {
     HLMC_TRY(check_bn_shape<T>(C));
     HLMC_TRY(check_acc(mom, 2 * C));
     if (bias_acc.on()) HLMC_TRY(check_acc(bias_acc, C));
@@ -1352,16 +1422,33 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
         bn_bwd_finalize_kernel<<<fin_grid(C), 64, 0, s>>>(mom, C, dgamma, dbeta, sums);
         HLMC_LAUNCHED();
     }
+    if (wg) {  // the first conv's weight gradient from the apply pass (no dy stored)
+        HLMC_CHECK_ARG(fin_here && !mask && act == 0 && C == 32 && lda == C && R < (1ll << 31) && wg->x && wg->dW &&
+                       wg->part && wg->part_floats >= (int64_t)nblk * C * 9 && R == (int64_t)wg->B * wg->Hl * wg->Wl,
+                       "bn_act_bwd: fused first-layer weight gradient arguments");
+        Wc1 wc;
+        wc.x = wg->x; wc.Hl = wg->Hl; wc.Wl = wg->Wl; wc.dWl = FastDiv((uint32_t)wg->Wl); wc.dHl = FastDiv((uint32_t)wg->Hl);
+        wc.part = wg->part;
+        HLMC_BN_PROBED(s, 2.0 * sizeof(T) * R * C + 4.0 * R * 4,
+                       (bn_bwd_apply_kernel<T, false, true, 0, true><<<nblk, kThreads, 0, s>>>(
+                           da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums, dy, rpb, bias_acc, bf, wc)));
+        HLMC_LAUNCHED();
+        sum_partials_f32_kernel<<<C * 9, 256, 0, s>>>(wg->part, nblk, C * 9, wg->dW);
+        HLMC_LAUNCHED();
+        if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
+        return HLMC_OK;
+    }
     auto ka = mask ? (fin_here ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
               : act == 0 ? (fin_here ? bn_bwd_apply_kernel<T, false, true, 0> : bn_bwd_apply_kernel<T, false, false, 0>)
                          : (fin_here ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
     HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C,
                    (ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
-                                                 dy, rpb, bias_acc, bf)));
+                                                 dy, rpb, bias_acc, bf, Wc1{})));
     HLMC_LAUNCHED();
     if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
     return HLMC_OK;
 }
+int bn_wc1_part_floats(int64_t R, int C) { return bn_blocks(R, C) * C * 9; }
 int colsum_to_f64(hipStream_t s, XAcc acc, int C, double* out) {
     HLMC_CHECK_ARG(out && C > 0, "colsum_to_f64: bad arguments");
     HLMC_TRY(check_acc(acc, C));
@@ -1697,7 +1784,7 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
                                  T*, int);                                                                           \
     template int bn_act_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,          \
                                const float*, const float*, int, const uint8_t*, float, T*, float*, float*, XAcc,      \
-                               const BnBwdFuse*, XAcc, float*, float*);                                              \
+                               const BnBwdFuse*, XAcc, float*, float*, const Wc1Grad*);                              \
     template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*,        \
                                ColStats*, BnBwdFuse*);                                                               \
     template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);         \

@@ -135,10 +135,22 @@ int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const
 // of dy (the conv bias gradient) are added there; dbias (nullable, needs bias_acc): also reduce them into dbias
 // here (else the caller runs colsum_finalize, e.g. on the weight-gradient stream).  sums: 2C floats of scratch,
 // needed for C > 512 only.
+// The encoder's first conv (1 input channel) weight gradient computed by the BatchNorm backward of its output
+// (bn_act_bwd wg): dW[co][tap] = sum over the rows of dy[row][co] * x[tap of the row's pixel]; dy is not stored.
+// part: >= bn_wc1_part_floats(R, C) floats of scratch.
+struct Wc1Grad {
+    const float* x = nullptr;  // [B, 2 Hl, 2 Wl]
+    int B = 0, Hl = 0, Wl = 0;
+    float* dW = nullptr;        // [C][1][3][3]
+    float* part = nullptr;
+    int64_t part_floats = 0;
+};
+int bn_wc1_part_floats(int64_t R, int C);
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
-               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums);
+               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums,
+               const Wc1Grad* wg = nullptr);
 // out[c] = total of column c of acc (C columns)
 int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out);
 // out[c] (f64) = column c of an exact accumulator (the op-level statistics entry)

@@ -472,6 +472,22 @@ class NetT : public NetBase {
             return f(q, sc);
         }, side_batch());
     }
+    // the last decoder BatchNorm + LeakyReLU inside the output convT (train mode; needs the fused convT gradient, which
+    // recomputes the activation).  HLMC_LAST_BN_IN=0: a bn_act pass (A/B aid)
+    static bool last_bn_in_convt() {
+        static const bool on = [] {
+            const char* e = std::getenv("HLMC_LAST_BN_IN");
+            return !(e && e[0] == '0');
+        }();
+        return on && convt_grad_fused();
+    }
+    static bool convt_grad_fused() {
+        static const bool on = [] {
+            const char* e = std::getenv("HLMC_CONVT_GRAD_FUSE");
+            return !(e && e[0] == '0');
+        }();
+        return on;
+    }
     // HLMC_WC1_FUSE=0: the encoder's first-layer weight gradient as its own launch reading the stored dy (A/B aid)
     static bool wc1_fused() {
         static const bool on = [] {
@@ -661,6 +677,7 @@ class NetT : public NetBase {
             } else {
                 need(ops::wgrad_c1_ws((int)B, h, w, ci));
                 need(ops::colsum_ws((int)(B * 4 * h * w), 1));
+                need((size_t)ops::convt_c1_part_floats((int)B, 2 * h, 2 * w) * sizeof(float));
             }
             h *= 2;
             w *= 2;
@@ -682,6 +699,9 @@ class NetT : public NetBase {
                 HLMC_TRY(ops::subpixel<T>(s, fused_prev ? AT(dec.y[l - 1]) : x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co,
                                           y, scratch, &st, fused_prev ? &xin : nullptr));
                 fused_prev = train && l + 1 < 5 && ops::subpixel_takes_input_bn<T>(B, 2 * h, 2 * w, co, DEC_CH[l + 2]);
+                // the last BatchNorm layer: applied by the output convT as it loads (its activation is then never
+                // stored: the backward recomputes it, conv_c1_s2 MODE 3)
+                fused_prev = fused_prev || (train && l == 4 && last_bn_in_convt());
                 if (fused_prev) {
                     if (!st.done) HLMC_TRY(ops::bn_moments<T>(s, y, R, co, acc_fwd(dec.bb[l])));  // split-K producer
                     xin = bn_input(dec.bb[l], dec.bn[l], dec.g[l], dec.beta[l], R, dec.a[l]);
@@ -690,7 +710,8 @@ class NetT : public NetBase {
                                     AT(dec.a[l]), co, &st));
                 x = AT(dec.a[l]);
             } else {
-                HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon));
+                HLMC_TRY(ops::convT_c1<T>(s, fused_prev ? AT(dec.y[4]) : x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon,
+                                          fused_prev ? &xin : nullptr));
             }
             h *= 2;
             w *= 2;
@@ -710,15 +731,25 @@ class NetT : public NetBase {
             float* gw = G[dec.w[5]];
             float* gb = G[dec.b[5]];
             const int npix = B * hs[6] * ws_[6];
-            HLMC_TRY(side(s, [=](hipStream_t q, Ws sc) {
-                HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
-                return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
-            }));
-            // layer 4's BN-backward moments come with the edge conv that writes its output gradient
+            // layer 4's BN-backward moments come with the edge conv that writes its output gradient, and (default)
+            // the output convT's weight / bias gradients with them: its input a4 = LeakyReLU(BN(y4)) is recomputed
+            // from the y4 rows that pass loads anyway (HLMC_CONVT_GRAD_FUSE=0: a wgrad_c1 launch on the side stream)
             fuse4 = ops::BnBwdFuse{AT(dec.y[4]), AF(dec.bb[4].mean), AF(dec.bb[4].inv), P[dec.g[4]], P[dec.beta[4]],
                                    acc_mom(dec.bb[4]), false};
-            HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA, nullptr,
-                                        &fuse4));
+            if (convt_grad_fused()) {
+                ops::ConvTGrad cg;
+                cg.dW = gw; cg.db = gb; cg.part = scratch.p;
+                cg.part_floats = (int64_t)(scratch.bytes / sizeof(float));
+                HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA, nullptr,
+                                            &fuse4, &cg));
+            } else {
+                HLMC_TRY(side(s, [=](hipStream_t q, Ws sc) {
+                    HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
+                    return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
+                }));
+                HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA, nullptr,
+                                            &fuse4));
+            }
         }
         ops::BnBwdFuse fuse = fuse4;
         for (int l = 4; l >= 0; --l) {

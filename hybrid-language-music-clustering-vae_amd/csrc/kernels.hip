@@ -185,6 +185,7 @@ struct BnFin {
     int64_t* nbt = nullptr;
     float momentum = 0.f, eps = 0.f;
     float *dgamma = nullptr, *dbeta = nullptr;  // backward outputs (block 0)
+    const float *gamma = nullptr, *beta = nullptr;  // (convT_c1's input BatchNorm)
 };
 // The per-channel values from the totals tot (LDS, 2C doubles): fwd mean / invstd, bwd sum dz / sum dz*xhat
 template <bool kFwd>
@@ -620,18 +621,30 @@ struct C1Fuse {
     XAcc acc;  // 2 CO columns
     const void* ybn = nullptr;
     const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
+    // MODE 3 = MODE 2 + the output convT's weight and bias gradients: the layer's input activation
+    // a = LeakyReLU(BN(ybn)) (recomputed from the loaded ybn, rounded to T as the forward stored it) times the same
+    // 9 x taps the data gradient reads; the block's [CO * 9] partial and its bias partial (the 4 taps kh, kw >= 1 cover
+    // every high-res pixel once) go to part[blockIdx.x][CO * 9 + 1]
+    float* part = nullptr;
 };
 // Weights in LDS as [tap][CO] (each tap's 8 channels of a thread: two float4 reads), U = 2 pixels' tap loads in flight
 // per step; launch bounds keep >= 4 waves per SIMD (the per-pixel register set is small: no weights in registers).
 template <typename T, int CO, int MODE>
-__global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
+__global__ __launch_bounds__(256, MODE == 3 ? 2 : MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
                                                             const float* __restrict__ w, const float* __restrict__ bias,
                                                             T* __restrict__ y, FastDiv dWo, FastDiv dHo, C1Fuse fz) {
     constexpr int V = Vec16<T>::N, G = CO / V;  // threads per pixel
     constexpr int U = 2;                        // pixels per thread per step
+    constexpr bool kWg = MODE == 3;
     __shared__ __attribute__((aligned(16))) float wsh[9 * CO];
     __shared__ __attribute__((aligned(16))) float bsh[CO];
     __shared__ double fred[MODE ? 4 * CO : 1];
+    __shared__ float wred[kWg ? 4 * (9 * CO + 1) : 1];
+    float wacc[kWg ? V : 1][kWg ? 9 : 1], bacc = 0.f;
+#pragma unroll
+    for (int v = 0; v < (kWg ? V : 1); ++v)
+#pragma unroll
+        for (int k = 0; k < (kWg ? 9 : 1); ++k) wacc[v][k] = 0.f;
     for (int i = threadIdx.x; i < 9 * CO; i += blockDim.x) {
         const int tap = i / CO, c = i - tap * CO;
         wsh[i] = w[c * 9 + tap];
@@ -643,7 +656,7 @@ __global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(cons
     float bmu[V], bis[V], bga[V], bbe[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) fa[v] = fb[v] = 0.f;
-    if constexpr (MODE == 2) {
+    if constexpr (MODE >= 2) {
         BnChan::load(fz.mean, c0, bmu);
         BnChan::load(fz.invstd, c0, bis);
         BnChan::load(fz.gamma, c0, bga);
@@ -671,7 +684,7 @@ __global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(cons
 #pragma unroll
                 for (int kw = 0; kw < 3; ++kw)
                     in[u][kh * 3 + kw] = (2 * oh - 1 + kh >= 0 && 2 * ow - 1 + kw >= 0) ? xr[kh * Wi + kw] : 0.f;
-            if constexpr (MODE == 2) yraw[u] = load16_raw(static_cast<const T*>(fz.ybn) + (int64_t)p * CO + c0);
+            if constexpr (MODE >= 2) yraw[u] = load16_raw(static_cast<const T*>(fz.ybn) + (int64_t)p * CO + c0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -701,19 +714,51 @@ __global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(cons
                     fa[v] += q;
                     fb[v] = fmaf(q, q, fb[v]);
                 }
-            } else if constexpr (MODE == 2) {
+            } else if constexpr (MODE >= 2) {
                 float xb[V];
                 cvt16_f32<T>(yraw[u], xb);
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                     const float g = to_f32<T>(from_f32<T>(o[v]));  // the stored gradient
                     const float xh = (xb[v] - bmu[v]) * bis[v];
-                    const float dz = g * (xh * bga[v] + bbe[v] > 0.f ? 1.f : 0.01f);
+                    const float z = xh * bga[v] + bbe[v];
+                    const float dz = g * (z > 0.f ? 1.f : 0.01f);
                     fa[v] += dz;
                     fb[v] = fmaf(dz, xh, fb[v]);
+                    if constexpr (kWg) {
+                        const float a = to_f32<T>(from_f32<T>(z > 0.f ? z : 0.01f * z));  // the forward's activation
+#pragma unroll
+                        for (int k = 0; k < 9; ++k) wacc[v][k] = fmaf(a, in[u][k], wacc[v][k]);
+                    }
                 }
+                if constexpr (kWg)
+                    if (c0 == 0) bacc += (in[u][4] + in[u][5]) + (in[u][7] + in[u][8]);
             }
         }
+    }
+    if constexpr (kWg) {
+        // the block's [CO][9] weight-gradient partial and its bias partial: lanes of one channel group (lane % G)
+        // by xor shuffles, the 4 waves in order through LDS
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                float s = wacc[v][k];
+                for (int o = G; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
+                wacc[v][k] = s;
+            }
+        for (int o = G; o < 64; o <<= 1) bacc += __shfl_xor(bacc, o, 64);
+        constexpr int NP = 9 * CO + 1;
+        if (lane < G)
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) wred[wave * NP + (c0 + v) * 9 + k] = wacc[v][k];
+        if (lane == 0) wred[wave * NP + 9 * CO] = bacc;  // lane 0: channel group 0
+        __syncthreads();
+        for (int i = threadIdx.x; i < NP; i += blockDim.x)
+            fz.part[(int64_t)blockIdx.x * NP + i] = (wred[i] + wred[NP + i]) + (wred[2 * NP + i] + wred[3 * NP + i]);
     }
     if constexpr (MODE != 0) {
         double da_[V], db_[V];
@@ -734,15 +779,29 @@ __global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(cons
 // (Supersedes one thread per output pixel, whose per-tap loads waited one round trip each: 47 us at B = 256.)
 // (launch bounds: >= 4 waves per SIMD; unbounded, hipcc hoisted every LDS weight read out of the pixel loop into
 // 450 registers -> one wave per SIMD)
-template <typename T, int CI>
+// XIN (train mode): x is the PRE-BatchNorm map of the last decoder layer; its BatchNorm (statistics folded from the
+// producer's exact accumulator, block 0 storing mean / invstd / running statistics, as bn_act_kernel<kFin>) and
+// LeakyReLU are applied to every loaded chunk, rounded to T as bn_act would store the activation -- that bn_act launch
+// (a read and a write of the whole map) is gone; the backward recomputes the activation where it needs it
+// (conv_c1_s2 MODE 3).
+template <typename T, int CI, bool XIN = false>
 __global__ __launch_bounds__(256, 4) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
-                                                       float* __restrict__ y, FastDiv dWi, FastDiv dHi) {
+                                                       float* __restrict__ y, FastDiv dWi, FastDiv dHi, BnFin fin) {
     constexpr int V = Vec16<T>::N, NC = CI / V;  // 16-byte chunks per pixel
     __shared__ __attribute__((aligned(16))) float wt[9 * CI];
+    __shared__ __attribute__((aligned(16))) float bnp[XIN ? 4 * CI : 4];  // mean | invstd | gamma | beta
+    __shared__ double fsh[XIN ? 2 * CI + 3 * kThreads : 1];
     for (int i = threadIdx.x; i < 9 * CI; i += blockDim.x) {
         const int tap = i / CI, ci = i - tap * CI;
         wt[i] = w[ci * 9 + tap];
+    }
+    if constexpr (XIN) {
+        for (int c = threadIdx.x; c < CI; c += blockDim.x) {
+            bnp[2 * CI + c] = fin.gamma[c];
+            bnp[3 * CI + c] = fin.beta[c];
+        }
+        bn_fin_prologue<true>(fin, CI, fsh, reinterpret_cast<long long*>(fsh + 2 * CI), bnp, bnp + CI);  // + barrier
     }
     __syncthreads();
     const float b0 = bias ? bias[0] : 0.f;
@@ -776,6 +835,23 @@ __global__ __launch_bounds__(256, 4) void convT_c1_kernel(const T* __restrict__ 
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
                 cvt16_f32<T>(raw[n][j], v[n]);
+                if constexpr (XIN) {
+#pragma unroll
+                    for (int e4 = 0; e4 < V / 4; ++e4) {
+                        const int c = j * V + 4 * e4;
+                        const float4 mu = *reinterpret_cast<const float4*>(bnp + c);
+                        const float4 is = *reinterpret_cast<const float4*>(bnp + CI + c);
+                        const float4 ga = *reinterpret_cast<const float4*>(bnp + 2 * CI + c);
+                        const float4 be = *reinterpret_cast<const float4*>(bnp + 3 * CI + c);
+                        const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {is.x, is.y, is.z, is.w};
+                        const float g4[4] = {ga.x, ga.y, ga.z, ga.w}, b4[4] = {be.x, be.y, be.z, be.w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float z = (v[n][4 * e4 + q] - m4[q]) * i4[q] * g4[q] + b4[q];
+                            v[n][4 * e4 + q] = to_f32<T>(from_f32<T>(act_fwd(z, 0)));
+                        }
+                    }
+                }
 #pragma unroll
                 for (int e = 0; e < V; ++e) v[n][e] = nbok[n] ? v[n][e] : 0.f;
             }
@@ -1449,6 +1525,10 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
     return HLMC_OK;
 }
 int bn_wc1_part_floats(int64_t R, int C) { return bn_blocks(R, C) * C * 9; }
+int convt_c1_part_floats(int B, int Hi, int Wi) {
+    const int64_t nthr = (int64_t)B * (Hi / 2) * (Wi / 2) * 4;
+    return grid_for(nthr, kThreads, kC1FusedBlocks) * (9 * 32 + 1);
+}
 int colsum_to_f64(hipStream_t s, XAcc acc, int C, double* out) {
     HLMC_CHECK_ARG(out && C > 0, "colsum_to_f64: bad arguments");
     HLMC_TRY(check_acc(acc, C));
@@ -1467,7 +1547,7 @@ int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out) {
 
 template <typename T>
 int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y,
-               ColStats* st, BnBwdFuse* bf) {
+               ColStats* st, BnBwdFuse* bf, const ConvTGrad* wg) {
     HLMC_CHECK_ARG(Co == 32 && Hi % 2 == 0 && Wi % 2 == 0, "conv_c1_s2: only Co == 32, even H/W");
     int64_t nthr = (int64_t)B * (Hi / 2) * (Wi / 2) * (32 / Vec16<T>::N);
     HLMC_CHECK_ARG(nthr < (int64_t)1 << 31, "conv_c1_s2: too many pixels");
@@ -1487,7 +1567,19 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
         const int g = grid_for(nthr, kThreads, kC1FusedBlocks);
         fz.acc = bf->acc;
         fz.ybn = bf->y; fz.mean = bf->mean; fz.invstd = bf->invstd; fz.gamma = bf->gamma; fz.beta = bf->beta;
-        conv_c1_s2_kernel<T, 32, 2><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
+        if (wg) {  // + the output convT's weight and bias gradients (its input activation is this layer's)
+            constexpr int NP = 9 * 32 + 1;
+            HLMC_CHECK_ARG(wg->dW && wg->db && wg->part && wg->part_floats >= (int64_t)g * NP,
+                           "conv_c1_s2: fused convT gradient arguments");
+            fz.part = wg->part;
+            conv_c1_s2_kernel<T, 32, 3><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
+            HLMC_LAUNCHED();
+            sum_partials_f32_kernel<<<NP - 1, 256, 0, s>>>(wg->part, g, NP, wg->dW);
+            HLMC_LAUNCHED();
+            sum_partials_f32_kernel<<<1, 256, 0, s>>>(wg->part + (NP - 1), g, NP, wg->db);
+        } else {
+            conv_c1_s2_kernel<T, 32, 2><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
+        }
         bf->done = true;
     } else {
         conv_c1_s2_kernel<T, 32, 0><<<grid_for(nthr, kThreads, 16384), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH,
@@ -1498,14 +1590,26 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
 }
 
 template <typename T>
-int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y) {
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y,
+             const BnInput* xin) {
     HLMC_CHECK_ARG(Ci == 32, "convT_c1: only Ci == 32");
     int64_t npix = (int64_t)B * 4 * Hi * Wi;
     HLMC_CHECK_ARG(npix < (int64_t)1 << 31, "convT_c1: too many pixels");
     HLMC_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "convT_c1: alignment");
     const FastDiv dW((uint32_t)Wi), dH((uint32_t)Hi);
-    convT_c1_kernel<T, 32><<<(unsigned)((npix / 4 + kThreads - 1) / kThreads), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y,
-                                                                                              dW, dH);
+    const unsigned g = (unsigned)((npix / 4 + kThreads - 1) / kThreads);
+    if (xin) {
+        HLMC_TRY(check_acc(xin->acc, 2 * Ci));
+        HLMC_CHECK_ARG(xin->R == (int64_t)B * Hi * Wi && xin->mean && xin->invstd && xin->gamma && xin->beta,
+                       "convT_c1: input BatchNorm arguments");
+        BnFin f;
+        f.acc = xin->acc; f.R = xin->R; f.mean = xin->mean; f.invstd = xin->invstd; f.rmean = xin->rmean;
+        f.rvar = xin->rvar; f.nbt = xin->nbt; f.momentum = xin->momentum; f.eps = xin->eps;
+        f.gamma = xin->gamma; f.beta = xin->beta;
+        convT_c1_kernel<T, 32, true><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, f);
+    } else {
+        convT_c1_kernel<T, 32><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, BnFin{});
+    }
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1786,8 +1890,9 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
                                const float*, const float*, int, const uint8_t*, float, T*, float*, float*, XAcc,      \
                                const BnBwdFuse*, XAcc, float*, float*, const Wc1Grad*);                              \
     template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*,        \
-                               ColStats*, BnBwdFuse*);                                                               \
-    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);         \
+                               ColStats*, BnBwdFuse*, const ConvTGrad*);                                             \
+    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*,         \
+                             const BnInput*);                                                                        \
     template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws);                    \
     template int cast_from_f32<T>(hipStream_t, const float*, T*, int64_t);                                           \
     template int cast_to_f32<T>(hipStream_t, const T*, float*, int64_t);                                             \

@@ -92,12 +92,24 @@ size_t linear_wgrad_ws(int Mb, int N, int K);
 
 // ---------------------------------------------------------------- edge convs with one channel (kernels.hip)
 // y[B,Hi/2,Wi/2,32] = sum_taps x[B,Hi,Wi] * w[co*9+tap] (+ bias)  (conv1 fwd, convT6 dgrad)
+// wg (with bf, the output convT's data gradient): that convT's weight gradient dW[ci][1][3][3] and bias gradient
+// db[1] from the same pass (its input activation recomputed from bf's pre-BN map); part: convt_c1_part_floats floats
+struct ConvTGrad {
+    float* dW = nullptr;
+    float* db = nullptr;
+    float* part = nullptr;
+    int64_t part_floats = 0;
+};
+int convt_c1_part_floats(int B, int Hi, int Wi);
 template <typename T>
 int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y,
-               ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
-// y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel)
+               ColStats* st = nullptr, BnBwdFuse* bf = nullptr, const ConvTGrad* wg = nullptr);
+// y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel).  xin (train mode,
+// nullable): x is the pre-BatchNorm map; its BatchNorm + LeakyReLU (statistics from xin->acc) applied as it is loaded
+// (xin->a_out unused: the activation is not stored)
 template <typename T>
-int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y);
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y,
+             const BnInput* xin = nullptr);
 // dW[m*9+tap] = sum L[b,r,c,m] * Xh[b, 2r-1+kh, 2c-1+kw]   (Xh single channel f32)
 template <typename T>
 int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws);

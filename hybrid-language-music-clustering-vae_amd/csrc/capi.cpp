@@ -406,34 +406,23 @@ int hlmc_cluster_scores(void* stream, const float* X, int64_t n, int d, const in
 // ------------------------------------------------------------------------------------ op-level entries
 // Individual GEMM-family kernels (the building blocks of hlmc_net_*), exposed for testing and reuse.
 #define DT_DISPATCH(dtype, CALL_F32, CALL_BF16) ((dtype) == HLMC_BF16 ? (CALL_BF16) : (CALL_F32))
-// the op entries' split-K arrival counters (gemm.hpp SplitFix): one zeroed device block, allocated on first use and
-// kept zero by the combining blocks; op entries on concurrent streams must not overlap in time (test / bench entries)
-static Ws op_ws(void* ws, int64_t ws_bytes) {
-    static unsigned* cnt = nullptr;
-    constexpr int kN = 8192;
-    if (!cnt) {
-        if (hipMalloc(&cnt, kN * sizeof(unsigned)) != hipSuccess || hipMemset(cnt, 0, kN * sizeof(unsigned)) != hipSuccess)
-            cnt = nullptr;
-    }
-    return Ws{reinterpret_cast<float*>(ws), (size_t)ws_bytes, cnt, cnt ? kN : 0};
-}
 int hlmc_op_conv_s2(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
                     const float* bias, int Co, void* y, void* ws, int64_t ws_bytes) {
-    Ws w = op_ws(ws, ws_bytes);
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
     return DT_DISPATCH(dtype,
         ops::conv_s2<float>(S(stream), (const float*)x, B, Hi, Wi, Ci, (const float*)wp, bias, Co, (float*)y, w),
         ops::conv_s2<bf16>(S(stream), (const bf16*)x, B, Hi, Wi, Ci, (const bf16*)wp, bias, Co, (bf16*)y, w));
 }
 int hlmc_op_subpixel(void* stream, int dtype, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
                      const float* bias, int Co, void* y, void* ws, int64_t ws_bytes) {
-    Ws w = op_ws(ws, ws_bytes);
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
     return DT_DISPATCH(dtype,
         ops::subpixel<float>(S(stream), (const float*)x, B, Hi, Wi, Ci, (const float*)wp, bias, Co, (float*)y, w),
         ops::subpixel<bf16>(S(stream), (const bf16*)x, B, Hi, Wi, Ci, (const bf16*)wp, bias, Co, (bf16*)y, w));
 }
 int hlmc_op_wgrad_s2(void* stream, int dtype, const void* Lo, int B, int Hl, int Wl, int M, const void* Xh, int C,
                      float* dW, void* ws, int64_t ws_bytes) {
-    Ws w = op_ws(ws, ws_bytes);
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
     return DT_DISPATCH(dtype,
         ops::wgrad_s2<float>(S(stream), (const float*)Lo, B, Hl, Wl, M, (const float*)Xh, C, dW, w),
         ops::wgrad_s2<bf16>(S(stream), (const bf16*)Lo, B, Hl, Wl, M, (const bf16*)Xh, C, dW, w));
@@ -441,7 +430,7 @@ int hlmc_op_wgrad_s2(void* stream, int dtype, const void* Lo, int B, int Hl, int
 int hlmc_op_linear(void* stream, int dtype, const void* x, int ldx, int M, int K, const void* wt, int ldw,
                    const float* bias, int N, void* y, int ldy, int act, int accumulate, int out_f32, void* ws,
                    int64_t ws_bytes, const void* relu_ref) {
-    Ws w = op_ws(ws, ws_bytes);
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
     if (dtype == HLMC_BF16 && out_f32)
         return ops::linear<bf16, float>(S(stream), (const bf16*)x, ldx, M, K, (const bf16*)wt, ldw, bias, N, (float*)y,
                                         ldy, act, accumulate, w, (const float*)relu_ref);
@@ -453,7 +442,7 @@ int hlmc_op_linear(void* stream, int dtype, const void* x, int ldx, int M, int K
 }
 int hlmc_op_linear_wgrad(void* stream, int dtype, const void* dy, int lddy, const void* x, int ldx, int Mb, int N,
                          int K, float* dW, float* db, void* ws, int64_t ws_bytes) {
-    Ws w = op_ws(ws, ws_bytes);
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
     return DT_DISPATCH(dtype,
         ops::linear_wgrad<float>(S(stream), (const float*)dy, lddy, (const float*)x, ldx, Mb, N, K, dW, db, w),
         ops::linear_wgrad<bf16>(S(stream), (const bf16*)dy, lddy, (const bf16*)x, ldx, Mb, N, K, dW, db, w));
@@ -470,7 +459,7 @@ int hlmc_op_convT_c1(void* stream, int dtype, const void* x, int B, int Hi, int 
 }
 int hlmc_op_wgrad_c1(void* stream, int dtype, const void* Lo, int B, int Hl, int Wl, int M, const float* Xh,
                      float* dW, void* ws, int64_t ws_bytes) {
-    Ws w = op_ws(ws, ws_bytes);
+    Ws w{reinterpret_cast<float*>(ws), (size_t)ws_bytes};
     return DT_DISPATCH(dtype, ops::wgrad_c1<float>(S(stream), (const float*)Lo, B, Hl, Wl, M, Xh, dW, w),
                        ops::wgrad_c1<bf16>(S(stream), (const bf16*)Lo, B, Hl, Wl, M, Xh, dW, w));
 }

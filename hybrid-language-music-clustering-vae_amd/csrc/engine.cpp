@@ -147,18 +147,10 @@ class NetT : public NetBase {
     // backward moments and bias column sums in the next; zeroed by one memset per train forward (and by backward
     // when it runs again without a forward in between)
     size_t xf_total = 0, xb_total = 0, xf_base = 0, xb_base = 0;
-    // split-K arrival counters of the in-launch combine (gemm.hpp SplitFix), kFixCnt per stream, directly after the
-    // accumulators: zeroed with them (train) or alone (other forwards); every combining block resets its own
-    static constexpr int kFixCnt = 4096;
-    size_t cnt_base = 0;
     bool bwd_acc_clean = false;
     int zero_acc_fwd(hipStream_t s) {
-        HLMC_HIP(hipMemsetAsync(ws + xf_base, 0, cnt_base + 2 * kFixCnt * 4 - xf_base, s));
+        if (xf_total + xb_total) HLMC_HIP(hipMemsetAsync(ws + xf_base, 0, xf_total + xb_total, s));
         bwd_acc_clean = true;
-        return HLMC_OK;
-    }
-    int zero_fix_counters(hipStream_t s) {
-        HLMC_HIP(hipMemsetAsync(ws + cnt_base, 0, 2 * kFixCnt * 4, s));
         return HLMC_OK;
     }
     int zero_acc_bwd(hipStream_t s) {
@@ -176,9 +168,8 @@ class NetT : public NetBase {
             plan(A, B);
             scratch_off = A.take(scratch_bytes + 256);
             scratch2_off = A.take(scratch_bytes + 256);
-            xf_base = A.take(xf_total);  // xb and the counters directly after xf (one memset: 256-aligned sizes)
+            xf_base = A.take(xf_total);  // xb directly after xf (one memset covers both: 256-aligned sizes)
             xb_base = A.take(xb_total);
-            cnt_base = A.take(2 * kFixCnt * 4);
             ws_total = A.used;
             planned_B = B;
         }
@@ -186,9 +177,8 @@ class NetT : public NetBase {
     }
     void set_ws(void* w) {
         ws = reinterpret_cast<char*>(w);
-        unsigned* cnt = reinterpret_cast<unsigned*>(ws + cnt_base);
-        scratch = Ws{reinterpret_cast<float*>(ws + scratch_off), scratch_bytes + 256, cnt, kFixCnt};
-        scratch2 = Ws{reinterpret_cast<float*>(ws + scratch2_off), scratch_bytes + 256, cnt + kFixCnt, kFixCnt};
+        scratch = Ws{reinterpret_cast<float*>(ws + scratch_off), scratch_bytes + 256};
+        scratch2 = Ws{reinterpret_cast<float*>(ws + scratch2_off), scratch_bytes + 256};
     }
 
     // ---------------------------------------------------------------- weight-gradient stream
@@ -436,12 +426,12 @@ class NetT : public NetBase {
     // gradient: every fork puts an event marker on the main stream, measured as a ~10 us bubble)
     int bn_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const BnBufs& bb, int g, int beta,
                int act, const uint8_t* mask, float mscale, T* dy, int bias, const ops::BnBwdFuse* fused = nullptr,
-               bool bias_side = false, bool defer_bias = false, const ops::Wc1Grad* wg = nullptr) {
+               bool bias_side = false, bool defer_bias = false) {
         const bool on_side = bias >= 0 && use_side && bias_side;
         const XAcc bacc = bias >= 0 ? acc_bias(bb) : XAcc{};
         HLMC_TRY(ops::bn_act_bwd<T>(s, da, lda, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], act, mask, mscale, dy,
                                     G[g], G[beta], acc_mom(bb), fused, bacc,
-                                    (bias >= 0 && !on_side) ? G[bias] : nullptr, AF(bb.sums), wg));
+                                    (bias >= 0 && !on_side) ? G[bias] : nullptr, AF(bb.sums)));
         if (on_side) {
             float* gb = G[bias];
             if (defer_bias)
@@ -471,30 +461,6 @@ class NetT : public NetBase {
             if (pb.gb) HLMC_TRY(ops::colsum_finalize(q, pb.acc, pb.C, pb.gb));
             return f(q, sc);
         }, side_batch());
-    }
-    // the last decoder BatchNorm + LeakyReLU inside the output convT (train mode; needs the fused convT gradient, which
-    // recomputes the activation).  HLMC_LAST_BN_IN=0: a bn_act pass (A/B aid)
-    static bool last_bn_in_convt() {
-        static const bool on = [] {
-            const char* e = std::getenv("HLMC_LAST_BN_IN");
-            return !(e && e[0] == '0');
-        }();
-        return on && convt_grad_fused();
-    }
-    static bool convt_grad_fused() {
-        static const bool on = [] {
-            const char* e = std::getenv("HLMC_CONVT_GRAD_FUSE");
-            return !(e && e[0] == '0');
-        }();
-        return on;
-    }
-    // HLMC_WC1_FUSE=0: the encoder's first-layer weight gradient as its own launch reading the stored dy (A/B aid)
-    static bool wc1_fused() {
-        static const bool on = [] {
-            const char* e = std::getenv("HLMC_WC1_FUSE");
-            return !(e && e[0] == '0');
-        }();
-        return on;
     }
     // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
     static bool tail_on_main() {
@@ -538,7 +504,6 @@ class NetT : public NetBase {
                 need(ops::wgrad_s2_ws<T>((int)B, h / 2, w / 2, co, ci));
             } else {
                 need(ops::wgrad_c1_ws((int)B, h / 2, w / 2, co));
-                need((size_t)ops::bn_wc1_part_floats((int64_t)B * (h / 2) * (w / 2), co) * sizeof(float));
             }
             h /= 2;
             w /= 2;
@@ -600,19 +565,9 @@ class NetT : public NetBase {
             const int ho = hs[l + 1], wo = ws_[l + 1];
             const int64_t R = (int64_t)B * ho * wo;
             T* dy = AT(enc.dy[l]);
-            float* gw = G[enc.w[l]];
-            if (l == 0 && wc1_fused()) {
-                // the first conv's weight gradient inside its BatchNorm backward (ops::Wc1Grad): dy is never stored
-                ops::Wc1Grad wg;
-                wg.x = audio; wg.B = B; wg.Hl = ho; wg.Wl = wo; wg.dW = gw;
-                wg.part = scratch.p;
-                wg.part_floats = (int64_t)(scratch.bytes / sizeof(float));
-                HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy,
-                                enc.b[l], nullptr, false, false, &wg));  // (bias gradient finalized in there)
-                continue;
-            }
             HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
                             nullptr, true, true));
+            float* gw = G[enc.w[l]];
             if (l == 0 && tail_on_main()) {
                 // the last weight gradient of backward: on the main stream, which would otherwise only wait for
                 // the weight-gradient stream here (that stream is still reducing layer 1's gradient)
@@ -677,7 +632,6 @@ class NetT : public NetBase {
             } else {
                 need(ops::wgrad_c1_ws((int)B, h, w, ci));
                 need(ops::colsum_ws((int)(B * 4 * h * w), 1));
-                need((size_t)ops::convt_c1_part_floats((int)B, 2 * h, 2 * w) * sizeof(float));
             }
             h *= 2;
             w *= 2;
@@ -699,9 +653,6 @@ class NetT : public NetBase {
                 HLMC_TRY(ops::subpixel<T>(s, fused_prev ? AT(dec.y[l - 1]) : x, B, h, w, ci, P1(dec.w[l]), P[dec.b[l]], co,
                                           y, scratch, &st, fused_prev ? &xin : nullptr));
                 fused_prev = train && l + 1 < 5 && ops::subpixel_takes_input_bn<T>(B, 2 * h, 2 * w, co, DEC_CH[l + 2]);
-                // the last BatchNorm layer: applied by the output convT as it loads (its activation is then never
-                // stored: the backward recomputes it, conv_c1_s2 MODE 3)
-                fused_prev = fused_prev || (train && l == 4 && last_bn_in_convt());
                 if (fused_prev) {
                     if (!st.done) HLMC_TRY(ops::bn_moments<T>(s, y, R, co, acc_fwd(dec.bb[l])));  // split-K producer
                     xin = bn_input(dec.bb[l], dec.bn[l], dec.g[l], dec.beta[l], R, dec.a[l]);
@@ -710,8 +661,7 @@ class NetT : public NetBase {
                                     AT(dec.a[l]), co, &st));
                 x = AT(dec.a[l]);
             } else {
-                HLMC_TRY(ops::convT_c1<T>(s, fused_prev ? AT(dec.y[4]) : x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon,
-                                          fused_prev ? &xin : nullptr));
+                HLMC_TRY(ops::convT_c1<T>(s, x, B, h, w, ci, P[dec.w[5]], P[dec.b[5]], recon));
             }
             h *= 2;
             w *= 2;
@@ -731,25 +681,15 @@ class NetT : public NetBase {
             float* gw = G[dec.w[5]];
             float* gb = G[dec.b[5]];
             const int npix = B * hs[6] * ws_[6];
-            // layer 4's BN-backward moments come with the edge conv that writes its output gradient, and (default)
-            // the output convT's weight / bias gradients with them: its input a4 = LeakyReLU(BN(y4)) is recomputed
-            // from the y4 rows that pass loads anyway (HLMC_CONVT_GRAD_FUSE=0: a wgrad_c1 launch on the side stream)
+            HLMC_TRY(side(s, [=](hipStream_t q, Ws sc) {
+                HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
+                return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
+            }));
+            // layer 4's BN-backward moments come with the edge conv that writes its output gradient
             fuse4 = ops::BnBwdFuse{AT(dec.y[4]), AF(dec.bb[4].mean), AF(dec.bb[4].inv), P[dec.g[4]], P[dec.beta[4]],
                                    acc_mom(dec.bb[4]), false};
-            if (convt_grad_fused()) {
-                ops::ConvTGrad cg;
-                cg.dW = gw; cg.db = gb; cg.part = scratch.p;
-                cg.part_floats = (int64_t)(scratch.bytes / sizeof(float));
-                HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA, nullptr,
-                                            &fuse4, &cg));
-            } else {
-                HLMC_TRY(side(s, [=](hipStream_t q, Ws sc) {
-                    HLMC_TRY(ops::wgrad_c1<T>(q, a4, B, hl, wl, DEC_CH[5], d_recon, gw, sc));
-                    return ops::colsum<float>(q, d_recon, 1, npix, 1, gb, sc);
-                }));
-                HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA, nullptr,
-                                            &fuse4));
-            }
+            HLMC_TRY(ops::conv_c1_s2<T>(s, d_recon, B, hs[6], ws_[6], P[dec.w[5]], nullptr, DEC_CH[5], gA, nullptr,
+                                        &fuse4));
         }
         ops::BnBwdFuse fuse = fuse4;
         for (int l = 4; l >= 0; --l) {
@@ -935,7 +875,7 @@ class HybridNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        HLMC_TRY(a.train ? this->zero_acc_fwd(s) : this->zero_fix_counters(s));
+        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z), src/Convolutional_VAE.py:167-179
             HLMC_CHECK_ARG(a.in0 && a.recon, "z and recon required");
@@ -1125,7 +1065,7 @@ class CvaeNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        HLMC_TRY(a.train ? this->zero_acc_fwd(s) : this->zero_fix_counters(s));
+        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z, condition), src/Conditional_VAE.py:206-225
             HLMC_CHECK_ARG(a.in0 && a.in2 && a.recon && a.recon_text, "z / condition / recon / recon_text required");
@@ -1320,7 +1260,7 @@ class SimpleNet : public NetT<T> {
         this->set_ws(a.ws);
         HLMC_TRY(this->settle(s));
         HLMC_TRY(this->pack_all(s));
-        HLMC_TRY(a.train ? this->zero_acc_fwd(s) : this->zero_fix_counters(s));
+        if (a.train) HLMC_TRY(this->zero_acc_fwd(s));
         this->last_full_forward = !a.encode_only && !a.decode_only;
         if (a.decode_only) {  // decode(z), src/Simple_VAE.py:95-96 (decoder blocks' dropout from the same mask layout)
             HLMC_CHECK_ARG(a.in0 && a.recon, "z and recon required");

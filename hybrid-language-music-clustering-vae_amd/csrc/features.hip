@@ -362,11 +362,7 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
         // ---- stage 1 (radix 16, Ns = 1): z[j + 64 r] = windowed sample pairs (prefetched one frame ahead)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-#if defined(HLMC_STFT_ABL) && (HLMC_STFT_ABL & 2)
-            const float2 w = make_float2(0.5f + 0.001f * r + 1e-6f * ln, 0.5f - 0.001f * r);
-#else
             const float2 w = *reinterpret_cast<const float2*>(window + 2 * (ln + 64 * r));
-#endif
             a[r] = make_float2(nxt[r].x * w.x, nxt[r].y * w.y);
         }
         if (fl + kWaves < nf) fetch(t0 + fl + kWaves, ln, nxt);
@@ -408,15 +404,9 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
         // ---- real-FFT split: X[f] = E[f] + e^{-2 pi i f / 2048} O[f], f = 0..1024
         float p[17];
         float2 w[17];   // real-split twiddles from global (issued before the LDS reads they pair with)
-#if defined(HLMC_STFT_ABL) && (HLMC_STFT_ABL & 2)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) w[q] = make_float2(0.7f + 1e-6f * ln, 0.7f - 0.01f * q);
-        w[16] = make_float2(-1.f, 0.f);
-#else
 #pragma unroll
         for (int q = 0; q < 16; ++q) w[q] = rtw[ln + 64 * q];
         w[16] = rtw[kFFT];
-#endif
         // conjugate partner 1024 - f of f = ln + 64 q: zpad = 68 (16 - q) + bcj (f = 0 pairs with itself)
         const int bcj = -ln + ((-ln) >> 4);
         auto split = [&](float2 zf, float2 zc, float2 w) -> float {
@@ -454,11 +444,7 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
             float acc0 = 0.f, acc1 = 0.f;
             for (int c = 0; c < bl.y; c += 2) {
                 const float4 p0 = pw4[(bl.x >> 2) + c], p1 = pw4[(bl.x >> 2) + c + 1];
-#if defined(HLMC_STFT_ABL) && (HLMC_STFT_ABL & 1)
-                const float4 w0 = make_float4(0.1f * c, 0.2f, 0.3f, 0.4f), w1 = make_float4(0.5f, 0.6f * c, 0.7f, 0.8f);
-#else
                 const float4 w0 = gw4[c * kMelLanes + ln], w1 = gw4[(c + 1) * kMelLanes + ln];
-#endif
                 acc0 = fmaf(p0.x, w0.x, acc0); acc0 = fmaf(p0.y, w0.y, acc0);
                 acc0 = fmaf(p0.z, w0.z, acc0); acc0 = fmaf(p0.w, w0.w, acc0);
                 acc0 = fmaf(p1.x, w1.x, acc0); acc0 = fmaf(p1.y, w1.y, acc0);
@@ -467,11 +453,7 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
             for (int c = 0; c < bl.w; c += 2) {
                 const int cw = bl.y + c;
                 const float4 p0 = pw4[(bl.z >> 2) + c], p1 = pw4[(bl.z >> 2) + c + 1];
-#if defined(HLMC_STFT_ABL) && (HLMC_STFT_ABL & 1)
-                const float4 w0 = make_float4(0.1f * c, 0.2f, 0.3f, 0.4f), w1 = make_float4(0.5f, 0.6f * c, 0.7f, 0.8f);
-#else
                 const float4 w0 = gw4[cw * kMelLanes + ln], w1 = gw4[(cw + 1) * kMelLanes + ln];
-#endif
                 acc1 = fmaf(p0.x, w0.x, acc1); acc1 = fmaf(p0.y, w0.y, acc1);
                 acc1 = fmaf(p0.z, w0.z, acc1); acc1 = fmaf(p0.w, w0.w, acc1);
                 acc1 = fmaf(p1.x, w1.x, acc1); acc1 = fmaf(p1.y, w1.y, acc1);

@@ -562,121 +562,6 @@ __device__ __forceinline__ f32x4_t mfma_f32(float a, float b, const f32x4_t& c) 
     else return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// ============================================================================ in-launch split-K combine
-// A split-K launch without a reduce launch: every block stores its fp32 partial tile WRITE-THROUGH (sc1 buffer
-// stores: no release fence, cdna_hip_programming.md Guideline 16 R1), drains them (every wave's vmcnt(0)), and one
-// lane draws a ticket from the tile's arrival counter (relaxed agent-scope atomic); the block that draws S - 1 is
-// the tile's last: it takes the agent-scope acquire (invalidating its CU's L1), resets the counter for the next
-// launch, re-reads the S partials in split order -- the same fp32 additions, in the same order, as
-// splitk_reduce_kernel, so the result is bit-identical -- and runs the final epilogue (bias, activation, statistics)
-// exactly as a single-pass launch does.  Correct for any dispatch order or XCD placement; placement is speed only.
-struct SplitFix {
-    float* ws = nullptr;      // partial slabs [phase][S][M][N] (fp32)
-    unsigned* cnt = nullptr;  // one arrival counter per (phase, M x N tile): zero on entry, reset by the combiner
-    unsigned bytes = 0;       // bytes of the slab region (the store descriptor's range)
-    int S = 1;
-};
-// store this wave's accumulator tiles into slab element offset `slab0` (TR: 4 consecutive columns per lane and tile
-// as one 16-byte store; else one 4-byte store per element), write-through
-template <bool TR, int TM, int TN>
-__device__ __forceinline__ void fix_store(const SplitFix& fx, const f32x4_t (&acc)[TM][TN], int64_t slab0, int mb, int nb,
-                                          int lane, int M, int N) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(fx.ws, 0, fx.bytes, 0x00020000);
-    typedef int v4i __attribute__((ext_vector_type(4)));
-    if constexpr (TR) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int m = mb + i * 16 + (lane & 15);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n4 = nb + j * 16 + 4 * (lane >> 4);
-                if (m >= M || n4 >= N) continue;
-                const v4i v = {__float_as_int(acc[i][j][0]), __float_as_int(acc[i][j][1]), __float_as_int(acc[i][j][2]),
-                               __float_as_int(acc[i][j][3])};
-                __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)((slab0 + (int64_t)m * N + n4) * 4), 0, 16);
-            }
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int m = mb + i * 16 + (lane >> 4) * 4 + q;
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n = nb + j * 16 + (lane & 15);
-                    if (m >= M || n >= N) continue;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(acc[i][j][q]), r,
-                                                          (int)((slab0 + (int64_t)m * N + n) * 4), 0, 16);
-                }
-            }
-    }
-}
-// acc <- sum over the S slabs of phase base `pbase` (element offset of split 0), k ascending from 0.f
-template <bool TR, int TM, int TN>
-__device__ __forceinline__ void fix_combine(const SplitFix& fx, f32x4_t (&acc)[TM][TN], int64_t pbase, int64_t MN,
-                                            int mb, int nb, int lane, int M, int N) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < fx.S; ++k) {
-        const float* sl = fx.ws + pbase + (int64_t)k * MN;
-        f32x4_t x[TM][TN];
-        if constexpr (TR) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int m = min(mb + i * 16 + (lane & 15), M - 1);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int n4 = min(nb + j * 16 + 4 * (lane >> 4), N - 4);
-                    const float4 v = *reinterpret_cast<const float4*>(sl + (int64_t)m * N + n4);
-                    x[i][j] = f32x4_t{v.x, v.y, v.z, v.w};
-                }
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int m = min(mb + i * 16 + (lane >> 4) * 4 + q, M - 1);
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) x[i][j][q] = sl[(int64_t)m * N + min(nb + j * 16 + (lane & 15), N - 1)];
-                }
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] += x[i][j];
-    }
-}
-// After the main loop of a split-K block (fx.S > 1): store the partial, draw the ticket; returns true in the tile's
-// combining block (acc then holds the combined sums), false in every other block (which must exit).  flag: one
-// word of block-shared LDS no wave reads or writes between the two barriers.
-template <bool TR, int TM, int TN>
-__device__ __forceinline__ bool fix_arrive(const SplitFix& fx, f32x4_t (&acc)[TM][TN], unsigned* flag, int phase, int bz,
-                                           unsigned slot, int mb, int nb, int lane, int M, int N) {
-    const int64_t MN = (int64_t)M * N;
-    const int64_t pbase = (int64_t)phase * fx.S * MN;
-    fix_store<TR, TM, TN>(fx, acc, pbase + (int64_t)bz * MN, mb, nb, lane, M, N);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned old = __hip_atomic_fetch_add(fx.cnt + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned last = old == (unsigned)(fx.S - 1);
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            __hip_atomic_store(fx.cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate completes before the barrier
-        }
-        *flag = last;
-    }
-    __syncthreads();
-    if (*flag == 0u) return false;
-    fix_combine<TR, TM, TN>(fx, acc, pbase, MN, mb, nb, lane, M, N);
-    return true;
-}
-
 // Block coordinates of the NT kernels after the XCD remap: logical id -> (phase fastest, then tile, then
 // K-split), so the phases and N-tiles of one M-tile (which gather the same A rows) run on one XCD.
 #define NT_BLOCK_COORDS()                                                                                  \
@@ -706,7 +591,7 @@ __device__ __forceinline__ int nt_lds_chunk(int row, int c) {
 // phase's blocks streaming the whole input again).
 template <typename T, int BM, int BN, int WM, int WN, int KCH, class AL, class BL, class EP, bool TR = false>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap,
-                                                      int ploop, SplitFix fx) {
+                                                      int ploop) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;  // LDS rows of KCH 16-byte chunks, chunk positions swizzled (nt_lds_chunk)
     constexpr int WAVES_N = BN / WN;
@@ -849,12 +734,6 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(AL al, BL bl, EP ep, int M
             __syncthreads();
         }
     }
-    if (fx.S > 1) {  // in-launch split-K combine (ploop == 1: the launcher's condition)
-        __shared__ unsigned fixflag;
-        if (!fix_arrive<TR, TM, TN>(fx, acc, &fixflag, ph, bz, (unsigned)(ph * gridDim.x + tile_), m0 + wm0, n0 + wn0,
-                                    lane, M, N))
-            return;
-    }
     double cs[TR ? TN * 4 : TN], cq[TR ? TN * 4 : TN];
     if constexpr (TR)
         epilogue_tile_t<TM, TN, EP, sizeof(T) == 2>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N,
@@ -914,8 +793,7 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int NS, class AL, class BL, class EP, bool TR = false>
-__global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap,
-                                                           SplitFix fx) {
+__global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = 8 * V;                       // 128-byte tile rows
     constexpr int ASZ = BM * 128, BSZ = BN * 128, STG = ASZ + BSZ;
@@ -1015,11 +893,6 @@ __global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, 
             }
         }
     }
-    // in-launch split-K combine; the flag word is the ring's first word (every DMA has landed: the last K-step
-    // waited vmcnt(0), and every wave is past its MFMAs at fix_arrive's first barrier)
-    if (fx.S > 1 && !fix_arrive<TR, TM, TN>(fx, acc, reinterpret_cast<unsigned*>(smem), phase, bz,
-                                            (unsigned)(phase * gx_ + tile_), m0 + wm0, n0 + wn0, lane, M, N))
-        return;
     double cs[TR ? TN * 4 : TN], cq[TR ? TN * 4 : TN];
     if constexpr (TR)
         epilogue_tile_t<TM, TN, EP, sizeof(T) == 2>(ep, acc, m0 + wm0, n0 + wn0, lane, M, N,

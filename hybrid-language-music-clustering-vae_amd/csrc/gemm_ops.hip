@@ -109,31 +109,20 @@ inline bool use_ploop(int phases, int tmn, int pipe, bool with_stats) {
 // strides: the conv / sub-pixel NHWC outputs and their split-K slabs), else the per-element epilogue (linears)
 template <typename T, int BM, int BN, int WM, int WN, bool TR, class AL, class BL, class E>
 void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
-                         bool long_k, int pipe, SplitFix fx = SplitFix{}) {
+                         bool long_k, int pipe) {
     const int rm = xcd_remap_for_site();
-    const int ploop = (fx.S <= 1 && use_ploop((int)grid.y, (int)grid.x, pipe, E::kStatMode == 1)) ? (int)grid.y : 1;
+    const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe, E::kStatMode == 1) ? (int)grid.y : 1;
     if (ploop > 1) grid.y = 1;
     HLMC_PROBE_BEGIN(s);
     if (pipe == 3)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, fx);
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (pipe == 4)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, fx);
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (long_k)
-        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop, fx);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     else
-        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop, fx);
+        gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     HLMC_PROBE_END(s);
-}
-// In-launch split-K combine (gemm.hpp SplitFix) where S x tile bytes <= HLMC_SPLITK_FIX KiB; default 0 = never.
-// Measured (round 4, bench_gemm.py and 3 alternating bench rounds): 128 x 128 tiles at S = 4 (256 KiB) +3 us and at
-// S = 15 (960 KiB) +20 us per layer against the separate reduce launch (the combining block reads the partials
-// serially); step 122.1k / 122.8k / 122.4k clips/s at 128 / 64 / 256 KiB against 123.4k with the reduce launches.
-inline int splitk_fix_max_kib() {
-    static const int kib = [] {
-        const char* e = std::getenv("HLMC_SPLITK_FIX");
-        return e ? std::atoi(e) : 0;
-    }();
-    return kib;
 }
 // HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid).  Measured per layer
 // (scripts/bench_gemm.py, round 3): the transposed epilogue takes the split-K / LDS-DMA conv and sub-pixel GEMMs from
@@ -175,23 +164,6 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     }
     size_t need = (size_t)phases * pl.S * M * N * sizeof(float);
     HLMC_CHECK_ARG(ws.p && ws.bytes >= need, "split-K workspace too small");
-    if (ws.cnt && (int64_t)pl.S * BM * BN * 4 <= (int64_t)splitk_fix_max_kib() * 1024 &&
-        (int64_t)tmn * phases <= ws.ncnt && need < 0x80000000ull) {
-        // in-launch combine (gemm.hpp SplitFix): the tile's last block reduces the slabs and runs the final epilogue
-        const SplitFix fx{ws.p, ws.cnt, (unsigned)need, pl.S};
-        if (stats) {
-            WithStats<EP> eps;
-            static_cast<EP&>(eps) = ep;
-            eps.acc = st->acc;
-            nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, eps, M, N, pl.ksl, long_k, pipe, fx);
-            HLMC_LAUNCHED();
-            st->done = true;
-            return HLMC_OK;
-        }
-        nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, ep, M, N, pl.ksl, long_k, pipe, fx);
-        HLMC_LAUNCHED();
-        return HLMC_OK;
-    }
     StorePartialZ part;
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
     nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe);

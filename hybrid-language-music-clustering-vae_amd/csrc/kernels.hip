@@ -185,7 +185,6 @@ struct BnFin {
     int64_t* nbt = nullptr;
     float momentum = 0.f, eps = 0.f;
     float *dgamma = nullptr, *dbeta = nullptr;  // backward outputs (block 0)
-    const float *gamma = nullptr, *beta = nullptr;  // (convT_c1's input BatchNorm)
 };
 // The per-channel values from the totals tot (LDS, 2C doubles): fwd mean / invstd, bwd sum dz / sum dz*xhat
 template <bool kFwd>
@@ -385,17 +384,7 @@ __global__ __launch_bounds__(64) void bn_bwd_finalize_kernel(XAcc acc, int C, fl
 // kFin: sum dz / sum dz*xhat folded here from the moments' partial table (bn_fin_prologue; block 0 stores
 // dgamma / dbeta) instead of read from `sums`
 // (unconditional clamped loads and stores: bn_bwd_moments_kernel; a clamped row's store rewrites the same value)
-// kWc1 (the encoder's first BatchNorm layer, whose dy feeds only the single-channel input conv's weight gradient):
-// instead of storing dy, each thread accumulates that gradient's products dy[row][c] * x[tap of row] (the 9 f32 input
-// taps of the row's output pixel, prefetched with the row) and the block writes its [C x 9] partial to
-// wc.part[blockIdx.x] -- the wgrad_c1 launch and one write + read of dy are gone.
-struct Wc1 {
-    const float* x = nullptr;  // [B, 2 Hl, 2 Wl] single-channel input of the conv
-    int Hl = 0, Wl = 0;         // conv output (= this BatchNorm layer's) height / width
-    FastDiv dWl, dHl;
-    float* part = nullptr;      // [gridDim.x][C * 9] (co-major, tap minor: the torch [co][1][kh][kw] order)
-};
-template <typename T, bool kMask, bool kFin, int ACT = -1, bool kWc1 = false>
+template <typename T, bool kMask, bool kFin, int ACT = -1>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
                                                            int64_t R, int C, const float* __restrict__ mean,
                                                            const float* __restrict__ invstd,
@@ -403,7 +392,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ beta, int act,
                                                            const uint8_t* __restrict__ mask, float mscale,
                                                            const float* __restrict__ sums, T* __restrict__ dy,
-                                                           int64_t rows_per_blk, XAcc bias_acc, BnFin fin, Wc1 wc) {
+                                                           int64_t rows_per_blk, XAcc bias_acc, BnFin fin) {
     constexpr int V = Vec16<T>::N;
     __shared__ double s1[2048];
     const int tpr = C / V, rpp = kThreads / tpr;
@@ -420,35 +409,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 #pragma unroll
     for (int v = 0; v < V; ++v) a[v] = 0.f;
     uint4 nx[kUb], ng[kUb];  // next step's rows (clamped, always in-bounds)
-    constexpr int NT = kWc1 ? 9 : 1;
-    float nt[kUb][NT];       // kWc1: the next rows' input taps (zero outside the image: the conv's padding)
-    float wacc[kWc1 ? V : 1][NT];
-#pragma unroll
-    for (int v = 0; v < (kWc1 ? V : 1); ++v)
-#pragma unroll
-        for (int t = 0; t < NT; ++t) wacc[v][t] = 0.f;
     auto fetch = [&](int64_t rb) {
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
             const int64_t rc = min(rb + u * rpp, r1 - 1);
             nx[u] = load16_raw(y + rc * C + c0);
             ng[u] = load16_raw(da + rc * lda + c0);
-            if constexpr (kWc1) {
-                const int q = (int)rc;  // rows < 2^31 (checked by the launcher)
-                const int t = (int)wc.dWl.div((uint32_t)q), ow = q - t * wc.Wl;
-                const int b = (int)wc.dHl.div((uint32_t)t), oh = t - b * wc.Hl;
-                const int Wi = 2 * wc.Wl;
-                const float* xr = wc.x + ((int64_t)b * 2 * wc.Hl + 2 * oh - 1) * Wi + 2 * ow - 1;
-#pragma unroll
-                for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-                    for (int kw = 0; kw < 3; ++kw) {
-                        const bool in = 2 * oh - 1 + kh >= 0 && 2 * ow - 1 + kw >= 0;
-                        const float* p = in ? xr + kh * Wi + kw : wc.x;  // clamped address, zeroed below
-                        const float xv = *p;
-                        nt[u][kh * 3 + kw] = in ? xv : 0.f;
-                    }
-            }
         }
     };
     fetch(r0 + rr);  // in flight during the finalize prologue
@@ -466,14 +432,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     }
     for (int64_t r = r0 + rr; r < r1; r += kUb * rpp) {
         uint4 rx[kUb], rg[kUb];
-        float tx[kUb][NT];
 #pragma unroll
-        for (int u = 0; u < kUb; ++u) {
-            rx[u] = nx[u];
-            rg[u] = ng[u];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) tx[u][t] = nt[u][t];
-        }
+        for (int u = 0; u < kUb; ++u) { rx[u] = nx[u]; rg[u] = ng[u]; }
         fetch(r + kUb * rpp);
 #pragma unroll
         for (int u = 0; u < kUb; ++u) {
@@ -492,41 +452,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                 if constexpr (kMask) dz = mask[rc * C + c0 + v] ? dz * mscale : 0.f;
                 o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
             }
-            if constexpr (!kWc1) store16_f32(dy + rc * C + c0, o);
+            store16_f32(dy + rc * C + c0, o);
             // the bias grad is the sum of the dy actually stored (rounded to T), each row once
 #pragma unroll
-            for (int v = 0; v < V; ++v) {
-                const float d = valid ? to_f32<T>(from_f32<T>(o[v])) : 0.f;
-                a[v] += d;
-                if constexpr (kWc1) {
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) wacc[v][t] = fmaf(d, tx[u][t], wacc[v][t]);
-                }
-            }
+            for (int v = 0; v < V; ++v) a[v] += valid ? to_f32<T>(from_f32<T>(o[v])) : 0.f;
         }
-    }
-    if constexpr (kWc1) {
-        // the block's [C][9] partial: the tpr-strided lanes of one channel group (lane % tpr) summed by xor shuffles,
-        // the waves in order through LDS (s1 as floats, before the bias block_colsum reuses it)
-        float* red = reinterpret_cast<float*>(s1);  // [4 waves][C * 9]
-        const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-        for (int v = 0; v < V; ++v)
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                float w = wacc[v][t];
-                for (int o = tpr; o < 64; o <<= 1) w += __shfl_xor(w, o, 64);
-                wacc[v][t] = w;
-            }
-        if (lane < tpr)
-#pragma unroll
-            for (int v = 0; v < V; ++v)
-#pragma unroll
-                for (int t = 0; t < NT; ++t) red[wave * C * 9 + (c0 + v) * 9 + t] = wacc[v][t];
-        __syncthreads();
-        for (int i = tid; i < C * 9; i += kThreads)
-            wc.part[(int64_t)blockIdx.x * C * 9 + i] = (red[i] + red[C * 9 + i]) + (red[2 * C * 9 + i] + red[3 * C * 9 + i]);
-        __syncthreads();  // s1 reused below
     }
     if (bias_acc.on()) {
         double ad[V];
@@ -621,30 +551,18 @@ struct C1Fuse {
     XAcc acc;  // 2 CO columns
     const void* ybn = nullptr;
     const float *mean = nullptr, *invstd = nullptr, *gamma = nullptr, *beta = nullptr;
-    // MODE 3 = MODE 2 + the output convT's weight and bias gradients: the layer's input activation
-    // a = LeakyReLU(BN(ybn)) (recomputed from the loaded ybn, rounded to T as the forward stored it) times the same
-    // 9 x taps the data gradient reads; the block's [CO * 9] partial and its bias partial (the 4 taps kh, kw >= 1 cover
-    // every high-res pixel once) go to part[blockIdx.x][CO * 9 + 1]
-    float* part = nullptr;
 };
 // Weights in LDS as [tap][CO] (each tap's 8 channels of a thread: two float4 reads), U = 2 pixels' tap loads in flight
 // per step; launch bounds keep >= 4 waves per SIMD (the per-pixel register set is small: no weights in registers).
 template <typename T, int CO, int MODE>
-__global__ __launch_bounds__(256, MODE == 3 ? 2 : MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
+__global__ __launch_bounds__(256, MODE == 2 ? 3 : 4) void conv_c1_s2_kernel(const float* __restrict__ x, int B, int Hi, int Wi,
                                                             const float* __restrict__ w, const float* __restrict__ bias,
                                                             T* __restrict__ y, FastDiv dWo, FastDiv dHo, C1Fuse fz) {
     constexpr int V = Vec16<T>::N, G = CO / V;  // threads per pixel
     constexpr int U = 2;                        // pixels per thread per step
-    constexpr bool kWg = MODE == 3;
     __shared__ __attribute__((aligned(16))) float wsh[9 * CO];
     __shared__ __attribute__((aligned(16))) float bsh[CO];
     __shared__ double fred[MODE ? 4 * CO : 1];
-    __shared__ float wred[kWg ? 4 * (9 * CO + 1) : 1];
-    float wacc[kWg ? V : 1][kWg ? 9 : 1], bacc = 0.f;
-#pragma unroll
-    for (int v = 0; v < (kWg ? V : 1); ++v)
-#pragma unroll
-        for (int k = 0; k < (kWg ? 9 : 1); ++k) wacc[v][k] = 0.f;
     for (int i = threadIdx.x; i < 9 * CO; i += blockDim.x) {
         const int tap = i / CO, c = i - tap * CO;
         wsh[i] = w[c * 9 + tap];
@@ -656,7 +574,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 2 : MODE == 2 ? 3 : 4) void conv_c
     float bmu[V], bis[V], bga[V], bbe[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) fa[v] = fb[v] = 0.f;
-    if constexpr (MODE >= 2) {
+    if constexpr (MODE == 2) {
         BnChan::load(fz.mean, c0, bmu);
         BnChan::load(fz.invstd, c0, bis);
         BnChan::load(fz.gamma, c0, bga);
@@ -684,7 +602,7 @@ __global__ __launch_bounds__(256, MODE == 3 ? 2 : MODE == 2 ? 3 : 4) void conv_c
 #pragma unroll
                 for (int kw = 0; kw < 3; ++kw)
                     in[u][kh * 3 + kw] = (2 * oh - 1 + kh >= 0 && 2 * ow - 1 + kw >= 0) ? xr[kh * Wi + kw] : 0.f;
-            if constexpr (MODE >= 2) yraw[u] = load16_raw(static_cast<const T*>(fz.ybn) + (int64_t)p * CO + c0);
+            if constexpr (MODE == 2) yraw[u] = load16_raw(static_cast<const T*>(fz.ybn) + (int64_t)p * CO + c0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -714,51 +632,19 @@ __global__ __launch_bounds__(256, MODE == 3 ? 2 : MODE == 2 ? 3 : 4) void conv_c
                     fa[v] += q;
                     fb[v] = fmaf(q, q, fb[v]);
                 }
-            } else if constexpr (MODE >= 2) {
+            } else if constexpr (MODE == 2) {
                 float xb[V];
                 cvt16_f32<T>(yraw[u], xb);
 #pragma unroll
                 for (int v = 0; v < V; ++v) {
                     const float g = to_f32<T>(from_f32<T>(o[v]));  // the stored gradient
                     const float xh = (xb[v] - bmu[v]) * bis[v];
-                    const float z = xh * bga[v] + bbe[v];
-                    const float dz = g * (z > 0.f ? 1.f : 0.01f);
+                    const float dz = g * (xh * bga[v] + bbe[v] > 0.f ? 1.f : 0.01f);
                     fa[v] += dz;
                     fb[v] = fmaf(dz, xh, fb[v]);
-                    if constexpr (kWg) {
-                        const float a = to_f32<T>(from_f32<T>(z > 0.f ? z : 0.01f * z));  // the forward's activation
-#pragma unroll
-                        for (int k = 0; k < 9; ++k) wacc[v][k] = fmaf(a, in[u][k], wacc[v][k]);
-                    }
                 }
-                if constexpr (kWg)
-                    if (c0 == 0) bacc += (in[u][4] + in[u][5]) + (in[u][7] + in[u][8]);
             }
         }
-    }
-    if constexpr (kWg) {
-        // the block's [CO][9] weight-gradient partial and its bias partial: lanes of one channel group (lane % G)
-        // by xor shuffles, the 4 waves in order through LDS
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-        for (int v = 0; v < V; ++v)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                float s = wacc[v][k];
-                for (int o = G; o < 64; o <<= 1) s += __shfl_xor(s, o, 64);
-                wacc[v][k] = s;
-            }
-        for (int o = G; o < 64; o <<= 1) bacc += __shfl_xor(bacc, o, 64);
-        constexpr int NP = 9 * CO + 1;
-        if (lane < G)
-#pragma unroll
-            for (int v = 0; v < V; ++v)
-#pragma unroll
-                for (int k = 0; k < 9; ++k) wred[wave * NP + (c0 + v) * 9 + k] = wacc[v][k];
-        if (lane == 0) wred[wave * NP + 9 * CO] = bacc;  // lane 0: channel group 0
-        __syncthreads();
-        for (int i = threadIdx.x; i < NP; i += blockDim.x)
-            fz.part[(int64_t)blockIdx.x * NP + i] = (wred[i] + wred[NP + i]) + (wred[2 * NP + i] + wred[3 * NP + i]);
     }
     if constexpr (MODE != 0) {
         double da_[V], db_[V];
@@ -779,29 +665,15 @@ __global__ __launch_bounds__(256, MODE == 3 ? 2 : MODE == 2 ? 3 : 4) void conv_c
 // (Supersedes one thread per output pixel, whose per-tap loads waited one round trip each: 47 us at B = 256.)
 // (launch bounds: >= 4 waves per SIMD; unbounded, hipcc hoisted every LDS weight read out of the pixel loop into
 // 450 registers -> one wave per SIMD)
-// XIN (train mode): x is the PRE-BatchNorm map of the last decoder layer; its BatchNorm (statistics folded from the
-// producer's exact accumulator, block 0 storing mean / invstd / running statistics, as bn_act_kernel<kFin>) and
-// LeakyReLU are applied to every loaded chunk, rounded to T as bn_act would store the activation -- that bn_act launch
-// (a read and a write of the whole map) is gone; the backward recomputes the activation where it needs it
-// (conv_c1_s2 MODE 3).
-template <typename T, int CI, bool XIN = false>
+template <typename T, int CI>
 __global__ __launch_bounds__(256, 4) void convT_c1_kernel(const T* __restrict__ x, int B, int Hi, int Wi,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
-                                                       float* __restrict__ y, FastDiv dWi, FastDiv dHi, BnFin fin) {
+                                                       float* __restrict__ y, FastDiv dWi, FastDiv dHi) {
     constexpr int V = Vec16<T>::N, NC = CI / V;  // 16-byte chunks per pixel
     __shared__ __attribute__((aligned(16))) float wt[9 * CI];
-    __shared__ __attribute__((aligned(16))) float bnp[XIN ? 4 * CI : 4];  // mean | invstd | gamma | beta
-    __shared__ double fsh[XIN ? 2 * CI + 3 * kThreads : 1];
     for (int i = threadIdx.x; i < 9 * CI; i += blockDim.x) {
         const int tap = i / CI, ci = i - tap * CI;
         wt[i] = w[ci * 9 + tap];
-    }
-    if constexpr (XIN) {
-        for (int c = threadIdx.x; c < CI; c += blockDim.x) {
-            bnp[2 * CI + c] = fin.gamma[c];
-            bnp[3 * CI + c] = fin.beta[c];
-        }
-        bn_fin_prologue<true>(fin, CI, fsh, reinterpret_cast<long long*>(fsh + 2 * CI), bnp, bnp + CI);  // + barrier
     }
     __syncthreads();
     const float b0 = bias ? bias[0] : 0.f;
@@ -835,23 +707,6 @@ __global__ __launch_bounds__(256, 4) void convT_c1_kernel(const T* __restrict__ 
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
                 cvt16_f32<T>(raw[n][j], v[n]);
-                if constexpr (XIN) {
-#pragma unroll
-                    for (int e4 = 0; e4 < V / 4; ++e4) {
-                        const int c = j * V + 4 * e4;
-                        const float4 mu = *reinterpret_cast<const float4*>(bnp + c);
-                        const float4 is = *reinterpret_cast<const float4*>(bnp + CI + c);
-                        const float4 ga = *reinterpret_cast<const float4*>(bnp + 2 * CI + c);
-                        const float4 be = *reinterpret_cast<const float4*>(bnp + 3 * CI + c);
-                        const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {is.x, is.y, is.z, is.w};
-                        const float g4[4] = {ga.x, ga.y, ga.z, ga.w}, b4[4] = {be.x, be.y, be.z, be.w};
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const float z = (v[n][4 * e4 + q] - m4[q]) * i4[q] * g4[q] + b4[q];
-                            v[n][4 * e4 + q] = to_f32<T>(from_f32<T>(act_fwd(z, 0)));
-                        }
-                    }
-                }
 #pragma unroll
                 for (int e = 0; e < V; ++e) v[n][e] = nbok[n] ? v[n][e] : 0.f;
             }
@@ -1469,8 +1324,7 @@ int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, XAcc acc, bool hav
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
-               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums,
-               const Wc1Grad* wg) {
+               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums) {
     HLMC_TRY(check_bn_shape<T>(C));
     HLMC_TRY(check_acc(mom, 2 * C));
     if (bias_acc.on()) HLMC_TRY(check_acc(bias_acc, C));
@@ -1498,36 +1352,15 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
         bn_bwd_finalize_kernel<<<fin_grid(C), 64, 0, s>>>(mom, C, dgamma, dbeta, sums);
         HLMC_LAUNCHED();
     }
-    if (wg) {  // the first conv's weight gradient from the apply pass (no dy stored)
-        HLMC_CHECK_ARG(fin_here && !mask && act == 0 && C == 32 && lda == C && R < (1ll << 31) && wg->x && wg->dW &&
-                       wg->part && wg->part_floats >= (int64_t)nblk * C * 9 && R == (int64_t)wg->B * wg->Hl * wg->Wl,
-                       "bn_act_bwd: fused first-layer weight gradient arguments");
-        Wc1 wc;
-        wc.x = wg->x; wc.Hl = wg->Hl; wc.Wl = wg->Wl; wc.dWl = FastDiv((uint32_t)wg->Wl); wc.dHl = FastDiv((uint32_t)wg->Hl);
-        wc.part = wg->part;
-        HLMC_BN_PROBED(s, 2.0 * sizeof(T) * R * C + 4.0 * R * 4,
-                       (bn_bwd_apply_kernel<T, false, true, 0, true><<<nblk, kThreads, 0, s>>>(
-                           da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums, dy, rpb, bias_acc, bf, wc)));
-        HLMC_LAUNCHED();
-        sum_partials_f32_kernel<<<C * 9, 256, 0, s>>>(wg->part, nblk, C * 9, wg->dW);
-        HLMC_LAUNCHED();
-        if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
-        return HLMC_OK;
-    }
     auto ka = mask ? (fin_here ? bn_bwd_apply_kernel<T, true, true> : bn_bwd_apply_kernel<T, true, false>)
               : act == 0 ? (fin_here ? bn_bwd_apply_kernel<T, false, true, 0> : bn_bwd_apply_kernel<T, false, false, 0>)
                          : (fin_here ? bn_bwd_apply_kernel<T, false, true> : bn_bwd_apply_kernel<T, false, false>);
     HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C,
                    (ka<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, mask, mscale, sums,
-                                                 dy, rpb, bias_acc, bf, Wc1{})));
+                                                 dy, rpb, bias_acc, bf)));
     HLMC_LAUNCHED();
     if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
     return HLMC_OK;
-}
-int bn_wc1_part_floats(int64_t R, int C) { return bn_blocks(R, C) * C * 9; }
-int convt_c1_part_floats(int B, int Hi, int Wi) {
-    const int64_t nthr = (int64_t)B * (Hi / 2) * (Wi / 2) * 4;
-    return grid_for(nthr, kThreads, kC1FusedBlocks) * (9 * 32 + 1);
 }
 int colsum_to_f64(hipStream_t s, XAcc acc, int C, double* out) {
     HLMC_CHECK_ARG(out && C > 0, "colsum_to_f64: bad arguments");
@@ -1547,7 +1380,7 @@ int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out) {
 
 template <typename T>
 int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y,
-               ColStats* st, BnBwdFuse* bf, const ConvTGrad* wg) {
+               ColStats* st, BnBwdFuse* bf) {
     HLMC_CHECK_ARG(Co == 32 && Hi % 2 == 0 && Wi % 2 == 0, "conv_c1_s2: only Co == 32, even H/W");
     int64_t nthr = (int64_t)B * (Hi / 2) * (Wi / 2) * (32 / Vec16<T>::N);
     HLMC_CHECK_ARG(nthr < (int64_t)1 << 31, "conv_c1_s2: too many pixels");
@@ -1567,19 +1400,7 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
         const int g = grid_for(nthr, kThreads, kC1FusedBlocks);
         fz.acc = bf->acc;
         fz.ybn = bf->y; fz.mean = bf->mean; fz.invstd = bf->invstd; fz.gamma = bf->gamma; fz.beta = bf->beta;
-        if (wg) {  // + the output convT's weight and bias gradients (its input activation is this layer's)
-            constexpr int NP = 9 * 32 + 1;
-            HLMC_CHECK_ARG(wg->dW && wg->db && wg->part && wg->part_floats >= (int64_t)g * NP,
-                           "conv_c1_s2: fused convT gradient arguments");
-            fz.part = wg->part;
-            conv_c1_s2_kernel<T, 32, 3><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
-            HLMC_LAUNCHED();
-            sum_partials_f32_kernel<<<NP - 1, 256, 0, s>>>(wg->part, g, NP, wg->dW);
-            HLMC_LAUNCHED();
-            sum_partials_f32_kernel<<<1, 256, 0, s>>>(wg->part + (NP - 1), g, NP, wg->db);
-        } else {
-            conv_c1_s2_kernel<T, 32, 2><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
-        }
+        conv_c1_s2_kernel<T, 32, 2><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, fz);
         bf->done = true;
     } else {
         conv_c1_s2_kernel<T, 32, 0><<<grid_for(nthr, kThreads, 16384), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH,
@@ -1590,26 +1411,14 @@ int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float
 }
 
 template <typename T>
-int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y,
-             const BnInput* xin) {
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y) {
     HLMC_CHECK_ARG(Ci == 32, "convT_c1: only Ci == 32");
     int64_t npix = (int64_t)B * 4 * Hi * Wi;
     HLMC_CHECK_ARG(npix < (int64_t)1 << 31, "convT_c1: too many pixels");
     HLMC_CHECK_ARG(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "convT_c1: alignment");
     const FastDiv dW((uint32_t)Wi), dH((uint32_t)Hi);
-    const unsigned g = (unsigned)((npix / 4 + kThreads - 1) / kThreads);
-    if (xin) {
-        HLMC_TRY(check_acc(xin->acc, 2 * Ci));
-        HLMC_CHECK_ARG(xin->R == (int64_t)B * Hi * Wi && xin->mean && xin->invstd && xin->gamma && xin->beta,
-                       "convT_c1: input BatchNorm arguments");
-        BnFin f;
-        f.acc = xin->acc; f.R = xin->R; f.mean = xin->mean; f.invstd = xin->invstd; f.rmean = xin->rmean;
-        f.rvar = xin->rvar; f.nbt = xin->nbt; f.momentum = xin->momentum; f.eps = xin->eps;
-        f.gamma = xin->gamma; f.beta = xin->beta;
-        convT_c1_kernel<T, 32, true><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, f);
-    } else {
-        convT_c1_kernel<T, 32><<<g, kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y, dW, dH, BnFin{});
-    }
+    convT_c1_kernel<T, 32><<<(unsigned)((npix / 4 + kThreads - 1) / kThreads), kThreads, 0, s>>>(x, B, Hi, Wi, w, bias, y,
+                                                                                              dW, dH);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
@@ -1888,11 +1697,10 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
                                  T*, int);                                                                           \
     template int bn_act_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,          \
                                const float*, const float*, int, const uint8_t*, float, T*, float*, float*, XAcc,      \
-                               const BnBwdFuse*, XAcc, float*, float*, const Wc1Grad*);                              \
+                               const BnBwdFuse*, XAcc, float*, float*);                                              \
     template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*,        \
-                               ColStats*, BnBwdFuse*, const ConvTGrad*);                                             \
-    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*,         \
-                             const BnInput*);                                                                        \
+                               ColStats*, BnBwdFuse*);                                                               \
+    template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);         \
     template int wgrad_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, float*, Ws);                    \
     template int cast_from_f32<T>(hipStream_t, const float*, T*, int64_t);                                           \
     template int cast_to_f32<T>(hipStream_t, const T*, float*, int64_t);                                             \

@@ -8,10 +8,6 @@ namespace hlmc {
 struct Ws {  // split-K / reduction scratch handed down by the caller
     float* p;
     size_t bytes;
-    // in-launch split-K combine (gemm.hpp SplitFix): ncnt arrival counters, zero on entry to every launch that uses
-    // them (each combining block resets its own); nullptr = a separate reduce launch
-    unsigned* cnt = nullptr;
-    int ncnt = 0;
 };
 
 namespace ops {
@@ -92,24 +88,12 @@ size_t linear_wgrad_ws(int Mb, int N, int K);
 
 // ---------------------------------------------------------------- edge convs with one channel (kernels.hip)
 // y[B,Hi/2,Wi/2,32] = sum_taps x[B,Hi,Wi] * w[co*9+tap] (+ bias)  (conv1 fwd, convT6 dgrad)
-// wg (with bf, the output convT's data gradient): that convT's weight gradient dW[ci][1][3][3] and bias gradient
-// db[1] from the same pass (its input activation recomputed from bf's pre-BN map); part: convt_c1_part_floats floats
-struct ConvTGrad {
-    float* dW = nullptr;
-    float* db = nullptr;
-    float* part = nullptr;
-    int64_t part_floats = 0;
-};
-int convt_c1_part_floats(int B, int Hi, int Wi);
 template <typename T>
 int conv_c1_s2(hipStream_t s, const float* x, int B, int Hi, int Wi, const float* w, const float* bias, int Co, T* y,
-               ColStats* st = nullptr, BnBwdFuse* bf = nullptr, const ConvTGrad* wg = nullptr);
-// y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel).  xin (train mode,
-// nullable): x is the pre-BatchNorm map; its BatchNorm + LeakyReLU (statistics from xin->acc) applied as it is loaded
-// (xin->a_out unused: the activation is not stored)
+               ColStats* st = nullptr, BnBwdFuse* bf = nullptr);
+// y[B,2Hi,2Wi] = convT(x[B,Hi,Wi,Ci]) with w[ci*9+tap] + bias (convT6 fwd, 1 output channel)
 template <typename T>
-int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y,
-             const BnInput* xin = nullptr);
+int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const float* w, const float* bias, float* y);
 // dW[m*9+tap] = sum L[b,r,c,m] * Xh[b, 2r-1+kh, 2c-1+kw]   (Xh single channel f32)
 template <typename T>
 int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws);
@@ -147,22 +131,10 @@ int bn_act(hipStream_t s, const T* y, int64_t R, int C, const float* mean, const
 // of dy (the conv bias gradient) are added there; dbias (nullable, needs bias_acc): also reduce them into dbias
 // here (else the caller runs colsum_finalize, e.g. on the weight-gradient stream).  sums: 2C floats of scratch,
 // needed for C > 512 only.
-// The encoder's first conv (1 input channel) weight gradient computed by the BatchNorm backward of its output
-// (bn_act_bwd wg): dW[co][tap] = sum over the rows of dy[row][co] * x[tap of the row's pixel]; dy is not stored.
-// part: >= bn_wc1_part_floats(R, C) floats of scratch.
-struct Wc1Grad {
-    const float* x = nullptr;  // [B, 2 Hl, 2 Wl]
-    int B = 0, Hl = 0, Wl = 0;
-    float* dW = nullptr;        // [C][1][3][3]
-    float* part = nullptr;
-    int64_t part_floats = 0;
-};
-int bn_wc1_part_floats(int64_t R, int C);
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
-               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums,
-               const Wc1Grad* wg = nullptr);
+               float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums);
 // out[c] = total of column c of acc (C columns)
 int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out);
 // out[c] (f64) = column c of an exact accumulator (the op-level statistics entry)

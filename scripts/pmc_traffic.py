@@ -19,9 +19,9 @@ import re
 import sys
 
 KINDS = {  # op kind of include/hlmc.h hlmc_probe_arm -> kernel-name pattern
-    "conv_s2": r"gemm_nt\w*<.*ConvS2Loader",
-    "subpixel": r"gemm_nt\w*<.*SubpixelLoader",
-    "wgrad_s2": r"gemm_tn_kernel<.*KRowConvS2",
+    "conv_s2": r"(gemm_nt\w*<.*ConvS2Loader|conv_s2_halo_kernel)",
+    "subpixel": r"(gemm_nt\w*<.*SubpixelLoader|subpixel_halo_kernel)",
+    "wgrad_s2": r"(gemm_tn_kernel<.*KRowConvS2|wgrad_halo_kernel)",
     "linear": r"gemm_nt\w*<[^<>]*, hlmc::DenseLoader<",
     "linear_wgrad": r"gemm_tn_kernel<[^<>]*, hlmc::(\(anonymous namespace\)::)?KRowDenseV?<[^<>]*>, hlmc::(\(anonymous namespace\)::)?KRowDenseV?<",
     "stft_mel": r"stft_mel0?_kernel",

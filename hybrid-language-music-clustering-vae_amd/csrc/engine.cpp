@@ -231,8 +231,9 @@ class NetT : public NetBase {
         if (use_side && !s2) {
             HLMC_HIP(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
             evs.resize(32);
-            for (auto& e : evs) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            HLMC_HIP(hipEventCreateWithFlags(&prelate_ev, hipEventDisableTiming));
+            const unsigned fl = hipEventDisableTiming | fork_event_scope();
+            for (auto& e : evs) HLMC_HIP(hipEventCreateWithFlags(&e, fl));
+            HLMC_HIP(hipEventCreateWithFlags(&prelate_ev, fl));
         }
         if (this->bucket_sync && this->bucket_ev.size() != this->bucket_starts.size()) {
             for (auto e : this->bucket_ev) (void)hipEventDestroy(e);
@@ -240,6 +241,20 @@ class NetT : public NetBase {
             for (auto& e : this->bucket_ev) HLMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         return HLMC_OK;
+    }
+    // fence of the fork / join events.  Both streams run on this device: the kernels' own device-scope
+    // release / acquire order every cross-stream hand-off, and the system-scope fence HIP adds to an event by
+    // default (host visibility, which no fork needs) is what made every fork a main-stream bubble.  Measured (3
+    // alternating rounds): hipEventDisableSystemFence 126.7k vs 125.1k clips/s with HIP's default and 125.0k with
+    // hipEventReleaseToDevice.  HLMC_FORK_EV (A/B aid): 0 HIP's default, 1 device-scope release, 2 (default) no
+    // system fence
+    static unsigned fork_event_scope() {
+        static const unsigned f = [] {
+            const char* e = std::getenv("HLMC_FORK_EV");
+            const int v = e ? std::atoi(e) : 2;
+            return v == 1 ? (unsigned)hipEventReleaseToDevice : v == 2 ? (unsigned)hipEventDisableSystemFence : 0u;
+        }();
+        return f;
     }
     hipEvent_t next_ev() {
         hipEvent_t e = evs[ev_next];

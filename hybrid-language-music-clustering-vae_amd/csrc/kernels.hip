@@ -32,9 +32,20 @@ inline int bn_block_target() {
     }();
     return t;
 }
+// block target of the wide-channel layers (C >= 128: each block's partial row costs 2C x 3 accumulator atomics and
+// each apply block folds the shards of 2C columns, for 16-64 KB of rows per block at 1024 blocks).  Measured (3
+// alternating rounds): 256 blocks 127.85k clips/s vs 126.76k at 1024, 127.1k at 512, 126.8k at 128, 127.6k at 384;
+// the same target from C >= 64 127.4k, from C >= 256 127.4k.  HLMC_BN_BLOCKS_WIDE: A/B aid
+inline int bn_block_target_wide() {
+    static const int t = [] {
+        const char* e = std::getenv("HLMC_BN_BLOCKS_WIDE");
+        return e ? std::max(16, std::atoi(e)) : 256;
+    }();
+    return t;
+}
 inline int64_t bn_rows_per_blk(int64_t R, int C) {
     const int64_t step = std::max(1, 8192 / C);
-    const int64_t tb = bn_block_target();
+    const int64_t tb = C >= 128 ? bn_block_target_wide() : bn_block_target();
     const int64_t want = std::max<int64_t>(1, (R + tb - 1) / tb);
     return (want + step - 1) / step * step;
 }

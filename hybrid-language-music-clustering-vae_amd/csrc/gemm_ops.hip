@@ -449,8 +449,8 @@ __device__ __forceinline__ uint4 bn_in_apply(uint4 v, const float (&pr)[4][8]) {
 // Template: CI input channels, COB output channels per block (NSPL blocks share a tile's Co = NSPL * COB), WO
 // output width, ROWS output rows per tile (TP = ROWS * WO pixels), DB: double-buffered halo (else one buffer and
 // an extra barrier).  Shapes: 2 WO * CI / 8 == 256 (one 16-byte chunk per thread per input row).
-template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP, bool TR = true, bool XIN = false>
-__global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
+template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP, bool TR = true, bool XIN = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void conv_s2_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
                                                            const bf16* __restrict__ wp, EP ep, int M, BnIn xin) {
     constexpr int WI = 2 * WO, HR = 2 * ROWS + 1, HC = WI + 1, PS = CI + 8;  // halo rows / cols / pixel pitch
     constexpr int TP = ROWS * WO, CPP = CI / 8;                             // tile pixels, chunks per pixel
@@ -634,8 +634,9 @@ __global__ __launch_bounds__(256) void conv_s2_halo_kernel(const bf16* __restric
 // 4 phases' taps (1 + 2 + 2 + 4) read their fragments from there.
 // Template: CI input channels, COB output channels per block (NSPL blocks per tile), WI low-res width, ROWS
 // low-res rows per tile (TP = ROWS * WI = 128 pixels), DB: double-buffered halo.  WI * CI / 8 == 256.
-template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP, bool TR = true, bool XIN = false>
-__global__ __launch_bounds__(256) void subpixel_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
+// WPE: waves per SIMD the register allocation targets (2: two blocks per CU, with DB = false to fit the LDS)
+template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP, bool TR = true, bool XIN = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void subpixel_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
                                                             const bf16* __restrict__ wp, EP ep, int M, BnIn xin) {
     constexpr int HR = ROWS + 1, HC = WI + 1, PS = CI + 8, CPP = CI / 8, TP = ROWS * WI;
     static_assert(WI * CPP == 256 && TP == 128 && (COB == 32 || COB == 16), "halo chunk map / wave tiling");
@@ -1003,11 +1004,11 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
     if constexpr (std::is_same<T, bf16>::value) {
         int which;
         conv_halo_shape(Ci, Co, Wi, Hi, which);
-        // (CI, Co, Wi): (32, 64, 64) 128-pixel tiles, double-buffered halo; (64, 128, 32) two 64-channel halves per
-        // 64-pixel tile, one halo buffer (the weights take half the LDS)
-        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int tp, int nspl) -> int {
+        // (CI, Co, Wi): (32, 64, 64) below; (64, 128, 32) two 64-channel halves per 64-pixel tile, one halo buffer
+        // (the weights take half the LDS)
+        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int tp, int nspl, int cap = 256) -> int {
             const int ntiles = M / tp;  // whole output rows: tiles stay inside an image
-            const int grid = std::min(ntiles * nspl, 256);
+            const int grid = std::min(ntiles * nspl, cap);
             HLMC_PROBE_BEGIN(s);
             if (st && st->acc.on()) {
                 WithStats<StoreRM<T>> eps;
@@ -1025,10 +1026,15 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             return (int)HLMC_OK;
         };
         using StRM = WithStats<StoreRM<T>>;  // per-element epilogue (TR = false), see nt_tr_enabled
+        // (32, 64, 64): 2-row (64-pixel) tiles and one halo buffer: 64 KB (73 KB with the input BatchNorm) and 176
+        // VGPRs, two blocks per CU on a 512-block grid.  Measured in the step: forward with the input BatchNorm +
+        // statistics 49.6 -> 42.7 us, the decoder data gradient 32.2 -> 31.5 us (4-row tiles, double-buffered, one
+        // block per CU before); the same with 4-row tiles and two 32-channel blocks per tile (the halo read twice)
+        // lost (50 -> 55 us)
         if (which == 1 && conv_halo_on(1))
-            return run(conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StoreRM<T>, false>,
-                       conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false>,
-                       conv_s2_halo_kernel<32, 64, 1, 32, 4, true, StRM, false, true>, 128, 1);
+            return run(conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StoreRM<T>, false, false, 2>,
+                       conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StRM, false, false, 2>,
+                       conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StRM, false, true, 2>, 64, 1, 512);
         if (which == 2 && conv_halo_on(2))
             return run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, false>,
                        conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false>,
@@ -1061,11 +1067,13 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
     if constexpr (std::is_same<T, bf16>::value) {
         int which;
         subpixel_halo_shape(Ci, Co, Wi, Hi, which);
-        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int nspl) -> int {
+        // (nspl, cap): channel splits and grid cap of the statistics / input-BN launches; (nspl_p, cap_p): of the
+        // plain launch
+        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int nspl, int cap, int nspl_p, int cap_p) -> int {
             const int ntiles = M / 128;  // 128 low-res pixels (whole rows) per tile, inside one image
-            const int grid = std::min(ntiles * nspl, 256);
             HLMC_PROBE_BEGIN(s);
             if (st && st->acc.on()) {
+                const int grid = std::min(ntiles * nspl, cap);
                 WithStats<StoreSubpixel<T>> eps;
                 static_cast<StoreSubpixel<T>&>(eps) = ep;
                 eps.acc = st->acc;
@@ -1074,21 +1082,28 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
                 st->done = true;
             } else {
                 if (st) st->done = false;
-                kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{});
+                kern_plain<<<std::min(ntiles * nspl_p, cap_p), 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{});
             }
             HLMC_PROBE_END(s);
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
         using StSP = WithStats<StoreSubpixel<T>>;  // per-element epilogue (TR = false), see nt_tr_enabled
+        // Two blocks per CU where a block fits in half the LDS (<= 80 KB) and 256 VGPRs: one halo buffer (no
+        // double buffering: the co-resident block covers the extra barrier) and a 512-block grid.  Measured
+        // (3 alternating rounds): the 32 x 32 / Ci 64 -> Co 32 shape, all three launches, 129.3k vs 128.0k clips/s
+        // (forward 53 -> 46 us, data gradient 72 -> 56 us in the step); the 16 x 16 / Ci 128 -> Co 64 data
+        // gradient with 16 channels per block (four blocks per tile, 79 KB) 38 -> 33 us, while its statistics /
+        // input-BN forms need 90 KB (one block per CU) and lost 48 -> 68 us; the Ci 32 -> Co 64 conv with two
+        // 32-channel blocks per tile (the halo read twice) lost 50 -> 55 / 32 -> 36 us
         if (which == 1 && sp_halo_on(1))
-            return run(subpixel_halo_kernel<64, 32, 1, 32, 4, true, StoreSubpixel<T>, false>,
-                       subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false>,
-                       subpixel_halo_kernel<64, 32, 1, 32, 4, true, StSP, false, true>, 1);
+            return run(subpixel_halo_kernel<64, 32, 1, 32, 4, false, StoreSubpixel<T>, false, false, 2>,
+                       subpixel_halo_kernel<64, 32, 1, 32, 4, false, StSP, false, false, 2>,
+                       subpixel_halo_kernel<64, 32, 1, 32, 4, false, StSP, false, true, 2>, 1, 512, 1, 512);
         if (which == 2 && sp_halo_on(2))
-            return run(subpixel_halo_kernel<128, 32, 2, 16, 8, false, StoreSubpixel<T>, false>,
+            return run(subpixel_halo_kernel<128, 16, 4, 16, 8, false, StoreSubpixel<T>, false, false, 2>,
                        subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false>,
-                       subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2);
+                       subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2, 256, 4, 512);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
 }

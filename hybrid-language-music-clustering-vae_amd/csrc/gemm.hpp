@@ -792,8 +792,10 @@ __device__ __forceinline__ void glds16(const void* g, void* l) {
                                      (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, class AL, class BL, class EP, bool TR = false>
-__global__ __launch_bounds__(256) void gemm_nt_glds_kernel(AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap) {
+// WPE: waves per SIMD the register allocation targets (2 with the 2-stage ring: two blocks per CU)
+template <typename T, int BM, int BN, int WM, int WN, int NS, class AL, class BL, class EP, bool TR = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void gemm_nt_glds_kernel(
+    AL al, BL bl, EP ep, int M, int N, int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = 8 * V;                       // 128-byte tile rows
     constexpr int ASZ = BM * 128, BSZ = BN * 128, STG = ASZ + BSZ;

@@ -56,7 +56,7 @@ inline Plan plan_tn(int tiles, int K, int BK) {
     return {S, ksl};
 }
 
-// NT pipeline: 0 register-staged (gemm_nt_kernel), 3/4 = LDS-DMA ring of that many stages (gemm_nt_glds_kernel).
+// NT pipeline: 0 register-staged (gemm_nt_kernel), 2/3/4 = LDS-DMA ring of that many stages (gemm_nt_glds_kernel).
 // Measured (scripts/bench_gemm.py): the 4-stage DMA ring wins when a block reduces >= 1024 (16 K-steps),
 // the register path below that (short reductions: more co-resident blocks hide the pipeline prologue) --
 // except on split-K grids of <= 256 blocks (one block per CU: no co-residency to lose), where the ring's
@@ -72,8 +72,16 @@ inline int nt_pipe_select(int ksl, int S, int blocks) {
         const char* e = std::getenv("HLMC_GLDS_SPLIT_MAX");
         return e ? std::atoi(e) : 512;
     }();
-    if (S > 1 && blocks <= split_max) return 4;
-    return ksl >= 1024 ? 4 : 0;
+    // the ring's depth: 2 stages (64 KB of LDS, 176 VGPRs: two blocks per CU, each one K-step ahead) measured
+    // 131.9k vs 129.3k clips/s with 4 stages (128 KB, one block per CU, three K-steps ahead) and 129.7k with 3;
+    // with it, NT grid target 1024 121.7k, 384 131.6k, ring for split grids <= 1024 blocks 132.0k (3 rounds each).
+    // HLMC_GLDS_NS: A/B aid
+    static const int ring = [] {
+        const char* e = std::getenv("HLMC_GLDS_NS");
+        return e ? std::atoi(e) : 2;
+    }();
+    if (S > 1 && blocks <= split_max) return ring;
+    return ksl >= 1024 ? ring : 0;
 }
 
 // XCD-aware block order per op kind (bit = probe::k* kind; gemm.hpp xcd_logical_block).  Default from the
@@ -114,7 +122,9 @@ void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, c
     const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe, E::kStatMode == 1) ? (int)grid.y : 1;
     if (ploop > 1) grid.y = 1;
     HLMC_PROBE_BEGIN(s);
-    if (pipe == 3)
+    if (pipe == 2)
+        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 2, AL, BL, E, TR, 2><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
+    else if (pipe == 3)
         gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (pipe == 4)
         gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);

@@ -13,7 +13,7 @@ namespace {
 // linears) 512: 101.8k vs 101.2k at 256 (round 2, after the small split-K grids moved to the LDS-DMA ring;
 // round 1 measured 256 ahead of 512 and 128); TN (weight gradients) 512: 93.2k vs 92.8k at 1024, 90.7k at 2048
 constexpr int kNtTargetBlocks = 512;
-constexpr int kTnTargetBlocks = 512;
+constexpr int kTnTargetBlocks = 256;
 constexpr int kTnLongK = 131072;
 constexpr int kTnKch8Min = 1024;
 constexpr int kXcdRemapDefault = probe::kWgradS2 | probe::kLinearWgrad;  // measured: helps the TN (wgrad) family, hurts sub-pixel
@@ -43,12 +43,19 @@ inline Plan plan_tn(int tiles, int K, int BK) {
     // (>= 4 k-tiles per split); the slab reduction keeps 4 loads in flight.  The longest reductions (the
     // 32 / 64-channel layers, K = 262 144) take a 1024-block grid: per layer (scripts/gpu_wgrad_blocks.sh,
     // bench_gemm.py) 47 vs 60 us at 512, while every shorter layer is fastest at 512 (1024: +10-20 %).
-    // HLMC_TN_BLOCKS: one target grid for every layer (measurement aid).
-    static const int forced = [] {
+    // Round 4 (with the NT GEMMs at two blocks per CU beside them): one 256-block target for every layer measured
+    // 134.1k vs 132.9k clips/s at 512 / 1024 (128: 129.6k, 192: 133.6k, 320: 133.6k, 384: 132.1k, 768: 130.8k);
+    // the long layers at 512 then 134.5k vs 134.0k (1024: 134.1k).
+    // HLMC_TN_BLOCKS / HLMC_TN_BLOCKS_LONG: the targets of the shorter / K >= kTnLongK layers (measurement aids).
+    static const int t_short = [] {
         const char* e = std::getenv("HLMC_TN_BLOCKS");
-        return e ? std::max(64, std::atoi(e)) : 0;
+        return e ? std::max(64, std::atoi(e)) : kTnTargetBlocks;
     }();
-    const int target = forced ? forced : (K >= kTnLongK ? 2 * kTnTargetBlocks : kTnTargetBlocks);
+    static const int t_long = [] {
+        const char* e = std::getenv("HLMC_TN_BLOCKS_LONG");
+        return e ? std::max(64, std::atoi(e)) : 2 * t_short;
+    }();
+    const int target = K >= kTnLongK ? t_long : t_short;
     int S = cdiv(target, tiles);
     S = std::max(1, std::min(S, K / (4 * BK)));
     int ksl = cdiv(cdiv(K, S), BK) * BK;

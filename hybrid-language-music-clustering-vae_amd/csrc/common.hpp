@@ -163,7 +163,10 @@ struct XAcc {
 };
 // shards for a BatchNorm pair table (2C columns): the consumer folds shards x 6C words per block, so fewer shards for
 // wider layers (whose producers also have fewer blocks)
-inline int xacc_shards(int C) { return C >= 512 ? 2 : C >= 256 ? 4 : C >= 128 ? 8 : 16; }
+// accumulator copies per layer (block id mod shards): fewer atomics on one address vs more words for the consumers
+// to fold (xacc_fold handles <= 8 shards when 2C >= 256 columns).  Round 4: 4 / 8 / 8 for C >= 512 / 256 / 128 (was
+// 2 / 4 / 8) measured 133.9k vs 133.4k clips/s (4 rounds; 8 / 8 / 8: 133.3k)
+inline int xacc_shards(int C) { return C >= 512 ? 4 : C >= 128 ? 8 : 16; }
 constexpr int kXAccMaxShards = 16;
 
 // A non-finite partial (NaN, inf, or beyond the +-4e18 range the integer word holds) sets bit 63 of the shard's

@@ -328,23 +328,50 @@ def _free_port():
         return so.getsockname()[1]
 
 
-def relaunch_under_torchrun(n):
+def relaunch_under_torchrun(n, timeout=1800.0):
     """`--gpus N > 1` outside torch.distributed.run: run this same command line as N ranks in a child
     torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1).  Called before any GPU or libhlmc use,
     so the parent never initialises the device; the child is a subprocess, never an exec.  Rank 0's JSON line is
-    relayed to stdout, everything else the ranks print goes to stderr.  Returns the child's exit status."""
+    relayed to stdout, everything else the ranks print goes to stderr.  Returns the child's exit status, or 124 when
+    the child's process group had to be ended after `timeout` seconds (a hung rank would otherwise block forever)."""
     import subprocess
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    import signal
+    import threading
     env = dict(os.environ, HLMC_BENCH_SELF_LAUNCHED="1")
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
-    for line in proc.stdout:
-        if line.startswith("{") and '"metric"' in line:
-            sys.stdout.write(line)
-            sys.stdout.flush()
-        else:
-            sys.stderr.write(line)
-    return proc.wait()
+    # own process group, so a hung rank (e.g. stuck in a rendezvous) can be ended as a whole after the timeout
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1, start_new_session=True)
+    expired = threading.Event()
+
+    def _expire():
+        expired.set()
+        sys.stderr.write(f"bench: the {n}-rank child exceeded {timeout:.0f} s; terminating its process group\n")
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            try:
+                os.killpg(proc.pid, sig)
+            except ProcessLookupError:
+                return
+            try:
+                proc.wait(timeout=10)
+                return
+            except subprocess.TimeoutExpired:
+                pass
+
+    timer = threading.Timer(timeout, _expire)
+    timer.daemon = True
+    timer.start()
+    try:
+        for line in proc.stdout:
+            if line.startswith("{") and '"metric"' in line:
+                sys.stdout.write(line)
+                sys.stdout.flush()
+            else:
+                sys.stderr.write(line)
+        rc = proc.wait()
+    finally:
+        timer.cancel()
+    return 124 if expired.is_set() else rc
 
 
 PROBE_STEPS = int(os.environ.get("HLMC_PROBE_STEPS", "3"))  # timed steps whose dominant-kernel launches are timed

@@ -137,8 +137,10 @@ int hlmc_mfcc(const hlmc_mel_plan* cp, void* stream, const float* pcm, int64_t B
         std::vector<float> D((size_t)n_mfcc * M);
         for (int k = 0; k < n_mfcc; ++k)
             for (int m = 0; m < M; ++m) {
-                double c = std::cos(M_PI * k * (2.0 * m + 1) / (2.0 * M)) * std::sqrt(2.0 / M);
-                if (k == 0) c /= std::sqrt(2.0);
+                // scipy.fftpack.dct(type=2, norm='ortho') as a matrix; the phase k (2m + 1) reduced modulo 4M in
+                // integers so cos sees an argument below 2 pi (oracle/mel_oracle.py dct_ortho_matrix)
+                const long ph = ((long)k * (2 * m + 1)) % (4L * M);
+                const double c = k == 0 ? std::sqrt(1.0 / M) : std::cos(M_PI * ph / (2.0 * M)) * std::sqrt(2.0 / M);
                 D[(size_t)k * M + m] = (float)c;
             }
         if (p->d_dct) (void)hipFree(p->d_dct);

@@ -246,16 +246,8 @@ class NetT : public NetBase {
     // release / acquire order every cross-stream hand-off, and the system-scope fence HIP adds to an event by
     // default (host visibility, which no fork needs) is what made every fork a main-stream bubble.  Measured (3
     // alternating rounds): hipEventDisableSystemFence 126.7k vs 125.1k clips/s with HIP's default and 125.0k with
-    // hipEventReleaseToDevice.  HLMC_FORK_EV (A/B aid): 0 HIP's default, 1 device-scope release, 2 (default) no
-    // system fence
-    static unsigned fork_event_scope() {
-        static const unsigned f = [] {
-            const char* e = std::getenv("HLMC_FORK_EV");
-            const int v = e ? std::atoi(e) : 2;
-            return v == 1 ? (unsigned)hipEventReleaseToDevice : v == 2 ? (unsigned)hipEventDisableSystemFence : 0u;
-        }();
-        return f;
-    }
+    // hipEventReleaseToDevice
+    static unsigned fork_event_scope() { return (unsigned)hipEventDisableSystemFence; }
     hipEvent_t next_ev() {
         hipEvent_t e = evs[ev_next];
         ev_next = (ev_next + 1) % (int)evs.size();
@@ -320,15 +312,8 @@ class NetT : public NetBase {
     }
     // run f on the weight-gradient stream now (with everything queued before it)
     int side(hipStream_t s, SideFn f) { return defer_side(s, std::move(f), 1); }
-    // weight gradients of the dense layers: on the second stream (HLMC_DENSE_SIDE=1, default) or inline on s
-    // (their GEMMs are 5-20 us, about the main-stream bubble a fork's event marker costs)
-    bool dense_side_on() const {
-        static const bool on = [] {
-            const char* e = std::getenv("HLMC_DENSE_SIDE");
-            return !(e && e[0] == '0');
-        }();
-        return on && use_side;
-    }
+    // weight gradients of the dense layers: on the second stream (measured round 1: 93.3k vs 86.5k clips/s inline)
+    bool dense_side_on() const { return use_side; }
     // bucket k of the data-parallel all-reduce is final once both streams pass this point
     int mark(hipStream_t s, int k) {
         if (!this->bucket_sync) return HLMC_OK;
@@ -477,14 +462,6 @@ class NetT : public NetBase {
             return f(q, sc);
         }, side_batch());
     }
-    // HLMC_TAIL_MAIN=0: the encoder's first-layer weight gradient forked like every other one (A/B aid)
-    static bool tail_on_main() {
-        static const bool on = [] {
-            const char* e = std::getenv("HLMC_TAIL_MAIN");
-            return !(e && e[0] == '0');
-        }();
-        return on;
-    }
     ops::BnBwdFuse fuse4{};  // the decoder's last BN layer: moments from the output convT's data gradient
 
     // ---------------------------------------------------------------- conv encoder (6 x conv-BN-LReLU)
@@ -583,7 +560,7 @@ class NetT : public NetBase {
             HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
                             nullptr, true, true));
             float* gw = G[enc.w[l]];
-            if (l == 0 && tail_on_main()) {
+            if (l == 0) {
                 // the last weight gradient of backward: on the main stream, which would otherwise only wait for
                 // the weight-gradient stream here (that stream is still reducing layer 1's gradient)
                 const PendingBias pb = pend_bias;

@@ -847,7 +847,14 @@ int plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax
     p->nbins = 1 + n_fft / 2;
     p->dense = slaney_filterbank(sr, n_fft, n_mels, fmin, fmax);
     std::vector<float> win(n_fft);
-    for (int j = 0; j < n_fft; ++j) win[j] = (float)(0.5 - 0.5 * std::cos(2.0 * M_PI * j / n_fft));
+    // periodic Hann as scipy.signal.get_window('hann', n_fft, fftbins=True) evaluates it (what librosa.stft
+    // calls): 0.5 + 0.5 cos(fac) on fac = linspace(-pi, pi, n_fft + 1) (oracle/mel_oracle.py hann_window)
+    const double wstep = (M_PI - (-M_PI)) / n_fft;
+    for (int j = 0; j < n_fft; ++j) {
+        const double jt = j * wstep;   // separate statements: no fused multiply-add, numpy's two roundings
+        const double fac = jt + (-M_PI);
+        win[j] = (float)(0.5 + 0.5 * std::cos(fac));
+    }
     // stage twiddles of the radix-16/16/4 FFT: tw2[(r-1)*16 + k] = e^{-2 pi i r k / 256} (r 1..15, k 0..15),
     // tw3[(r-1)*256 + j] = e^{-2 pi i r j / 1024} (r 1..3, j 0..255)
     std::vector<float2> tw(kTw2 + kTw3), rtw(kFFT + 1);

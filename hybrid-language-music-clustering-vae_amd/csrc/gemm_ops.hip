@@ -16,7 +16,9 @@ constexpr int kNtTargetBlocks = 512;
 constexpr int kTnTargetBlocks = 256;
 constexpr int kTnLongK = 131072;
 constexpr int kTnKch8Min = 1024;
-constexpr int kXcdRemapDefault = probe::kWgradS2 | probe::kLinearWgrad;  // measured: helps the TN (wgrad) family, hurts sub-pixel
+// XCD-aware block order (gemm.hpp xcd_logical_block) for these op kinds: measured per layer (scripts/bench_gemm.py),
+// it helps the TN (weight-gradient) family and slows the sub-pixel / conv NT families by 10-20 %
+constexpr int kXcdRemapKinds = probe::kWgradS2 | probe::kLinearWgrad;
 
 // Split-K plan shared by the launcher and the workspace query (must agree).
 struct Plan {
@@ -25,10 +27,7 @@ struct Plan {
 // BK = the largest K-step (split ranges are multiples of it); the minimum work per split is counted in
 // steps of the short (BK/2) K-step the kernel uses for short ranges
 inline Plan plan_nt(int tiles, int Kmax, int BK) {
-    static const int target = [] {  // HLMC_NT_BLOCKS: target grid of the split-K plan (measurement aid)
-        const char* e = std::getenv("HLMC_NT_BLOCKS");
-        return e ? std::max(64, std::atoi(e)) : kNtTargetBlocks;
-    }();
+    constexpr int target = kNtTargetBlocks;
     int S = 1;
     if (tiles < target / 2) {
         S = cdiv(target, tiles);
@@ -46,16 +45,7 @@ inline Plan plan_tn(int tiles, int K, int BK) {
     // Round 4 (with the NT GEMMs at two blocks per CU beside them): one 256-block target for every layer measured
     // 134.1k vs 132.9k clips/s at 512 / 1024 (128: 129.6k, 192: 133.6k, 320: 133.6k, 384: 132.1k, 768: 130.8k);
     // the long layers at 512 then 134.5k vs 134.0k (1024: 134.1k).
-    // HLMC_TN_BLOCKS / HLMC_TN_BLOCKS_LONG: the targets of the shorter / K >= kTnLongK layers (measurement aids).
-    static const int t_short = [] {
-        const char* e = std::getenv("HLMC_TN_BLOCKS");
-        return e ? std::max(64, std::atoi(e)) : kTnTargetBlocks;
-    }();
-    static const int t_long = [] {
-        const char* e = std::getenv("HLMC_TN_BLOCKS_LONG");
-        return e ? std::max(64, std::atoi(e)) : 2 * t_short;
-    }();
-    const int target = K >= kTnLongK ? t_long : t_short;
+    const int target = K >= kTnLongK ? 2 * kTnTargetBlocks : kTnTargetBlocks;
     int S = cdiv(target, tiles);
     S = std::max(1, std::min(S, K / (4 * BK)));
     int ksl = cdiv(cdiv(K, S), BK) * BK;
@@ -63,62 +53,27 @@ inline Plan plan_tn(int tiles, int K, int BK) {
     return {S, ksl};
 }
 
-// NT pipeline: 0 register-staged (gemm_nt_kernel), 2/3/4 = LDS-DMA ring of that many stages (gemm_nt_glds_kernel).
-// Measured (scripts/bench_gemm.py): the 4-stage DMA ring wins when a block reduces >= 1024 (16 K-steps),
-// the register path below that (short reductions: more co-resident blocks hide the pipeline prologue) --
-// except on split-K grids of <= 256 blocks (one block per CU: no co-residency to lose), where the ring's
-// three K-steps in flight win even on 9-step reductions (the 4x4x512 conv / its data gradient: 21.5 vs 31.8 us).
-// HLMC_GEMM_PIPE=0/3/4 forces one (A/B measurement aid).
+// NT pipeline: 0 register-staged (gemm_nt_kernel), 2 = the 2-stage LDS-DMA ring (gemm_nt_glds_kernel).
+// Measured (scripts/bench_gemm.py): the DMA ring wins when a block reduces >= 1024 (16 K-steps), the register path
+// below that (short reductions: more co-resident blocks hide the pipeline prologue) -- except on split-K grids of
+// <= 512 blocks, where the ring wins even on 9-step reductions (the 4x4x512 conv / its data gradient: 21.5 vs
+// 31.8 us).  The ring's depth: 2 stages (64 KB of LDS, 176 VGPRs: two blocks per CU, each one K-step ahead)
+// measured 131.9k vs 129.3k clips/s with 4 stages (128 KB, one block per CU, three K-steps ahead) and 129.7k with 3;
+// split grids on the ring up to 1024 blocks 132.0k (3 rounds each; round 4).
+constexpr int kGldsSplitMax = 512;
 inline int nt_pipe_select(int ksl, int S, int blocks) {
-    static const int forced = [] {
-        const char* e = std::getenv("HLMC_GEMM_PIPE");
-        return e ? std::atoi(e) : -1;
-    }();
-    if (forced >= 0) return forced;
-    static const int split_max = [] {  // HLMC_GLDS_SPLIT_MAX: largest split-K grid on the ring (A/B aid)
-        const char* e = std::getenv("HLMC_GLDS_SPLIT_MAX");
-        return e ? std::atoi(e) : 512;
-    }();
-    // the ring's depth: 2 stages (64 KB of LDS, 176 VGPRs: two blocks per CU, each one K-step ahead) measured
-    // 131.9k vs 129.3k clips/s with 4 stages (128 KB, one block per CU, three K-steps ahead) and 129.7k with 3;
-    // with it, NT grid target 1024 121.7k, 384 131.6k, ring for split grids <= 1024 blocks 132.0k (3 rounds each).
-    // HLMC_GLDS_NS: A/B aid
-    static const int ring = [] {
-        const char* e = std::getenv("HLMC_GLDS_NS");
-        return e ? std::atoi(e) : 2;
-    }();
-    if (S > 1 && blocks <= split_max) return ring;
-    return ksl >= 1024 ? ring : 0;
+    if (S > 1 && blocks <= kGldsSplitMax) return 2;
+    return ksl >= 1024 ? 2 : 0;
 }
 
-// XCD-aware block order per op kind (bit = probe::k* kind; gemm.hpp xcd_logical_block).  Default from the
-// per-layer A/B of scripts/bench_gemm.py; HLMC_XCD_REMAP=<mask> overrides (measurement aid).
-inline int xcd_remap_for_site() {
-    static const int mask = [] {
-        const char* e = std::getenv("HLMC_XCD_REMAP");
-        return e ? std::atoi(e) : kXcdRemapDefault;
-    }();
-    return (mask & probe::g_site.kind) ? 1 : 0;
-}
+inline int xcd_remap_for_site() { return (kXcdRemapKinds & probe::g_site.kind) ? 1 : 0; }
 
 // Register-path launches with 4 sub-pixel phases and >= kPloopTiles M x N tiles (>= 4 blocks per CU without
 // the phases) run the phases inside each block (gemm_nt_kernel ploop): the 64 x 64 / 32 x 32 layers' phases
-// otherwise stream the low-res input from HBM once per phase.  HLMC_SP_PLOOP=0 / 2: never / always (A/B aid).
+// otherwise stream the low-res input from HBM once per phase (measured round 2: 105.2k vs 104.25k clips/s without,
+// both the forward and the data-gradient launches gain).
 constexpr int kPloopTiles = 1024;
-inline bool use_ploop(int phases, int tmn, int pipe, bool with_stats) {
-    static const int mode = [] {
-        const char* e = std::getenv("HLMC_SP_PLOOP");
-        return e ? std::atoi(e) : 1;
-    }();
-    static const int min_tiles = [] {  // HLMC_SP_PLOOP_TILES: the tile threshold (A/B aid)
-        const char* e = std::getenv("HLMC_SP_PLOOP_TILES");
-        return e ? std::atoi(e) : kPloopTiles;
-    }();
-    if (phases < 2 || pipe != 0 || mode == 0) return false;
-    if (mode == 3 && !with_stats) return false;  // A/B aid: forward (statistics epilogue) launches only
-    if (mode == 4 && with_stats) return false;   // A/B aid: data-gradient launches only
-    return mode == 2 || tmn >= min_tiles;
-}
+inline bool use_ploop(int phases, int tmn, int pipe) { return phases >= 2 && pipe == 0 && tmn >= kPloopTiles; }
 
 // TR: transposed accumulators + 4-column vector stores (epilogue_tile_t; needs N % 4 == 0 and 4-aligned row
 // strides: the conv / sub-pixel NHWC outputs and their split-K slabs), else the per-element epilogue (linears)
@@ -126,32 +81,21 @@ template <typename T, int BM, int BN, int WM, int WN, bool TR, class AL, class B
 void nt_kernel_launch_tr(hipStream_t s, dim3 grid, const AL& al, const BL& bl, const E& ep, int M, int N, int ksl,
                          bool long_k, int pipe) {
     const int rm = xcd_remap_for_site();
-    const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe, E::kStatMode == 1) ? (int)grid.y : 1;
+    const int ploop = use_ploop((int)grid.y, (int)grid.x, pipe) ? (int)grid.y : 1;
     if (ploop > 1) grid.y = 1;
     HLMC_PROBE_BEGIN(s);
     if (pipe == 2)
         gemm_nt_glds_kernel<T, BM, BN, WM, WN, 2, AL, BL, E, TR, 2><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
-    else if (pipe == 3)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 3, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
-    else if (pipe == 4)
-        gemm_nt_glds_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm);
     else if (long_k)
         gemm_nt_kernel<T, BM, BN, WM, WN, 8, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     else
         gemm_nt_kernel<T, BM, BN, WM, WN, 4, AL, BL, E, TR><<<grid, 256, 0, s>>>(al, bl, ep, M, N, ksl, rm, ploop);
     HLMC_PROBE_END(s);
 }
-// HLMC_NT_TR=0: the per-element epilogue for the conv families too (A/B aid).  Measured per layer
-// (scripts/bench_gemm.py, round 3): the transposed epilogue takes the split-K / LDS-DMA conv and sub-pixel GEMMs from
-// 28-42 to 22-32 us (the 8 x 8 .. 2 x 2 layers), but makes the LDS halo-tile kernels 4-15 % slower (their stores were
-// not the bound; the swapped fragments cost LDS issue) -> halo kernels keep the per-element epilogue.
-inline bool nt_tr_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("HLMC_NT_TR");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// The transposed-accumulator epilogue for the conv families (N % 4 == 0).  Measured per layer (scripts/bench_gemm.py,
+// round 3): it takes the split-K / LDS-DMA conv and sub-pixel GEMMs from 28-42 to 22-32 us (the 8 x 8 .. 2 x 2
+// layers), but makes the LDS halo-tile kernels 4-15 % slower (their stores were not the bound; the swapped fragments
+// cost LDS issue) -> halo kernels keep the per-element epilogue.
 
 template <typename T, int BM, int BN, int WM, int WN, bool TR, class AL, class BL, class EP>
 int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
@@ -185,11 +129,7 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
     part.ws = ws.p; part.M = M; part.N = N; part.S = pl.S; part.phase = 0; part.split = 0;
     nt_kernel_launch_tr<T, BM, BN, WM, WN, TR>(s, grid, al, bl, part, M, N, pl.ksl, long_k, pipe);
     HLMC_LAUNCHED();
-    static const bool red_stats = [] {  // HLMC_SPLITK_STATS=0: statistics from a separate moments pass (A/B aid)
-        const char* e = std::getenv("HLMC_SPLITK_STATS");
-        return !(e && e[0] == '0');
-    }();
-    if (red_stats && stats && N % 64 == 0 && (double)phases * pl.S * M * N < 2147483648.0) {  // the reduce delivers them
+    if (stats && N % 64 == 0 && (double)phases * pl.S * M * N < 2147483648.0) {  // the reduce delivers them
         const int rows = phases * M, ntc = N / 64;
         // the tallest tile (fewest accumulator adds) that still gives >= 1024 blocks (A/B: 128 / 256 / 512 / 1024)
         const int RU = cdiv(rows, 128) * ntc >= 1024 ? 32 : cdiv(rows, 64) * ntc >= 1024 ? 16 : 8;
@@ -223,14 +163,9 @@ inline int nt_tile(int M, int N, int phases) {
     // 128 x 64 tiles where 128 x 128 tiles would give an unsplit grid of target/2 .. target blocks (one block per
     // CU where two fit: the 2-stage ring and the register path hold two): twice the blocks, no split-K slabs.
     // Measured: 133.1k vs 132.3k clips/s (3 rounds); also for target/4 .. target/2 (then split-K) 131.3k.
-    // HLMC_NT_TILE64: 0 off, 2 the wider rule (A/B aid)
-    static const int narrow = [] {
-        const char* e = std::getenv("HLMC_NT_TILE64");
-        return e ? std::atoi(e) : 1;
-    }();
-    if (N >= 128 && narrow) {
+    if (N >= 128) {
         const int t = cdiv(M, 128) * cdiv(N, 128) * phases;
-        if (t >= kNtTargetBlocks / (narrow == 2 ? 4 : 2) && t < kNtTargetBlocks) return 1;
+        if (t >= kNtTargetBlocks / 2 && t < kNtTargetBlocks) return 1;
     }
     if (N >= 128) return 0;
     if (N > 32) return 1;
@@ -240,7 +175,7 @@ template <typename T, class AL, class BL, class EP>
 int dispatch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, int N, int Kmax, int phases, Ws ws,
                 ops::ColStats* st = nullptr) {
     // conv / sub-pixel outputs are NHWC rows of N (a multiple of 8) channels: transposed-accumulator epilogue
-    if (nt_tr_enabled() && N % 4 == 0) {
+    if (N % 4 == 0) {
         switch (nt_tile(M, N, phases)) {
             case 0: return launch_nt<T, 128, 128, 64, 64, true>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
             case 1: return launch_nt<T, 128, 64, 32, 64, true>(s, al, bl, ep, M, N, Kmax, phases, ws, st);
@@ -327,12 +262,8 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
     const int rm = xcd_remap_for_site();
     HLMC_PROBE_BEGIN(s);
     // the 64-deep K-step for splits of >= 1024 rows (measured: 490.9 vs 450.9 us for the 9 conv layers when
-    // every split took it), the 32-deep one below
-    static const bool vec_env = [] {  // HLMC_TN_VEC=0: the per-element loader path everywhere (A/B aid)
-        const char* e = std::getenv("HLMC_TN_VEC");
-        return !(e && e[0] == '0');
-    }();
-    const bool vec = vec_env && ll.vec_ok() && hl.vec_ok();
+    // every split took it), the 32-deep one below; branch-free 16-byte loads where both operands allow them
+    const bool vec = ll.vec_ok() && hl.vec_ok();
     if (pl.ksl >= kTnKch8Min) {
         if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, true><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
         else gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
@@ -467,7 +398,7 @@ __device__ __forceinline__ uint4 bn_in_apply(uint4 v, const float (&pr)[4][8]) {
     return o;
 }
 
-// ---- stride-2 3x3 conv over LDS halo tiles (HLMC_CONV_HALO=0 disables): Ci = 32, Wo = 32, bf16, Co = CO.
+// ---- stride-2 3x3 conv over LDS halo tiles: Ci = 32, Wo = 32, bf16, Co = CO.
 // Measured (scripts/bench_gemm.py): the 64x64x32 -> 64 conv and the matching decoder data gradient 46.3 / 44.1 ->
 // 36.7 / 34.2 us; bench A/B 106.4k vs 105.0k clips/s (3 alternating rounds).
 // A persistent block (one per CU) keeps the packed weights [CO][9 x 32] in LDS and walks 128-pixel M-tiles (4
@@ -655,7 +586,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
-// ---- sub-pixel (stride-2 transposed 3x3) conv over LDS halo tiles (HLMC_SP_HALO=0 disables): Ci = 64,
+// ---- sub-pixel (stride-2 transposed 3x3) conv over LDS halo tiles: Ci = 64,
 // Co = 32, low-res width 32, bf16 (the decoder's last sub-pixel layer and the encoder layer-2 data gradient).
 // A persistent block keeps the packed weights [32][9 x 64] in LDS and walks 128-pixel low-res tiles (4 rows);
 // each tile's 5 input rows (the 4 plus the next, and a zero column right of the image) are staged once, and all
@@ -838,118 +769,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 
-// ---- weight gradient of a stride-2 3x3 conv over LDS halo tiles (the 32 / 64-channel layers whose reductions run
-// over 65k-262k pixels): dW[m][ci][tap] = sum_{b,r,c} L[b,r,c,m] Xh[b, 2r-1+kh, 2c-1+kw, ci] (zero outside Xh).
-// A persistent block owns tiles of ROWS low-res rows x WL columns (TP = 128 pixels = the tile's K) and keeps its
-// whole M x 9C partial in registers over all its tiles: per tile it stages L's rows [TP][M] and Xh's halo rows
-// [2 ROWS + 1][2 WL + 1][C] (column 0 = input column -1, zero) in LDS once, and reads both MFMA operands with
-// transposed LDS reads (ds_read_b64_tr_b16: pixels are the k dimension) -- no im2col gather, no per-K-step slab.
-// The next tile's rows are loaded into registers during the MFMAs.  Each block writes one fp32 partial slab
-// ws[blockIdx.x][m][tap * C + ci]; reduce_splits sums them in block order (deterministic) into the torch layout.
-// Waves: 2 (M halves) x 2 (N halves of 9 x 16 columns).
-template <int M, int C, int WL, int ROWS>
-__global__ __launch_bounds__(256) void wgrad_halo_kernel(const bf16* __restrict__ L, const bf16* __restrict__ Xh, int Hl,
-                                                         int ntiles, float* __restrict__ ws) {
-    constexpr int TP = ROWS * WL, N = 9 * C, HR = 2 * ROWS + 1, HC = 2 * WL + 1;
-    // LDS pixel pitches (bf16): 160 / 80 bytes.  A transposed read (one 32-lane half) takes 8 rows of 32 bytes: with
-    // the k-order below those are 8 consecutive L pixels (160-byte pitch) or 8 Xh pixels 2 apart (160 bytes): bank
-    // offsets 40 c mod 64 -> 8 disjoint 8-bank spans, conflict-free
-    constexpr int PSL = M + 16, PSX = C + 8;
-    constexpr int CPX = C / 8, CPL = M / 8;     // 16-byte chunks per pixel
-    constexpr int LCH = TP * CPL / 256;         // L chunks per thread per tile
-    static_assert(2 * WL * CPX == 256 && TP == 128 && WL == 32 && LCH * 256 == TP * CPL, "halo chunk maps");
-    static_assert(M == 64 && N % 32 == 0, "2 x 2 waves of 32 rows x N / 2 columns");
-    constexpr int NB = N / 32;                  // 16-column blocks per wave (9 for C = 32)
-    __shared__ __attribute__((aligned(16))) bf16 Ls[TP * PSL];
-    __shared__ __attribute__((aligned(16))) bf16 Xs[HR * HC * PSX];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave & 1, wn = wave >> 1;
-    const int tpi = Hl / ROWS;
-    const int Hh = 2 * Hl, Wh = 2 * WL;
-    for (int c = tid; c < HR * CPX; c += 256) {  // input column -1: zero for every tile
-        const int u = c / CPX, q = c - u * CPX;
-        *reinterpret_cast<uint4*>(&Xs[(u * HC) * PSX + q * 8]) = make_uint4(0, 0, 0, 0);
-    }
-    uint4 xr[HR], lr[LCH];
-    const int xcol = tid / CPX, xq = tid % CPX;
-    auto load = [&](int t) {  // unconditional (row -1 clamped to row 0, zeroed when staged)
-        const int b = t / tpi, r0 = (t - b * tpi) * ROWS;
-#pragma unroll
-        for (int u = 0; u < HR; ++u) {
-            const int ih = 2 * r0 - 1 + u;
-            xr[u] = *reinterpret_cast<const uint4*>(Xh + (((int64_t)b * Hh + (ih < 0 ? 0 : ih)) * Wh + xcol) * C + xq * 8);
-        }
-        const bf16* lt = L + ((int64_t)b * Hl + r0) * WL * M;  // the tile's TP x M block is contiguous
-#pragma unroll
-        for (int i = 0; i < LCH; ++i) lr[i] = *reinterpret_cast<const uint4*>(lt + (int64_t)(tid + 256 * i) * 8);
-    };
-    auto stage = [&](int t) {
-        const bool top = (t % tpi) == 0;
-#pragma unroll
-        for (int u = 0; u < HR; ++u)
-            *reinterpret_cast<uint4*>(&Xs[(u * HC + xcol + 1) * PSX + xq * 8]) = (u == 0 && top) ? make_uint4(0, 0, 0, 0) : xr[u];
-#pragma unroll
-        for (int i = 0; i < LCH; ++i) {
-            const int c = tid + 256 * i, px = c / CPL, q = c - px * CPL;
-            *reinterpret_cast<uint4*>(&Ls[px * PSL + q * 8]) = lr[i];
-        }
-    };
-    f32x4_t acc[2][NB];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-    // k-order of a 32-pixel K-step (any bijection serves both operands): lane group g's k = 8 g + j holds pixel
-    // column 16 (g >> 1) + 8 (j >> 2) + 4 (g & 1) + (j & 3), so each 32-lane half's lo / hi read covers 8
-    // consecutive pixels
-    const int cc = 16 * (g >> 1) + 4 * (g & 1) + q;  // lo rows; hi rows are cc + 8
-    int t = blockIdx.x;
-    if (t < ntiles) {
-        load(t);
-        stage(t);
-    }
-    __syncthreads();
-    for (; t < ntiles; t += gridDim.x) {
-        load(min(t + (int)gridDim.x, ntiles - 1));  // next tile in flight during the MFMAs (unconditional)
-#pragma unroll
-        for (int ks = 0; ks < ROWS; ++ks) {  // one low-res row (32 pixels) per 32-deep K-step
-            bf16x8_t af[2], bfr[NB];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const bf16* a = Ls + (32 * ks + cc) * PSL + wm * 32 + i * 16 + 4 * p;
-                const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)a);
-                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(a + 8 * PSL));
-                af[i] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            }
-#pragma unroll
-            for (int j = 0; j < NB; ++j) {
-                const int n0 = (wn * NB + j) * 16, tap = n0 / C, ci0 = n0 % C, kh = tap / 3, kw = tap % 3;
-                // pixel (row ks, column cc) -> halo (2 ks + kh, 2 cc + kw); the hi rows are 8 pixels = 16 columns on
-                const bf16* x = Xs + ((2 * ks + kh) * HC + 2 * cc + kw) * PSX + ci0 + 4 * p;
-                const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)x);
-                const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(x + 16 * PSX));
-                bfr[j] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < NB; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
-        __syncthreads();  // every wave is done with this tile's images
-        if (t + (int)gridDim.x < ntiles) stage(t + (int)gridDim.x);
-        __syncthreads();
-    }
-    float* slab = ws + (int64_t)blockIdx.x * M * N;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                slab[(int64_t)(wm * 32 + i * 16 + 4 * g + r) * N + (wn * NB + j) * 16 + li] = acc[i][j][r];
-}
 }  // namespace
 
 namespace ops {
@@ -970,52 +789,17 @@ static bool subpixel_halo_shape(int Ci, int Co, int Wi, int Hi, int& which) {
     which = (Ci == 64 && Co == 32 && Wi == 32 && Hi % 4 == 0) ? 1 : (Ci == 128 && Co == 64 && Wi == 16 && Hi % 8 == 0) ? 2 : 0;
     return which != 0;
 }
-// environment switches read once per process (A/B aids; every one defaults on)
-static bool env_on(const char* name) {
-    const char* e = std::getenv(name);
-    return !(e && e[0] == '0');
-}
-inline bool bn_in_enabled() {  // HLMC_BN_IN=0: input BatchNorm stays a bn_act pass
-    static const bool on = env_on("HLMC_BN_IN");
-    return on;
-}
-inline bool conv_halo_on(int which) {  // HLMC_CONV_HALO=0 / HLMC_CONV_HALO2=0: that shape on the gather GEMM
-    static const bool h1 = env_on("HLMC_CONV_HALO"), h2 = env_on("HLMC_CONV_HALO2");
-    return which == 1 ? h1 : which == 2 ? h2 : false;
-}
-inline bool sp_halo_on(int which) {  // HLMC_SP_HALO=0 / HLMC_SP_HALO2=0
-    static const bool h1 = env_on("HLMC_SP_HALO"), h2 = env_on("HLMC_SP_HALO2");
-    return which == 1 ? h1 : which == 2 ? h2 : false;
-}
-// the LDS halo-tile weight gradient (wgrad_halo_kernel): the 32 x 32 low-res, M = 64, C = 32 shape (encoder layer 2,
-// the decoder's layer-4 transposed conv).  Opt-in (HLMC_WGRAD_HALO=1): once the TN GEMM's split-K grids were halved
-// the TN path measured faster in the step (133.9k vs 133.4k clips/s, 4 alternating rounds).  HLMC_WGRAD_HALO_BLOCKS:
-// persistent grid size (default 256)
-inline bool wgrad_halo_shape(int Hl, int Wl, int M, int C) {
-    static const bool on = [] {
-        const char* e = std::getenv("HLMC_WGRAD_HALO");
-        return e && e[0] == '1';
-    }();
-    return on && Wl == 32 && M == 64 && C == 32 && Hl % 4 == 0;
-}
-inline int wgrad_halo_blocks() {
-    static const int n = [] {
-        const char* e = std::getenv("HLMC_WGRAD_HALO_BLOCKS");
-        return e ? std::max(8, std::atoi(e)) : 256;
-    }();
-    return n;
-}
 template <typename T>
 bool conv_s2_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co) {
     (void)B;
     int w;
-    return std::is_same<T, bf16>::value && bn_in_enabled() && conv_halo_shape(Ci, Co, Wi, Hi, w) && conv_halo_on(w);
+    return std::is_same<T, bf16>::value && conv_halo_shape(Ci, Co, Wi, Hi, w);
 }
 template <typename T>
 bool subpixel_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co) {
     (void)B;
     int w;
-    return std::is_same<T, bf16>::value && bn_in_enabled() && subpixel_halo_shape(Ci, Co, Wi, Hi, w) && sp_halo_on(w);
+    return std::is_same<T, bf16>::value && subpixel_halo_shape(Ci, Co, Wi, Hi, w);
 }
 
 template <typename T>
@@ -1057,17 +841,17 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
-        using StRM = WithStats<StoreRM<T>>;  // per-element epilogue (TR = false), see nt_tr_enabled
+        using StRM = WithStats<StoreRM<T>>;  // per-element epilogue (TR = false), see dispatch_nt
         // (32, 64, 64): 2-row (64-pixel) tiles and one halo buffer: 64 KB (73 KB with the input BatchNorm) and 176
         // VGPRs, two blocks per CU on a 512-block grid.  Measured in the step: forward with the input BatchNorm +
         // statistics 49.6 -> 42.7 us, the decoder data gradient 32.2 -> 31.5 us (4-row tiles, double-buffered, one
         // block per CU before); the same with 4-row tiles and two 32-channel blocks per tile (the halo read twice)
         // lost (50 -> 55 us)
-        if (which == 1 && conv_halo_on(1))
+        if (which == 1)
             return run(conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StoreRM<T>, false, false, 2>,
                        conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StRM, false, false, 2>,
                        conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StRM, false, true, 2>, 64, 1, 512);
-        if (which == 2 && conv_halo_on(2))
+        if (which == 2)
             return run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, false>,
                        conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false>,
                        conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false, true>, 64, 2);
@@ -1120,7 +904,7 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
             HLMC_LAUNCHED();
             return (int)HLMC_OK;
         };
-        using StSP = WithStats<StoreSubpixel<T>>;  // per-element epilogue (TR = false), see nt_tr_enabled
+        using StSP = WithStats<StoreSubpixel<T>>;  // per-element epilogue (TR = false), see dispatch_nt
         // Two blocks per CU where a block fits in half the LDS (<= 80 KB) and 256 VGPRs: one halo buffer (no
         // double buffering: the co-resident block covers the extra barrier) and a 512-block grid.  Measured
         // (3 alternating rounds): the 32 x 32 / Ci 64 -> Co 32 shape, all three launches, 129.3k vs 128.0k clips/s
@@ -1128,11 +912,11 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
         // gradient with 16 channels per block (four blocks per tile, 79 KB) 38 -> 33 us, while its statistics /
         // input-BN forms need 90 KB (one block per CU) and lost 48 -> 68 us; the Ci 32 -> Co 64 conv with two
         // 32-channel blocks per tile (the halo read twice) lost 50 -> 55 / 32 -> 36 us
-        if (which == 1 && sp_halo_on(1))
+        if (which == 1)
             return run(subpixel_halo_kernel<64, 32, 1, 32, 4, false, StoreSubpixel<T>, false, false, 2>,
                        subpixel_halo_kernel<64, 32, 1, 32, 4, false, StSP, false, false, 2>,
                        subpixel_halo_kernel<64, 32, 1, 32, 4, false, StSP, false, true, 2>, 1, 512, 1, 512);
-        if (which == 2 && sp_halo_on(2))
+        if (which == 2)
             return run(subpixel_halo_kernel<128, 16, 4, 16, 8, false, StoreSubpixel<T>, false, false, 2>,
                        subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false>,
                        subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2, 256, 4, 512);
@@ -1156,28 +940,11 @@ int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* X
     StoreWgradConv ep{dW, C, bias_acc, dbias};
     probe::site(probe::kWgradS2, 2.0 * M * N * K,
                 (double)sizeof(T) * ((double)K * M + 4.0 * K * C) + 4.0 * M * N);
-    if constexpr (std::is_same<T, bf16>::value) {
-        if (wgrad_halo_shape(Hl, Wl, M, C)) {
-            const int ntiles = B * Hl / 4, grid = std::min(ntiles, wgrad_halo_blocks());
-            HLMC_CHECK_ARG(ws.p && ws.bytes >= (size_t)grid * M * N * sizeof(float), "wgrad workspace too small");
-            HLMC_CHECK_ARG(aligned16(L) && aligned16(Xh), "wgrad_s2: 16-byte alignment");
-            HLMC_PROBE_BEGIN(s);
-            wgrad_halo_kernel<64, 32, 32, 4><<<grid, 256, 0, s>>>(L, Xh, Hl, ntiles, ws.p);
-            HLMC_PROBE_END(s);
-            HLMC_LAUNCHED();
-            reduce_splits(s, ws.p, ep, M, N, grid);
-            HLMC_LAUNCHED();
-            return HLMC_OK;
-        }
-    }
     return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
 }
 template <typename T>
 size_t wgrad_s2_ws(int B, int Hl, int Wl, int M, int C) {
-    size_t w = dispatch_tn_ws<T>(M, 9 * C, B * Hl * Wl);
-    if (std::is_same<T, bf16>::value && wgrad_halo_shape(Hl, Wl, M, C))
-        w = std::max(w, (size_t)std::min(B * Hl / 4, wgrad_halo_blocks()) * M * 9 * C * sizeof(float));
-    return w;
+    return dispatch_tn_ws<T>(M, 9 * C, B * Hl * Wl);
 }
 
 template <typename T, typename OutT>

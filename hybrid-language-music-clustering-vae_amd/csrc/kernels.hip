@@ -26,27 +26,16 @@ inline int grid_for(int64_t n, int per_block = kThreads, int cap = 8192) {
 // the former 1024-block cap left the wide-channel layers with 16-64 blocks, latency-bound at 5-20% of HBM.)
 // <= 1024 blocks (about 4 per CU); each range is a multiple of 8192 / C rows (one 4-row-per-thread step for bf16)
 // and the backward kernels prefetch the next step's rows into registers while reducing the current one.
-inline int bn_block_target() {
-    static const int t = [] {
-        const char* e = std::getenv("HLMC_BN_BLOCKS");
-        return e ? std::max(64, std::atoi(e)) : 1024;
-    }();
-    return t;
-}
+// (round 3: 2048 / 512 within noise of 1024)
+constexpr int kBnBlockTarget = 1024;
 // block target of the wide-channel layers (C >= 128: each block's partial row costs 2C x 3 accumulator atomics and
 // each apply block folds the shards of 2C columns, for 16-64 KB of rows per block at 1024 blocks).  Measured (3
 // alternating rounds): 256 blocks 127.85k clips/s vs 126.76k at 1024, 127.1k at 512, 126.8k at 128, 127.6k at 384;
-// the same target from C >= 64 127.4k, from C >= 256 127.4k.  HLMC_BN_BLOCKS_WIDE: A/B aid
-inline int bn_block_target_wide() {
-    static const int t = [] {
-        const char* e = std::getenv("HLMC_BN_BLOCKS_WIDE");
-        return e ? std::max(16, std::atoi(e)) : 256;
-    }();
-    return t;
-}
+// the same target from C >= 64 127.4k, from C >= 256 127.4k
+constexpr int kBnBlockTargetWide = 256;
 inline int64_t bn_rows_per_blk(int64_t R, int C) {
     const int64_t step = std::max(1, 8192 / C);
-    const int64_t tb = C >= 128 ? bn_block_target_wide() : bn_block_target();
+    const int64_t tb = C >= 128 ? kBnBlockTargetWide : kBnBlockTarget;
     const int64_t want = std::max<int64_t>(1, (R + tb - 1) / tb);
     return (want + step - 1) / step * step;
 }
@@ -159,11 +148,8 @@ __global__ __launch_bounds__(64) void bn_finalize_kernel(XAcc acc, int C, int64_
                                                          float eps) {
     const int c = blockIdx.x * 64 + threadIdx.x;
     if (c >= C) return;
-    long long w[2][3] = {{0, 0, 0}, {0, 0, 0}};
-    for (int sh = 0; sh < acc.shards; ++sh)
-        for (int k = 0; k < 2; ++k)
-            for (int j = 0; j < 3; ++j) w[k][j] += (long long)acc.p[((size_t)sh * 3 + j) * acc.ncols + k * C + c];
-    const double s = xacc_value(w[0][0], w[0][1], w[0][2]), q = xacc_value(w[1][0], w[1][1], w[1][2]);
+    // xacc_column masks the sticky non-finite flag (common.hpp kXAccBad): a diverged column comes out NaN
+    const double s = xacc_column(acc, c), q = xacc_column(acc, C + c);
     if (c == 0 && nbt) nbt[0] += 1;
     const double m = s / (double)R;
     double var = q / (double)R - m * m;

@@ -67,15 +67,17 @@ class Trainer:
         self.buckets = self._bucket_ranges()
         self._comm = None
         self._fwd_done = None
+        self._rng_key = 0
         if self.distributed:
             # per-rank reparameterisation noise: every rank builds its model after the same torch.manual_seed, so
             # the engine's Philox streams start equal; rank r > 0 re-keys its seed (rank 0 keeps the single-process
             # stream), so the ranks' clips get independent eps as separate torch.randn_like draws would
             import torch.distributed as dist
             rank = dist.get_rank(process_group) if process_group is not None else dist.get_rank()
+            self._rng_key = rank_rng_key(rank)
             if rank:
                 seed, off = model.get_rng_state()
-                model.set_rng_state(((seed + rank * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF, off))
+                model.set_rng_state((keyed_seed(seed, self._rng_key), off))
         if self.distributed and dev.type == "cuda":
             self._fwd_done = torch.cuda.Event()
             L.check(L.lib().hlmc_net_set_bucket_sync(self.net.h, 1), "hlmc_net_set_bucket_sync")
@@ -115,15 +117,19 @@ class Trainer:
 
     def state_dict(self):
         """Optimizer + noise state for checkpoint / resume (the model's own state_dict holds the parameters and
-        BatchNorm buffers): Adam step count and moments, and the engine's Philox (seed, offset)."""
+        BatchNorm buffers): Adam step count and moments, and the engine's Philox (seed, offset).  The seed is stored
+        un-keyed (the single-process / rank-0 stream), so the usual DP checkpoint -- written by rank 0, loaded on every
+        rank -- restores each rank's own noise stream: load_state_dict re-applies the loading rank's key."""
+        seed, off = self.model.get_rng_state()
         return {"step": self.step_count, "exp_avg": self.m.detach().clone(), "exp_avg_sq": self.v.detach().clone(),
-                "rng": self.model.get_rng_state()}
+                "rng": (keyed_seed(seed, -self._rng_key), off)}
 
     def load_state_dict(self, sd):
         self.step_count = int(sd["step"])
         self.m.copy_(sd["exp_avg"])
         self.v.copy_(sd["exp_avg_sq"])
-        self.model.set_rng_state(sd["rng"])
+        seed, off = sd["rng"]
+        self.model.set_rng_state((keyed_seed(int(seed), self._rng_key), int(off)))
 
     def step(self, in0, in1=None, in2=None, eps=None, dropout=None, before_adam=None):
         """One optimisation step on a batch; returns device float64 sums (sum sq audio err, sum sq text err,
@@ -266,6 +272,19 @@ class Trainer:
             return la + self.beta * kl, la, 0.0, kl
         kld = -0.5 * s[2]
         return s[0] + self.text_weight * s[1] + self.beta * kld, s[0], s[1], kld
+
+
+_RNG_KEY_STEP = 0x9E3779B97F4A7C15  # 2^64 / golden ratio: distinct, well-spread Philox keys per rank
+
+
+def rank_rng_key(rank):
+    """The additive Philox seed key of a data-parallel rank (0 for rank 0: the single-process stream)."""
+    return (int(rank) * _RNG_KEY_STEP) & 0xFFFFFFFFFFFFFFFF
+
+
+def keyed_seed(seed, key):
+    """seed + key modulo 2^64 (key may be negative: un-keying)."""
+    return (int(seed) + int(key)) & 0xFFFFFFFFFFFFFFFF
 
 
 def bucket_ranges(starts, offsets):

@@ -82,9 +82,15 @@ def mel_filterbank(sr: int = SR, n_fft: int = N_FFT, n_mels: int = N_MELS, fmin:
 
 
 def hann_window(n_fft: int = N_FFT) -> np.ndarray:
-    """scipy.signal.get_window('hann', n_fft, fftbins=True): periodic Hann, float64."""
-    k = np.arange(n_fft, dtype=np.float64)
-    return 0.5 - 0.5 * np.cos(2.0 * np.pi * k / n_fft)
+    """scipy.signal.get_window('hann', n_fft, fftbins=True) (what librosa.filters.get_window calls), restated
+    operation for operation so it is bit-identical (tests/test_oracle_cpu.py): scipy 1.15's
+    windows.general_cosine(M, [0.5, 0.5], sym=False) extends the window to M + 1 points, evaluates
+    w = 0 + 0.5 cos(0 fac) + 0.5 cos(fac) on fac = linspace(-pi, pi, M + 1) and drops the last point."""
+    fac = np.linspace(-np.pi, np.pi, n_fft + 1)
+    w = np.zeros(n_fft + 1)
+    for k, a in enumerate((0.5, 0.5)):
+        w += a * np.cos(k * fac)
+    return w[:-1]
 
 
 def n_frames(n_samples: int, hop: int = HOP) -> int:
@@ -148,11 +154,15 @@ def extract_mel_spectrogram(y: np.ndarray, fixed_time_steps: int | None = None) 
 
 
 def dct_ortho_matrix(n_in: int = N_MELS, n_out: int = N_MFCC) -> np.ndarray:
-    """DCT-II, norm='ortho' (scipy.fftpack.dct type 2) as a [n_out, n_in] float64 matrix."""
+    """DCT-II, norm='ortho' (scipy.fftpack.dct type 2, what librosa.feature.mfcc calls) as a [n_out, n_in] float64
+    matrix: D[k, n] = s_k cos(pi k (2n + 1) / (2 N)), s_0 = sqrt(1/N), s_k = sqrt(2/N).  The phase k (2n + 1) is
+    reduced modulo 4N in integers first, so the cosine's argument is below 2 pi and carries one rounding (scipy's
+    pocketfft result agrees to 1e-15, tests/test_oracle_cpu.py)."""
     k = np.arange(n_out)[:, None]
     n = np.arange(n_in)[None, :]
-    D = np.cos(np.pi * k * (2 * n + 1) / (2.0 * n_in)) * np.sqrt(2.0 / n_in)
-    D[0] *= 1.0 / np.sqrt(2.0)
+    m = (k * (2 * n + 1)) % (4 * n_in)
+    D = np.cos(np.pi * m / (2.0 * n_in)) * np.sqrt(2.0 / n_in)
+    D[0] = np.sqrt(1.0 / n_in)
     return D
 
 

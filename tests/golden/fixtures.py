@@ -11,6 +11,10 @@ import numpy as np
 import torch
 
 MODEL_CASES = [
+    # BASELINE config[1] (the benchmarked model): the reference HybridVAE with its text branch, fusion slice and
+    # text loss term removed by an AST rewrite (make_golden._AudioOnlyRewrite); inputs (audio, None)
+    dict(name="audio_128x128", kind="hybrid", hw=(128, 128), B=4, audio_only=True,
+         ctor=dict(latent_dim=128, text_dim=768)),
     dict(name="hybrid_128x128_td768", kind="hybrid", hw=(128, 128), B=4, ctor=dict(latent_dim=128, text_dim=768)),
     dict(name="hybrid_128x128_td384", kind="hybrid", hw=(128, 128), B=4, ctor=dict(latent_dim=128, text_dim=384)),
     dict(name="hybrid_128x1024_td768", kind="hybrid", hw=(128, 1024), B=2, ctor=dict(latent_dim=128, text_dim=768)),
@@ -54,6 +58,8 @@ def oracle_ctor(case):
     ctor = dict(case["ctor"])
     if case["kind"] in ("hybrid", "cvae"):
         ctor["input_hw"] = tuple(case["hw"])
+    if case.get("audio_only"):
+        ctor["audio_only"] = True
     return ctor
 
 
@@ -77,6 +83,8 @@ def inputs_fn(case):
         audio = torch.randn(B, 1, H, W, generator=g)
         text = torch.randn(B, td, generator=g) / td ** 0.5
         eps = torch.randn(B, case["ctor"]["latent_dim"], generator=g)
+        if case.get("audio_only"):
+            return (audio, None), eps
         if kind == "cvae":
             C = case["ctor"]["num_classes"]
             cls = torch.randint(0, C, (B,), generator=g)

@@ -54,13 +54,94 @@ class _FlattenRewrite(ast.NodeTransformer):
         return node
 
 
-def load_reference(fname, names, input_hw=(128, 1024)):
+class _AudioOnlyRewrite(ast.NodeTransformer):
+    """BASELINE config[1]'s audio-only ConvVAE from the reference HybridVAE / loss_function:
+    the text branch, its fusion slice and its loss term removed, everything else untouched.
+
+      * ``self.text_encoder = ...`` / ``self.text_decoder = ...`` registrations dropped (src/Convolutional_VAE.py
+        :103-110, :142-147), so the remaining modules draw the same torch.manual_seed stream as the restatement;
+      * ``t = self.text_encoder(text)`` dropped and ``torch.cat((a, t), dim=1)`` -> ``a`` (:153-155);
+      * the fusion slice ``1024 + 128`` -> ``1024`` in fc_fusion and decoder_split (:112, :118);
+      * ``recon_text = self.text_decoder(t_hidden)`` -> ``None`` (:177);
+      * loss: ``recon_loss_text`` -> a zero scalar and the ``recon_loss_text * 350`` term removed (:190, :194).
+    Every rewrite is counted; a reference that no longer has exactly these sites fails loudly."""
+
+    EXPECT = {"drop_module": 2, "drop_text_call": 1, "cat": 1, "slice": 2, "recon_text": 1, "loss_text": 1,
+              "loss_term": 1}
+
+    def __init__(self):
+        self.n = {k: 0 for k in self.EXPECT}
+        self.dropped = set()
+
+    @staticmethod
+    def _is_self_attr(node, names):
+        return (isinstance(node, ast.Attribute) and isinstance(node.value, ast.Name) and node.value.id == "self"
+                and node.attr in names)
+
+    def _calls(self, node, attr):
+        return isinstance(node, ast.Call) and self._is_self_attr(node.func, {attr})
+
+    def visit_Assign(self, node):
+        tgt = node.targets[0]
+        if self._is_self_attr(tgt, {"text_encoder", "text_decoder"}):
+            self.n["drop_module"] += 1
+            return None
+        if self._calls(node.value, "text_encoder"):
+            self.n["drop_text_call"] += 1
+            self.dropped.add(tgt.id)
+            return None
+        if self._calls(node.value, "text_decoder"):
+            self.n["recon_text"] += 1
+            node.value = ast.Constant(None)
+            return node
+        if (isinstance(tgt, ast.Name) and tgt.id == "recon_loss_text" and isinstance(node.value, ast.Call)
+                and getattr(node.value.func, "attr", None) == "mse_loss"):
+            self.n["loss_text"] += 1
+            node.value = ast.parse("torch.zeros_like(recon_loss_audio)", mode="eval").body
+            return node
+        self.generic_visit(node)
+        return node
+
+    def visit_Call(self, node):
+        self.generic_visit(node)
+        if (isinstance(node.func, ast.Attribute) and node.func.attr == "cat" and node.args
+                and isinstance(node.args[0], ast.Tuple)):
+            elts = [e for e in node.args[0].elts if not (isinstance(e, ast.Name) and e.id in self.dropped)]
+            if len(elts) == 1 and len(node.args[0].elts) == 2:
+                self.n["cat"] += 1
+                return elts[0]
+        return node
+
+    def visit_BinOp(self, node):
+        self.generic_visit(node)
+        if (isinstance(node.op, ast.Add) and isinstance(node.left, ast.Constant) and isinstance(node.right, ast.Constant)
+                and (node.left.value, node.right.value) == (1024, 128)):
+            self.n["slice"] += 1
+            return ast.copy_location(ast.Constant(1024), node)
+        r = node.right
+        if (isinstance(node.op, ast.Add) and isinstance(r, ast.BinOp) and isinstance(r.op, ast.Mult)
+                and isinstance(r.left, ast.Name) and r.left.id == "recon_loss_text"):
+            self.n["loss_term"] += 1
+            return node.left
+        return node
+
+    def check(self):
+        if self.n != self.EXPECT:
+            raise AssertionError(f"audio-only rewrite sites differ from the reference: {self.n} != {self.EXPECT}")
+
+
+def load_reference(fname, names, input_hw=(128, 1024), audio_only=False):
     src = open(os.path.join(REF, fname)).read()
     tree = ast.parse(src)
     keep = [n for n in tree.body if isinstance(n, (ast.ClassDef, ast.FunctionDef)) and n.name in names]
     flat, unflat = models_oracle.flat_dims(input_hw)
     mod = ast.Module(body=keep, type_ignores=[])
-    mod = ast.fix_missing_locations(_FlattenRewrite(flat, unflat).visit(mod))
+    mod = _FlattenRewrite(flat, unflat).visit(mod)
+    if audio_only:
+        rw = _AudioOnlyRewrite()
+        mod = rw.visit(mod)
+        rw.check()
+    mod = ast.fix_missing_locations(mod)
     ns = {"torch": torch, "nn": nn, "np": np}
     exec(compile(mod, f"<reference {fname}>", "exec"), ns)
     return ns
@@ -145,15 +226,17 @@ def run_case(kind, ref_cls, ref_loss, ora_cls, ora_loss, ctor, ora_ctor, inputs_
     return out
 
 
-def make_models():
-    conv = lambda hw: load_reference("Convolutional_VAE.py", {"HybridVAE", "loss_function"}, hw)  # noqa: E731
+def make_models(only=None):
+    conv = lambda hw, ao=False: load_reference("Convolutional_VAE.py", {"HybridVAE", "loss_function"}, hw, ao)  # noqa: E731
     cond = lambda hw: load_reference("Conditional_VAE.py", {"ConditionalVAE", "cvae_loss_function", "SimpleAutoencoder"}, hw)  # noqa: E731
     simple = load_reference("Simple_VAE.py", {"VAE", "vae_loss"})
     for case in fixtures.MODEL_CASES:
         kind, hw = case["kind"], case.get("hw")
+        if only and case["name"] not in only:
+            continue
         print("case", case["name"], flush=True)
         if kind == "hybrid":
-            ns = conv(hw)
+            ns = conv(hw, bool(case.get("audio_only")))
             res = run_case(kind, ns["HybridVAE"], ns["loss_function"], models_oracle.HybridVAE,
                            models_oracle.loss_function, case["ctor"], fixtures.oracle_ctor(case), fixtures.inputs_fn(case), {})
         elif kind == "cvae":
@@ -166,6 +249,8 @@ def make_models():
         else:
             raise ValueError(kind)
         np.savez_compressed(os.path.join(HERE, f"model_{case['name']}.npz"), **res)
+    if only:
+        return
     # SimpleAutoencoder: forward only (the CVAE baseline)
     ns = cond((128, 1024))
     torch.manual_seed(42)
@@ -297,6 +382,10 @@ def make_features():
 if __name__ == "__main__":
     torch.set_num_threads(8)
     what = sys.argv[1:] or ["models", "kmeans", "kmeans_overlap", "kmeans_latents", "metrics", "features"]
+    # "models=<case>[,<case>]" regenerates only the named model fixtures
+    only = [c for w in what if w.startswith("models=") for c in w.split("=", 1)[1].split(",")]
+    if only:
+        what.append("models")
     if "features" in what:
         make_features()
     if "kmeans" in what:
@@ -308,4 +397,4 @@ if __name__ == "__main__":
     if "metrics" in what:
         make_metrics()
     if "models" in what:
-        make_models()
+        make_models(only or None)

@@ -170,3 +170,18 @@ def test_pipeline_shards_and_equal_step_counts():
         for p, size in zip(plans, sizes):
             assert p[0][0] == 0 and p[-1][1] == size and all(a[1] == b[0] for a, b in zip(p, p[1:]))
             assert all(b - a >= 2 for a, b in p)
+
+
+def test_checkpoint_rng_keying_round_trip():
+    """Trainer.state_dict stores the un-keyed Philox seed; load_state_dict re-keys it for the loading rank
+    (hlmc_amd.train.keyed_seed / rank_rng_key): rank 0's checkpoint gives every rank its own stream back."""
+    from hlmc_amd.train import keyed_seed, rank_rng_key
+    base = 0x1234_5678_9ABC_DEF0
+    assert rank_rng_key(0) == 0
+    keys = [rank_rng_key(r) for r in range(8)]
+    assert len(set(keys)) == 8
+    for r, k in enumerate(keys):
+        live = keyed_seed(base, k)
+        assert keyed_seed(live, -k) == base                     # rank r saves the base
+        assert keyed_seed(keyed_seed(live, -k), k) == live      # and gets its own stream back
+    assert keyed_seed(2 ** 64 - 1, 1) == 0

@@ -38,8 +38,8 @@ def ws(cuda):
                                           (2, 32, 32, 64, 128), (3, 8, 32, 64, 128), (2, 16, 16, 128, 256),
                                           (3, 32, 16, 128, 256)])
 def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
-    """(also the shapes of the LDS halo-tile kernels: Ci 32 -> Co 64 at Wi 64 (default on), Ci 64 -> Co 128 at
-    Wi 32 (HLMC_CONV_HALO2=1))"""
+    """(bf16 also covers the shapes of the LDS halo-tile kernels: Ci 32 -> Co 64 at Wi 64 and Ci 64 -> Co 128 at Wi 32;
+    fp32 runs the gather GEMM at every shape)"""
     code, tdt, tol = DT[dt]
     g = torch.Generator().manual_seed(B * 1000 + Ci)
     x = torch.randn(B, Hi, Wi, Ci, generator=g)
@@ -61,7 +61,8 @@ def test_conv_s2(cuda, ws, dt, B, Hi, Wi, Ci, Co):
                                           (2, 4, 4, 32, 64), (3, 8, 32, 64, 32), (2, 16, 16, 128, 64),
                                           (3, 8, 16, 128, 64), (2, 16, 8, 256, 128)])
 def test_subpixel_convT(cuda, ws, dt, B, Hi, Wi, Ci, Co):
-    """(the Ci 64 -> Co 32, 32-wide shapes run the LDS halo-tile kernel in bf16; HLMC_SP_HALO=0 disables it)"""
+    """(the Ci 64 -> Co 32, 32-wide and Ci 128 -> Co 64, 16-wide shapes run the LDS halo-tile kernels in bf16; fp32
+    runs the gather GEMM)"""
     code, tdt, tol = DT[dt]
     g = torch.Generator().manual_seed(B * 7 + Ci + Co)
     x = torch.randn(B, Hi, Wi, Ci, generator=g)
@@ -83,9 +84,8 @@ def test_subpixel_convT(cuda, ws, dt, B, Hi, Wi, Ci, Co):
                                         (3, 1, 1, 512, 512), (2, 16, 16, 32, 64), (4, 2, 8, 256, 128),
                                         (3, 8, 32, 64, 32), (1, 32, 32, 64, 32)])
 def test_wgrad_s2_conv(cuda, ws, dt, B, Hl, Wl, M, C):
-    """Conv2d weight gradient: L = dY (low-res, M=Co), Xh = X (high-res, C=Ci).  (The Wl = 32, M = 64, C = 32 shapes
-    run the LDS halo-tile weight gradient in bf16: 6 / 8 tiles, fewer than the persistent grid; the B = 256 bench
-    shape is test_wgrad_s2_bench_shapes_bf16.)"""
+    """Conv2d weight gradient: L = dY (low-res, M=Co), Xh = X (high-res, C=Ci), through the weight-gradient TN GEMM
+    (the B = 256 bench shapes are test_wgrad_s2_bench_shapes_bf16)."""
     code, tdt, tol = DT[dt]
     g = torch.Generator().manual_seed(M + C + B)
     dy = torch.randn(B, Hl, Wl, M, generator=g)

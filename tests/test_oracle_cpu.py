@@ -23,6 +23,22 @@ def test_librosa_documented_filterbank_value():
     assert (nz0[0], nz0[-1]) == (1, 4) and (nz127[0], nz127[-1]) == (971, 1023)
 
 
+def test_window_and_dct_match_scipy():
+    """The two scipy primitives librosa's mel / MFCC path calls (src/1_preprocessing_advanced.py:99-106 via
+    librosa.stft's get_window; src/1_preprocessing.py:61-70 via librosa.feature.mfcc's scipy.fftpack.dct), pinned
+    against scipy itself (importable here and on the GPU box): the periodic Hann window bit for bit, the
+    DCT-II ortho matrix to 1e-15."""
+    import scipy.fftpack
+    import scipy.signal
+    for n in (2048, 1024, 400):
+        np.testing.assert_array_equal(MO.hann_window(n), scipy.signal.get_window("hann", n, fftbins=True))
+    D = scipy.fftpack.dct(np.eye(128), type=2, norm="ortho", axis=0)[:40]
+    assert float(np.abs(MO.dct_ortho_matrix() - D).max()) <= 1e-15
+    x = np.random.default_rng(3).standard_normal((128, 7))
+    np.testing.assert_allclose(MO.dct_ortho_matrix() @ x, scipy.fftpack.dct(x, type=2, norm="ortho", axis=0)[:40],
+                               rtol=0, atol=1e-13)
+
+
 def test_frames_and_shapes():
     assert MO.n_frames(65024) == 128 and MO.n_frames(661500) == 1292
     y = MO.synthetic_pcm(1, 65024, seed=1)[0]
@@ -110,7 +126,7 @@ def test_scaler_oracle_matches_fixture():
     np.testing.assert_array_equal(KO.standard_scaler_transform(cols, m, s), fx["scaler_out"])
 
 
-@pytest.mark.parametrize("name", ["hybrid_128x128_td768", "cvae_128x128", "simple_370"])
+@pytest.mark.parametrize("name", ["audio_128x128", "hybrid_128x128_td768", "cvae_128x128", "simple_370"])
 def test_model_oracle_reproduces_fixture(name):
     case = FX.case_by_name(name)
     fx = np.load(f"tests/golden/model_{name}.npz")
@@ -222,7 +238,7 @@ def test_philox_known_answers():
     np.testing.assert_array_equal(normals(8, seed=1234, offset=4096 - 8), a[-8:])
 
 
-@pytest.mark.parametrize("name", ["hybrid_128x128_td768", "cvae_128x128", "simple_370"])
+@pytest.mark.parametrize("name", ["audio_128x128", "hybrid_128x128_td768", "cvae_128x128", "simple_370"])
 def test_oracle_training_chain_reproduces_fixture_latents(name):
     """The oracle's 3-step train chain (tests/test_models_gpu._oracle_trained: the fixture generator's Adam steps
     and dropout seeds) then eval-mode encode reproduces the reference classes' fixture eval_mu bit for bit on the

@@ -89,6 +89,13 @@ _SIGS = {
     "hlmc_km_sums_part": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_i64]),
     "hlmc_km_rowdist": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),
     "hlmc_km_inertia": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "hlmc_km_assign_batch": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, C.c_uint64, c_vp, c_vp, c_vp]),
+    "hlmc_km_sums_batch": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, C.c_uint64, c_vp, c_vp, c_vp, c_i64]),
+    "hlmc_km_update_batch": (c_int, [c_vp, c_int, c_int, c_int, C.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "hlmc_km_pp_search": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_int, C.POINTER(C.c_int32), C.POINTER(c_f64), c_vp,
+                                  c_vp]),
+    "hlmc_km_pp_dist": (c_int, [c_vp, c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_int, C.POINTER(C.c_int32), c_vp]),
+    "hlmc_km_inertia_batch": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
     "hlmc_silhouette_workspace": (c_i64, [c_i64, c_int]),
     "hlmc_silhouette": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_i64]),
     "hlmc_cluster_scores_workspace": (c_i64, [c_int, c_int]),

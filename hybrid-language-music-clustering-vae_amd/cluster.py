@@ -4,15 +4,18 @@ Replaces ``sklearn.cluster.KMeans(n_clusters=k, random_state=42, n_init=10).fit_
 src/Convolutional_VAE.py:317-319,379-380, src/Conditional_VAE.py:293-295 (and the n_init='auto'
 call at :528), src/Simple_VAE.py:244-261.
 
-Host (this file) keeps exactly what sklearn 1.7.2 does on the host side: one numpy RandomState stream
-across all inits, k-means++ candidate draws (``choice``, ``uniform * pot``, float64 cumsum +
-searchsorted), potentials as float32 BLAS dot products, the best-of-n_init rule with
-``_is_same_clustering``, empty-cluster relocation, centre averaging (float32 ``*= 1/w``),
-centre shifts and the strict / tolerance convergence tests.  Device kernels (libhlmc) compute the
-numpy-order column mean/variance, the float64-upcast candidate distances, the float32 E-step
-(||c||^2 - 2 x.c, first minimum) in the exact rounding order of sklearn's einsum row norms and its OpenBLAS
-sgemm call (oracle/kmeans_oracle.py estep_dist), per-cluster sums in sklearn's single-thread row order, and
-inertia.
+The n_init restarts run in lockstep on the device (round 5): every stage is one launch for all of them.
+sklearn draws every restart's random numbers from one RandomState stream in a data-independent amount
+(``seeding_draws``), so they are drawn up front in sklearn's order.  Device kernels (libhlmc) compute the
+numpy-order column mean/variance, the k-means++ candidate draw (searchsorted of the float64 cumsum, exact
+through an error bracket with a numpy fallback for undecidable draws), the float64-upcast candidate distances
+and their running minimum, the float32 E-step (||c||^2 - 2 x.c, first minimum) in the exact rounding order of
+sklearn's einsum row norms and its OpenBLAS sgemm call (oracle/kmeans_oracle.py estep_dist), per-cluster sums in
+sklearn's single-thread row order, the centre update (float32 ``*= 1/w``) with its shifts, and inertia.  The
+host keeps what sklearn's order depends on BLAS for or decides per restart: the float32 potentials (BLAS dot
+products of the copied-back distances), the candidate argmin, empty-cluster relocation, the strict / tolerance
+convergence tests and the best-of-n_init rule with ``_is_same_clustering``; one copy back per k-means++ step
+and per Lloyd iteration serves all restarts.
 
 Multi-GPU (``process_group=``): the n_init restarts are independent objects, so they shard across ranks
 with no collective on the data path.  Every rank holds the same (small, [N, D] f32) latents and runs the
@@ -92,94 +95,180 @@ class KMeans:
                                             out.data_ptr()), "hlmc_km_sqdist_rows")
         return out
 
-    def _kmeans_plusplus(self, Xc, rs, w):
-        n, d = Xc.shape
+    def _draw_seeds(self, rs, n, n_init, mine):
+        """Consume the one RandomState stream exactly as sklearn's sequential restarts do (data-independent
+        counts, seeding_draws): per restart the first centre's choice(n, p=w / w.sum()) and the k - 1 per-centre
+        uniform(size=trials) vectors -- kept for this rank's restarts, drawn and discarded for the others."""
         k = self.n_clusters
         trials = 2 + int(np.log(k))
-        cid = rs.choice(n, p=w / w.sum())
-        idx = np.full(k, -1, dtype=int)
-        idx[0] = cid
-        closest = self._sqdist(Xc, [cid]).cpu().numpy()          # [1, n] float32
-        pot = closest @ w
-        for c in range(1, k):
-            rand_vals = rs.uniform(size=trials) * pot
-            cand = np.searchsorted(np.cumsum(w * closest, axis=None, dtype=np.float64), rand_vals)
-            np.clip(cand, None, closest.size - 1, out=cand)
-            dist = self._sqdist(Xc, [int(x) for x in cand]).cpu().numpy()
-            np.minimum(closest, dist, out=dist)
-            cpot = dist @ w.reshape(-1, 1)
-            best = int(np.argmin(cpot))
-            pot = cpot[best]
-            closest = dist[best]
-            idx[c] = cand[best]
-        return Xc[torch.as_tensor(idx, device=Xc.device)].contiguous(), idx
+        w = np.ones(n, dtype=np.float32)
+        draws = {}
+        for i in range(n_init):
+            if i not in mine:
+                rs.random_sample(self.seeding_draws(k))
+                continue
+            cid = rs.choice(n, p=w / w.sum())
+            draws[i] = (int(cid), [rs.uniform(size=trials) for _ in range(1, k)])
+        return draws, trials
 
-    def _lloyd(self, Xc, centers, tol):
+    def _kmeans_plusplus_batch(self, Xc, seeds, trials):
+        """sklearn _kmeans_plusplus for R restarts in lockstep (one launch per stage for all of them): the
+        candidate draw (searchsorted of the float64 cumsum, hlmc_km_pp_search) and the candidates' distances with
+        the running minimum (hlmc_km_pp_dist) on the device; the host keeps sklearn's float32 BLAS potentials
+        (closest @ w, dist @ w: numpy on the copied-back distances) and argmin, and redoes with numpy the rare
+        draws the device's error bracket flags as undecidable."""
         n, d = Xc.shape
-        k = self.n_clusters
+        k, R, T = self.n_clusters, len(seeds), trials
         dev = Xc.device
-        labels = torch.full((n,), -1, dtype=torch.int32, device=dev)
-        labels_new = torch.empty_like(labels)
-        # one device buffer [sums k*d | weights k | changed (int32 bits)]: one copy back per iteration
-        pack = torch.empty(k * d + k + 1, dtype=torch.float32, device=dev)
-        sums, wts = pack[:k * d], pack[k * d:k * d + k]
-        changed = pack[k * d + k:].view(torch.int32)
-        # M-step workspace: per-tile cluster histograms + bases, cluster offsets, the label-partitioned row list
-        ws_bytes = int(L.lib().hlmc_km_sums_workspace(n, k))
+        lib = L.lib()
+        w = np.ones(n, dtype=np.float32)
+        idx = np.full((R, k), -1, dtype=np.int64)
+        idx[:, 0] = [c for c, _ in seeds]
+        cand = torch.as_tensor(idx[:, 0].copy(), device=dev)
+        prev = torch.empty(R, 1, n, dtype=torch.float32, device=dev)
+        L.check(lib.hlmc_km_pp_dist(L.stream(), Xc.data_ptr(), n, d, R, 1, cand.data_ptr(), None, 1, None,
+                                    prev.data_ptr()), "hlmc_km_pp_dist")
+        prev_h = prev.cpu().numpy()
+        pots = [prev_h[r] @ w for r in range(R)]               # closest_dist_sq @ sample_weight: float32 (1,)
+        best = np.zeros(R, dtype=np.int32)
+        bufs = [torch.empty(R, T, n, dtype=torch.float32, device=dev) for _ in range(2)]
+        cand = torch.empty(R * T, dtype=torch.int64, device=dev)
+        amb = torch.empty(R * T, dtype=torch.int32, device=dev)
+        pin = torch.empty(R, T, n, dtype=torch.float32).pin_memory() if dev.type == "cuda" else None
+        for c in range(1, k):
+            out = bufs[c % 2]
+            rv = np.stack([seeds[r][1][c - 1] * pots[r] for r in range(R)]).astype(np.float64)   # rand_vals
+            prevT = prev.shape[1]
+            bh = best.ctypes.data_as(C.POINTER(C.c_int32))
+            L.check(lib.hlmc_km_pp_search(L.stream(), n, R, T, prev.data_ptr(), prevT, bh,
+                                          np.ascontiguousarray(rv).ctypes.data_as(C.POINTER(C.c_double)),
+                                          cand.data_ptr(), amb.data_ptr()), "hlmc_km_pp_search")
+            L.check(lib.hlmc_km_pp_dist(L.stream(), Xc.data_ptr(), n, d, R, T, cand.data_ptr(), prev.data_ptr(),
+                                        prevT, bh, out.data_ptr()), "hlmc_km_pp_dist")
+            if pin is not None:
+                pin.copy_(out, non_blocking=True)
+                cand_h, amb_h = cand.cpu().numpy().reshape(R, T), amb.cpu().numpy().reshape(R, T)
+                out_h = pin.numpy()
+            else:
+                cand_h, amb_h = cand.cpu().numpy().reshape(R, T), amb.cpu().numpy().reshape(R, T)
+                out_h = out.cpu().numpy()
+            for r in range(R):
+                closest = prev_h[r, best[r]][None, :]
+                dist = out_h[r]
+                if amb_h[r].any():
+                    # numpy's own cumsum / searchsorted for this restart's draw (the device bracket could not decide)
+                    cc = np.searchsorted(np.cumsum(w * closest, axis=None, dtype=np.float64), rv[r])
+                    np.clip(cc, None, closest.size - 1, out=cc)
+                    cand_h[r] = cc
+                    dist = self._sqdist(Xc, [int(x) for x in cc]).cpu().numpy()
+                    np.minimum(closest, dist, out=dist)
+                    out[r].copy_(torch.from_numpy(dist))
+                    out_h[r] = dist
+                cpot = dist @ w.reshape(-1, 1)
+                b = int(np.argmin(cpot))
+                pots[r] = cpot[b]
+                best[r] = b
+                idx[r, c] = cand_h[r, b]
+            prev, prev_h = out, out_h.copy()
+        cent = Xc[torch.as_tensor(idx.reshape(-1), device=dev)].reshape(R, k, d).contiguous()
+        return cent, idx
+
+    def _lloyd_batch(self, Xc, centers, tol):
+        """sklearn _kmeans_single_lloyd for R restarts in lockstep: one assign / partitioned-sums / centre-update
+        launch per iteration for all running restarts, one small copy back per iteration (label-change counts,
+        centre shifts, the new centres) for sklearn's host-side tests: strict convergence (labels unchanged),
+        sum(shift^2) <= tol, max_iter; a restart with an empty cluster is updated on the host that iteration
+        (sklearn _relocate_empty_clusters_dense on host copies, as before)."""
+        n, d = Xc.shape
+        k, R = self.n_clusters, centers.shape[0]
+        dev = Xc.device
+        lib = L.lib()
+        cbuf = [centers.contiguous(), torch.empty_like(centers)]
+        labels = [torch.full((R, n), -1, dtype=torch.int32, device=dev), torch.empty(R, n, dtype=torch.int32, device=dev)]
+        # [info R*(k+1) | changed R (int32 bits)]: one copy back per iteration together with the new centres
+        pack = torch.empty(R * (k + 1) + R, dtype=torch.float32, device=dev)
+        info = pack[:R * (k + 1)]
+        changed = pack[R * (k + 1):].view(torch.int32)
+        sums = torch.empty(R, k, d, dtype=torch.float32, device=dev)
+        wts = torch.empty(R, k, dtype=torch.float32, device=dev)
+        ws_bytes = int(lib.hlmc_km_sums_workspace(n, k)) * R
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        old_c = centers.cpu().numpy()
-        strict = False
-        it = 0
+        old_c = cbuf[0].cpu().numpy()
+        final_c = old_c.copy()
+        final_lab = torch.empty(R, n, dtype=torch.int32, device=dev)
+        n_iter = np.zeros(R, dtype=np.int64)
+        strict = np.zeros(R, dtype=bool)
+        active = (1 << R) - 1
+        Xh = None
         for it in range(self.max_iter):
+            if not active:
+                break
+            cur, nxt = cbuf[it % 2], cbuf[(it + 1) % 2]
+            lab_old, lab_new = labels[it % 2], labels[(it + 1) % 2]
             changed.zero_()
-            L.check(L.lib().hlmc_km_assign(L.stream(), Xc.data_ptr(), n, d, centers.data_ptr(), k,
-                                           labels_new.data_ptr(), labels.data_ptr(), changed.data_ptr()))
-            L.check(L.lib().hlmc_km_sums_part(L.stream(), Xc.data_ptr(), n, d, labels_new.data_ptr(), k,
-                                              sums.data_ptr(), wts.data_ptr(), ws.data_ptr(), ws_bytes))
+            L.check(lib.hlmc_km_assign_batch(L.stream(), Xc.data_ptr(), n, d, cur.data_ptr(), k, R, active,
+                                             lab_new.data_ptr(), lab_old.data_ptr(), changed.data_ptr()))
+            L.check(lib.hlmc_km_sums_batch(L.stream(), Xc.data_ptr(), n, d, lab_new.data_ptr(), k, R, active,
+                                           sums.data_ptr(), wts.data_ptr(), ws.data_ptr(), ws_bytes))
+            L.check(lib.hlmc_km_update_batch(L.stream(), k, d, R, active, sums.data_ptr(), wts.data_ptr(),
+                                             cur.data_ptr(), nxt.data_ptr(), info.data_ptr()))
             pack_h = pack.cpu().numpy()
-            new = pack_h[:k * d].reshape(k, d)
-            wic = pack_h[k * d:k * d + k]
-            n_changed = int(pack_h[k * d + k:].view(np.int32)[0])
-            empty = np.where(wic == 0)[0]
-            if empty.size:
-                # _relocate_empty_clusters_dense (sklearn/cluster/_k_means_common.pyx) ranks rows by the numpy
-                # expression ((X - C[labels])**2).sum(axis=1) (pairwise row sums): evaluated here on host copies
-                # exactly as written, so near-tied farthest points resolve as in sklearn (empty clusters are rare)
-                lab_h = labels_new.cpu().numpy()
-                Xh = Xc.cpu().numpy()
-                dist = ((Xh - old_c[lab_h]) ** 2).sum(axis=1)
-                if dist.max() > 0:
-                    far = np.argpartition(dist, -empty.size)[:-empty.size - 1:-1]
-                    rows = Xh[far]
-                    for e, f, xr in zip(empty, far, rows):
-                        old = lab_h[f]
-                        new[old] -= xr
-                        new[e] = xr
-                        wic[e] = 1.0
-                        wic[old] -= 1.0
-            amax = int(np.argmax(wic))
-            for j in range(k):
-                if wic[j] > 0:
-                    new[j] *= np.float32(1.0 / float(wic[j]))
+            nxt_h = nxt.cpu().numpy()
+            info_h = pack_h[:R * (k + 1)].reshape(R, k + 1)
+            chg = pack_h[R * (k + 1):].view(np.int32)
+            for r in range(R):
+                if not (active >> r) & 1:
+                    continue
+                if info_h[r, k] != 0:   # an empty cluster: this restart's update on the host, as sklearn does it
+                    if Xh is None:
+                        Xh = Xc.cpu().numpy()
+                    new = sums[r].cpu().numpy()
+                    wic = wts[r].cpu().numpy()
+                    lab_h = lab_new[r].cpu().numpy()
+                    dist = ((Xh - old_c[r][lab_h]) ** 2).sum(axis=1)
+                    empty = np.where(wic == 0)[0]
+                    if dist.max() > 0:
+                        far = np.argpartition(dist, -empty.size)[:-empty.size - 1:-1]
+                        for e, f in zip(empty, far):
+                            o = lab_h[f]
+                            new[o] -= Xh[f]
+                            new[e] = Xh[f]
+                            wic[e] = 1.0
+                            wic[o] -= 1.0
+                    amax = int(np.argmax(wic))
+                    for j in range(k):
+                        if wic[j] > 0:
+                            new[j] *= np.float32(1.0 / float(wic[j]))
+                        else:
+                            new[j] = new[amax]
+                    shift = np.sqrt(_euclid_f32(new, old_c[r])).astype(np.float32)
+                    nxt[r].copy_(torch.from_numpy(new))
                 else:
-                    new[j] = new[amax]
-            shift = np.sqrt(_euclid_f32(new, old_c)).astype(np.float32)
-            centers = torch.from_numpy(new).to(dev)
-            old_c = new
-            labels, labels_new = labels_new, labels
-            if n_changed == 0 and it > 0:
-                strict = True
-                break
-            if (shift ** 2).sum() <= tol:
-                break
-        if not strict:
-            L.check(L.lib().hlmc_km_assign(L.stream(), Xc.data_ptr(), n, d, centers.data_ptr(), k,
-                                           labels.data_ptr(), None, None))
-        inertia = torch.empty(1, dtype=torch.float32, device=dev)
-        tmp = torch.empty(n, dtype=torch.float32, device=dev)
-        L.check(L.lib().hlmc_km_inertia(L.stream(), Xc.data_ptr(), n, d, centers.data_ptr(), labels.data_ptr(),
-                                        inertia.data_ptr(), tmp.data_ptr()))
-        return labels, float(inertia.item()), centers, it + 1
+                    new = nxt_h[r]
+                    shift = np.sqrt(info_h[r, :k]).astype(np.float32)
+                old_c[r] = new
+                done = False
+                if chg[r] == 0 and it > 0:
+                    strict[r] = done = True
+                elif (shift ** 2).sum() <= tol:
+                    done = True
+                elif it + 1 == self.max_iter:
+                    done = True
+                if done:
+                    n_iter[r] = it + 1
+                    final_c[r] = new
+                    final_lab[r].copy_(lab_new[r])
+                    active &= ~(1 << r)
+        fc = torch.from_numpy(final_c).to(dev)
+        redo = sum(1 << r for r in range(R) if not strict[r])
+        if redo:   # not strictly converged: labels from the final centres (sklearn's last lloyd_iter, no update)
+            L.check(lib.hlmc_km_assign_batch(L.stream(), Xc.data_ptr(), n, d, fc.data_ptr(), k, R, redo,
+                                             final_lab.data_ptr(), None, None))
+        inertia = torch.empty(R, dtype=torch.float32, device=dev)
+        tmp = torch.empty(R, n, dtype=torch.float32, device=dev)
+        L.check(lib.hlmc_km_inertia_batch(L.stream(), Xc.data_ptr(), n, d, fc.data_ptr(), k, final_lab.data_ptr(), R,
+                                          inertia.data_ptr(), tmp.data_ptr()))
+        return final_lab.cpu().numpy(), inertia.cpu().numpy().astype(np.float64), final_c, n_iter
 
     @staticmethod
     def seeding_draws(k):
@@ -213,22 +302,21 @@ class KMeans:
         rs = self.random_state if isinstance(self.random_state, np.random.RandomState) \
             else np.random.RandomState(self.random_state)
         n_init = 1 if self.n_init == "auto" else int(self.n_init)
-        w = np.ones(n, dtype=np.float32)
         world, rank = 1, 0
         if self.process_group is not None:
             world = dist.get_world_size(self.process_group)
             rank = dist.get_rank(self.process_group)
+        mine = [i for i in range(n_init) if i % world == rank]
+        seeds, trials = self._draw_seeds(rs, n, n_init, set(mine))
         runs = []
-        draws = self.seeding_draws(self.n_clusters)
-        for i in range(n_init):
-            if i % world != rank:
-                # another rank's restart: advance the one RandomState stream past its seeding (a fixed count of
-                # doubles) instead of computing it, so every rank seeds only its own restarts
-                rs.random_sample(draws)
-                continue
-            c0, _ = self._kmeans_plusplus(Xc, rs, w)
-            labels, inertia, centers, n_iter = self._lloyd(Xc, c0, tol)
-            runs.append((i, labels.cpu().numpy(), inertia, centers.cpu().numpy(), n_iter))
+        # restarts in lockstep: <= 16 per batch, R x trials <= 64 (hlmc_km_pp_*), their candidate rows in LDS
+        g = max(1, min(16, 64 // trials, (150 * 1024) // (8 * trials * (d + 1))))
+        for g0 in range(0, len(mine), g):
+            grp = mine[g0:g0 + g]
+            c0, _ = self._kmeans_plusplus_batch(Xc, [seeds[i] for i in grp], trials)
+            labels, inertia, centers, n_iter = self._lloyd_batch(Xc, c0, tol)
+            for j, i in enumerate(grp):
+                runs.append((i, labels[j], float(inertia[j]), centers[j], int(n_iter[j])))
         if world > 1:
             gathered = [None] * world
             dist.all_gather_object(gathered, runs, group=self.process_group)

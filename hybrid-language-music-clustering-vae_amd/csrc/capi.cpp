@@ -388,6 +388,30 @@ int hlmc_km_inertia(void* stream, const float* X, int64_t n, int d, const float*
                     float* tmp) {
     return km::inertia(S(stream), X, n, d, C, labels, out, tmp);
 }
+int hlmc_km_assign_batch(void* stream, const float* X, int64_t n, int d, const float* C, int k, int R, uint64_t active,
+                         int32_t* labels, const int32_t* old, int32_t* n_changed) {
+    return km::assign_batch(S(stream), X, n, d, C, k, R, active, labels, old, n_changed);
+}
+int hlmc_km_sums_batch(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, int R,
+                       uint64_t active, float* sums, float* w, void* ws, int64_t ws_bytes) {
+    return km::sums_batch(S(stream), X, n, d, labels, k, R, active, sums, w, ws, (size_t)std::max<int64_t>(0, ws_bytes));
+}
+int hlmc_km_update_batch(void* stream, int k, int d, int R, uint64_t active, const float* sums, const float* w,
+                         const float* C_old, float* C_new, float* info) {
+    return km::update_batch(S(stream), k, d, R, active, sums, w, C_old, C_new, info);
+}
+int hlmc_km_pp_search(void* stream, int64_t n, int R, int T, const float* prev, int prevT, const int32_t* best,
+                      const double* rvals, int64_t* cand, int32_t* amb) {
+    return km::pp_search(S(stream), n, R, T, prev, prevT, best, rvals, cand, amb);
+}
+int hlmc_km_pp_dist(void* stream, const float* X, int64_t n, int d, int R, int T, const int64_t* cand, const float* prev,
+                    int prevT, const int32_t* best, float* out) {
+    return km::pp_dist(S(stream), X, n, d, R, T, cand, prev, prevT, best, out);
+}
+int hlmc_km_inertia_batch(void* stream, const float* X, int64_t n, int d, const float* C, int k, const int32_t* labels,
+                          int R, float* out, float* tmp) {
+    return km::inertia_batch(S(stream), X, n, d, C, k, labels, R, out, tmp);
+}
 int hlmc_km_rowdist(void* stream, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out) {
     return km::rowdist(S(stream), X, n, d, C, labels, out);
 }

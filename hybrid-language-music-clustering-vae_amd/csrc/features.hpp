@@ -65,6 +65,19 @@ int sums_part(hipStream_t s, const float* X, int64_t n, int d, const int32_t* la
 int inertia(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out,
             float* tmp);
 int rowdist(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out);
+// restart-batched (R restarts in lockstep; active = bitmask of the restarts to run)
+int assign_batch(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, int R, uint64_t active,
+                 int32_t* labels, const int32_t* old, int32_t* n_changed);
+int sums_batch(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, int R, uint64_t active,
+               float* sm, float* w, void* ws, size_t ws_bytes);
+int update_batch(hipStream_t s, int k, int d, int R, uint64_t active, const float* sm, const float* w,
+                 const float* C_old, float* C_new, float* info);
+int pp_search(hipStream_t s, int64_t n, int R, int T, const float* prev, int prevT, const int32_t* best,
+              const double* rvals, int64_t* cand, int32_t* amb);
+int pp_dist(hipStream_t s, const float* X, int64_t n, int d, int R, int T, const int64_t* cand, const float* prev,
+            int prevT, const int32_t* best, float* out);
+int inertia_batch(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, const int32_t* labels, int R,
+                  float* out, float* tmp);
 }  // namespace km
 
 // cluster-quality metrics (metrics.hip): silhouette (sklearn silhouette_score / silhouette_samples),

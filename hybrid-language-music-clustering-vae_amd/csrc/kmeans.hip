@@ -98,11 +98,19 @@ __device__ __forceinline__ float km_tree_halves(float* a) {
     return a[0];
 }
 
+// Restart-batched (blockIdx.y = restart r of R in lockstep, cluster.KMeans): centres C + r k d, labels / old +
+// r n, n_changed + r; restarts outside the active mask are skipped.
 __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict__ X, int64_t n, int d,
                                                         const float* __restrict__ C, int k,
                                                         int32_t* __restrict__ labels,
                                                         const int32_t* __restrict__ old,
-                                                        int32_t* __restrict__ n_changed) {
+                                                        int32_t* __restrict__ n_changed, uint64_t active) {
+    const int rs = blockIdx.y;
+    if (!((active >> rs) & 1)) return;
+    C += (int64_t)rs * k * d;
+    labels += (int64_t)rs * n;
+    if (old) old += (int64_t)rs * n;
+    if (n_changed) n_changed += rs;
     extern __shared__ float smem[];
     const int ldc = d + 1;               // padded: the 4 centres a wave reads per c sit in distinct banks
     float* Cs = smem;                    // [k][d + 1]
@@ -221,7 +229,13 @@ __device__ __forceinline__ float km_gather_add(const float* __restrict__ Xc, int
 
 __global__ __launch_bounds__(64) void km_sums_kernel(const float* __restrict__ X, int n, int d,
                                                      const int32_t* __restrict__ labels, int k,
-                                                     float* __restrict__ sums, float* __restrict__ weight) {
+                                                     float* __restrict__ sums, float* __restrict__ weight,
+                                                     uint64_t active) {
+    const int rs = blockIdx.z;   // restart (batched lockstep)
+    if (!((active >> rs) & 1)) return;
+    labels += (int64_t)rs * n;
+    sums += (int64_t)rs * k * d;
+    weight += (int64_t)rs * k;
     __shared__ int list[64 * kLabQ + kSumGrp];     // carried partial group + one super-tile of hits
     const int j = blockIdx.y;
     const int lane = threadIdx.x;
@@ -281,8 +295,22 @@ __device__ __forceinline__ uint64_t km_same_label(int lab, int nbits, bool valid
     return eq;
 }
 // hist[tile][c] = rows of cluster c in the tile
+// restart-batched: blockIdx.y = restart, each with its own labels [n] and workspace (km::PartWs)
+struct PartWs {
+    char* base;
+    int64_t bytes;   // per restart
+    int tiles, k;
+    __device__ int* hist(int r) const { return reinterpret_cast<int*>(base + r * bytes); }
+    __device__ int* bas(int r) const { return hist(r) + (int64_t)tiles * k; }
+    __device__ int* off(int r) const { return bas(r) + (int64_t)tiles * k; }
+    __device__ int* order(int r) const { return off(r) + (k + 1); }
+};
 __global__ __launch_bounds__(64) void km_part_hist_kernel(const int32_t* __restrict__ labels, int n, int k, int nbits,
-                                                          int* __restrict__ hist) {
+                                                          PartWs pw, uint64_t active) {
+    const int rs = blockIdx.y;
+    if (!((active >> rs) & 1)) return;
+    labels += (int64_t)rs * n;
+    int* __restrict__ hist = pw.hist(rs);
     extern __shared__ int cnt[];  // [k]
     const int lane = threadIdx.x, tile = blockIdx.x;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -313,8 +341,13 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
     }
     return v;
 }
-__global__ __launch_bounds__(1024) void km_part_scan_kernel(const int* __restrict__ hist, int tiles, int k,
-                                                            int* __restrict__ base, int* __restrict__ off) {
+__global__ __launch_bounds__(1024) void km_part_scan_kernel(PartWs pw, uint64_t active) {
+    const int rs = blockIdx.x;
+    if (!((active >> rs) & 1)) return;
+    const int tiles = pw.tiles, k = pw.k;
+    const int* __restrict__ hist = pw.hist(rs);
+    int* __restrict__ base = pw.bas(rs);
+    int* __restrict__ off = pw.off(rs);
     extern __shared__ int tot[];  // [k + 1]
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     for (int c = wave; c < k; c += 16) {
@@ -352,8 +385,12 @@ __global__ __launch_bounds__(1024) void km_part_scan_kernel(const int* __restric
 }
 // order[base[tile][c] + rank] = row, rank = rows of cluster c before it in the tile (ballot prefix, row order)
 __global__ __launch_bounds__(64) void km_part_scatter_kernel(const int32_t* __restrict__ labels, int n, int k,
-                                                             int nbits, const int* __restrict__ base,
-                                                             int* __restrict__ order) {
+                                                             int nbits, PartWs pw, uint64_t active) {
+    const int rs = blockIdx.y;
+    if (!((active >> rs) & 1)) return;
+    labels += (int64_t)rs * n;
+    const int* __restrict__ base = pw.bas(rs);
+    int* __restrict__ order = pw.order(rs);
     extern __shared__ int cur[];  // [k] next free position per cluster
     const int lane = threadIdx.x, tile = blockIdx.x;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -385,10 +422,21 @@ __device__ __forceinline__ void lds_release(int* p, int v) {
 // kMode 0: cluster j = blockIdx.y, entries order[off[j] .. off[j+1]) -> out0[j][c] = sum, out1[j] = count.
 // kMode 1: all n rows in order, one pass (out1 == nullptr) or two -> out0[c] = X.mean(axis=0) and
 // out1[c] = np.var(X, axis=0) (numpy: sequential float32 sums, / n; the second pass adds (x - mean)^2).
+// kMode 0 is restart-batched: blockIdx.z = restart (order / off from its PartWs, out0 + r k d, out1 + r k)
 template <int kMode>
 __global__ __launch_bounds__(64 * (kRingLoaders + 1)) void km_ring_kernel(
-    const float* __restrict__ X, int n, int d, const int* __restrict__ order, const int* __restrict__ off,
-    float* __restrict__ out0, float* __restrict__ out1) {
+    const float* __restrict__ X, int n, int d, PartWs pw, float* __restrict__ out0, float* __restrict__ out1,
+    uint64_t active) {
+    const int* __restrict__ order = nullptr;
+    const int* __restrict__ off = nullptr;
+    if constexpr (kMode == 0) {
+        const int rs = blockIdx.z;
+        if (!((active >> rs) & 1)) return;
+        order = pw.order(rs);
+        off = pw.off(rs);
+        out0 += (int64_t)rs * pw.k * d;
+        out1 += (int64_t)rs * pw.k;
+    }
     // [slot][column][row]: a lane's 64 rows of its column are contiguous (b128 writes and reads; the 68-float
     // pitch puts 16 consecutive lanes' 16-byte accesses in distinct banks), 139 KB
     __shared__ __align__(16) float ring[kRingSlots][64][kRingPitch];
@@ -482,8 +530,12 @@ __global__ __launch_bounds__(64 * (kRingLoaders + 1)) void km_ring_kernel(
 }
 
 // _euclidean_dense_dense(squared=True): float32 sum of 4-element groups, then the tail
-__global__ void km_rowdist_kernel(const float* __restrict__ X, int64_t n, int d, const float* __restrict__ C,
+// restart-batched: blockIdx.y = restart (C + r k d, labels / out + r n)
+__global__ void km_rowdist_kernel(const float* __restrict__ X, int64_t n, int d, const float* __restrict__ C, int k,
                                   const int32_t* __restrict__ labels, float* __restrict__ out) {
+    C += (int64_t)blockIdx.y * k * d;
+    labels += (int64_t)blockIdx.y * n;
+    out += (int64_t)blockIdx.y * n;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float* a = X + i * d;
         const float* b = C + (int64_t)labels[i] * d;
@@ -504,6 +556,8 @@ __global__ void km_rowdist_kernel(const float* __restrict__ X, int64_t n, int d,
 // float32 sum of v[0..n) in index order: one wave stages 1024 values per round in LDS (coalesced loads,
 // the next round prefetched in registers); lane 0 adds them sequentially from LDS.
 __global__ __launch_bounds__(64) void km_seqsum_kernel(const float* __restrict__ v, int64_t n, float* out) {
+    v += (int64_t)blockIdx.x * n;   // restart-batched: one wave per restart
+    out += blockIdx.x;
     __shared__ __align__(16) float buf[64 * kLabQ];
     const int lane = threadIdx.x;
     float cur[kLabQ], nxt[kLabQ];
@@ -548,6 +602,193 @@ __global__ __launch_bounds__(64) void km_seqsum_kernel(const float* __restrict__
     if (lane == 0) out[0] = s;
 }
 
+// ---- k-means++ for R restarts in lockstep (cluster.KMeans._kmeans_plusplus_batch; sklearn _kmeans_plusplus)
+// Per restart r the previous step's distances prev [R][prevT][n] hold its closest-distance row at trial best[r].
+constexpr int kPpMax = 64;      // restarts x trials per launch
+struct PpArgs {
+    int best[kPpMax];           // per restart: the row of prev holding closest_dist_sq (0 on the first step)
+    double rv[kPpMax];          // per (restart, trial): rand_vals = uniform * pot (host: numpy's f64 product)
+};
+// searchsorted(np.cumsum(closest, dtype=float64), rv) without the sequential cumsum: a parallel prefix S^ of the
+// non-negative float64 terms is within B_i = 2 (i + h + 8) 2^-53 S^_i of BOTH the exact prefix and numpy's
+// sequential c_i (recursive-summation bounds gamma_i, gamma_h; h = the additions along S^'s evaluation tree), so
+//   lo = first i with S^_i + B_i >= rv  and  hi = first i with S^_i - B_i >= rv
+// bracket numpy's answer: lo == hi is it exactly; lo != hi (rv within ~1e-11 relative of a prefix, or inside a
+// run of zero distances) is flagged and the host redoes that trial with numpy.  cand = min(ans, n - 1) (sklearn's
+// clip).  One 1024-thread block per restart: 16 waves x contiguous segments, a lane-strided pass for the segment
+// totals, then per 64-element row a wave scan; the first hit per trial and wave is kept with one LDS atomicMin.
+__global__ __launch_bounds__(1024) void km_pp_search_kernel(const float* __restrict__ prev, int prevT, int64_t n,
+                                                            int T, PpArgs a, int64_t* __restrict__ cand,
+                                                            int32_t* __restrict__ amb) {
+    const int r = blockIdx.x;
+    const float* __restrict__ v = prev + ((int64_t)r * prevT + a.best[r]) * n;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __shared__ double wtot[16], wbase[16];
+    __shared__ long long lo[kPpMax], hi[kPpMax];
+    const int64_t rows = ((n + 63) / 64 + 15) / 16;            // 64-element rows per wave segment
+    const int64_t s0 = (int64_t)w * rows * 64;
+    if (threadIdx.x < T) {
+        lo[threadIdx.x] = n;
+        hi[threadIdx.x] = n;
+    }
+    double part = 0.0;
+    for (int64_t q = 0; q < rows; ++q) {
+        const int64_t i = s0 + q * 64 + l;
+        part += i < n ? (double)v[i] : 0.0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (l == 0) wtot[w] = part;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double run = 0.0;
+        for (int k = 0; k < 16; ++k) {
+            wbase[k] = run;
+            run += wtot[k];
+        }
+    }
+    __syncthreads();
+    const double h = 2.0 * (double)rows + 40.0;
+    const double u2 = 2.0 * 0x1p-53;
+    double run = wbase[w];
+    uint64_t open = (T >= 64 ? ~0ull : ((1ull << T) - 1)) << 0;  // trials whose lo / hi this wave still seeks
+    uint64_t open_hi = open;
+    for (int64_t q = 0; q < rows && (open | open_hi); ++q) {
+        const int64_t i = s0 + q * 64 + l;
+        double x = i < n ? (double)v[i] : 0.0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_up(x, o, 64);
+            if (l >= o) x += y;
+        }
+        const double S = run + x;
+        const double B = u2 * ((double)i + h + 8.0) * S;
+        for (int t = 0; t < T; ++t) {
+            const uint64_t bit = 1ull << t;
+            if (open & bit) {
+                const uint64_t m = __ballot(i < n && S + B >= a.rv[r * T + t]);
+                if (m) {
+                    if (l == 0) atomicMin(&lo[t], (long long)(s0 + q * 64 + __builtin_ctzll(m)));
+                    open &= ~bit;
+                }
+            }
+            if (open_hi & bit) {
+                const uint64_t m = __ballot(i < n && S - B >= a.rv[r * T + t]);
+                if (m) {
+                    if (l == 0) atomicMin(&hi[t], (long long)(s0 + q * 64 + __builtin_ctzll(m)));
+                    open_hi &= ~bit;
+                }
+            }
+        }
+        run += __shfl(x, 63, 64);
+    }
+    __syncthreads();
+    if (threadIdx.x < T) {
+        const int t = threadIdx.x;
+        const long long a0 = lo[t], a1 = hi[t];
+        cand[r * T + t] = (a1 < n ? a1 : n - 1);
+        amb[r * T + t] = a0 != a1;
+    }
+}
+
+// out[r][t][i] = min(closest_r[i], float32(max(0, (-2 a.x_i + ||a||^2) + ||x_i||^2))) in float64 with
+// a = X[cand[r][t]] (sklearn _euclidean_distances_upcast + np.minimum(closest, dist)); prev == NULL: no minimum
+// (the first centre's distances).  Candidate rows (float64) in LDS; 8 candidates per pass over a row.
+__global__ __launch_bounds__(256) void km_pp_dist_kernel(const float* __restrict__ X, int64_t n, int d, int R, int T,
+                                                         const int64_t* __restrict__ cand,
+                                                         const float* __restrict__ prev, int prevT, PpArgs a,
+                                                         float* __restrict__ out) {
+    extern __shared__ double sh[];  // [RT][d] + norms [RT]
+    const int RT = R * T;
+    double* A = sh;
+    double* An = sh + (int64_t)RT * d;
+    for (int i = threadIdx.x; i < RT * d; i += blockDim.x) A[i] = (double)X[cand[i / d] * d + (i % d)];
+    __syncthreads();
+    for (int t = threadIdx.x; t < RT; t += blockDim.x)
+        An[t] = einsum_sq_f64([&](int c) { return A[(int64_t)t * d + c]; }, d);
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float* xr = X + i * d;
+        const double xx = einsum_sq_f64([&](int c) { return (double)xr[c]; }, d);
+        for (int t0 = 0; t0 < RT; t0 += 8) {
+            double dot[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) dot[t] = 0.0;
+            for (int k = 0; k < d; ++k) {
+                const double xv = xr[k];
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    if (t0 + t < RT) dot[t] = fma(A[(int64_t)(t0 + t) * d + k], xv, dot[t]);
+            }
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int rt = t0 + t;
+                if (rt >= RT) break;
+                const double dd = -2.0 * dot[t] + An[rt] + xx;
+                float o = fmaxf((float)dd, 0.f);
+                if (prev) {
+                    const int r = rt / T;
+                    o = fminf(prev[((int64_t)r * prevT + a.best[r]) * n + i], o);
+                }
+                out[(int64_t)rt * n + i] = o;
+            }
+        }
+    }
+}
+
+// ---- Lloyd centre update for R restarts (cluster.KMeans._lloyd_batch): C_new[j] = sums[j] * float32(1 / w[j])
+// (sklearn's centers_new *= 1 / weight_in_clusters, the reciprocal in double), info[r] = [||C_new[j] - C_old[j]||^2
+// in _euclidean_dense_dense float32 order (j < k), empty-cluster flag].  A restart with an empty cluster writes only
+// the flag: the host relocates (sklearn _relocate_empty_clusters_dense) and updates that one.
+__global__ __launch_bounds__(256) void km_update_kernel(int k, int d, const float* __restrict__ sums,
+                                                        const float* __restrict__ w, const float* __restrict__ C_old,
+                                                        float* __restrict__ C_new, float* __restrict__ info,
+                                                        uint64_t active) {
+    const int r = blockIdx.x;
+    if (!((active >> r) & 1)) return;
+    sums += (int64_t)r * k * d;
+    w += (int64_t)r * k;
+    C_old += (int64_t)r * k * d;
+    C_new += (int64_t)r * k * d;
+    info += (int64_t)r * (k + 1);
+    __shared__ int empty;
+    if (threadIdx.x == 0) empty = 0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < k; j += blockDim.x)
+        if (w[j] == 0.f) empty = 1;
+    __syncthreads();
+    if (empty) {
+        if (threadIdx.x == 0) info[k] = 1.f;
+        return;
+    }
+    for (int i = threadIdx.x; i < k * d; i += blockDim.x) {
+        const int j = i / d;
+        C_new[i] = sums[i] * (float)(1.0 / (double)w[j]);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < k; j += blockDim.x) {
+        const float* a = C_new + (int64_t)j * d;
+        const float* b = C_old + (int64_t)j * d;
+        float acc = 0.f;
+        const int q = d / 4;
+        for (int g = 0; g < q; ++g) {
+            const float e0 = a[4 * g] - b[4 * g], e1 = a[4 * g + 1] - b[4 * g + 1];
+            const float e2 = a[4 * g + 2] - b[4 * g + 2], e3 = a[4 * g + 3] - b[4 * g + 3];
+            float sg = e0 * e0;
+            sg = sg + e1 * e1;
+            sg = sg + e2 * e2;
+            sg = sg + e3 * e3;
+            acc = acc + sg;
+        }
+        for (int c = 4 * q; c < d; ++c) {
+            const float e = a[c] - b[c];
+            acc = acc + e * e;
+        }
+        info[j] = acc;
+    }
+    if (threadIdx.x == 0) info[k] = 0.f;
+}
+
 }  // namespace
 
 namespace km {
@@ -555,8 +796,8 @@ namespace km {
 int center(hipStream_t s, const float* X, int64_t n, int d, float* mean, float* var, float* Xc) {
     HLMC_CHECK_ARG(X && mean && Xc && n > 0 && d > 0, "bad km_center arguments");
     HLMC_CHECK_ARG(n < (int64_t)1 << 30, "km_center: n too large");
-    km_ring_kernel<1><<<(unsigned)((d + 63) / 64), 64 * (kRingLoaders + 1), 0, s>>>(X, (int)n, d, nullptr, nullptr,
-                                                                                   mean, var);
+    km_ring_kernel<1><<<(unsigned)((d + 63) / 64), 64 * (kRingLoaders + 1), 0, s>>>(X, (int)n, d, PartWs{}, mean, var,
+                                                                                   1);
     HLMC_LAUNCHED();
     km_sub_kernel<<<(unsigned)std::min<int64_t>(8192, (n * d + 255) / 256), 256, 0, s>>>(X, n, d, mean, Xc);
     HLMC_LAUNCHED();
@@ -577,67 +818,128 @@ int sqdist_rows(hipStream_t s, const float* X, int64_t n, int d, const int64_t* 
     return HLMC_OK;
 }
 
-int assign(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, int32_t* labels, const int32_t* old,
-           int32_t* n_changed) {
-    HLMC_CHECK_ARG(X && C && labels && n > 0 && d > 0 && k > 0, "bad km_assign arguments");
+static uint64_t mask_of(int R) { return R >= 64 ? ~0ull : ((1ull << R) - 1); }
+
+int assign_batch(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, int R, uint64_t active,
+                 int32_t* labels, const int32_t* old, int32_t* n_changed) {
+    HLMC_CHECK_ARG(X && C && labels && n > 0 && d > 0 && k > 0 && R >= 1 && R <= 64, "bad km_assign arguments");
     const size_t sh = ((size_t)k * (d + 1) + k + (size_t)kRows * (d + 1)) * sizeof(float);
     HLMC_CHECK_ARG(sh <= 160 * 1024, "k * d too large for LDS");
-    km_assign_kernel<<<(unsigned)((n + kRows - 1) / kRows), 256, sh, s>>>(X, n, d, C, k, labels, old, n_changed);
+    km_assign_kernel<<<dim3((unsigned)((n + kRows - 1) / kRows), (unsigned)R), 256, sh, s>>>(X, n, d, C, k, labels, old,
+                                                                                           n_changed, active & mask_of(R));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
+int assign(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, int32_t* labels, const int32_t* old,
+           int32_t* n_changed) {
+    return assign_batch(s, X, n, d, C, k, 1, 1, labels, old, n_changed);
+}
 
+static int sums_small(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, int R,
+                      uint64_t active, float* sm, float* w) {
+    km_sums_kernel<<<dim3((unsigned)((d + 63) / 64), (unsigned)k, (unsigned)R), 64, 0, s>>>(X, (int)n, d, labels, k, sm,
+                                                                                          w, active);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
 int sums(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w) {
     HLMC_CHECK_ARG(X && labels && sm && w && k > 0, "bad km_sums arguments");
     HLMC_CHECK_ARG(n > 0 && n < (int64_t)1 << 30 && d > 0 && k <= 65535, "bad km_sums sizes");
-    km_sums_kernel<<<dim3((unsigned)((d + 63) / 64), (unsigned)k), 64, 0, s>>>(X, (int)n, d, labels, k, sm, w);
-    HLMC_LAUNCHED();
-    return HLMC_OK;
+    return sums_small(s, X, n, d, labels, k, 1, 1, sm, w);
 }
 
 constexpr int64_t kPartMinRows = 4096;
 size_t sums_ws(int64_t n, int k) {
     const int64_t tiles = (n + kPartTile - 1) / kPartTile;
-    return (size_t)(2 * tiles * k + (k + 1) + n) * sizeof(int) + 256;
+    return (((size_t)(2 * tiles * k + (k + 1) + n) * sizeof(int)) + 255) & ~(size_t)255;
 }
-int sums_part(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w,
-              void* ws, size_t ws_bytes) {
-    HLMC_CHECK_ARG(X && labels && sm && w && ws && k > 0 && d > 0, "bad km_sums_part arguments");
+int sums_batch(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, int R, uint64_t active,
+               float* sm, float* w, void* ws, size_t ws_bytes) {
+    HLMC_CHECK_ARG(X && labels && sm && w && ws && k > 0 && d > 0 && R >= 1 && R <= 64, "bad km_sums_part arguments");
     HLMC_CHECK_ARG(n > 0 && n < (int64_t)1 << 30 && k <= 8192, "bad km_sums_part sizes");
-    HLMC_CHECK_ARG(ws_bytes >= sums_ws(n, k), "km_sums_part workspace too small");
-    if (n <= kPartMinRows) return sums(s, X, n, d, labels, k, sm, w);   // one pass beats four launches here
+    HLMC_CHECK_ARG(ws_bytes >= (size_t)R * sums_ws(n, k), "km_sums_part workspace too small");
+    active &= mask_of(R);
+    if (n <= kPartMinRows) return sums_small(s, X, n, d, labels, k, R, active, sm, w);  // one pass beats four here
     const int tiles = (int)((n + kPartTile - 1) / kPartTile);
-    int* hist = reinterpret_cast<int*>(ws);
-    int* base = hist + (int64_t)tiles * k;
-    int* off = base + (int64_t)tiles * k;
-    int* order = off + (k + 1);
+    PartWs pw{static_cast<char*>(ws), (int64_t)sums_ws(n, k), tiles, k};
     const size_t klds = (size_t)k * sizeof(int);
     int nbits = 0;
     while ((1 << nbits) < k) ++nbits;
-    km_part_hist_kernel<<<tiles, 64, klds, s>>>(labels, (int)n, k, nbits, hist);
+    km_part_hist_kernel<<<dim3(tiles, R), 64, klds, s>>>(labels, (int)n, k, nbits, pw, active);
     HLMC_LAUNCHED();
-    km_part_scan_kernel<<<1, 1024, klds + sizeof(int), s>>>(hist, tiles, k, base, off);
+    km_part_scan_kernel<<<R, 1024, klds + sizeof(int), s>>>(pw, active);
     HLMC_LAUNCHED();
-    km_part_scatter_kernel<<<tiles, 64, klds, s>>>(labels, (int)n, k, nbits, base, order);
+    km_part_scatter_kernel<<<dim3(tiles, R), 64, klds, s>>>(labels, (int)n, k, nbits, pw, active);
     HLMC_LAUNCHED();
-    km_ring_kernel<0><<<dim3((unsigned)((d + 63) / 64), (unsigned)k), 64 * (kRingLoaders + 1), 0, s>>>(
-        X, (int)n, d, order, off, sm, w);
+    km_ring_kernel<0><<<dim3((unsigned)((d + 63) / 64), (unsigned)k, (unsigned)R), 64 * (kRingLoaders + 1), 0, s>>>(
+        X, (int)n, d, pw, sm, w, active);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+int sums_part(hipStream_t s, const float* X, int64_t n, int d, const int32_t* labels, int k, float* sm, float* w,
+              void* ws, size_t ws_bytes) {
+    return sums_batch(s, X, n, d, labels, k, 1, 1, sm, w, ws, ws_bytes);
+}
+
+int update_batch(hipStream_t s, int k, int d, int R, uint64_t active, const float* sm, const float* w,
+                 const float* C_old, float* C_new, float* info) {
+    HLMC_CHECK_ARG(sm && w && C_old && C_new && info && k > 0 && d > 0 && R >= 1 && R <= 64, "bad km_update arguments");
+    km_update_kernel<<<R, 256, 0, s>>>(k, d, sm, w, C_old, C_new, info, active & mask_of(R));
     HLMC_LAUNCHED();
     return HLMC_OK;
 }
 
-int inertia(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out,
-            float* tmp) {
-    HLMC_CHECK_ARG(X && C && labels && out && tmp, "bad km_inertia arguments");
-    km_rowdist_kernel<<<(unsigned)std::min<int64_t>(4096, (n + 255) / 256), 256, 0, s>>>(X, n, d, C, labels, tmp);
-    HLMC_LAUNCHED();
-    km_seqsum_kernel<<<1, 64, 0, s>>>(tmp, n, out);
+int pp_search(hipStream_t s, int64_t n, int R, int T, const float* prev, int prevT, const int32_t* best,
+              const double* rvals, int64_t* cand, int32_t* amb) {
+    HLMC_CHECK_ARG(prev && best && rvals && cand && amb && n > 0 && R >= 1 && T >= 1 && R * T <= kPpMax && prevT >= 1,
+                   "bad km_pp_search arguments");
+    PpArgs a{};
+    for (int r = 0; r < R; ++r) {
+        HLMC_CHECK_ARG(best[r] >= 0 && best[r] < prevT, "km_pp_search: best row out of range");
+        a.best[r] = best[r];
+    }
+    for (int i = 0; i < R * T; ++i) a.rv[i] = rvals[i];
+    km_pp_search_kernel<<<R, 1024, 0, s>>>(prev, prevT, n, T, a, cand, amb);
     HLMC_LAUNCHED();
     return HLMC_OK;
+}
+
+int pp_dist(hipStream_t s, const float* X, int64_t n, int d, int R, int T, const int64_t* cand, const float* prev,
+            int prevT, const int32_t* best, float* out) {
+    HLMC_CHECK_ARG(X && cand && out && n > 0 && d > 0 && R >= 1 && T >= 1 && R * T <= kPpMax, "bad km_pp_dist arguments");
+    const size_t sh = ((size_t)R * T * d + (size_t)R * T) * sizeof(double);
+    HLMC_CHECK_ARG(sh <= 160 * 1024, "km_pp_dist: restarts x trials x d too large for LDS");
+    PpArgs a{};
+    if (prev) {
+        HLMC_CHECK_ARG(best && prevT >= 1, "km_pp_dist: prev needs best rows");
+        for (int r = 0; r < R; ++r) {
+            HLMC_CHECK_ARG(best[r] >= 0 && best[r] < prevT, "km_pp_dist: best row out of range");
+            a.best[r] = best[r];
+        }
+    }
+    km_pp_dist_kernel<<<(unsigned)std::min<int64_t>(4096, (n + 255) / 256), 256, sh, s>>>(X, n, d, R, T, cand, prev,
+                                                                                         prevT, a, out);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+
+int inertia_batch(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, const int32_t* labels, int R,
+                  float* out, float* tmp) {
+    HLMC_CHECK_ARG(X && C && labels && out && tmp && R >= 1, "bad km_inertia arguments");
+    km_rowdist_kernel<<<dim3((unsigned)std::min<int64_t>(4096, (n + 255) / 256), (unsigned)R), 256, 0, s>>>(
+        X, n, d, C, k, labels, tmp);
+    HLMC_LAUNCHED();
+    km_seqsum_kernel<<<R, 64, 0, s>>>(tmp, n, out);
+    HLMC_LAUNCHED();
+    return HLMC_OK;
+}
+int inertia(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out,
+            float* tmp) {
+    return inertia_batch(s, X, n, d, C, 1, labels, 1, out, tmp);
 }
 
 int rowdist(hipStream_t s, const float* X, int64_t n, int d, const float* C, const int32_t* labels, float* out) {
-    km_rowdist_kernel<<<(unsigned)std::min<int64_t>(4096, (n + 255) / 256), 256, 0, s>>>(X, n, d, C, labels, out);
+    km_rowdist_kernel<<<(unsigned)std::min<int64_t>(4096, (n + 255) / 256), 256, 0, s>>>(X, n, d, C, 1, labels, out);
     HLMC_LAUNCHED();
     return HLMC_OK;
 }

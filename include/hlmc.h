@@ -260,6 +260,35 @@ int hlmc_km_rowdist(void* stream, const float* X, int64_t n, int d, const float*
 int hlmc_km_inertia(void* stream, const float* X, int64_t n, int d, const float* centers, const int32_t* labels,
                     float* out, float* tmp);
 
+/* ---- R <= 64 restarts (n_init) in lockstep: the same arithmetic per restart, one launch per stage for all.
+ * Restart r's centres are centers + r*k*d, its labels labels + r*n; `active` is a bitmask of the restarts a launch
+ * runs (the others are left untouched).  The restarts of KMeans(n_init=10) share X and are independent objects. */
+int hlmc_km_assign_batch(void* stream, const float* X, int64_t n, int d, const float* centers, int k, int R,
+                         uint64_t active, int32_t* labels, const int32_t* labels_old, int32_t* n_changed);
+/* hlmc_km_sums_part per restart; ws: R * hlmc_km_sums_workspace(n, k) bytes; sums [R][k][d], weight [R][k] */
+int hlmc_km_sums_batch(void* stream, const float* X, int64_t n, int d, const int32_t* labels, int k, int R,
+                       uint64_t active, float* sums, float* weight, void* ws, int64_t ws_bytes);
+/* Lloyd centre update (sklearn: centers_new *= 1 / weight_in_clusters, reciprocal in double):
+ * C_new[r][j] = sums[r][j] * (float)(1.0 / weight[r][j]); info[r][j] (j < k) = ||C_new[r][j] - C_old[r][j]||^2 in
+ * _euclidean_dense_dense float32 order, info[r][k] = 1 when a cluster of restart r is empty (nothing else is written
+ * for it: the host relocates, sklearn _relocate_empty_clusters_dense), else 0.  info: [R][k + 1] floats */
+int hlmc_km_update_batch(void* stream, int k, int d, int R, uint64_t active, const float* sums, const float* weight,
+                         const float* C_old, float* C_new, float* info);
+/* k-means++ candidate draw of every restart (sklearn _kmeans_plusplus): restart r's closest distances are the row
+ * prev + (r*prevT + best[r])*n; cand[r][t] = min(searchsorted(np.cumsum(closest, dtype=float64), rvals[r][t]), n-1)
+ * from a parallel float64 prefix with a rigorous error bracket around numpy's sequential cumsum; amb[r][t] = 1 where
+ * the bracket cannot decide (the caller redoes that trial with numpy; rvals within ~1e-11 relative of a prefix).
+ * best, rvals: HOST arrays [R], [R*T]; cand (int64), amb (int32): device [R*T]; R*T <= 64 */
+int hlmc_km_pp_search(void* stream, int64_t n, int R, int T, const float* prev, int prevT, const int32_t* best,
+                      const double* rvals, int64_t* cand, int32_t* amb);
+/* out[r][t][i] = min(closest_r[i], sqdist(X[cand[r][t]], X[i])) (hlmc_km_sqdist_rows arithmetic, candidates from the
+ * DEVICE array cand [R*T]); prev == NULL: the plain distances (first centre), else closest_r as in hlmc_km_pp_search */
+int hlmc_km_pp_dist(void* stream, const float* X, int64_t n, int d, int R, int T, const int64_t* cand, const float* prev,
+                    int prevT, const int32_t* best, float* out);
+/* hlmc_km_inertia per restart: out [R], tmp [R][n] */
+int hlmc_km_inertia_batch(void* stream, const float* X, int64_t n, int d, const float* centers, int k,
+                          const int32_t* labels, int R, float* out, float* tmp);
+
 /* ============================================================== cluster-quality metrics
  * sklearn.metrics.silhouette_score / silhouette_samples (metric "euclidean"), replacing the calls at
  * src/Convolutional_VAE.py:320,337,361,399, src/Conditional_VAE.py:298, src/Simple_VAE.py:247,256,262.

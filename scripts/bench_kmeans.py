@@ -45,14 +45,14 @@ def case(n, d, k, n_init, sklearn_too):
     torch.cuda.synchronize()
     fit_ms = (time.perf_counter() - t0) * 1e3
     iters = 0
-    orig = km._lloyd
+    orig = km._lloyd_batch
 
     def counting(*a, **kw):
         nonlocal iters
         r = orig(*a, **kw)
-        iters += r[3]
+        iters += int(np.sum(r[3]))
         return r
-    km._lloyd = counting
+    km._lloyd_batch = counting
     km.fit(X)
     Xd = torch.as_tensor(X, device="cuda")
     C = Xd[:k].contiguous()

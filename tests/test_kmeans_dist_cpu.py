@@ -1,6 +1,6 @@
 """Restart-sharded KMeans(process_group=...) host logic on CPU with world_size-2 gloo.
 
-The device helpers (_center, _sqdist, _lloyd) are swapped for the numpy oracle's pieces so the test runs
+The device helpers (_center, _sqdist, _kmeans_plusplus_batch, _lloyd_batch) are swapped for the numpy oracle's pieces so the test runs
 without a GPU; what is under test is the sharding of the n_init restarts over ranks, the replicated
 k-means++ RandomState stream and the gathered best-of rule.  Both ranks must return the single-process
 result, and that must equal the oracle KMeans (itself pinned to sklearn 1.7.2 by tests/golden)."""
@@ -36,11 +36,34 @@ def _cpu_kmeans_cls():
             X = Xc.numpy()
             return torch.from_numpy(KO._sqdist_upcast(X[np.asarray(cand)], X))
 
-        def _lloyd(self, Xc, centers, tol):
+        def _kmeans_plusplus_batch(self, Xc, seeds, trials):
+            # the oracle's k-means++ (sklearn _kmeans_plusplus) fed with the pre-drawn random numbers
+            X = Xc.numpy()
+            n, k = X.shape[0], self.n_clusters
+            w = np.ones(n, np.float32)
+            cents = []
+            for cid, us in seeds:
+                idx = [cid]
+                closest = KO._sqdist_upcast(X[cid][None, :], X)
+                pot = closest @ w
+                for c in range(1, k):
+                    cand = np.searchsorted(np.cumsum((w * closest).astype(np.float64), dtype=np.float64), us[c - 1] * pot)
+                    np.clip(cand, None, n - 1, out=cand)
+                    dc = KO._sqdist_upcast(X[cand], X)
+                    np.minimum(closest, dc, out=dc)
+                    cpot = dc @ w.reshape(-1, 1)
+                    b = int(np.argmin(cpot))
+                    pot, closest = cpot[b], dc[b]
+                    idx.append(int(cand[b]))
+                cents.append(X[idx])
+            return torch.from_numpy(np.stack(cents)), None
+
+        def _lloyd_batch(self, Xc, centers, tol):
             X = Xc.numpy()
             w = np.ones(X.shape[0], np.float32)
-            lab, inertia, cen, nit = KO.kmeans_single_lloyd(X, w, centers.numpy(), self.max_iter, tol)
-            return torch.from_numpy(lab), inertia, torch.from_numpy(cen), nit
+            res = [KO.kmeans_single_lloyd(X, w, c, self.max_iter, tol) for c in centers.numpy()]
+            return (np.stack([r[0] for r in res]), np.array([r[1] for r in res]), np.stack([r[2] for r in res]),
+                    np.array([r[3] for r in res]))
 
     return CpuKMeans
 
@@ -88,17 +111,21 @@ def test_select_best_keeps_first_of_equal_partitions():
 
 
 def test_seeding_draws_match_the_stream():
-    """A rank skips another rank's k-means++ seeding by drawing KMeans.seeding_draws(k) doubles: the RandomState
-    must then stand exactly where the seeding itself would have left it (any k, any data)."""
+    """The restarts' random numbers are drawn up front (KMeans._draw_seeds) and a rank skips another rank's seeding
+    by drawing KMeans.seeding_draws(k) doubles: either way the RandomState must stand exactly where sklearn's
+    sequential k-means++ seedings (the oracle's kmeans_plusplus) leave it, and the kept draws must be the ones that
+    seeding consumes (any k, any data)."""
     cls = _cpu_kmeans_cls()
     X = _data()
-    Xc = torch.from_numpy(X - X.mean(axis=0))
-    w = np.ones(N, np.float32)
+    Xc = X - X.mean(axis=0)
     for k in (2, 3, 7, 10, 14):
-        a, b = np.random.RandomState(42), np.random.RandomState(42)
-        for _ in range(3):
-            cls(n_clusters=k)._kmeans_plusplus(Xc, a, w)
-        b.random_sample(3 * cls.seeding_draws(k))
-        sa, sb = a.get_state(), b.get_state()
-        assert np.array_equal(sa[1], sb[1]) and sa[2:] == sb[2:], k
-        assert a.random_sample() == b.random_sample()
+        a, b, c = np.random.RandomState(42), np.random.RandomState(42), np.random.RandomState(42)
+        want = [KO.kmeans_plusplus(Xc, k, a)[1] for _ in range(3)]
+        seeds, trials = cls(n_clusters=k)._draw_seeds(b, N, 3, {0, 1, 2})
+        cls(n_clusters=k)._draw_seeds(c, N, 3, set())
+        for rs in (b, c):
+            sa, sb = a.get_state(), rs.get_state()
+            assert np.array_equal(sa[1], sb[1]) and sa[2:] == sb[2:], k
+        got, _ = cls(n_clusters=k)._kmeans_plusplus_batch(torch.from_numpy(Xc), [seeds[i] for i in range(3)], trials)
+        np.testing.assert_array_equal(got.numpy(), np.stack([Xc[w] for w in want]))
+        assert a.random_sample() == b.random_sample() == c.random_sample()

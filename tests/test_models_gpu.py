@@ -446,11 +446,18 @@ def test_three_adam_steps_match_fixture_trajectory(cuda, name):
     differ by 2·lr.  Contract: those BN-fed biases are excluded; of the sampled entries of every other
     parameter ≥ 97% agree within 1e-2·lr after step 1 (≥ 90% after step 3) and all within 2·lr·steps; the
     per-tensor sum rows are not asserted (a few flips move them by 2·lr each).  BN running stats: within
-    1e-4 relative + 10·lr absolute (the running means carry the BN-fed biases' drift)."""
+    1e-4 relative + 10·lr absolute (the running means carry the BN-fed biases' drift).
+
+    How many entries a differently-rounded computation keeps within 1e-2·lr after 3 steps depends on the model:
+    the float64 oracle (the same chain in exact-er arithmetic) keeps 94 % for the hybrid but only 65 % for the
+    audio-only model, whose fusion layer feeds on the audio branch alone.  So the step-3 bar is the float64
+    yardstick's own fraction less 0.10 (capped at 0.90), computed here from the oracle chain in float64."""
     case = FX.case_by_name(name)
     fx = np.load(f"tests/golden/model_{name}.npz")
     ora, ours = build(case)
     lr = 1e-4
+    yard = _f64_trajectory_fractions(case, fx, lr)
+    bars = {0: min(0.97, yard[0] - 0.03), 2: min(0.90, yard[2] - 0.10)}
     opt = hlmc_amd.Adam(ours.parameters(), lr=lr)
     names = [n for n, _ in ours.named_parameters()]
     assert list(fx["param_names"]) == names
@@ -467,10 +474,34 @@ def test_three_adam_steps_match_fixture_trajectory(cuda, name):
             d = np.abs(samp_g - samp_r)
             assert float(d.max()) <= 2 * lr * (step + 1) + 1e-6, float(d.max())
             frac = float((d <= 1e-2 * lr).mean())
-            assert frac >= (0.97 if step == 0 else 0.90), f"step {step + 1}: {frac:.3f} of samples within 1e-2·lr"
+            print(f"{name} step {step + 1}: {frac:.3f} of samples within 1e-2·lr (float64 oracle {yard[step]:.3f})")
+            assert frac >= bars[step], f"step {step + 1}: {frac:.3f} of samples within 1e-2·lr (bar {bars[step]:.3f})"
             bg = FX.buffer_summary(_cpu_copy(ours))[:, 2:]
             br = fx[f"buffer_summary_after{step + 1}"][:, 2:]
             np.testing.assert_allclose(bg, br, rtol=1e-4, atol=10 * lr)
+
+
+def _f64_trajectory_fractions(case, fx, lr):
+    """{0: f, 2: f}: the fraction of the fixture's sampled parameter entries (BN-fed biases excluded) that the
+    float64 oracle chain (same init, inputs, eps, torch Adam) keeps within 1e-2·lr of the reference's fp32 chain
+    after steps 1 and 3 -- the yardstick of how rounding-sensitive the trajectory is."""
+    torch.manual_seed(42)
+    ora = OM.HybridVAE(**FX.oracle_ctor(case)).double()
+    opt = torch.optim.Adam(ora.parameters(), lr=lr)
+    keep = [i for i, (n, _) in enumerate(ora.named_parameters()) if not _bias_feeds_bn(ora, n)]
+    out = {}
+    for step in range(3):
+        ins, eps = FX.inputs_fn(case)(step)
+        ins = [None if t is None else t.double() for t in ins]
+        ora.train()
+        opt.zero_grad()
+        o = ora(*ins, eps=eps.double())
+        OM.loss_function(o[0], ins[0], o[1], ins[1], o[2], o[3])[0].backward()
+        opt.step()
+        if step in (0, 2):
+            d = np.abs(FX.param_summary(ora)[keep, 2:] - fx[f"param_summary_after{step + 1}"][keep, 2:])
+            out[step] = float((d <= 1e-2 * lr).mean())
+    return out
 
 
 class _cpu_copy:

@@ -102,13 +102,17 @@ class KMeans:
         k = self.n_clusters
         trials = 2 + int(np.log(k))
         w = np.ones(n, dtype=np.float32)
+        # rs.choice(n, p=w / w.sum()) is one random_sample() searched in the normalised float64 cdf of p
+        # (numpy mtrand.RandomState.choice); the cdf is the same for every restart, so it is built once
+        cdf = np.array(w / w.sum(), dtype=np.float64).cumsum()
+        cdf /= cdf[-1]
         draws = {}
         for i in range(n_init):
             if i not in mine:
                 rs.random_sample(self.seeding_draws(k))
                 continue
-            cid = rs.choice(n, p=w / w.sum())
-            draws[i] = (int(cid), [rs.uniform(size=trials) for _ in range(1, k)])
+            cid = int(cdf.searchsorted(rs.random_sample(), side="right"))
+            draws[i] = (cid, [rs.uniform(size=trials) for _ in range(1, k)])
         return draws, trials
 
     def _kmeans_plusplus_batch(self, Xc, seeds, trials):
@@ -134,9 +138,14 @@ class KMeans:
         bufs = [torch.empty(R, T, n, dtype=torch.float32, device=dev) for _ in range(2)]
         cand = torch.empty(R * T, dtype=torch.int64, device=dev)
         amb = torch.empty(R * T, dtype=torch.int32, device=dev)
-        pin = torch.empty(R, T, n, dtype=torch.float32).pin_memory() if dev.type == "cuda" else None
+        # two pinned host images of the distances (this step's and the previous step's closest rows)
+        pins = [torch.empty(R, T, n, dtype=torch.float32).pin_memory() for _ in range(2)] if dev.type == "cuda" else None
+        if pins is not None:
+            cpin = torch.empty(R * T, dtype=torch.int64).pin_memory()
+            apin = torch.empty(R * T, dtype=torch.int32).pin_memory()
         for c in range(1, k):
             out = bufs[c % 2]
+            pin = pins[c % 2] if pins is not None else None
             rv = np.stack([seeds[r][1][c - 1] * pots[r] for r in range(R)]).astype(np.float64)   # rand_vals
             prevT = prev.shape[1]
             bh = best.ctypes.data_as(C.POINTER(C.c_int32))
@@ -145,9 +154,12 @@ class KMeans:
                                           cand.data_ptr(), amb.data_ptr()), "hlmc_km_pp_search")
             L.check(lib.hlmc_km_pp_dist(L.stream(), Xc.data_ptr(), n, d, R, T, cand.data_ptr(), prev.data_ptr(),
                                         prevT, bh, out.data_ptr()), "hlmc_km_pp_dist")
-            if pin is not None:
+            if pin is not None:   # one synchronisation per step: the distances, candidates and flags
                 pin.copy_(out, non_blocking=True)
-                cand_h, amb_h = cand.cpu().numpy().reshape(R, T), amb.cpu().numpy().reshape(R, T)
+                cpin.copy_(cand, non_blocking=True)
+                apin.copy_(amb, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+                cand_h, amb_h = cpin.numpy().reshape(R, T).copy(), apin.numpy().reshape(R, T)
                 out_h = pin.numpy()
             else:
                 cand_h, amb_h = cand.cpu().numpy().reshape(R, T), amb.cpu().numpy().reshape(R, T)
@@ -169,7 +181,7 @@ class KMeans:
                 pots[r] = cpot[b]
                 best[r] = b
                 idx[r, c] = cand_h[r, b]
-            prev, prev_h = out, out_h.copy()
+            prev, prev_h = out, (out_h if pin is not None else out_h.copy())
         cent = Xc[torch.as_tensor(idx.reshape(-1), device=dev)].reshape(R, k, d).contiguous()
         return cent, idx
 
@@ -194,6 +206,9 @@ class KMeans:
         ws_bytes = int(lib.hlmc_km_sums_workspace(n, k)) * R
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         old_c = cbuf[0].cpu().numpy()
+        pinned = dev.type == "cuda"
+        pack_p = torch.empty(pack.shape, dtype=torch.float32).pin_memory() if pinned else None
+        cen_p = torch.empty(centers.shape, dtype=torch.float32).pin_memory() if pinned else None
         final_c = old_c.copy()
         final_lab = torch.empty(R, n, dtype=torch.int32, device=dev)
         n_iter = np.zeros(R, dtype=np.int64)
@@ -212,8 +227,13 @@ class KMeans:
                                            sums.data_ptr(), wts.data_ptr(), ws.data_ptr(), ws_bytes))
             L.check(lib.hlmc_km_update_batch(L.stream(), k, d, R, active, sums.data_ptr(), wts.data_ptr(),
                                              cur.data_ptr(), nxt.data_ptr(), info.data_ptr()))
-            pack_h = pack.cpu().numpy()
-            nxt_h = nxt.cpu().numpy()
+            if pinned:   # one synchronisation per iteration: counts, shifts and the new centres
+                pack_p.copy_(pack, non_blocking=True)
+                cen_p.copy_(nxt, non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+                pack_h, nxt_h = pack_p.numpy(), cen_p.numpy()
+            else:
+                pack_h, nxt_h = pack.cpu().numpy(), nxt.cpu().numpy()
             info_h = pack_h[:R * (k + 1)].reshape(R, k + 1)
             chg = pack_h[R * (k + 1):].view(np.int32)
             for r in range(R):
@@ -244,7 +264,7 @@ class KMeans:
                     shift = np.sqrt(_euclid_f32(new, old_c[r])).astype(np.float32)
                     nxt[r].copy_(torch.from_numpy(new))
                 else:
-                    new = nxt_h[r]
+                    new = nxt_h[r].copy()
                     shift = np.sqrt(info_h[r, :k]).astype(np.float32)
                 old_c[r] = new
                 done = False

@@ -795,6 +795,88 @@ __global__ __launch_bounds__(256, 4) void wgrad_c1_kernel(const T* __restrict__ 
     }
 }
 
+// The same weight gradient for the 64-wide layers (every use in the model), streamed by low-res ROWS: thread
+// (pixel c = tid / 4, channel group cg = tid % 4) of a block takes U rows per step with every load of the U rows
+// issued up front -- its 8 channels of L (one 16-byte load) and its 3 x 3 high-res taps as 6 float2 loads (columns
+// 2c-2 .. 2c+1 of rows 2r-1 .. 2r+1; the 4 channel groups of a pixel share the lines in L1) -- so a block keeps
+// U rows of loads in flight with no barrier in the loop.  acc[8 channels][9 taps] per thread; at the end lanes of
+// equal cg are summed with xor shuffles over the wave's 16 pixels, then the 4 waves in LDS, in a fixed order ->
+// part[block][co * 9 + tap] (sum_partials_f32_kernel adds the blocks).
+template <typename T>
+__global__ __launch_bounds__(256, 2) void wgrad_c1_rows_kernel(const T* __restrict__ L, int rows, int Hl,
+                                                             const float* __restrict__ Xh, float* __restrict__ part) {
+    constexpr int WL = 64, WH = 128, M = 32, U = 4;
+    __shared__ float red[4][4][8 * 9];
+    const int tid = threadIdx.x, c = tid >> 2, cg = tid & 3, lane = tid & 63, wave = tid >> 6;
+    float acc[8][9];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) acc[i][j] = 0.f;
+    const int stride = gridDim.x;
+    for (int r0 = blockIdx.x; r0 < rows; r0 += U * stride) {
+        float lv[U][8], xv[U][3][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // every load of the U rows issued before any use (rows past the end: row 0)
+            const int row = r0 + u * stride < rows ? r0 + u * stride : 0;
+            const T* lp = L + ((int64_t)row * WL + c) * M + 8 * cg;
+            if constexpr (sizeof(T) == 2) {
+                cvt16_f32<T>(*reinterpret_cast<const uint4*>(lp), lv[u]);
+            } else {
+                const float4 a = *reinterpret_cast<const float4*>(lp), b = *reinterpret_cast<const float4*>(lp + 4);
+                lv[u][0] = a.x; lv[u][1] = a.y; lv[u][2] = a.z; lv[u][3] = a.w;
+                lv[u][4] = b.x; lv[u][5] = b.y; lv[u][6] = b.z; lv[u][7] = b.w;
+            }
+            const int b = row / Hl, r = row - b * Hl;
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                const int ih = 2 * r - 1 + kh;
+                const float* xr = Xh + ((int64_t)b * 2 * Hl + (ih < 0 ? 0 : ih)) * WH + 2 * c;
+                const float2 lo = *reinterpret_cast<const float2*>(xr - (c > 0 ? 2 : 0));   // columns 2c-2, 2c-1
+                const float2 hi = *reinterpret_cast<const float2*>(xr);                     // columns 2c, 2c+1
+                const bool okr = ih >= 0;
+                xv[u][kh][0] = (okr && c > 0) ? lo.y : 0.f;   // column 2c - 1 (left padding at c = 0)
+                xv[u][kh][1] = okr ? hi.x : 0.f;
+                xv[u][kh][2] = okr ? hi.y : 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float m = r0 + u * stride < rows ? 1.f : 0.f;   // rows past the end add zero
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float l = lv[u][i] * m;
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) acc[i][kh * 3 + kw] = fmaf(l, xv[u][kh][kw], acc[i][kh * 3 + kw]);
+            }
+        }
+    }
+    // lanes 4 p + cg of a wave: sum over the 16 pixels p (xor over lane bits 2..5), fixed order
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            float v = acc[i][j];
+#pragma unroll
+            for (int o = 4; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+            acc[i][j] = v;
+        }
+    if (lane < 4) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 9; ++j) red[wave][lane][i * 9 + j] = acc[i][j];
+    }
+    __syncthreads();
+    for (int o = tid; o < M * 9; o += 256) {
+        const int co = o / 9, tap = o - co * 9, g = co >> 3, i = co & 7;
+        const float v = (red[0][g][i * 9 + tap] + red[1][g][i * 9 + tap]) + (red[2][g][i * 9 + tap] + red[3][g][i * 9 + tap]);
+        part[(int64_t)blockIdx.x * (M * 9) + o] = v;
+    }
+}
+
 __global__ __launch_bounds__(256) void sum_partials_f32_kernel(const float* __restrict__ part, int nblk, int n,
                                                                float* out) {
     __shared__ double sh[256];
@@ -1424,13 +1506,29 @@ int convT_c1(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const flo
 }
 
 static int wgrad_c1_blocks(int64_t K) { return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (K + 1023) / 1024)); }
+static int wgrad_c1_row_blocks(int64_t rows);
 size_t wgrad_c1_ws(int B, int Hl, int Wl, int M) {
-    return (size_t)wgrad_c1_blocks((int64_t)B * Hl * Wl) * M * 9 * sizeof(float);
+    return (size_t)std::max(wgrad_c1_blocks((int64_t)B * Hl * Wl), wgrad_c1_row_blocks((int64_t)B * Hl)) * M * 9 *
+           sizeof(float);
 }
+
+// 64-wide layers (every use in the model): the row-staged kernel on <= 512 blocks (two per CU)
+static int wgrad_c1_row_blocks(int64_t rows) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, rows)); }
 
 template <typename T>
 int wgrad_c1(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const float* Xh, float* dW, Ws ws) {
     HLMC_CHECK_ARG(M == 32, "wgrad_c1: only M == 32");
+    if (Wl == 64 && ((uintptr_t)L & 15) == 0 && ((uintptr_t)Xh & 15) == 0) {
+        const int64_t rows = (int64_t)B * Hl;
+        HLMC_CHECK_ARG(rows < (int64_t)1 << 31, "wgrad_c1: too many rows");
+        const int nb = wgrad_c1_row_blocks(rows);
+        HLMC_CHECK_ARG(ws.bytes >= (size_t)nb * M * 9 * sizeof(float), "wgrad_c1 workspace");
+        wgrad_c1_rows_kernel<T><<<nb, kThreads, 0, s>>>(L, (int)rows, Hl, Xh, ws.p);
+        HLMC_LAUNCHED();
+        sum_partials_f32_kernel<<<M * 9, 256, 0, s>>>(ws.p, nb, M * 9, dW);
+        HLMC_LAUNCHED();
+        return HLMC_OK;
+    }
     int64_t K = (int64_t)B * Hl * Wl;
     int nblk = wgrad_c1_blocks(K);
     HLMC_CHECK_ARG(ws.bytes >= wgrad_c1_ws(B, Hl, Wl, M), "wgrad_c1 workspace");

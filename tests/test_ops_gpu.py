@@ -193,8 +193,9 @@ def test_linear_wgrad(cuda, ws, dt, Mb, N, K):
             assert bool(db.isnan().all())
 
 
-# the bench's 128 x 128 clip and a 128 x 1024 mel row band besides the small case
-@pytest.mark.parametrize("shape", [(3, 16, 32), (2, 128, 128), (2, 32, 64), (1, 16, 1024)])
+# the bench's 128 x 128 clip and a 128 x 1024 mel row band besides the small case; (16, 128, 128) gives the row-staged
+# weight gradient (64-wide layers) two rows per block
+@pytest.mark.parametrize("shape", [(3, 16, 32), (2, 128, 128), (2, 32, 64), (1, 16, 1024), (16, 128, 128)])
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 def test_edge_convs(cuda, ws, dt, shape):
     code, tdt, tol = DT[dt]

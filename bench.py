@@ -454,8 +454,15 @@ def main():
             st = probe_read()
             if st["launches"]:
                 r = kind_roofline(kind, st)
-                breakdown[r["op"]] = {"us_per_step": round(st["ms"] * 1e3, 1), "launches_per_step": st["launches"],
-                                      "achieved": r["achieved"], "unit": r["unit"], "frac": r["frac"]}
+                e = {"us_per_step": round(st["ms"] * 1e3, 1), "launches_per_step": st["launches"],
+                     "achieved": r["achieved"], "unit": r["unit"], "frac": r["frac"],
+                     "bytes_per_launch": round(r["bytes_per_launch"]), "flops_per_launch": round(r["flops_per_launch"])}
+                # HBM traffic of the kind from the committed PMC summary against its algorithmic bytes
+                pm = pmc_traffic(kind)
+                if pm.get("hbm_bytes_per_launch") and r["bytes_per_launch"] > 0:
+                    e["traffic_per_launch"] = round(pm["hbm_bytes_per_launch"])
+                    e["traffic_ratio"] = round(pm["hbm_bytes_per_launch"] / r["bytes_per_launch"], 3)
+                breakdown[r["op"]] = e
         # the dominant single kernel (the BatchNorm family is 7 kernel types over ~96 launches per step: reported
         # from this untimed calibration only — event pairs around all its launches would cost the timed steps ~2.5 %)
         dominant = max((k for k in PROBE_KINDS if k != 64),

@@ -89,6 +89,9 @@ _SIGS = {
     "hlmc_km_sums_part": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_i64]),
     "hlmc_km_rowdist": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp]),
     "hlmc_km_inertia": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "hlmc_op_bn_bwd_workspace": (c_i64, [c_int]),
+    "hlmc_op_bn_bwd": (c_int, [c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                               c_i64]),
     "hlmc_km_assign_batch": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, C.c_uint64, c_vp, c_vp, c_vp]),
     "hlmc_km_sums_batch": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_int, c_int, C.c_uint64, c_vp, c_vp, c_vp, c_i64]),
     "hlmc_km_update_batch": (c_int, [c_vp, c_int, c_int, c_int, C.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -494,6 +494,30 @@ int hlmc_op_wgrad_c1(void* stream, int dtype, const void* Lo, int B, int Hl, int
 // the layer below's BatchNorm + LeakyReLU(0.01) applied while the input is staged (the engine's BnInput path):
 // x is then the pre-BN map, whose exact statistics this entry first accumulates with the moments pass the engine's
 // producers would have delivered.  out_sums[2 Co] = (sum y | sum y^2) over the stored bf16 outputs.
+int64_t hlmc_op_bn_bwd_workspace(int C) {
+    if (C <= 0) return 0;
+    return (int64_t)(((ops::bn_acc_bytes(C) + 255) & ~(size_t)255) + ((ops::bias_acc_bytes(C) + 255) & ~(size_t)255) +
+                     2 * (size_t)C * sizeof(float));
+}
+int hlmc_op_bn_bwd(void* stream, int dtype, const void* da, const void* y, int64_t R, int C, const float* mean,
+                   const float* invstd, const float* gamma, const float* beta, void* dy, float* dgamma, float* dbeta,
+                   float* dbias, void* ws, int64_t ws_bytes) {
+    HLMC_CHECK_ARG(da && y && mean && invstd && gamma && beta && dy && dgamma && dbeta && ws && R > 1 && C > 0,
+                   "hlmc_op_bn_bwd: arguments");
+    HLMC_CHECK_ARG(ws_bytes >= hlmc_op_bn_bwd_workspace(C), "hlmc_op_bn_bwd: workspace too small");
+    hipStream_t s = S(stream);
+    unsigned char* w = static_cast<unsigned char*>(ws);
+    const size_t o1 = (ops::bn_acc_bytes(C) + 255) & ~(size_t)255, o2 = o1 + ((ops::bias_acc_bytes(C) + 255) & ~(size_t)255);
+    HLMC_HIP(hipMemsetAsync(ws, 0, o2, s));
+    XAcc mom{reinterpret_cast<unsigned long long*>(w), xacc_shards(C), 2 * C};
+    XAcc bacc{reinterpret_cast<unsigned long long*>(w + o1), xacc_shards(C), C};
+    float* sums = reinterpret_cast<float*>(w + o2);
+    return DT_DISPATCH(dtype,
+        ops::bn_act_bwd<float>(s, (const float*)da, C, (const float*)y, R, C, mean, invstd, gamma, beta, 0, nullptr,
+                               1.f, (float*)dy, dgamma, dbeta, mom, nullptr, dbias ? bacc : XAcc{}, dbias, sums),
+        ops::bn_act_bwd<bf16>(s, (const bf16*)da, C, (const bf16*)y, R, C, mean, invstd, gamma, beta, 0, nullptr, 1.f,
+                              (bf16*)dy, dgamma, dbeta, mom, nullptr, dbias ? bacc : XAcc{}, dbias, sums));
+}
 static size_t halo_acc_off(int Ci) { return (XAcc::bytes(xacc_shards(Ci), 2 * Ci) + 255) & ~(size_t)255; }
 int64_t hlmc_op_halo_workspace(int Ci, int Co) {
     return (int64_t)(halo_acc_off(Ci) + XAcc::bytes(xacc_shards(Co), 2 * Co));

@@ -464,6 +464,110 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     }
 }
 
+// The whole BatchNorm backward of a SMALL layer (R <= 256 * kSmallRpt rows: the 4 x 4 / 2 x 2 conv maps and the
+// BatchNorm1d layers) in one launch: block b owns the V channels c0 = b V of every row, each of its 256 threads
+// holds its rows (r = t, t + 256, ...; <= kSmallRpt) of y and da in registers, so the moments are a block reduction
+// (f32 per thread, f64 xor-tree over the wave, then the 4 waves in order) and the apply pass reuses the held rows:
+// no accumulator atomics, no shard fold, no second read, one launch instead of two.  dgamma / dbeta written
+// directly; the conv-bias column sums of the stored dy go into the exact accumulator (one add per column).
+constexpr int kSmallRpt = 4;   // R <= 1024 (the 2 x 2 maps, BatchNorm1d at B <= 1024); at 16 rows per thread (4 x 4 maps) it lost to the two passes (34.8 vs 28.7 us)
+template <int V>
+__device__ __forceinline__ void block_sum_v(double (&x)[V], double (*lds)[V]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int v = 0; v < V; ++v)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x[v] += __shfl_xor(x[v], o, 64);
+    if (lane == 0)
+#pragma unroll
+        for (int v = 0; v < V; ++v) lds[w][v] = x[v];
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < V; ++v) x[v] = (lds[0][v] + lds[1][v]) + (lds[2][v] + lds[3][v]);
+    __syncthreads();
+}
+template <typename T, int ACT>
+__global__ __launch_bounds__(256) void bn_bwd_small_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
+                                                           int R, int C, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, int act, T* __restrict__ dy,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           XAcc bias_acc) {
+    constexpr int V = Vec16<T>::N;
+    __shared__ double red[4][V];
+    const int c0 = blockIdx.x * V, t = threadIdx.x;
+    float mu[V], is[V], ga[V], be[V];
+    BnChan::load(mean, c0, mu);
+    BnChan::load(invstd, c0, is);
+    BnChan::load(gamma, c0, ga);
+    BnChan::load(beta, c0, be);
+    uint4 ry[kSmallRpt], rg[kSmallRpt];
+#pragma unroll
+    for (int i = 0; i < kSmallRpt; ++i) {  // every load issued up front (clamped rows, masked below)
+        const int r = min(t + 256 * i, R - 1);
+        ry[i] = load16_raw(y + (int64_t)r * C + c0);
+        rg[i] = load16_raw(da + (int64_t)r * lda + c0);
+    }
+    float a[V], b[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) a[v] = b[v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSmallRpt; ++i) {
+        const bool ok = t + 256 * i < R;
+        float x[V], g[V];
+        cvt16_f32<T>(ry[i], x);
+        cvt16_f32<T>(rg[i], g);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const float xh = (x[v] - mu[v]) * is[v];
+            const float dz = ok ? g[v] * act_grad_t<ACT>(xh * ga[v] + be[v], act) : 0.f;
+            a[v] += dz;
+            b[v] = fmaf(dz, xh, b[v]);
+        }
+    }
+    double sa[V], sb[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) { sa[v] = a[v]; sb[v] = b[v]; }
+    block_sum_v<V>(sa, red);
+    block_sum_v<V>(sb, red);
+    float s0[V], sx[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) { s0[v] = (float)sa[v]; sx[v] = (float)sb[v]; }
+    if (t < V) {
+        dbeta[c0 + t] = s0[t];
+        dgamma[c0 + t] = sx[t];
+    }
+    const float invR = 1.f / (float)R;
+    float bs[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) bs[v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSmallRpt; ++i) {
+        const int r = t + 256 * i;
+        if (r >= R) break;
+        float x[V], g[V], o[V];
+        cvt16_f32<T>(ry[i], x);
+        cvt16_f32<T>(rg[i], g);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const float xh = (x[v] - mu[v]) * is[v];
+            const float dz = g[v] * act_grad_t<ACT>(xh * ga[v] + be[v], act);
+            o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
+        }
+        store16_f32(dy + (int64_t)r * C + c0, o);
+#pragma unroll
+        for (int v = 0; v < V; ++v) bs[v] += to_f32<T>(from_f32<T>(o[v]));   // the stored dy, rounded to T
+    }
+    if (bias_acc.on()) {
+        double sbias[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) sbias[v] = bs[v];
+        block_sum_v<V>(sbias, red);
+        if (t < V) xacc_add_shard(bias_acc, 0, c0 + t, sbias[t]);
+    }
+}
+
 // out[c] = column c of an exact accumulator (bias gradients); grid ceil(C / 64) x 64
 __global__ __launch_bounds__(64) void xacc_to_f32_kernel(XAcc acc, int C, float* out) {
     const int c = blockIdx.x * 64 + threadIdx.x;
@@ -1410,6 +1514,15 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
     if (bias_acc.on()) HLMC_TRY(check_acc(bias_acc, C));
     HLMC_CHECK_ARG(!dbias || bias_acc.on(), "bn_act_bwd: dbias needs its accumulator");
     HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_act_bwd: grad row stride must be a multiple of 16 bytes");
+    if (!mask && !(fused && fused->done) && R <= 256 * kSmallRpt) {  // small layer: one launch (bn_bwd_small_kernel)
+        auto k = act == 0 ? bn_bwd_small_kernel<T, 0> : bn_bwd_small_kernel<T, -1>;
+        HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C,
+                       (k<<<C / Vec16<T>::N, kThreads, 0, s>>>(da, lda, y, (int)R, C, mean, invstd, gamma, beta, act, dy,
+                                                              dgamma, dbeta, bias_acc)));
+        HLMC_LAUNCHED();
+        if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
+        return HLMC_OK;
+    }
     const int nblk = bn_blocks(R, C);
     const int64_t rpb = bn_rows_per_blk(R, C);
     if (fused && fused->done) {  // moments came with the producer of da

@@ -206,115 +206,6 @@ __global__ __launch_bounds__(256) void km_assign_kernel(const float* __restrict_
     }
 }
 
-// The same E-step, one thread per row and every cluster's chain in that thread (k <= kAsgK): a block is one
-// 256-row sklearn chunk.  Its rows are staged in LDS 32 columns at a time (pitch 36 floats: 16-byte reads of 4
-// consecutive columns, conflict-free), each centre value is an LDS broadcast, and the k fma chains run side by
-// side in registers (sequential over the columns, as the regular sgemm kernel sums them) -- per fma about one
-// LDS float instead of two, and no cross-lane combine.  The chunk's small-kernel case (the short last chunk)
-// runs the 16-lane partial sums of km_assign_kernel in the same thread.  Restart-batched like km_assign_kernel.
-constexpr int kAsgK = 16, kAsgCols = 32, kAsgPitch = 36;
-__global__ __launch_bounds__(256) void km_assign_rows_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                             const float* __restrict__ C, int k,
-                                                             int32_t* __restrict__ labels,
-                                                             const int32_t* __restrict__ old,
-                                                             int32_t* __restrict__ n_changed, uint64_t active) {
-    const int rs = blockIdx.y;
-    if (!((active >> rs) & 1)) return;
-    C += (int64_t)rs * k * d;
-    labels += (int64_t)rs * n;
-    if (old) old += (int64_t)rs * n;
-    if (n_changed) n_changed += rs;
-    extern __shared__ float sm[];
-    float* Cs = sm;                                 // [k][d]
-    float* cn = Cs + (int64_t)k * d;                // [k]
-    float* Xs = cn + kAsgK;                         // [256][kAsgPitch]
-    for (int i = threadIdx.x; i < k * d; i += 256) Cs[i] = C[i];
-    __syncthreads();
-    for (int j = threadIdx.x; j < k; j += 256) {    // ||c||^2: numpy einsum order (km_assign_kernel)
-        const float* cj = Cs + j * d;
-        float a4[4] = {0.f, 0.f, 0.f, 0.f};
-        int i = 0;
-        for (; d - i >= 16; i += 16)
-            for (int t = 3; t >= 0; --t)
-#pragma unroll
-                for (int l = 0; l < 4; ++l) {
-                    const float v = cj[i + 4 * t + l];
-                    a4[l] = v * v + a4[l];
-                }
-        for (; i < d; i += 4)
-#pragma unroll
-            for (int l = 0; l < 4; ++l) {
-                const float v = i + l < d ? cj[i + l] : 0.f;
-                a4[l] = v * v + a4[l];
-            }
-        cn[j] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-    }
-    const int64_t r0 = (int64_t)blockIdx.x * kChunk;
-    const int N = (int)min((int64_t)kChunk, n - r0);   // rows of this chunk
-    const bool small = (int64_t)k * N <= 1200 && d >= 32 && (double)k * N * d <= 1e6;
-    const int me = threadIdx.x;
-    const int64_t row = r0 + me;
-    float acc[kAsgK];
-#pragma unroll
-    for (int j = 0; j < kAsgK; ++j) acc[j] = 0.f;
-    float best = INFINITY;
-    int bj = 0x7fffffff;
-    if (!small) {
-        for (int c0 = 0; c0 < d; c0 += kAsgCols) {
-            const int w = min(kAsgCols, d - c0);
-            __syncthreads();   // the previous column block is consumed
-            // stage rows r0 .. r0 + 255, columns c0 .. c0 + w: wave v copies rows v, v + 4, ... lane-strided
-            for (int e = threadIdx.x; e < 256 * kAsgCols; e += 256) {
-                const int rr = e / kAsgCols, cc = e - rr * kAsgCols;
-                Xs[rr * kAsgPitch + cc] = (rr < N && cc < w) ? X[(r0 + rr) * d + c0 + cc] : 0.f;
-            }
-            __syncthreads();
-            const float* xr = Xs + me * kAsgPitch;
-            for (int c = 0; c < w; c += 4) {
-                const float4 xq = *reinterpret_cast<const float4*>(xr + c);
-                const float xv[4] = {xq.x, xq.y, xq.z, xq.w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (c + q >= w) break;
-#pragma unroll
-                    for (int j = 0; j < kAsgK; ++j)
-                        if (j < k) acc[j] = fmaf(xv[q], Cs[j * d + c0 + c + q], acc[j]);
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < kAsgK; ++j) {
-            if (j >= k) break;
-            const float dist = cn[j] + (-2.0f * acc[j]);
-            if (dist < best) { best = dist; bj = j; }   // ascending j: first minimum
-        }
-    } else if (row < n) {
-        // sklearn's small-matrix sgemm kernel (km_assign_kernel): 16 lanes of fma over k = l (mod 16), adjacent-pair
-        // tree, or halves-first where the element is in both remainders of 4
-        const int jl = (int)(row - r0);
-        const bool row_rem = jl >= 4 * (N / 4);
-        const int k4 = 4 * (k / 4);
-        const float* xg = X + row * d;
-        for (int j = 0; j < k; ++j) {
-            const float* cj = Cs + j * d;
-            float a[16];
-#pragma unroll
-            for (int l = 0; l < 16; ++l) a[l] = 0.f;
-            for (int b = 0; b < d; b += 16)
-#pragma unroll
-                for (int l = 0; l < 16; ++l)
-                    if (b + l < d) a[l] = fmaf(xg[b + l], cj[b + l], a[l]);
-            const float dot = (row_rem && j >= k4) ? km_tree_halves(a) : km_tree_adjacent(a);
-            const float dist = cn[j] + (-2.0f * dot);
-            if (dist < best) { best = dist; bj = j; }
-        }
-    }
-    if (row < n) {
-        labels[row] = bj;
-        if (old && n_changed && old[row] != bj) atomicAdd(n_changed, 1);
-    }
-}
-
 // sums[j][c] = sum_{i: l_i == j} X[i][c] in row order (float32); weight[j] = count.
 // One wave per (64-column slab, cluster j).  The wave walks the labels in super-tiles of 1024 rows (16 per
 // lane, the next super-tile prefetched into registers), compacts the rows of cluster j in row order with
@@ -932,15 +823,6 @@ static uint64_t mask_of(int R) { return R >= 64 ? ~0ull : ((1ull << R) - 1); }
 int assign_batch(hipStream_t s, const float* X, int64_t n, int d, const float* C, int k, int R, uint64_t active,
                  int32_t* labels, const int32_t* old, int32_t* n_changed) {
     HLMC_CHECK_ARG(X && C && labels && n > 0 && d > 0 && k > 0 && R >= 1 && R <= 64, "bad km_assign arguments");
-    // one thread per row with all k chains (k <= 16; full 256-row chunks take the regular sgemm order when
-    // k * 256 > 1200, i.e. k >= 5): km_assign_rows_kernel
-    const size_t shr = ((size_t)k * d + kAsgK + 256 * kAsgPitch) * sizeof(float);
-    if (k >= 5 && k <= kAsgK && shr <= 160 * 1024) {
-        km_assign_rows_kernel<<<dim3((unsigned)((n + kChunk - 1) / kChunk), (unsigned)R), 256, shr, s>>>(
-            X, n, d, C, k, labels, old, n_changed, active & mask_of(R));
-        HLMC_LAUNCHED();
-        return HLMC_OK;
-    }
     const size_t sh = ((size_t)k * (d + 1) + k + (size_t)kRows * (d + 1)) * sizeof(float);
     HLMC_CHECK_ARG(sh <= 160 * 1024, "k * d too large for LDS");
     km_assign_kernel<<<dim3((unsigned)((n + kRows - 1) / kRows), (unsigned)R), 256, sh, s>>>(X, n, d, C, k, labels, old,

@@ -344,6 +344,16 @@ int hlmc_op_wgrad_c1(void* stream, int dtype, const void* L, int B, int Hl, int 
  *     receive the batch statistics, running_mean / running_var / num_batches_tracked (nullable) are updated as
  *     torch does (momentum, unbiased variance), a_out [B,Hi,Wi,Ci] bf16 receives the activation.
  * ws: hlmc_op_halo_workspace(Ci, Co) bytes.  Returns an error for any other shape. */
+/* Train-mode BatchNorm2d + LeakyReLU(0.01) backward of one layer (the engine's bn_act_bwd: the moments pass
+ * [sum dz | sum dz * xhat] into an exact accumulator, then the apply pass dy = gamma invstd (dz - mean dz -
+ * xhat mean(dz xhat)) with its conv-bias column sums), src/Convolutional_VAE.py:80-100 / 124-139 backward.
+ * da / y / dy: [R][C] in `dtype` (bf16 or f32; da = grad of the activation, y = the pre-BN map); mean / invstd:
+ * the forward batch statistics; dgamma / dbeta [C] (f32) written; dbias (nullable, f32 [C]) = column sums of the
+ * stored dy.  ws: hlmc_op_bn_bwd_workspace(C) bytes (zeroed here). */
+int64_t hlmc_op_bn_bwd_workspace(int C);
+int hlmc_op_bn_bwd(void* stream, int dtype, const void* da, const void* y, int64_t R, int C, const float* mean,
+                   const float* invstd, const float* gamma, const float* beta, void* dy, float* dgamma, float* dbeta,
+                   float* dbias, void* ws, int64_t ws_bytes);
 int64_t hlmc_op_halo_workspace(int Ci, int Co);
 int hlmc_op_halo_fwd(void* stream, int kind, const void* x, int B, int Hi, int Wi, int Ci, const void* wp,
                      const float* bias, int Co, void* y, double* out_sums, const float* gamma, const float* beta,

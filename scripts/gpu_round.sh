@@ -26,6 +26,6 @@ timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $R/gpurun_out/p
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $R/gpurun_out/pmc_mfma -o run --output-format csv -- $BENCH --no-roofline > $R/gpurun_out/pmc_mfma.log 2>&1; rc=$?; echo "pmc mfma rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 cd $R
-python scripts/pmc_traffic.py gpurun_out/pmc_traffic.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof gpurun_out/pmc_mfma > /dev/null; echo "pmc_traffic rc=$?"
+python scripts/pmc_traffic.py gpurun_out/pmc_traffic.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/prof gpurun_out/pmc_mfma gpurun_out/bench.log > /dev/null; echo "pmc_traffic rc=$?"
 f=$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)
 python scripts/step_critical.py $f 2 > gpurun_out/crit.txt; head -3 gpurun_out/crit.txt

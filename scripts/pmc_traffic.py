@@ -1,12 +1,14 @@
 """HBM traffic per launch of every probed kernel kind from rocprofv3 PMC passes over bench.py, and the
 rocprofv3 kernel-trace average duration of the same kinds (the check on bench.py's live HIP-event timing).
 
-    python scripts/pmc_traffic.py OUT_JSON FETCH_DIR WRITE_DIR TRACE_DIR [MFMA_DIR]
+    python scripts/pmc_traffic.py OUT_JSON FETCH_DIR WRITE_DIR TRACE_DIR [MFMA_DIR] [BENCH_LOG]
 
 FETCH_DIR / WRITE_DIR: `rocprofv3 --kernel-trace --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` output directories;
 TRACE_DIR: a `--kernel-trace --stats` run of the bench command.  HBM bytes per dispatch =
 (2 x FETCH_SIZE + WRITE_SIZE) x 1024: rocprofv3 reports both in KiB, and on gfx950 FETCH_SIZE counts half the
 bytes of 16-B-per-lane streaming reads (/opt/skills/guides/MI355X_MICROARCH.md, HBM section).
+BENCH_LOG (optional): an unprofiled bench.py output; its roofline.per_kind_untimed bytes_per_launch (the probe
+sites' algorithmic bytes, common.hpp probe::site) are copied per kind with traffic_ratio = HBM bytes / algorithmic.
 MFMA_DIR (optional): a `--kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE` pass.
 MFMA busy per dispatch = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs): the MFMA-unit cycles
 (MI355X_MICROARCH.md: "counts cycles") over the SIMD-cycles of the dispatch (GRBM_GUI_ACTIVE is summed over
@@ -63,6 +65,12 @@ def trace_avg(d):
 def main():
     out, fdir, wdir, tdir = sys.argv[1:5]
     mdir = sys.argv[5] if len(sys.argv) > 5 else None
+    algo = {}
+    if len(sys.argv) > 6:
+        for line in open(sys.argv[6]):
+            if line.startswith("{") and '"roofline"' in line:
+                pk = json.loads(line)["roofline"].get("per_kind_untimed", {})
+                algo = {k: v.get("bytes_per_launch") for k, v in pk.items() if v.get("bytes_per_launch")}
     fetch, nf = counters(fdir, "FETCH_SIZE")
     write, nw = counters(wdir, "WRITE_SIZE")
     tr = trace_avg(tdir)
@@ -78,6 +86,9 @@ def main():
             e["write_kib"] = round(write[k], 1)
             e["hbm_bytes_per_launch"] = (2.0 * fetch[k] + write[k]) * 1024.0
             e["pmc_dispatches"] = min(nf[k], nw[k])
+            if algo.get(k):
+                e["bytes_per_launch"] = algo[k]
+                e["traffic_ratio"] = round(e["hbm_bytes_per_launch"] / algo[k], 3)
         if k in tr:
             e["trace_avg_us"] = round(tr[k][0], 2)
             e["trace_dispatches"] = tr[k][1]

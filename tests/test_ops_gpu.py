@@ -489,3 +489,47 @@ def test_halo_fwd_nan_propagates(cuda):
     others = torch.arange(Ci) != 3
     assert torch.isfinite(m[others]).all() and torch.isfinite(rm.cpu()[others]).all()
     assert torch.isnan(sums.cpu()).all()
+
+
+# every BatchNorm layer shape of the bench step (B = 256, 128 x 128) plus a small one
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("R,C", [(4 * 8 * 8, 64), (256 * 64 * 64, 32), (256 * 32 * 32, 64), (256 * 16 * 16, 128),
+                                 (256 * 8 * 8, 256), (256 * 4 * 4, 512), (256 * 2 * 2, 512)])
+def test_bn_bwd_op_matches_reference(cuda, dt, R, C):
+    """hlmc_op_bn_bwd (the engine's moments + apply passes of train-mode BatchNorm2d + LeakyReLU(0.01) backward,
+    src/Convolutional_VAE.py:80-100 backward) vs the float64 formula on the same (quantised) inputs:
+    dz = da * lrelu'(xhat gamma + beta), dy = gamma invstd (dz - sum dz / R - xhat sum(dz xhat) / R),
+    dgamma = sum dz xhat, dbeta = sum dz, dbias = column sums of the stored dy.  bf16: dy within 1e-2 relative L2
+    (its own rounding is 2^-9), the sums within 1e-4; fp32: 1e-5 / 1e-5."""
+    code, tdt, _ = DT[dt]
+    g = torch.Generator().manual_seed(R % 9973 + C)
+    y = torch.randn(R, C, generator=g) * 1.7 + 0.3
+    da = torch.randn(R, C, generator=g)
+    gamma = 1 + 0.2 * torch.randn(C, generator=g)
+    beta = 0.1 * torch.randn(C, generator=g)
+    yq, daq = q(y, tdt), q(da, tdt)
+    mean = yq.mean(0).float()
+    invstd = (1.0 / torch.sqrt(yq.var(0, unbiased=False) + 1e-5)).float()
+    xh = (yq - mean.double()) * invstd.double()
+    z = xh * gamma.double() + beta.double()
+    dz = daq * torch.where(z > 0, 1.0, 0.01).double()
+    s0, sx = dz.sum(0), (dz * xh).sum(0)
+    ref = gamma.double() * invstd.double() * (dz - s0 / R - xh * sx / R)
+    yd, dad = y.to(cuda, tdt).contiguous(), da.to(cuda, tdt).contiguous()
+    dy = torch.empty(R, C, dtype=tdt, device=cuda)
+    dg, db, dbias = (torch.empty(C, device=cuda) for _ in range(3))
+    wsb = int(L.lib().hlmc_op_bn_bwd_workspace(C))
+    bws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+    P = L.ptr
+    md, ivd, gd, bd = (t.to(cuda) for t in (mean, invstd, gamma, beta))   # kept alive across the async launch
+    L.check(L.lib().hlmc_op_bn_bwd(L.stream(), code, P(dad), P(yd), R, C, P(md), P(ivd), P(gd), P(bd), P(dy), P(dg),
+                                   P(db), P(dbias), P(bws), wsb))
+    torch.cuda.synchronize()
+    tol_dy, tol_s = (1e-2, 1e-4) if dt == "bf16" else (1e-5, 1e-5)
+    assert rel(dy, ref) < tol_dy
+    assert rel(dg, sx) < tol_s and rel(db, s0) < tol_s
+    # dbias: the stored dy's column sums (mathematically ~0 here: a bias feeding BatchNorm), checked absolutely
+    # against the stored values' float64 sums, at the per-thread float32 accumulation's scale
+    dyh = dy.double().cpu()
+    err = (dbias.cpu().double() - dyh.sum(0)).abs()
+    assert bool((err <= 1e-5 * dyh.abs().sum(0) + 1e-6).all()), float(err.max())

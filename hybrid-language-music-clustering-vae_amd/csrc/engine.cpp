@@ -293,23 +293,11 @@ class NetT : public NetBase {
         side_q.push_back(std::move(f));
         return (int)side_q.size() >= batch ? flush_side(s) : HLMC_OK;
     }
-    // conv layers / dense layers per fork (HLMC_SIDE_BATCH / HLMC_DENSE_BATCH: measurement aids).  Measured on the
-    // bench step (scripts/gpu_r3_knobs.sh, 3 alternating rounds): conv 1 / dense 1 108.4k, 2 / 1 109.7k, 2 / 2
-    // 110.3k, 3 / 1 108.2k, 6 / 1 104.3k (the weight-gradient stream starts too late), 2 / 9 108.1k
-    static int side_batch() {
-        static const int n = [] {
-            const char* e = std::getenv("HLMC_SIDE_BATCH");
-            return e ? std::max(1, std::atoi(e)) : 2;
-        }();
-        return n;
-    }
-    static int dense_batch() {
-        static const int n = [] {
-            const char* e = std::getenv("HLMC_DENSE_BATCH");
-            return e ? std::max(1, std::atoi(e)) : 2;
-        }();
-        return n;
-    }
+    // conv layers / dense layers per fork.  Measured on the bench step (scripts/gpu_r3_knobs.sh, 3 alternating
+    // rounds): conv 1 / dense 1 108.4k, 2 / 1 109.7k, 2 / 2 110.3k, 3 / 1 108.2k, 6 / 1 104.3k (the weight-gradient
+    // stream starts too late), 2 / 9 108.1k
+    static constexpr int side_batch() { return 2; }
+    static constexpr int dense_batch() { return 2; }
     // run f on the weight-gradient stream now (with everything queued before it)
     int side(hipStream_t s, SideFn f) { return defer_side(s, std::move(f), 1); }
     // weight gradients of the dense layers: on the second stream (measured round 1: 93.3k vs 86.5k clips/s inline)

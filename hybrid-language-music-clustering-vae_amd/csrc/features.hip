@@ -57,20 +57,53 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
 
 // ---------------------------------------------------------------- STFT -> |X|^2 -> mel, one wavefront per frame
 // A 2048-sample real frame is packed into z[n] = x[2n] w[2n] + i x[2n+1] w[2n+1] (n < 1024) and transformed
-// with a Stockham FFT of radices 16, 16, 4: every lane holds 16 complex points, the radix-16 butterflies run
-// in registers (as 4 x 4), and the stage-to-stage exchanges go through a wave-private LDS buffer (no block
-// barriers: one wave's LDS accesses complete in issue order).  The real-FFT split produces the 1025 power
-// bins, then lane l accumulates the banded Slaney filters l, l+64, ...  Twiddles are e^{-2 pi i m / 2048}
-// from a double-precision host table (LDS-resident); the filterbank is packed per band (first bin, count).
-constexpr int kMaxW = 8192;    // filterbank weight floats held in LDS (chunk-transposed, zero padded)
+// as 1024 = 16 x 64 (four-step): lane p holds z[p + 64 r] (r < 16); a radix-16 DFT over r runs in registers,
+// the twiddles W1024^{p k1} follow, and the 64-point DFTs over the lanes run as six radix-2 decimation-in-
+// frequency stages whose exchanges never touch LDS.  Each stage swaps the lane bit it works on with a
+// register bit (v_permlane32_swap / v_permlane16_swap for lane bits 5 and 4, DPP row shifts under bank masks
+// for bits 3 and 2, quad permutes for bits 1 and 0), after which every lane holds both inputs of its
+// butterflies.  The real-FFT split reads the conjugate partner with one ds_bpermute per word; the 1025 power
+// bins go to a wave-private LDS row in natural order, and lane l accumulates the banded Slaney filters
+// (l, n_mels-1-l).  Twiddles come from double-precision host tables.
 constexpr int kWaves = 4;      // frames in flight per workgroup
 constexpr int kFpw = 4;        // frames per wave
 constexpr int kFpb = kWaves * kFpw;
-constexpr int kZ = kFFT + kFFT / 16;  // padded complex buffer (one pad slot per 16: conflict-free stage writes)
-constexpr int kTw2 = 15 * 16, kTw3 = 3 * 256;
+constexpr int kPwRow = kFFT + 4;    // power row (floats, 16-byte aligned)
+constexpr int kTwB = 15 * 64;       // W1024^{p k1}, k1 = 1..15
+constexpr int kTwC = 5 * 64;        // radix-2 stage twiddles, lane bits 1..5
 constexpr int kMelLanes = 64;  // band pairs (n_mels <= 128)
+constexpr int kMaxWLds = 16384;     // filterbank bytes held in LDS (chunk-transposed); larger tables stay in global
+constexpr int64_t kMaxStftSamples = int64_t(1) << 29;  // clip length: byte offsets of the buffer loads fit 31 bits
 
-__device__ __forceinline__ int zpad(int i) { return i + (i >> 4); }
+template <typename F>
+__device__ __forceinline__ F as_(int v) { return __builtin_bit_cast(F, v); }
+__device__ __forceinline__ int bits_(float v) { return __builtin_bit_cast(int, v); }
+
+// Exchange lane bit J with the register bit that tells x (bit 0) from y (bit 1): afterwards x[l] holds the old
+// (l_J ? y[l - 2^J] : x[l]) and y[l] the old (l_J ? y[l] : x[l + 2^J]).
+template <int J>
+__device__ __forceinline__ void lane_swap(float& x, float& y, bool lj) {
+    if constexpr (J == 5) {
+        const auto r = __builtin_amdgcn_permlane32_swap(bits_(x), bits_(y), false, false);
+        x = as_<float>(r[0]); y = as_<float>(r[1]);
+    } else if constexpr (J == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(bits_(x), bits_(y), false, false);
+        x = as_<float>(r[0]); y = as_<float>(r[1]);
+    } else if constexpr (J == 3 || J == 2) {
+        // row_shr / row_shl by 2^J; bank_mask keeps the lanes whose bit J already matches
+        constexpr int d = 1 << J, hi = J == 3 ? 0xC : 0xA, lo = J == 3 ? 0x3 : 0x5;
+        const float nx = as_<float>(__builtin_amdgcn_update_dpp(bits_(x), bits_(y), 0x110 + d, 0xF, hi, false));
+        const float ny = as_<float>(__builtin_amdgcn_update_dpp(bits_(y), bits_(x), 0x100 + d, 0xF, lo, false));
+        x = nx; y = ny;
+    } else {
+        constexpr int qp = J == 1 ? 0x4E : 0xB1;  // quad_perm lane ^ 2 / lane ^ 1
+        // (bound_ctrl set, all quad sources valid: lets the compiler fold the move into the select as its DPP source)
+        const float ty = as_<float>(__builtin_amdgcn_mov_dpp(bits_(y), qp, 0xF, 0xF, true));
+        const float tx = as_<float>(__builtin_amdgcn_mov_dpp(bits_(x), qp, 0xF, 0xF, true));
+        x = lj ? ty : x;
+        y = lj ? y : tx;
+    }
+}
 // Lanes of one wavefront exchange data through LDS without a workgroup barrier: a wavefront-scope
 // release/acquire pair around wave_barrier orders the exchange's writes before the other lanes' reads.
 __device__ __forceinline__ void wave_lds_fence() {
@@ -295,226 +328,262 @@ __device__ __forceinline__ void piptrack_frame(const float* pw, int ln, const Pi
     if (ln == 63) pa.cnt[row] = min(inc, pa.maxpk);
 }
 
-// kMode 0: banded mel (stored [b][m][t]) + per-clip max/min.  kMode 1: spectral shape of |X| (power 1):
-// centroid, bandwidth (p = 2) and rolloff per frame, stored f64 [b][3][t] (sout); the mel tables are unused.
-template <int kMode>
-__device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int64_t n_samples, int T,
+// Radix-2 decimation-in-frequency stage on lane bit J of the 64-point lane DFTs: swap lane bit J into register
+// bit RB, then each lane forms both outputs of its butterflies in registers, (u + v) and (u - v) W.
+template <int J, int RB>
+__device__ __forceinline__ void lane_stage(float2 (&b)[16], float2 tw, bool lj) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        if (r & (1 << RB)) continue;
+        float2& x = b[r];
+        float2& y = b[r | (1 << RB)];
+        lane_swap<J>(x.x, y.x, lj);
+        lane_swap<J>(x.y, y.y, lj);
+        const float2 s = cadd(x, y), d = csub(x, y);
+        x = s;
+        y = J == 0 ? d : cmul(d, tw);
+    }
+}
+// After the six stages (lane bits 5,4,3,2,1,0 swapped with register bits 3,2,1,0,3,2) register r of lane l holds
+// X[bin_lane(l) + 64 bin_reg(r)].
+__device__ __forceinline__ constexpr int bin_reg(int r) { return ((r >> 1) & 1) | (r & 1) << 1 | ((r >> 3) & 1) << 2 | ((r >> 2) & 1) << 3; }
+__device__ __forceinline__ int bin_lane(int l) { return (l >> 2) | ((l >> 1) & 1) << 4 | (l & 1) << 5; }
+__device__ __forceinline__ int lane_of_bin(int g) { return ((g & 15) << 2) | ((g >> 4) & 1) << 1 | ((g >> 5) & 1); }
+
+// kMode 0: banded mel (stored [b][m][t]) + per-clip max/min; kWL: filterbank staged in LDS.  kMode 1: spectral
+// shape of |X| (power 1): centroid, bandwidth (p = 2) and rolloff per frame, stored f64 [b][3][t] (sout).
+// kMode 2: piptrack (PipArgs).  Modes 1 and 2 leave the mel tables unused.
+template <int kMode, bool kWL>
+__device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int nclips, int64_t n_samples, int T,
                                                        int hop, const float* __restrict__ window,
-                                                       const float2* __restrict__ rtw, const float2* __restrict__ tw23,
+                                                       const float2* __restrict__ rtw, const float2* __restrict__ tw,
                                                        const int* __restrict__ band,
                                                        const int* __restrict__ woff, const float* __restrict__ wts,
                                                        int n_mels, int nnz, float* __restrict__ out,
                                                        unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min,
                                                        double bin_hz, double roll, double* __restrict__ sout,
                                                        PipArgs pa) {
-    // LDS: stage-2/3 twiddles + the wave-private exchange buffers (43 KB static) + band info and mel staging
-    // (dynamic), 52 KB in all: 3 blocks per CU.  The real-split twiddles (rtw) and the chunk-transposed
-    // filterbank (wts, [c][lane][4]) are read from global memory (L1/L2-resident tables); in LDS they held the
-    // kernel at 2 blocks per CU.
-    __shared__ float2 stw23[kTw2 + kTw3];
-    __shared__ __align__(16) float2 zb[kWaves][kZ];
-    // dynamic: per-lane band info int4[64] | mel staging [kFpb][n_mels + 1]
+    // LDS: FFT twiddles + one power row per wave (27 KB static); dynamic: band info, the chunk-transposed
+    // filterbank (kWL, 16 KB at n_mels = 128) and the mel staging rows: 52 KB in all, 3 blocks per CU.
+    __shared__ float2 stw[kTwB + kTwC];
+    __shared__ __align__(16) float pwb[kWaves][kPwRow];
     extern __shared__ int4 sbl[];
-    float* smel = reinterpret_cast<float*>(sbl + kMelLanes);
+    float4* swt = reinterpret_cast<float4*>(sbl + kMelLanes);
+    float* smel = reinterpret_cast<float*>(swt + (kWL ? nnz / 4 : 0));
     const float4* __restrict__ gw4 = reinterpret_cast<const float4*>(wts);
-    const int b = blockIdx.y;
-    const int t0 = blockIdx.x * kFpb;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const float* x = pcm + (int64_t)b * n_samples;
-    for (int i = threadIdx.x; i < kTw2 + kTw3; i += 256) stw23[i] = tw23[i];
-    if constexpr (kMode == 0) {
-        for (int l = threadIdx.x; l < kMelLanes; l += 256) sbl[l] = reinterpret_cast<const int4*>(band)[l];
-    }
-    __syncthreads();
-    float2* z = zb[wave];
-    float* pw = reinterpret_cast<float*>(z);  // power bins overwrite the spectrum after the split
-    float lmax = 0.f, lmin = INFINITY;
-    const int nf = min(kFpb, T - t0);
-    // raw sample pairs (x[2n], x[2n+1]) of frame t: n = lane + 64 r; zero outside the clip (center padding)
-    auto fetch = [&](int t, int ln, float2 (&v)[16]) {
-        const int64_t start = (int64_t)t * hop - kFFT;  // center=True: n_fft/2 = 1024 zeros of padding
-        const bool interior = start >= 0 && start + 2 * kFFT <= n_samples && ((start & 1) == 0) &&
-                              ((reinterpret_cast<uintptr_t>(x) & 7) == 0);
-        if (interior) {
-            const float2* xs = reinterpret_cast<const float2*>(x + start);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = xs[ln + 64 * r];
-        } else {
-            // edge frame: clamped (always in-bounds) loads, zeroed outside the clip; no divergent branches
+    // Persistent blocks over the (clip, 16-frame group) items.  Blocks are dispatched round-robin over the 8
+    // XCDs; XCD k walks the contiguous item range [k n / 8, (k + 1) n / 8), so neighbouring groups of a clip (their
+    // frames share 1536 samples) run on one L2.  The tables are staged once per block, and each wave prefetches its
+    // first frame of the next item while it finishes the current one.
+    const int ng = (T + kFpb - 1) / kFpb;
+    const int nitems = nclips * ng;
+    const int xcd = blockIdx.x & 7, per = gridDim.x >> 3;
+    const int hi = (int)((int64_t)nitems * (xcd + 1) / 8);
+    int it = (int)((int64_t)nitems * xcd / 8) + (int)(blockIdx.x >> 3);
+    // raw sample pairs (x[2n], x[2n+1]) of frame t: n = lane + 64 r, through a buffer descriptor over the clip
+    // whose range check returns 0 outside it (center padding; negative offsets wrap past the range).  With an
+    // even clip length and hop a pair never straddles the clip's end, so one 8-byte load per pair.
+    const bool pairs = ((n_samples | hop) & 1) == 0;
+    auto fetch = [&](const float* x, int t, int ln, float2 (&v)[16]) {
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, (int)(n_samples * 4), 0x00020000);
+        const int start = t * hop - kFFT;  // center=True: n_fft/2 = 1024 zeros of padding
+        if (pairs) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int64_t i0 = start + 2 * (ln + 64 * r);
-                const int64_t c0 = min(max(i0, (int64_t)0), n_samples - 1), c1 = min(max(i0 + 1, (int64_t)0), n_samples - 1);
-                const float x0 = x[c0], x1 = x[c1];
-                v[r].x = (i0 >= 0 && i0 < n_samples) ? x0 : 0.f;
-                v[r].y = (i0 + 1 >= 0 && i0 + 1 < n_samples) ? x1 : 0.f;
+                // (bit_cast of the whole vector: extracting the builtin's elements one by one read word 0 twice)
+                v[r] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsrc, 4 * (start + 2 * (ln + 64 * r)), 0, 0));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int i0 = start + 2 * (ln + 64 * r);
+                v[r].x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, 4 * i0, 0, 0));
+                v[r].y = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, 4 * i0 + 4, 0, 0));
             }
         }
     };
     float2 nxt[16];
-    if (wave < nf) fetch(t0 + wave, lane, nxt);
-    for (int fl = wave; fl < nf; fl += kWaves) {
-        // opaque copy of the lane id: keeps the frame-invariant window / twiddle loads inside the loop
-        // (hoisted, they pin ~120 extra VGPRs and drop occupancy to one wave per SIMD)
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        float2 a[16];
-        // ---- stage 1 (radix 16, Ns = 1): z[j + 64 r] = windowed sample pairs (prefetched one frame ahead)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float2 w = *reinterpret_cast<const float2*>(window + 2 * (ln + 64 * r));
-            a[r] = make_float2(nxt[r].x * w.x, nxt[r].y * w.y);
+    bool have = false;  // nxt holds this wave's first frame of item `it`
+    if (it < hi) {       // first frame in flight while the tables are staged
+        const int b = it / ng, t0 = (it - b * ng) * kFpb;
+        if (wave < min(kFpb, T - t0)) {
+            fetch(pcm + (int64_t)b * n_samples, t0 + wave, lane, nxt);
+            have = true;
         }
-        if (fl + kWaves < nf) fetch(t0 + fl + kWaves, ln, nxt);
-        dft16(a);
-        // padded exchange addresses as lane base + compile-time offsets: zpad(i) = i + (i >> 4)
-        const int bw1 = ln * 17;                   // zpad(16 ln + r)        = 17 ln + r
-        const int brd = ln + (ln >> 4);            // zpad(ln + 64 q + 256 r) = brd + 68 q + 272 r
-        const int bw2 = (ln >> 4) * 272 + (ln & 15);  // zpad(256 g + k + 16 r) = 272 g + k + 17 r
+    }
+    for (int i = threadIdx.x; i < kTwB + kTwC; i += 256) stw[i] = tw[i];
+    if constexpr (kMode == 0) {
+        for (int l = threadIdx.x; l < kMelLanes; l += 256) sbl[l] = reinterpret_cast<const int4*>(band)[l];
+        if constexpr (kWL)
+            for (int i = threadIdx.x; i < nnz / 4; i += 256) swt[i] = gw4[i];
+    }
+    __syncthreads();
+    float* pw = pwb[wave];
+    // per-lane constants: this lane's bins, its conjugate partner's lane, the split twiddle base, stage twiddles,
+    // the window (frame-invariant, in registers)
+    const int fl = bin_lane(lane);
+    const int paddr = 4 * lane_of_bin((64 - fl) & 63);
+    const float2 wl = rtw[fl];
+    float2 tc[5];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) z[bw1 + r] = a[slot16(r)];
-        wave_lds_fence();
-        // ---- stage 2 (radix 16, Ns = 16)
-        const int k = ln & 15;
+    for (int j = 0; j < 5; ++j) tc[j] = stw[kTwB + 64 * j + lane];
+    const bool l0 = lane & 1, l1 = lane & 2;
+    float2 wnd[16];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) a[r] = z[brd + 68 * r];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) a[r] = cmul(a[r], stw23[(r - 1) * 16 + k]);
-        dft16(a);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) z[bw2 + 17 * r] = a[slot16(r)];
-        wave_lds_fence();
-        // ---- stage 3 (radix 4, Ns = 256): butterflies j = ln + 64 q, in place
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = ln + 64 * q;
-            float2 c0 = z[brd + 68 * q], c1 = z[brd + 68 * q + 272], c2 = z[brd + 68 * q + 544], c3 = z[brd + 68 * q + 816];
-            c1 = cmul(c1, stw23[kTw2 + j]);
-            c2 = cmul(c2, stw23[kTw2 + 256 + j]);
-            c3 = cmul(c3, stw23[kTw2 + 512 + j]);
-            dft4(c0, c1, c2, c3);
-            a[4 * q] = c0; a[4 * q + 1] = c1; a[4 * q + 2] = c2; a[4 * q + 3] = c3;
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) z[brd + 68 * q + 272 * r] = a[4 * q + r];
-        wave_lds_fence();
-        // ---- real-FFT split: X[f] = E[f] + e^{-2 pi i f / 2048} O[f], f = 0..1024
-        float p[17];
-        float2 w[17];   // real-split twiddles from global (issued before the LDS reads they pair with)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) w[q] = rtw[ln + 64 * q];
-        w[16] = rtw[kFFT];
-        // conjugate partner 1024 - f of f = ln + 64 q: zpad = 68 (16 - q) + bcj (f = 0 pairs with itself)
-        const int bcj = -ln + ((-ln) >> 4);
-        auto split = [&](float2 zf, float2 zc, float2 w) -> float {
-            const float2 e = make_float2(0.5f * (zf.x + zc.x), 0.5f * (zf.y - zc.y));
-            const float2 o = make_float2(0.5f * (zf.y + zc.y), -0.5f * (zf.x - zc.x));
-            const float2 ot = cmul(o, w);
-            const float re = e.x + ot.x, im = e.y + ot.y;
-            return fmaf(re, re, im * im);
-        };
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const float2 zf = z[brd + 68 * q];
-            const int ic = (q == 0 && ln == 0) ? 0 : 68 * (16 - q) + bcj;  // index select, one LDS read
-            const float2 zc = z[ic];
-            p[q] = split(zf, zc, w[q]);
-        }
-        {
-            const float2 z0 = z[0];
-            p[16] = split(z0, z0, w[16]);  // Nyquist bin (every lane computes it; lane 0 stores it)
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int q = 0; q < 16; ++q) pw[ln + 64 * q] = p[q];
-        if (ln == 0) pw[kFFT] = p[16];
-        wave_lds_fence();
-        // ---- banded mel: lane l owns the band pair (l, n_mels-1-l) (narrow + wide filter); each band is a
-        // fixed-order fma chain over 8-bin steps of b128 LDS reads (power bins and chunk-transposed weights)
-        if constexpr (kMode == 1) {
-            spectral_shape(pw, ln, bin_hz, roll, sout + (int64_t)b * 3 * T + t0 + fl, T);
-        } else if constexpr (kMode == 2) {
-            piptrack_frame(pw, ln, pa, (int64_t)b * T + t0 + fl);
-        } else {
-            const float4* pw4 = reinterpret_cast<const float4*>(pw);
-            const int4 bl = sbl[ln];
-            float acc0 = 0.f, acc1 = 0.f;
-            for (int c = 0; c < bl.y; c += 2) {
-                const float4 p0 = pw4[(bl.x >> 2) + c], p1 = pw4[(bl.x >> 2) + c + 1];
-                const float4 w0 = gw4[c * kMelLanes + ln], w1 = gw4[(c + 1) * kMelLanes + ln];
-                acc0 = fmaf(p0.x, w0.x, acc0); acc0 = fmaf(p0.y, w0.y, acc0);
-                acc0 = fmaf(p0.z, w0.z, acc0); acc0 = fmaf(p0.w, w0.w, acc0);
-                acc0 = fmaf(p1.x, w1.x, acc0); acc0 = fmaf(p1.y, w1.y, acc0);
-                acc0 = fmaf(p1.z, w1.z, acc0); acc0 = fmaf(p1.w, w1.w, acc0);
+    for (int r = 0; r < 16; ++r) wnd[r] = *reinterpret_cast<const float2*>(window + 2 * (lane + 64 * r));
+    for (; it < hi; it += per) {
+        const int b = it / ng, t0 = (it - b * ng) * kFpb, nf = min(kFpb, T - t0);
+        const float* x = pcm + (int64_t)b * n_samples;
+        const int nit = it + per;
+        if (!have && wave < nf) fetch(x, t0 + wave, lane, nxt);
+        have = false;
+        float lmax = 0.f, lmin = INFINITY;
+        for (int fi = wave; fi < nf; fi += kWaves) {
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            float2 a[16];
+            // ---- radix 16 over r in registers: z[ln + 64 r] = windowed sample pairs (prefetched one frame ahead)
+    #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                a[r] = make_float2(nxt[r].x * wnd[r].x, nxt[r].y * wnd[r].y);
             }
-            for (int c = 0; c < bl.w; c += 2) {
-                const int cw = bl.y + c;
-                const float4 p0 = pw4[(bl.z >> 2) + c], p1 = pw4[(bl.z >> 2) + c + 1];
-                const float4 w0 = gw4[cw * kMelLanes + ln], w1 = gw4[(cw + 1) * kMelLanes + ln];
-                acc1 = fmaf(p0.x, w0.x, acc1); acc1 = fmaf(p0.y, w0.y, acc1);
-                acc1 = fmaf(p0.z, w0.z, acc1); acc1 = fmaf(p0.w, w0.w, acc1);
-                acc1 = fmaf(p1.x, w1.x, acc1); acc1 = fmaf(p1.y, w1.y, acc1);
-                acc1 = fmaf(p1.z, w1.z, acc1); acc1 = fmaf(p1.w, w1.w, acc1);
-            }
-            const int m0 = ln, m1 = n_mels - 1 - ln;
-            if (m0 < (n_mels + 1) / 2) {
-                smel[fl * (n_mels + 1) + m0] = acc0;
-                lmax = fmaxf(lmax, acc0);
-                lmin = fminf(lmin, acc0);
-                if (m1 != m0) {
-                    smel[fl * (n_mels + 1) + m1] = acc1;
-                    lmax = fmaxf(lmax, acc1);
-                    lmin = fminf(lmin, acc1);
+            if (fi + kWaves < nf) {
+                fetch(x, t0 + fi + kWaves, ln, nxt);
+            } else if (nit < hi) {  // this wave's last frame of the item: prefetch its first frame of the next item
+                const int nb = nit / ng, nt0 = (nit - nb * ng) * kFpb;
+                if (wave < min(kFpb, T - nt0)) {
+                    fetch(pcm + (int64_t)nb * n_samples, nt0 + wave, ln, nxt);
+                    have = true;
                 }
             }
+            dft16(a);
+            float2 v[16];
+            v[0] = a[slot16(0)];
+    #pragma unroll
+            for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(a[slot16(k1)], stw[(k1 - 1) * 64 + ln]);
+            // ---- 64-point DFTs over the lanes (one per k1): six radix-2 DIF stages, lane exchanges in registers
+            lane_stage<5, 3>(v, tc[4], false);
+            lane_stage<4, 2>(v, tc[3], false);
+            lane_stage<3, 1>(v, tc[2], false);
+            lane_stage<2, 0>(v, tc[1], false);
+            lane_stage<1, 3>(v, tc[0], l1);
+            lane_stage<0, 2>(v, tc[0], l0);
+            // ---- real-FFT split, 2 X[f] = (Z[f] + Z*[N-f]) + e^{-2 pi i f / 2048} (-i)(Z[f] - Z*[N-f]), f = fl + 64 m:
+            // the partner N - f sits in lane lane_of_bin(64 - fl), register r ^ 15 (lane 0: its own register for
+            // (16 - m) mod 16, as bins 0, 64, ... pair among themselves)
+            float2 wlf = wl;  // opaque per frame: the 14 products wl W32^m would otherwise be hoisted (28 VGPRs)
+            asm volatile("" : "+v"(wlf.x), "+v"(wlf.y));
+            float p[16];
+    #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = bin_reg(r);
+                const float2 zf = v[r];
+                float2 zc;
+                zc.x = as_<float>(__builtin_amdgcn_ds_bpermute(paddr, bits_(v[r ^ 15].x)));
+                zc.y = as_<float>(__builtin_amdgcn_ds_bpermute(paddr, bits_(v[r ^ 15].y)));
+                const float2 z0 = v[bin_reg((16 - m) & 15)];
+                if (ln == 0) zc = z0;
+                float2 w;
+                if (m == 0) w = wlf;
+                else if (m == 8) w = make_float2(wlf.y, -wlf.x);
+                else w = cmul(wlf, rtw[64 * m]);
+                const float ex = zf.x + zc.x, ey = zf.y - zc.y, ox = zf.y + zc.y, oy = zc.x - zf.x;
+                const float re = fmaf(ox, w.x, fmaf(-oy, w.y, ex));
+                const float im = fmaf(ox, w.y, fmaf(oy, w.x, ey));
+                p[r] = 0.25f * fmaf(re, re, im * im);
+            }
+    #pragma unroll
+            for (int r = 0; r < 16; ++r) pw[fl + 64 * bin_reg(r)] = p[r];
+            if (ln == 0) {  // Nyquist bin: X[1024] = Re z0 - Im z0 (register 0 of lane 0 holds Z[0])
+                const float d = v[0].x - v[0].y;
+                pw[kFFT] = d * d;
+            }
+            wave_lds_fence();
+            // ---- banded mel: lane l owns the band pair (l, n_mels-1-l) (narrow + wide filter); each band is a
+            // fixed-order fma chain over 8-bin steps of b128 reads (power bins and chunk-transposed weights)
+            if constexpr (kMode == 1) {
+                spectral_shape(pw, ln, bin_hz, roll, sout + (int64_t)b * 3 * T + t0 + fi, T);
+            } else if constexpr (kMode == 2) {
+                piptrack_frame(pw, ln, pa, (int64_t)b * T + t0 + fi);
+            } else {
+                const float4* pw4 = reinterpret_cast<const float4*>(pw);
+                auto wt = [&](int c) -> float4 {
+                    if constexpr (kWL) return swt[c * kMelLanes + ln];
+                    else return gw4[c * kMelLanes + ln];
+                };
+                const int4 bl = sbl[ln];
+                // both bands in one loop (the pair's chunk counts sum to about the same for every lane, the larger of
+                // the two does not): chunks [0, bl.y) belong to band l, [bl.y, bl.y + bl.w) to band n_mels-1-l; the
+                // running sum restarts at the boundary, so each band keeps its own fixed-order chain
+                const int nch = bl.y + bl.w, o0 = bl.x >> 2, o1 = (bl.z >> 2) - bl.y;
+                float acc = 0.f, acc0 = 0.f;
+                for (int c = 0; c < nch; c += 2) {
+                    const bool bnd = c == bl.y;
+                    acc0 = bnd ? acc : acc0;
+                    acc = bnd ? 0.f : acc;
+                    const int o = (c < bl.y ? o0 : o1) + c;
+                    const float4 p0 = pw4[o], p1 = pw4[o + 1];
+                    const float4 w0 = wt(c), w1 = wt(c + 1);
+                    acc = fmaf(p0.x, w0.x, acc); acc = fmaf(p0.y, w0.y, acc);
+                    acc = fmaf(p0.z, w0.z, acc); acc = fmaf(p0.w, w0.w, acc);
+                    acc = fmaf(p1.x, w1.x, acc); acc = fmaf(p1.y, w1.y, acc);
+                    acc = fmaf(p1.z, w1.z, acc); acc = fmaf(p1.w, w1.w, acc);
+                }
+                float acc1 = acc;
+                if (bl.w == 0) { acc0 = acc; acc1 = 0.f; }
+                const int m0 = ln, m1 = n_mels - 1 - ln;
+                if (m0 < (n_mels + 1) / 2) {
+                    smel[fi * (n_mels + 1) + m0] = acc0;
+                    lmax = fmaxf(lmax, acc0);
+                    lmin = fminf(lmin, acc0);
+                    if (m1 != m0) {
+                        smel[fi * (n_mels + 1) + m1] = acc1;
+                        lmax = fmaxf(lmax, acc1);
+                        lmin = fminf(lmin, acc1);
+                    }
+                }
+            }
+            wave_lds_fence();
         }
-        wave_lds_fence();
-    }
-    if constexpr (kMode != 0) return;
-    __syncthreads();
-    // write [n_mels][frames] rows: out[b][m][t0 + f]
-    for (int i = threadIdx.x; i < n_mels * kFpb; i += 256) {
-        const int m = i / kFpb, f = i % kFpb;
-        if (f < nf) out[((int64_t)b * n_mels + m) * T + t0 + f] = smel[f * (n_mels + 1) + m];
-    }
-    // per-clip max / min (non-negative floats order like their bit patterns); wave-reduce first
-    for (int o = 32; o > 0; o >>= 1) {
-        lmax = fmaxf(lmax, __shfl_xor(lmax, o, 64));
-        lmin = fminf(lmin, __shfl_xor(lmin, o, 64));
-    }
-    if (lane == 0) {
-        if (lmax > 0.f) atomicMax(clip_max + b, __float_as_uint(lmax));
-        if (lmin < INFINITY) atomicMin(clip_min + b, __float_as_uint(lmin));
+        if constexpr (kMode == 0) {
+            __syncthreads();
+            // write [n_mels][frames] rows: out[b][m][t0 + f]
+            for (int i = threadIdx.x; i < n_mels * kFpb; i += 256) {
+                const int m = i / kFpb, f = i % kFpb;
+                if (f < nf) out[((int64_t)b * n_mels + m) * T + t0 + f] = smel[f * (n_mels + 1) + m];
+            }
+            // per-clip max / min (non-negative floats order like their bit patterns); wave-reduce first
+            for (int o = 32; o > 0; o >>= 1) {
+                lmax = fmaxf(lmax, __shfl_xor(lmax, o, 64));
+                lmin = fminf(lmin, __shfl_xor(lmin, o, 64));
+            }
+            if (lane == 0) {
+                if (lmax > 0.f) atomicMax(clip_max + b, __float_as_uint(lmax));
+                if (lmin < INFINITY) atomicMin(clip_min + b, __float_as_uint(lmin));
+            }
+            __syncthreads();  // the staging rows are reused by the next item
+        }
     }
 }
 
-// kMode 0 (the mel hot path) is built for 3 waves per SIMD (168 VGPRs, no spills; LDS 52 KB: 3 blocks per CU);
-// the spectral-shape / piptrack modes keep the default register budget (they would spill at 168).
+#define HLMC_STFT_ARGS                                                                                          \
+    const float* __restrict__ pcm, int nclips, int64_t n_samples, int T, int hop, const float* __restrict__ window,         \
+        const float2* __restrict__ rtw, const float2* __restrict__ tw, const int* __restrict__ band,             \
+        const int* __restrict__ woff, const float* __restrict__ wts, int n_mels, int nnz, float* __restrict__ out, \
+        unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min, double bin_hz, double roll,            \
+        double* __restrict__ sout, PipArgs pa
+#define HLMC_STFT_PASS pcm, nclips, n_samples, T, hop, window, rtw, tw, band, woff, wts, n_mels, nnz, out, clip_max, clip_min, bin_hz, roll, sout, pa
+
+// kMode 0 (the mel hot path) is built for 3 waves per SIMD (168 VGPRs; LDS 52 KB: 3 blocks per CU); the
+// spectral-shape / piptrack modes keep the default register budget.
 template <int kMode>
-__global__ __launch_bounds__(256) void stft_mel_kernel(const float* __restrict__ pcm, int64_t n_samples, int T,
-                                                       int hop, const float* __restrict__ window,
-                                                       const float2* __restrict__ rtw, const float2* __restrict__ tw23,
-                                                       const int* __restrict__ band,
-                                                       const int* __restrict__ woff, const float* __restrict__ wts,
-                                                       int n_mels, int nnz, float* __restrict__ out,
-                                                       unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min,
-                                                       double bin_hz, double roll, double* __restrict__ sout,
-                                                       PipArgs pa) {
-    stft_mel_body<kMode>(pcm, n_samples, T, hop, window, rtw, tw23, band, woff, wts, n_mels, nnz, out, clip_max, clip_min, bin_hz, roll, sout, pa);
+__global__ __launch_bounds__(256) void stft_mel_kernel(HLMC_STFT_ARGS) {
+    stft_mel_body<kMode, false>(HLMC_STFT_PASS);
 }
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stft_mel0_kernel(const float* __restrict__ pcm, int64_t n_samples, int T,
-                                                       int hop, const float* __restrict__ window,
-                                                       const float2* __restrict__ rtw, const float2* __restrict__ tw23,
-                                                       const int* __restrict__ band,
-                                                       const int* __restrict__ woff, const float* __restrict__ wts,
-                                                       int n_mels, int nnz, float* __restrict__ out,
-                                                       unsigned* __restrict__ clip_max, unsigned* __restrict__ clip_min,
-                                                       double bin_hz, double roll, double* __restrict__ sout,
-                                                       PipArgs pa) {
-    stft_mel_body<0>(pcm, n_samples, T, hop, window, rtw, tw23, band, woff, wts, n_mels, nnz, out, clip_max, clip_min, bin_hz, roll, sout, pa);
+template <bool kWL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stft_mel0_kernel(HLMC_STFT_ARGS) {
+    stft_mel_body<0, kWL>(HLMC_STFT_PASS);
 }
 
 __device__ __forceinline__ float db_of(float S, float amin) { return 10.f * log10f(fmaxf(amin, S)); }
@@ -855,16 +924,16 @@ int plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax
         const double fac = jt + (-M_PI);
         win[j] = (float)(0.5 + 0.5 * std::cos(fac));
     }
-    // stage twiddles of the radix-16/16/4 FFT: tw2[(r-1)*16 + k] = e^{-2 pi i r k / 256} (r 1..15, k 0..15),
-    // tw3[(r-1)*256 + j] = e^{-2 pi i r j / 1024} (r 1..3, j 0..255)
-    std::vector<float2> tw(kTw2 + kTw3), rtw(kFFT + 1);
-    for (int r = 1; r < 16; ++r)
-        for (int k = 0; k < 16; ++k)
-            tw[(r - 1) * 16 + k] = make_float2((float)std::cos(-2.0 * M_PI * r * k / 256), (float)std::sin(-2.0 * M_PI * r * k / 256));
-    for (int r = 1; r < 4; ++r)
-        for (int j = 0; j < 256; ++j)
-            tw[kTw2 + (r - 1) * 256 + j] = make_float2((float)std::cos(-2.0 * M_PI * r * j / kFFT),
-                                                       (float)std::sin(-2.0 * M_PI * r * j / kFFT));
+    // FFT twiddles: twB[(k1-1)*64 + p] = e^{-2 pi i p k1 / 1024} (k1 1..15, lane p), then the radix-2 lane
+    // stages twC[(j-1)*64 + p] = e^{-2 pi i (p mod 2^j) 2^{5-j} / 64} (lane bit j = 1..5)
+    std::vector<float2> tw(kTwB + kTwC), rtw(kFFT + 1);
+    auto cis = [](double num, double den) {
+        return make_float2((float)std::cos(-2.0 * M_PI * num / den), (float)std::sin(-2.0 * M_PI * num / den));
+    };
+    for (int k1 = 1; k1 < 16; ++k1)
+        for (int q = 0; q < 64; ++q) tw[(k1 - 1) * 64 + q] = cis((double)q * k1, kFFT);
+    for (int j = 1; j <= 5; ++j)
+        for (int q = 0; q < 64; ++q) tw[kTwB + (j - 1) * 64 + q] = cis((double)((q & ((1 << j) - 1)) << (5 - j)), 64);
     for (int f = 0; f <= kFFT; ++f) rtw[f] = make_float2((float)std::cos(-2.0 * M_PI * f / n_fft), (float)std::sin(-2.0 * M_PI * f / n_fft));
     // Banded filterbank for the kernel's mel stage.  Lane l of a wavefront owns the band pair
     // (l, n_mels-1-l) (a narrow and a wide filter).  Each band starts at its first non-zero bin rounded
@@ -935,24 +1004,44 @@ int64_t workspace(const MelPlanImpl* p, int64_t B, int64_t n) {
     return ((B * p->n_mels * frames(p, n) * 4 + 255) & ~int64_t(255)) + 2 * ((B * 4 + 255) & ~int64_t(255));
 }
 
+// Persistent grid of the STFT kernels: resident blocks over all CUs (a multiple of 8, one share per XCD), at most
+// one per item rounded up to the XCD count.
+template <typename K>
+static unsigned stft_grid(K kernel, size_t dyn, int64_t nitems) {
+    int dev = 0, cus = 0, occ = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 256, dyn) != hipSuccess || occ < 1) occ = 1;
+    const int64_t resident = (int64_t)std::max(cus, 1) * occ;
+    const int64_t want = std::min(resident, (nitems + 7) / 8 * 8);
+    return (unsigned)std::max<int64_t>(8, want / 8 * 8);
+}
+
 static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int64_t n, float* out,
                      unsigned* cmax, unsigned* cmin) {
     HLMC_CHECK_ARG(pcm && out && B > 0 && n > 0, "bad melspectrogram arguments");
     HLMC_CHECK_ARG(B <= 65535, "batch <= 65535");
+    HLMC_CHECK_ARG(n < kMaxStftSamples, "clip length < 2^29 samples");
     const int T = (int)frames(p, n);
     init_minmax_kernel<<<(unsigned)((B + 255) / 256), 256, 0, s>>>(cmax, cmin, B);  // 0x7f7f7f7f: large positive float
     HLMC_LAUNCHED();
     HLMC_CHECK_ARG(p->n_mels <= 2 * kMelLanes, "n_mels <= 128");
-    dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
-    const size_t dyn = (4 * kMelLanes + (size_t)kFpb * (p->n_mels + 1)) * 4;
+    const int64_t nitems = B * ((T + kFpb - 1) / kFpb);
+    const bool wl = (size_t)p->nnz * 4 <= (size_t)kMaxWLds;  // filterbank staged in LDS
+    const size_t dyn = (4 * kMelLanes + (wl ? (size_t)p->nnz : 0) + (size_t)kFpb * (p->n_mels + 1)) * 4;
     {  // algorithmic work: radix-2-equivalent FFT 2.5 N log2 N + window + |X|^2 + banded mel; PCM in, mel out
         const double nf = p->n_fft, lg = std::log2(nf);
         probe::site(probe::kStftMel, (double)B * T * (2.5 * nf * lg + nf + 3.0 * (nf / 2 + 1) + 2.0 * p->nnz),
                     (double)B * ((double)n * 4 + (double)p->n_mels * T * 4));
     }
     HLMC_PROBE_BEGIN(s);
-    stft_mel0_kernel<<<grid, 256, dyn, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
-                                              p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0, nullptr, PipArgs{});
+    if (wl)
+        stft_mel0_kernel<true><<<stft_grid(stft_mel0_kernel<true>, dyn, nitems), 256, dyn, s>>>(pcm, (int)B, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band,
+                                                      p->d_woff, p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0,
+                                                      nullptr, PipArgs{});
+    else
+        stft_mel0_kernel<false><<<stft_grid(stft_mel0_kernel<false>, dyn, nitems), 256, dyn, s>>>(pcm, (int)B, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band,
+                                                       p->d_woff, p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0,
+                                                       nullptr, PipArgs{});
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     return HLMC_OK;
@@ -1059,8 +1148,9 @@ int spectral_shape(const MelPlanImpl* p, hipStream_t s, const float* pcm, int64_
     HLMC_CHECK_ARG(pcm && out && B > 0 && n > 0 && B <= 65535, "bad spectral_shape arguments");
     HLMC_CHECK_ARG(roll_percent > 0.0 && roll_percent < 1.0, "0 < roll_percent < 1");
     const int T = (int)frames(p, n);
-    dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
-    stft_mel_kernel<1><<<grid, 256, 0, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
+    HLMC_CHECK_ARG(n < kMaxStftSamples, "clip length < 2^29 samples");
+    const unsigned grid = stft_grid(stft_mel_kernel<1>, 0, B * ((T + kFpb - 1) / kFpb));
+    stft_mel_kernel<1><<<grid, 256, 0, s>>>(pcm, (int)B, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
                                             p->d_w, 0, 0, nullptr, nullptr, nullptr, (double)p->sr / p->n_fft,
                                             roll_percent, out, PipArgs{});
     HLMC_LAUNCHED();
@@ -1171,8 +1261,9 @@ int chroma_stft(MelPlanImpl* p, hipStream_t s, const float* pcm, int64_t B, int6
     pa.kmax = p->pip_kmax;
     pa.sr = p->sr;
     pa.n_fft = p->n_fft;
-    dim3 grid((T + kFpb - 1) / kFpb, (unsigned)B);
-    stft_mel_kernel<2><<<grid, 256, 0, s>>>(pcm, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
+    HLMC_CHECK_ARG(n < kMaxStftSamples, "clip length < 2^29 samples");
+    const unsigned grid = stft_grid(stft_mel_kernel<2>, 0, B * ((T + kFpb - 1) / kFpb));
+    stft_mel_kernel<2><<<grid, 256, 0, s>>>(pcm, (int)B, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band, p->d_woff,
                                             p->d_w, 0, 0, nullptr, nullptr, nullptr, 0.0, 0.0, nullptr, pa);
     HLMC_LAUNCHED();
     tuning_kernel<<<(unsigned)B, 1024, 0, s>>>(pa.cand, pa.cnt, T, mp, p->d_tune_edges, tidx, tuning);

@@ -13,7 +13,7 @@ struct MelPlanImpl {
     std::vector<float> dense;        // [n_mels][nbins] (host copy, librosa.filters.mel)
     // device tables
     float* d_window = nullptr;       // [n_fft]
-    float2* d_tw = nullptr;          // stage twiddles of the radix-16/16/4 FFT (tw2 [15][16], tw3 [3][256])
+    float2* d_tw = nullptr;          // FFT twiddles: W1024^{p k1} [15][64], radix-2 lane stages [5][64]
     float2* d_rtw = nullptr;         // [n_fft/2+1] e^{-2 pi i f / n_fft}
     int* d_band = nullptr;           // [n_mels][2] first bin, count
     int* d_woff = nullptr;           // [n_mels] offset into d_w

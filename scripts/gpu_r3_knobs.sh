@@ -1,6 +1,6 @@
 # Alternating bench.py A/B over a list of environment settings (KNOBS, ';'-separated; "-" = defaults), after the
 # GPU tests in TESTS; then a kernel trace of the default build with its per-stream timeline.
-#   KNOBS="-;HLMC_SIDE_BATCH=2" bash scripts/gpu_r3_knobs.sh [ROUNDS]
+#   KNOBS="-;HLMC_SIDE_STREAM=0" bash scripts/gpu_r3_knobs.sh [ROUNDS]
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT

@@ -3,8 +3,8 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for v in ${VARIANTS:-0 1}; do
-  for wg in 0 1; do
-    echo "variant $v wg $wg: $(HLMC_LIB=build_ab/v$v/libhlmc.so HLMC_STFT_WG=$wg timeout -k 10 120 python -u scripts/bench_mel.py 2>&1 | grep -v amdgpu.ids)"
+  for rep in 1 2; do
+    echo "variant $v: $(HLMC_LIB=build_ab/v$v/libhlmc.so timeout -k 10 120 python -u scripts/bench_mel.py 2>&1 | grep -v amdgpu.ids)"
   done
 done
 if [ -n "${TESTS:-}" ]; then

@@ -24,8 +24,11 @@ def test_filterbank_matches_oracle(cuda):
     assert (fb > 0).sum() == 2018
 
 
-@pytest.mark.parametrize("n_samples,keep", [(65024, None), (65024, 128), (22050 * 3, 256), (661500, 1024)])
+@pytest.mark.parametrize("n_samples,keep", [(65024, None), (65024, 128), (22050 * 3, 256), (661500, 1024),
+                                             (22050 * 3 + 17, None), (1500, 8)])
 def test_mel_db(cuda, n_samples, keep):
+    """Even lengths take the kernel's 8-byte sample-pair loads, odd lengths the 4-byte ones; 1500 samples is
+    shorter than one frame (every frame reads the zero padding through the loads' range check)."""
     y = MO.synthetic_pcm(2, n_samples, seed=n_samples % 97)
     got = hlmc_amd.extract_mel_spectrogram(y, fixed_time_steps=keep)
     ref = np.stack([MO.extract_mel_spectrogram(c, fixed_time_steps=keep) for c in y])

@@ -409,8 +409,6 @@ def main():
     local_dev = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local_dev)
     device = torch.device("cuda", local_dev)
-    if os.environ.get("HLMC_BENCH_STREAM") == "1":  # A/B aid: the step on a created (non-null) stream
-        torch.cuda.set_stream(torch.cuda.Stream(device))
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -494,7 +494,7 @@ def test_halo_fwd_nan_propagates(cuda):
 # every BatchNorm layer shape of the bench step (B = 256, 128 x 128) plus a small one
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 @pytest.mark.parametrize("R,C", [(4 * 8 * 8, 64), (256 * 64 * 64, 32), (256 * 32 * 32, 64), (256 * 16 * 16, 128),
-                                 (256 * 8 * 8, 256), (256 * 4 * 4, 512), (256 * 2 * 2, 512)])
+                                 (256 * 8 * 8, 256), (256 * 4 * 4, 512), (256 * 2 * 2, 512), (1500, 64)])
 def test_bn_bwd_op_matches_reference(cuda, dt, R, C):
     """hlmc_op_bn_bwd (the engine's moments + apply passes of train-mode BatchNorm2d + LeakyReLU(0.01) backward,
     src/Convolutional_VAE.py:80-100 backward) vs the float64 formula on the same (quantised) inputs:

@@ -353,7 +353,7 @@ __device__ __forceinline__ int lane_of_bin(int g) { return ((g & 15) << 2) | ((g
 // kMode 0: banded mel (stored [b][m][t]) + per-clip max/min; kWL: filterbank staged in LDS.  kMode 1: spectral
 // shape of |X| (power 1): centroid, bandwidth (p = 2) and rolloff per frame, stored f64 [b][3][t] (sout).
 // kMode 2: piptrack (PipArgs).  Modes 1 and 2 leave the mel tables unused.
-template <int kMode, bool kWL>
+template <int kMode, bool kWL, bool kPairs>
 __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int nclips, int64_t n_samples, int T,
                                                        int hop, const float* __restrict__ window,
                                                        const float2* __restrict__ rtw, const float2* __restrict__ tw,
@@ -384,11 +384,13 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
     // raw sample pairs (x[2n], x[2n+1]) of frame t: n = lane + 64 r, through a buffer descriptor over the clip
     // whose range check returns 0 outside it (center padding; negative offsets wrap past the range).  With an
     // even clip length and hop a pair never straddles the clip's end, so one 8-byte load per pair.
-    const bool pairs = ((n_samples | hop) & 1) == 0;
+    // kPairs (launch-time choice, not a runtime branch): every fetch issues the same number of loads on every path,
+    // so the compiler's wait counts at the frame loop's merge points stay exact (a conditional fetch made it wait
+    // for the next frame's loads before using the current frame's, exposing their latency every frame)
     auto fetch = [&](const float* x, int t, int ln, float2 (&v)[16]) {
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, (int)(n_samples * 4), 0x00020000);
         const int start = t * hop - kFFT;  // center=True: n_fft/2 = 1024 zeros of padding
-        if (pairs) {
+        if constexpr (kPairs) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 // (bit_cast of the whole vector: extracting the builtin's elements one by one read word 0 twice)
@@ -405,12 +407,10 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
     };
     float2 nxt[16];
     bool have = false;  // nxt holds this wave's first frame of item `it`
-    if (it < hi) {       // first frame in flight while the tables are staged
-        const int b = it / ng, t0 = (it - b * ng) * kFpb;
-        if (wave < min(kFpb, T - t0)) {
-            fetch(pcm + (int64_t)b * n_samples, t0 + wave, lane, nxt);
-            have = true;
-        }
+    {  // first frame in flight while the tables are staged (unconditional loads: frame 0 of clip 0 when none)
+        const int b = it < hi ? it / ng : 0, t0 = it < hi ? (it - b * ng) * kFpb : 0;
+        have = it < hi && wave < min(kFpb, T - t0);
+        fetch(pcm + (int64_t)b * n_samples, have ? t0 + wave : 0, lane, nxt);
     }
     for (int i = threadIdx.x; i < kTwB + kTwC; i += 256) stw[i] = tw[i];
     if constexpr (kMode == 0) {
@@ -436,7 +436,10 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
         const int b = it / ng, t0 = (it - b * ng) * kFpb, nf = min(kFpb, T - t0);
         const float* x = pcm + (int64_t)b * n_samples;
         const int nit = it + per;
-        if (!have && wave < nf) fetch(x, t0 + wave, lane, nxt);
+        if (!have && wave < nf) {  // (rare: this wave had no frame in its previous item) fetch and wait here, so the
+            fetch(x, t0 + wave, lane, nxt);  // loop's wait counts see no loads pending from this path
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
         have = false;
         float lmax = 0.f, lmin = INFINITY;
         for (int fi = wave; fi < nf; fi += kWaves) {
@@ -448,14 +451,19 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
             for (int r = 0; r < 16; ++r) {
                 a[r] = make_float2(nxt[r].x * wnd[r].x, nxt[r].y * wnd[r].y);
             }
-            if (fi + kWaves < nf) {
-                fetch(x, t0 + fi + kWaves, ln, nxt);
-            } else if (nit < hi) {  // this wave's last frame of the item: prefetch its first frame of the next item
-                const int nb = nit / ng, nt0 = (nit - nb * ng) * kFpb;
-                if (wave < min(kFpb, T - nt0)) {
-                    fetch(pcm + (int64_t)nb * n_samples, nt0 + wave, ln, nxt);
-                    have = true;
+            {  // the next frame of this item, else this wave's first frame of the next item, else (data unused) this one
+                int fb = b, ft = t0 + fi;
+                if (fi + kWaves < nf) {
+                    ft = t0 + fi + kWaves;
+                } else if (nit < hi) {
+                    const int nb = nit / ng, nt0 = (nit - nb * ng) * kFpb;
+                    if (wave < min(kFpb, T - nt0)) {
+                        fb = nb;
+                        ft = nt0 + wave;
+                        have = true;
+                    }
                 }
+                fetch(pcm + (int64_t)fb * n_samples, ft, ln, nxt);
             }
             dft16(a);
             float2 v[16];
@@ -579,11 +587,12 @@ __device__ __forceinline__ void stft_mel_body(const float* __restrict__ pcm, int
 // spectral-shape / piptrack modes keep the default register budget.
 template <int kMode>
 __global__ __launch_bounds__(256) void stft_mel_kernel(HLMC_STFT_ARGS) {
-    stft_mel_body<kMode, false>(HLMC_STFT_PASS);
+    if (((n_samples | hop) & 1) == 0) stft_mel_body<kMode, false, true>(HLMC_STFT_PASS);
+    else stft_mel_body<kMode, false, false>(HLMC_STFT_PASS);
 }
-template <bool kWL>
+template <bool kWL, bool kPairs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void stft_mel0_kernel(HLMC_STFT_ARGS) {
-    stft_mel_body<0, kWL>(HLMC_STFT_PASS);
+    stft_mel_body<0, kWL, kPairs>(HLMC_STFT_PASS);
 }
 
 __device__ __forceinline__ float db_of(float S, float amin) { return 10.f * log10f(fmaxf(amin, S)); }
@@ -1034,14 +1043,19 @@ static int mel_power(const MelPlanImpl* p, hipStream_t s, const float* pcm, int6
                     (double)B * ((double)n * 4 + (double)p->n_mels * T * 4));
     }
     HLMC_PROBE_BEGIN(s);
-    if (wl)
-        stft_mel0_kernel<true><<<stft_grid(stft_mel0_kernel<true>, dyn, nitems), 256, dyn, s>>>(pcm, (int)B, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band,
-                                                      p->d_woff, p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0,
-                                                      nullptr, PipArgs{});
-    else
-        stft_mel0_kernel<false><<<stft_grid(stft_mel0_kernel<false>, dyn, nitems), 256, dyn, s>>>(pcm, (int)B, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw, p->d_band,
-                                                       p->d_woff, p->d_w, p->n_mels, p->nnz, out, cmax, cmin, 0.0, 0.0,
-                                                       nullptr, PipArgs{});
+    const bool pairs = ((n | p->hop) & 1) == 0;  // 8-byte sample-pair loads (even clip length and hop)
+    auto launch = [&](auto kern) {
+        kern<<<stft_grid(kern, dyn, nitems), 256, dyn, s>>>(pcm, (int)B, n, T, p->hop, p->d_window, p->d_rtw, p->d_tw,
+                                                            p->d_band, p->d_woff, p->d_w, p->n_mels, p->nnz, out, cmax,
+                                                            cmin, 0.0, 0.0, nullptr, PipArgs{});
+    };
+    if (wl) {
+        if (pairs) launch(stft_mel0_kernel<true, true>);
+        else launch(stft_mel0_kernel<true, false>);
+    } else {
+        if (pairs) launch(stft_mel0_kernel<false, true>);
+        else launch(stft_mel0_kernel<false, false>);
+    }
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     return HLMC_OK;

@@ -568,6 +568,176 @@ __global__ __launch_bounds__(256) void bn_bwd_small_kernel(const T* __restrict__
     }
 }
 
+// The whole BatchNorm backward of a MID-SIZE layer (the 8 x 8 and 4 x 4 conv maps: R = 4 k - 16 k rows, C = 256 /
+// 512; R * C <= kBnFusedMaxElems) in one launch with one grid-wide arrival count between the moments and the apply.  The two-pass form reads y
+// and da twice over two launches whose blocks each fold the full 2C-column accumulator (6C x shards words) before
+// their first row; here every block owns a channel slab (8 V channels: one 128-byte segment of each row) and kNR x 32
+// rows, holds its rows of y and da in registers across the count, and adds / folds only its slab's 2 x 8V columns.
+// Grid = slabs x row blocks, all co-resident (checked by the launcher against the occupancy query), so every block
+// reaches the count; the spin is bounded (kBnSpinMax sleeps, ~1 s) so that a grid that could not become resident ends
+// instead of hanging -- its totals would then be partial, which the launcher's residency check rules out.
+// The arrival counter is the zeroed tail word of the moments accumulator (bn_acc_bytes).  Visibility: the
+// accumulator adds are agent-scope atomics performed at the memory side; each thread waits for its own adds to
+// complete (s_waitcnt) before its block arrives, and the fold after the count reads the words with agent-scope
+// atomic loads (no L2 write-back fence per block: round 2 measured that cost).
+constexpr int kBnSpinMax = 1 << 24;
+template <typename T, int kNR, int ACT>
+__global__ __launch_bounds__(256) void bn_bwd_fused_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
+                                                           int R, int C, const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, int act, T* __restrict__ dy,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           XAcc mom, XAcc bias_acc, int nslab) {
+    constexpr int V = Vec16<T>::N, SW = 8 * V;   // 8 threads x V channels per slab row segment
+    __shared__ double red[4][2][SW];
+    __shared__ double tot[2 * SW];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, cg = t & 7, rr = t >> 3;
+    const int slab = blockIdx.x % nslab, rb = blockIdx.x / nslab;
+    const int c0 = slab * SW + cg * V;
+    const int r0 = rb * (32 * kNR) + rr;
+    uint4 hy[kNR], hg[kNR];
+#pragma unroll
+    for (int i = 0; i < kNR; ++i) {  // every row issued up front (clamped, masked below)
+        const int r = min(r0 + 32 * i, R - 1);
+        hy[i] = load16_raw(y + (int64_t)r * C + c0);
+        hg[i] = load16_raw(da + (int64_t)r * lda + c0);
+    }
+    float mu[V], is[V], ga[V], be[V];
+    BnChan::load(mean, c0, mu);
+    BnChan::load(invstd, c0, is);
+    BnChan::load(gamma, c0, ga);
+    BnChan::load(beta, c0, be);
+    float a[V], b[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) a[v] = b[v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kNR; ++i) {
+        const bool ok = r0 + 32 * i < R;
+        float x[V], g[V];
+        cvt16_f32<T>(hy[i], x);
+        cvt16_f32<T>(hg[i], g);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const float xh = (x[v] - mu[v]) * is[v];
+            float dz = g[v] * act_grad_t<ACT>(xh * ga[v] + be[v], act);
+            dz = ok ? dz : 0.f;
+            a[v] += dz;
+            b[v] = fmaf(dz, xh, b[v]);
+        }
+    }
+    // the apply pass recomputes x-hat / dz from the held raw rows: without this barrier to value propagation hipcc
+    // keeps the 2 x V x kNR unpacked floats live across the count (232 VGPRs at kNR = 8)
+#pragma unroll
+    for (int i = 0; i < kNR; ++i) {
+        asm volatile("" : "+v"(hy[i].x), "+v"(hy[i].y), "+v"(hy[i].z), "+v"(hy[i].w));
+        asm volatile("" : "+v"(hg[i].x), "+v"(hg[i].y), "+v"(hg[i].z), "+v"(hg[i].w));
+    }
+    // block column sums (f32 per thread, f64 across): lanes sharing cg (xor 8, 16, 32), then the 4 waves in order
+    auto slab_sums = [&](const float (&p)[V], const float (&q)[V], bool two) {
+        double sp[V], sq[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) { sp[v] = p[v]; sq[v] = two ? q[v] : 0.0; }
+#pragma unroll
+        for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                sp[v] += __shfl_xor(sp[v], o, 64);
+                if (two) sq[v] += __shfl_xor(sq[v], o, 64);
+            }
+        if (lane < 8)
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                red[w][0][lane * V + v] = sp[v];
+                red[w][1][lane * V + v] = sq[v];
+            }
+        __syncthreads();
+    };
+    slab_sums(a, b, true);
+    const int shard = rb % mom.shards;
+    if (t < 2 * SW) {
+        const int k = t / SW, j = t % SW;
+        const double s = (red[0][k][j] + red[1][k][j]) + (red[2][k][j] + red[3][k][j]);
+        xacc_add_shard(mom, shard, k * C + slab * SW + j, s);
+    }
+    // arrival: this thread's adds complete, then one count per block; wait for all blocks of the grid
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    unsigned* arrive = reinterpret_cast<unsigned*>(mom.p + (size_t)mom.shards * 3 * mom.ncols);
+    if (t == 0) {
+        __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned nblk = gridDim.x;
+        for (int spin = 0; spin < kBnSpinMax; ++spin) {
+            if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nblk) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    // fold this slab's 2 x SW columns over the shards (agent-scope loads: the other XCDs' adds)
+    if (t < 2 * SW) {
+        const int k = t / SW, j = t % SW;
+        const int col = k * C + slab * SW + j;
+        // every shard's three words in flight at once (clamped shard index, masked adds): a shard loop waits one
+        // memory-side round trip per shard
+        unsigned long long w0[kXAccMaxShards], w1[kXAccMaxShards], w2[kXAccMaxShards];
+#pragma unroll
+        for (int sh = 0; sh < kXAccMaxShards; ++sh) {
+            unsigned long long* q = mom.p + (size_t)min(sh, mom.shards - 1) * 3 * mom.ncols + col;
+            w0[sh] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w1[sh] = __hip_atomic_load(q + mom.ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            w2[sh] = __hip_atomic_load(q + 2 * mom.ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        long long s0w = 0, s1w = 0, s2w = 0;
+        unsigned long long bad = 0;
+#pragma unroll
+        for (int sh = 0; sh < kXAccMaxShards; ++sh)
+            if (sh < mom.shards) {
+                s0w += (long long)w0[sh];
+                s1w += (long long)w1[sh];
+                bad |= w2[sh] & kXAccBad;
+                s2w += (long long)(w2[sh] & ~kXAccBad);
+            }
+        const double v = bad ? __builtin_nan("") : xacc_value(s0w, s1w, s2w);
+        tot[t] = v;
+        if (rb == 0) (k == 0 ? dbeta : dgamma)[slab * SW + j] = (float)v;
+    }
+    __syncthreads();
+    float s0[V], sx[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        s0[v] = (float)tot[cg * V + v];
+        sx[v] = (float)tot[SW + cg * V + v];
+    }
+    const float invR = 1.f / (float)R;
+    float bs[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) bs[v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < kNR; ++i) {
+        const int r = r0 + 32 * i;
+        if (r >= R) break;
+        float x[V], g[V], o[V];
+        cvt16_f32<T>(hy[i], x);
+        cvt16_f32<T>(hg[i], g);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const float xh = (x[v] - mu[v]) * is[v];
+            const float dz = g[v] * act_grad_t<ACT>(xh * ga[v] + be[v], act);
+            o[v] = ga[v] * is[v] * (dz - s0[v] * invR - xh * sx[v] * invR);
+        }
+        store16_f32(dy + (int64_t)r * C + c0, o);
+#pragma unroll
+        for (int v = 0; v < V; ++v) bs[v] += to_f32<T>(from_f32<T>(o[v]));   // the stored dy, rounded to T
+    }
+    if (bias_acc.on()) {
+        slab_sums(bs, bs, false);
+        if (t < SW) {
+            const double s = (red[0][0][t] + red[1][0][t]) + (red[2][0][t] + red[3][0][t]);
+            xacc_add_shard(bias_acc, rb % bias_acc.shards, slab * SW + t, s);
+        }
+    }
+}
+
 // out[c] = column c of an exact accumulator (bias gradients); grid ceil(C / 64) x 64
 __global__ __launch_bounds__(64) void xacc_to_f32_kernel(XAcc acc, int C, float* out) {
     const int c = blockIdx.x * 64 + threadIdx.x;
@@ -1409,7 +1579,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const ops::AdamJob* __restric
 namespace ops {
 
 // the accumulator a layer's statistics use (xacc_shards(C) copies of 2C columns)
-size_t bn_acc_bytes(int C) { return XAcc::bytes(xacc_shards(C), 2 * C); }
+size_t bn_acc_bytes(int C) { return XAcc::bytes(xacc_shards(C), 2 * C) + 64; }  // + bn_bwd_fused_kernel's arrival count
 size_t bias_acc_bytes(int C) { return XAcc::bytes(xacc_shards(C), C); }
 
 template <typename T>
@@ -1505,6 +1675,61 @@ int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, XAcc acc, bool hav
     return HLMC_OK;
 }
 
+// bn_bwd_fused_kernel instances: rows per thread kNR (8, or 4 where 8 leaves fewer than 256 blocks), activation
+template <typename T>
+static void bn_bwd_fused_kernel_ptr(int nr, int act, void (*&k)(const T*, int, const T*, int, int, const float*,
+                                                                const float*, const float*, const float*, int, T*,
+                                                                float*, float*, XAcc, XAcc, int)) {
+    k = nr == 8 ? (act == 0 ? bn_bwd_fused_kernel<T, 8, 0> : bn_bwd_fused_kernel<T, 8, -1>)
+                : (act == 0 ? bn_bwd_fused_kernel<T, 4, 0> : bn_bwd_fused_kernel<T, 4, -1>);
+}
+// Which layers take the fused form: R * C <= kBnFusedMaxElems, C a multiple of the slab width, and the whole grid
+// co-resident (occupancy query x CUs) -- the kernel's arrival count needs every block running at once.  Measured
+// (scripts/bench_bn.py under rocprofv3, bf16 B = 256): 4 x 4 x 512 14.4 us vs 21.3 us for the two passes, 8 x 8 x 256
+// 15.4 vs 21.3, 16 x 16 x 128 30.8 vs 21.3 (512 blocks: the count waits for the slowest of two blocks per CU); the
+// step with 2^22: 138.6k vs 137.9k clips/s (3 rounds; 2^21: 138.3k, 2^23: 133.7k).  HLMC_BN_FUSED overrides the limit
+// (0: every layer on the two passes; the parity test compares the forms).
+constexpr int64_t kBnFusedMaxElems = (int64_t)1 << 22;
+template <typename T>
+static bool bn_fused_plan(int64_t R, int C, int act, int& nr, int& nslab, unsigned& grid) {
+    constexpr int SW = 8 * Vec16<T>::N;
+    int64_t lim = kBnFusedMaxElems;
+    if (const char* e = std::getenv("HLMC_BN_FUSED")) lim = (int64_t)std::atoll(e);
+    if (C % SW != 0 || R * C > lim || R >= ((int64_t)1 << 31)) return false;
+    nslab = C / SW;
+    nr = (int64_t)nslab * ((R + 255) / 256) >= 256 ? 8 : 4;
+    const int64_t G = (int64_t)nslab * ((R + 32 * nr - 1) / (32 * nr));
+    static int resident[2][2] = {{0, 0}, {0, 0}};  // [nr == 8][act == 0]
+    int& res = resident[nr == 8][act == 0];
+    if (res == 0) {
+        void (*k)(const T*, int, const T*, int, int, const float*, const float*, const float*, const float*, int, T*,
+                  float*, float*, XAcc, XAcc, int);
+        bn_bwd_fused_kernel_ptr<T>(nr, act, k);
+        int dev = 0, cus = 0, occ = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k), kThreads, 0) !=
+            hipSuccess)
+            occ = 0;
+        res = std::max(cus * occ, -1);
+        if (res == 0) res = -1;
+    }
+    if (res < 0 || G > res) return false;
+    grid = (unsigned)G;
+    return true;
+}
+template <typename T>
+static hipError_t bn_fused_launch(hipStream_t s, int nr, int act, unsigned g, const T* da, int lda, const T* y, int R,
+                                  int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
+                                  T* dy, float* dgamma, float* dbeta, XAcc mom, XAcc bias_acc, int nslab) {
+    void (*k)(const T*, int, const T*, int, int, const float*, const float*, const float*, const float*, int, T*, float*,
+              float*, XAcc, XAcc, int);
+    bn_bwd_fused_kernel_ptr<T>(nr, act, k);
+    k<<<g, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, dy, dgamma, dbeta, mom, bias_acc, nslab);
+    return hipSuccess;
+}
+
 template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
@@ -1522,6 +1747,18 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
         HLMC_LAUNCHED();
         if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
         return HLMC_OK;
+    }
+    if (!mask && !(fused && fused->done)) {  // mid-size layer: one launch with a grid-wide count (bn_bwd_fused_kernel)
+        int nr = 0, nslab = 0;
+        unsigned g = 0;
+        if (bn_fused_plan<T>(R, C, act, nr, nslab, g)) {
+            HLMC_BN_PROBED(s, 3.0 * sizeof(T) * R * C, bn_fused_launch<T>(s, nr, act, g, da, lda, y, (int)R, C, mean,
+                                                                       invstd, gamma, beta, dy, dgamma, dbeta, mom,
+                                                                       bias_acc, nslab));
+            HLMC_LAUNCHED();
+            if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
+            return HLMC_OK;
+        }
     }
     const int nblk = bn_blocks(R, C);
     const int64_t rpb = bn_rows_per_blk(R, C);

@@ -3,6 +3,7 @@
 fp32 path (exact-fp32 MFMA): relative L2 error <= 1e-5.  bf16 path: operands rounded to bf16 on
 both sides, fp32 accumulation; relative L2 error <= 1e-2 (bf16 output rounding ~4e-3)."""
 import ctypes as C
+import os
 
 import pytest
 import torch
@@ -494,7 +495,8 @@ def test_halo_fwd_nan_propagates(cuda):
 # every BatchNorm layer shape of the bench step (B = 256, 128 x 128) plus a small one
 @pytest.mark.parametrize("dt", ["fp32", "bf16"])
 @pytest.mark.parametrize("R,C", [(4 * 8 * 8, 64), (256 * 64 * 64, 32), (256 * 32 * 32, 64), (256 * 16 * 16, 128),
-                                 (256 * 8 * 8, 256), (256 * 4 * 4, 512), (256 * 2 * 2, 512), (1500, 64)])
+                                 (256 * 8 * 8, 256), (256 * 4 * 4, 512), (256 * 2 * 2, 512), (1500, 64),
+                                 (3001, 128), (5000, 256), (2049, 512)])
 def test_bn_bwd_op_matches_reference(cuda, dt, R, C):
     """hlmc_op_bn_bwd (the engine's moments + apply passes of train-mode BatchNorm2d + LeakyReLU(0.01) backward,
     src/Convolutional_VAE.py:80-100 backward) vs the float64 formula on the same (quantised) inputs:
@@ -533,3 +535,48 @@ def test_bn_bwd_op_matches_reference(cuda, dt, R, C):
     dyh = dy.double().cpu()
     err = (dbias.cpu().double() - dyh.sum(0)).abs()
     assert bool((err <= 1e-5 * dyh.abs().sum(0) + 1e-6).all()), float(err.max())
+
+
+@pytest.mark.parametrize("R,C", [(256 * 8 * 8, 256), (256 * 4 * 4, 512), (5000, 256), (2049, 512)])
+def test_bn_bwd_fused_repeatable(cuda, R, C):
+    """The one-launch BatchNorm backward of the mid-size layers (kernels.hip bn_bwd_fused_kernel: moments, a grid-wide
+    arrival count, then the apply on the rows held in registers).  Its statistics are exact integer sums, so every
+    block that folds them after the count must see every block's adds: 24 repeats give bit-identical dgamma / dbeta /
+    dy / dbias (a fold that ran ahead of an add would change them), and they agree with the two-pass form
+    (HLMC_BN_FUSED=0; its per-thread float32 partials cover other rows, so the totals differ in the last bits)."""
+    g = torch.Generator().manual_seed(R + C)
+    y = (torch.randn(R, C, generator=g) * 1.3 - 0.2).to(cuda, torch.bfloat16)
+    da = torch.randn(R, C, generator=g).to(cuda, torch.bfloat16)
+    mean = y.float().mean(0)
+    invstd = 1.0 / torch.sqrt(y.float().var(0, unbiased=False) + 1e-5)
+    gamma = (1 + 0.2 * torch.randn(C, generator=g)).to(cuda)
+    beta = (0.1 * torch.randn(C, generator=g)).to(cuda)
+    wsb = int(L.lib().hlmc_op_bn_bwd_workspace(C))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+    P = L.ptr
+
+    def run():
+        dy = torch.empty(R, C, dtype=torch.bfloat16, device=cuda)
+        dg, db, dbias = (torch.empty(C, device=cuda) for _ in range(3))
+        L.check(L.lib().hlmc_op_bn_bwd(L.stream(), L.HLMC_BF16, P(da), P(y), R, C, P(mean), P(invstd), P(gamma),
+                                       P(beta), P(dy), P(dg), P(db), P(dbias), P(ws), wsb))
+        return dy, dg, db, dbias
+
+    first = run()
+    outs = [run() for _ in range(24)]
+    torch.cuda.synchronize()
+    for o in outs:
+        for a, b in zip(first, o):
+            assert torch.equal(a, b)
+    old = os.environ.get("HLMC_BN_FUSED")
+    os.environ["HLMC_BN_FUSED"] = "0"
+    try:
+        two = run()
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            del os.environ["HLMC_BN_FUSED"]
+        else:
+            os.environ["HLMC_BN_FUSED"] = old
+    assert rel(first[1], two[1]) < 1e-5 and rel(first[2], two[2]) < 1e-5
+    assert rel(first[0], two[0]) < 1e-2

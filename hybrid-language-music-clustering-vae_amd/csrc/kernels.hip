@@ -581,6 +581,7 @@ __global__ __launch_bounds__(256) void bn_bwd_small_kernel(const T* __restrict__
 // complete (s_waitcnt) before its block arrives, and the fold after the count reads the words with agent-scope
 // atomic loads (no L2 write-back fence per block: round 2 measured that cost).
 constexpr int kBnSpinMax = 1 << 24;
+constexpr int kBnFusedShards = 8;  // accumulator copies the fold reads (xacc_shards(C) <= 8 for C >= 128; checked)
 template <typename T, int kNR, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_fused_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
                                                            int R, int C, const float* __restrict__ mean,
@@ -679,9 +680,9 @@ __global__ __launch_bounds__(256) void bn_bwd_fused_kernel(const T* __restrict__
         const int col = k * C + slab * SW + j;
         // every shard's three words in flight at once (clamped shard index, masked adds): a shard loop waits one
         // memory-side round trip per shard
-        unsigned long long w0[kXAccMaxShards], w1[kXAccMaxShards], w2[kXAccMaxShards];
+        unsigned long long w0[kBnFusedShards], w1[kBnFusedShards], w2[kBnFusedShards];
 #pragma unroll
-        for (int sh = 0; sh < kXAccMaxShards; ++sh) {
+        for (int sh = 0; sh < kBnFusedShards; ++sh) {
             unsigned long long* q = mom.p + (size_t)min(sh, mom.shards - 1) * 3 * mom.ncols + col;
             w0[sh] = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             w1[sh] = __hip_atomic_load(q + mom.ncols, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -690,7 +691,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fused_kernel(const T* __restrict__
         long long s0w = 0, s1w = 0, s2w = 0;
         unsigned long long bad = 0;
 #pragma unroll
-        for (int sh = 0; sh < kXAccMaxShards; ++sh)
+        for (int sh = 0; sh < kBnFusedShards; ++sh)
             if (sh < mom.shards) {
                 s0w += (long long)w0[sh];
                 s1w += (long long)w1[sh];
@@ -1686,8 +1687,9 @@ static void bn_bwd_fused_kernel_ptr(int nr, int act, void (*&k)(const T*, int, c
 // Which layers take the fused form: R * C <= kBnFusedMaxElems, C a multiple of the slab width, and the whole grid
 // co-resident (occupancy query x CUs) -- the kernel's arrival count needs every block running at once.  Measured
 // (scripts/bench_bn.py under rocprofv3, bf16 B = 256): 4 x 4 x 512 14.4 us vs 21.3 us for the two passes, 8 x 8 x 256
-// 15.4 vs 21.3, 16 x 16 x 128 30.8 vs 21.3 (512 blocks: the count waits for the slowest of two blocks per CU); the
-// step with 2^22: 138.6k vs 137.9k clips/s (3 rounds; 2^21: 138.3k, 2^23: 133.7k).  HLMC_BN_FUSED overrides the limit
+// 15.4 vs 21.3, 16 x 16 x 128 30.8 vs 21.3 (512 blocks: the count waits for the slowest of two blocks per CU; 26.6 vs
+// 26.6 us per op call with 16 rows per thread on 256 blocks, yet the step 136.1k vs 138.1k); the step with 2^22:
+// 138.6k vs 137.9k clips/s (3 rounds; 2^21: 138.3k, 2^23: 133.7k).  HLMC_BN_FUSED overrides the limit
 // (0: every layer on the two passes; the parity test compares the forms).
 constexpr int64_t kBnFusedMaxElems = (int64_t)1 << 22;
 template <typename T>
@@ -1695,7 +1697,7 @@ static bool bn_fused_plan(int64_t R, int C, int act, int& nr, int& nslab, unsign
     constexpr int SW = 8 * Vec16<T>::N;
     int64_t lim = kBnFusedMaxElems;
     if (const char* e = std::getenv("HLMC_BN_FUSED")) lim = (int64_t)std::atoll(e);
-    if (C % SW != 0 || R * C > lim || R >= ((int64_t)1 << 31)) return false;
+    if (C % SW != 0 || R * C > lim || R >= ((int64_t)1 << 31) || xacc_shards(C) > kBnFusedShards) return false;
     nslab = C / SW;
     nr = (int64_t)nslab * ((R + 255) / 256) >= 256 ? 8 : 4;
     const int64_t G = (int64_t)nslab * ((R + 32 * nr - 1) / (32 * nr));

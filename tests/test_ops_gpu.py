@@ -580,3 +580,31 @@ def test_bn_bwd_fused_repeatable(cuda, R, C):
             os.environ["HLMC_BN_FUSED"] = old
     assert rel(first[1], two[1]) < 1e-5 and rel(first[2], two[2]) < 1e-5
     assert rel(first[0], two[0]) < 1e-2
+
+
+@pytest.mark.parametrize("R,C", [(256 * 8 * 8, 256), (256 * 4 * 4, 512)])
+def test_bn_bwd_fused_nan_propagates(cuda, R, C):
+    """A non-finite gradient in one channel of a one-launch BatchNorm backward layer reaches the exact accumulator as
+    its sticky flag (common.hpp kXAccBad) and comes out NaN in that channel's dgamma / dbeta / dy only, as torch's
+    backward of a diverged run would; every other channel stays finite."""
+    g = torch.Generator().manual_seed(7 + C)
+    y = torch.randn(R, C, generator=g).to(cuda, torch.bfloat16)
+    da = torch.randn(R, C, generator=g)
+    da[R // 3, 5] = float("inf")
+    da = da.to(cuda, torch.bfloat16)
+    mean = y.float().mean(0)
+    invstd = 1.0 / torch.sqrt(y.float().var(0, unbiased=False) + 1e-5)
+    gamma, beta = torch.ones(C, device=cuda), torch.zeros(C, device=cuda)
+    wsb = int(L.lib().hlmc_op_bn_bwd_workspace(C))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+    dy = torch.empty(R, C, dtype=torch.bfloat16, device=cuda)
+    dg, db, dbias = (torch.empty(C, device=cuda) for _ in range(3))
+    P = L.ptr
+    L.check(L.lib().hlmc_op_bn_bwd(L.stream(), L.HLMC_BF16, P(da), P(y), R, C, P(mean), P(invstd), P(gamma), P(beta),
+                                   P(dy), P(dg), P(db), P(dbias), P(ws), wsb))
+    torch.cuda.synchronize()
+    dg, db, dy = dg.cpu(), db.cpu(), dy.float().cpu()
+    assert not torch.isfinite(dg[5]) and not torch.isfinite(db[5])
+    others = torch.arange(C) != 5
+    assert torch.isfinite(dg[others]).all() and torch.isfinite(db[others]).all()
+    assert torch.isfinite(dy[:, others]).all() and not torch.isfinite(dy[:, 5]).all()

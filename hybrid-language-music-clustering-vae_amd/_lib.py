@@ -24,6 +24,8 @@ NET_HYBRID, NET_CVAE, NET_SIMPLE = 0, 1, 2
 _SIGS = {
     "hlmc_version": (c_int, []),
     "hlmc_last_error": (c_char_p, []),
+    "hlmc_device_status": (c_int, [c_int]),
+    "hlmc_test_bn_fused": (c_int, [c_i64, c_int]),
     "hlmc_mel_plan_create": (c_int, [c_int, c_int, c_int, c_int, c_f64, c_f64, P_vp]),
     "hlmc_mel_plan_destroy": (c_int, [c_vp]),
     "hlmc_mel_filterbank": (c_int, [c_vp, c_vp]),
@@ -148,6 +150,16 @@ def check(status: int, what: str = "") -> None:
     if status != 0:
         msg = lib().hlmc_last_error().decode(errors="replace")
         raise HLMCError(f"{what or 'libhlmc'} failed (status {status}): {msg}")
+
+
+def check_device(what: str = "") -> None:
+    """Raise when a kernel raised a fault bit in the library's device status word (include/hlmc.h
+    hlmc_device_status: e.g. a one-launch BatchNorm backward whose grid-wide count timed out, outputs NaN).  Reads
+    pinned host memory, no synchronisation; a launch's bit is visible once the launch has completed."""
+    st = lib().hlmc_device_status(0)
+    if st:
+        raise HLMCError(f"{what or 'libhlmc'}: device status {st} (bit 0: BatchNorm backward grid-wide count timed "
+                        f"out; its outputs are NaN) -- clear with hlmc_device_status(1)")
 
 
 def ptr(t) -> int | None:

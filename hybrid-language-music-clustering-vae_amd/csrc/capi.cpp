@@ -12,6 +12,16 @@ namespace hlmc {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 const char* get_error() { return g_err.c_str(); }
+// HLMC_EDEVICE while a kernel's fault bit is raised in the device status word (common.hpp)
+static int device_status_ok() {
+    const unsigned st = ops::dev_status_take(false);
+    if (st == 0) return HLMC_OK;
+    set_error("device status " + std::to_string(st) +
+              (st & kDevBnCountTimeout ? ": a one-launch BatchNorm backward's grid-wide arrival count timed out (grid not "
+                                         "co-resident); that launch's dgamma / dbeta / dy are NaN" : "") +
+              " -- clear with hlmc_device_status(1)");
+    return HLMC_EDEVICE;
+}
 
 namespace probe {
 int g_mask = 0;
@@ -84,6 +94,11 @@ int hlmc_probe_read(int* launches, double* total_ms, double* flops, double* byte
     return HLMC_OK;
 }
 const char* hlmc_last_error(void) { return get_error(); }
+int hlmc_device_status(int clear) { return (int)ops::dev_status_take(clear != 0); }
+int hlmc_test_bn_fused(int64_t max_elems, int spin_max) {
+    ops::test_bn_fused(max_elems, spin_max);
+    return HLMC_OK;
+}
 
 // ------------------------------------------------------------------------------------ features
 int hlmc_mel_plan_create(int sr, int n_fft, int hop, int n_mels, double fmin, double fmax, hlmc_mel_plan** out) {
@@ -262,6 +277,7 @@ int hlmc_net_decode(hlmc_net* h, void* stream, int64_t batch, int train, const f
 int hlmc_net_backward(hlmc_net* h, void* stream, int64_t batch, const float* d_recon, const float* d_recon_text,
                       const float* d_mu, const float* d_logvar, void* ws) {
     HLMC_CHECK_ARG(h && ws && d_recon && d_mu && d_logvar, "bad arguments");
+    HLMC_TRY(device_status_ok());
     BackwardArgs a{batch, d_recon, d_recon_text, d_mu, d_logvar, ws};
     return h->impl->backward(S(stream), a);
 }
@@ -505,6 +521,7 @@ int hlmc_op_bn_bwd(void* stream, int dtype, const void* da, const void* y, int64
     HLMC_CHECK_ARG(da && y && mean && invstd && gamma && beta && dy && dgamma && dbeta && ws && R > 1 && C > 0,
                    "hlmc_op_bn_bwd: arguments");
     HLMC_CHECK_ARG(ws_bytes >= hlmc_op_bn_bwd_workspace(C), "hlmc_op_bn_bwd: workspace too small");
+    HLMC_TRY(device_status_ok());
     hipStream_t s = S(stream);
     unsigned char* w = static_cast<unsigned char*>(ws);
     const size_t o1 = (ops::bn_acc_bytes(C) + 255) & ~(size_t)255, o2 = o1 + ((ops::bias_acc_bytes(C) + 255) & ~(size_t)255);

@@ -52,6 +52,17 @@ const char* get_error();
         if (s__ != HLMC_OK) return s__;                                    \
     } while (0)
 
+// ------------------------------------------------------------------ device status word
+// Faults a kernel detects and reports instead of hanging or returning silently wrong values; the kernel writes the bit
+// with a system-scope store into pinned, mapped host memory (dev_status_word), the host reads it without synchronising
+// (dev_status_take, C ABI hlmc_device_status) and the backward entry points return HLMC_EDEVICE while a bit is raised.
+constexpr unsigned kDevBnCountTimeout = 1u;   // bn_bwd_fused_kernel: a block's grid-wide arrival spin ran out
+namespace ops {
+unsigned* dev_status_word();
+unsigned dev_status_take(bool clear);
+void test_bn_fused(int64_t max_elems, int spin_max);
+}  // namespace ops
+
 // ------------------------------------------------------------------ live kernel timing (bench.py roofline)
 // An op sets the site (its kind and ALGORITHMIC flops / HBM bytes) before its launcher runs; when the kind is
 // in the armed mask (hlmc_probe_arm) the launcher brackets its main kernel with a HIP event pair on the launch

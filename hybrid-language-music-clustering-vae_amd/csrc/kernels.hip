@@ -7,8 +7,12 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <type_traits>
 #include <vector>
+#include <atomic>
 
 namespace hlmc {
 namespace {
@@ -573,14 +577,21 @@ __global__ __launch_bounds__(256) void bn_bwd_small_kernel(const T* __restrict__
 // and da twice over two launches whose blocks each fold the full 2C-column accumulator (6C x shards words) before
 // their first row; here every block owns a channel slab (8 V channels: one 128-byte segment of each row) and kNR x 32
 // rows, holds its rows of y and da in registers across the count, and adds / folds only its slab's 2 x 8V columns.
-// Grid = slabs x row blocks, all co-resident (checked by the launcher against the occupancy query), so every block
-// reaches the count; the spin is bounded (kBnSpinMax sleeps, ~1 s) so that a grid that could not become resident ends
-// instead of hanging -- its totals would then be partial, which the launcher's residency check rules out.
-// The arrival counter is the zeroed tail word of the moments accumulator (bn_acc_bytes).  Visibility: the
-// accumulator adds are agent-scope atomics performed at the memory side; each thread waits for its own adds to
-// complete (s_waitcnt) before its block arrives, and the fold after the count reads the words with agent-scope
-// atomic loads (no L2 write-back fence per block: round 2 measured that cost).
-constexpr int kBnSpinMax = 1 << 24;
+// Grid = slabs x row blocks, all co-resident (checked by the launcher against the occupancy query, with half of the
+// chip left to grids co-running on the weight-gradient / comm streams), so every block reaches the count.  The spin
+// is bounded (spin_max polls) so that a grid that could not become resident ends instead of hanging, and a block whose
+// spin ran out is LOUD: its folded totals are replaced by NaN (its dgamma / dbeta / dy come out NaN, and so does every
+// gradient below it) and it raises bit kDevBnCountTimeout of the library's device status word, which the next C-ABI
+// backward call reports as HLMC_EDEVICE (hlmc_device_status).
+// The arrival counter is the zeroed tail word of the moments accumulator (bn_acc_bytes).  Visibility follows the
+// write-through hand-off form of the CDNA guide's Guideline 16 (every payload word written and read at the memory
+// side, no L2 write-back fence): the payload is the accumulator's agent-scope atomic adds; every thread drains them
+// (s_waitcnt vmcnt(0) with a memory clobber, so the compiler cannot sink an add below it) before the block's barrier
+// and its one arrival add; one lane polls the counter relaxed; after the poll a wavefront-scope acquire fence keeps
+// the fold's loads below it, and EVERY fold load is an agent-scope atomic load (sc1), never a plain load that could
+// hit a stale L1 line.  (A per-block agent release + acquire, buffer_wbl2 + buffer_inv, measured 3.9x slower for
+// the same kind of hand-off in round 2)
+constexpr int kBnSpinMax = 1 << 22;   // polls of ~64 sleep cycles + one memory round trip each: ~2-4 s
 constexpr int kBnFusedShards = 8;  // accumulator copies the fold reads (xacc_shards(C) <= 8 for C >= 128; checked)
 template <typename T, int kNR, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_fused_kernel(const T* __restrict__ da, int lda, const T* __restrict__ y,
@@ -589,10 +600,12 @@ __global__ __launch_bounds__(256) void bn_bwd_fused_kernel(const T* __restrict__
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, int act, T* __restrict__ dy,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                           XAcc mom, XAcc bias_acc, int nslab) {
+                                                           XAcc mom, XAcc bias_acc, int nslab, int spin_max,
+                                                           unsigned* status) {
     constexpr int V = Vec16<T>::N, SW = 8 * V;   // 8 threads x V channels per slab row segment
     __shared__ double red[4][2][SW];
     __shared__ double tot[2 * SW];
+    __shared__ int timed_out;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, cg = t & 7, rr = t >> 3;
     const int slab = blockIdx.x % nslab, rb = blockIdx.x / nslab;
     const int c0 = slab * SW + cg * V;
@@ -661,19 +674,28 @@ __global__ __launch_bounds__(256) void bn_bwd_fused_kernel(const T* __restrict__
         const double s = (red[0][k][j] + red[1][k][j]) + (red[2][k][j] + red[3][k][j]);
         xacc_add_shard(mom, shard, k * C + slab * SW + j, s);
     }
-    // arrival: this thread's adds complete, then one count per block; wait for all blocks of the grid
-    __builtin_amdgcn_s_waitcnt(0);
+    // arrival: this thread's adds complete (drained), then one count per block; wait for all blocks of the grid
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     unsigned* arrive = reinterpret_cast<unsigned*>(mom.p + (size_t)mom.shards * 3 * mom.ncols);
     if (t == 0) {
         __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned nblk = gridDim.x;
-        for (int spin = 0; spin < kBnSpinMax; ++spin) {
-            if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nblk) break;
+        int late = 1;
+        for (int spin = 0; spin < spin_max; ++spin) {
+            if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nblk) {
+                late = 0;
+                break;
+            }
             __builtin_amdgcn_s_sleep(2);
         }
+        if (late && __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nblk) late = 0;
+        if (late) __hip_atomic_store(status, kDevBnCountTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        timed_out = late;
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     __syncthreads();
+    const bool lost = timed_out != 0;
     // fold this slab's 2 x SW columns over the shards (agent-scope loads: the other XCDs' adds)
     if (t < 2 * SW) {
         const int k = t / SW, j = t % SW;
@@ -698,7 +720,7 @@ __global__ __launch_bounds__(256) void bn_bwd_fused_kernel(const T* __restrict__
                 bad |= w2[sh] & kXAccBad;
                 s2w += (long long)(w2[sh] & ~kXAccBad);
             }
-        const double v = bad ? __builtin_nan("") : xacc_value(s0w, s1w, s2w);
+        const double v = (bad || lost) ? __builtin_nan("") : xacc_value(s0w, s1w, s2w);
         tot[t] = v;
         if (rb == 0) (k == 0 ? dbeta : dgamma)[slab * SW + j] = (float)v;
     }
@@ -1680,7 +1702,7 @@ int bn_act_train(hipStream_t s, const T* y, int64_t R, int C, XAcc acc, bool hav
 template <typename T>
 static void bn_bwd_fused_kernel_ptr(int nr, int act, void (*&k)(const T*, int, const T*, int, int, const float*,
                                                                 const float*, const float*, const float*, int, T*,
-                                                                float*, float*, XAcc, XAcc, int)) {
+                                                                float*, float*, XAcc, XAcc, int, int, unsigned*)) {
     k = nr == 8 ? (act == 0 ? bn_bwd_fused_kernel<T, 8, 0> : bn_bwd_fused_kernel<T, 8, -1>)
                 : (act == 0 ? bn_bwd_fused_kernel<T, 4, 0> : bn_bwd_fused_kernel<T, 4, -1>);
 }
@@ -1689,47 +1711,94 @@ static void bn_bwd_fused_kernel_ptr(int nr, int act, void (*&k)(const T*, int, c
 // (scripts/bench_bn.py under rocprofv3, bf16 B = 256): 4 x 4 x 512 14.4 us vs 21.3 us for the two passes, 8 x 8 x 256
 // 15.4 vs 21.3, 16 x 16 x 128 30.8 vs 21.3 (512 blocks: the count waits for the slowest of two blocks per CU; 26.6 vs
 // 26.6 us per op call with 16 rows per thread on 256 blocks, yet the step 136.1k vs 138.1k); the step with 2^22:
-// 138.6k vs 137.9k clips/s (3 rounds; 2^21: 138.3k, 2^23: 133.7k).  HLMC_BN_FUSED overrides the limit
-// (0: every layer on the two passes; the parity test compares the forms).
+// 138.6k vs 137.9k clips/s (3 rounds; 2^21: 138.3k, 2^23: 133.7k).  The test hook hlmc_test_bn_fused overrides the
+// limit (0: every layer on the two passes; the parity test compares the forms) and the spin bound.
 constexpr int64_t kBnFusedMaxElems = (int64_t)1 << 22;
+static std::atomic<int64_t> g_bn_fused_lim{kBnFusedMaxElems};
+static std::atomic<int> g_bn_spin_max{kBnSpinMax};
+
+void test_bn_fused(int64_t max_elems, int spin_max) {
+    g_bn_fused_lim.store(max_elems < 0 ? kBnFusedMaxElems : max_elems);
+    g_bn_spin_max.store(spin_max < 0 ? kBnSpinMax : spin_max);
+}
+
+// The library's device status word: pinned, mapped host memory that kernels write with system-scope stores when they
+// detect a fault they must not hang on or hide (bn_bwd_fused_kernel's spin running out).  The host reads it without
+// synchronising; the C-ABI backward entry points report a raised bit as HLMC_EDEVICE.
+static unsigned* g_dev_status = nullptr;
+static std::mutex g_dev_status_mu;
+unsigned* dev_status_word() {
+    std::lock_guard<std::mutex> lk(g_dev_status_mu);
+    if (!g_dev_status) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
+            return nullptr;
+        std::memset(p, 0, 64);
+        g_dev_status = static_cast<unsigned*>(p);
+    }
+    return g_dev_status;
+}
+unsigned dev_status_take(bool clear) {
+    unsigned* w = dev_status_word();
+    if (!w) return 0;
+    return clear ? __atomic_exchange_n(w, 0u, __ATOMIC_SEQ_CST) : __atomic_load_n(w, __ATOMIC_SEQ_CST);
+}
+
+// Residency of a bn_bwd_fused_kernel instance on one device (blocks per CU x CUs), computed once per (device, kNR,
+// activation): the arrival count needs every block of the grid running at once.
+static int bn_fused_resident(int nr, int act, bool bf) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int, bool>, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_tuple(dev, nr, act, bf);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    const void* k = nullptr;
+    if (bf) {
+        void (*kp)(const bf16*, int, const bf16*, int, int, const float*, const float*, const float*, const float*, int,
+                   bf16*, float*, float*, XAcc, XAcc, int, int, unsigned*);
+        bn_bwd_fused_kernel_ptr<bf16>(nr, act, kp);
+        k = reinterpret_cast<const void*>(kp);
+    } else {
+        void (*kp)(const float*, int, const float*, int, int, const float*, const float*, const float*, const float*,
+                   int, float*, float*, float*, XAcc, XAcc, int, int, unsigned*);
+        bn_bwd_fused_kernel_ptr<float>(nr, act, kp);
+        k = reinterpret_cast<const void*>(kp);
+    }
+    int cus = 0, occ = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kThreads, 0) != hipSuccess) occ = 0;
+    const int res = cus * occ > 0 ? cus * occ : -1;
+    cache[key] = res;
+    return res;
+}
 template <typename T>
 static bool bn_fused_plan(int64_t R, int C, int act, int& nr, int& nslab, unsigned& grid) {
     constexpr int SW = 8 * Vec16<T>::N;
-    int64_t lim = kBnFusedMaxElems;
-    if (const char* e = std::getenv("HLMC_BN_FUSED")) lim = (int64_t)std::atoll(e);
+    const int64_t lim = g_bn_fused_lim.load(std::memory_order_relaxed);
     if (C % SW != 0 || R * C > lim || R >= ((int64_t)1 << 31) || xacc_shards(C) > kBnFusedShards) return false;
     nslab = C / SW;
     nr = (int64_t)nslab * ((R + 255) / 256) >= 256 ? 8 : 4;
     const int64_t G = (int64_t)nslab * ((R + 32 * nr - 1) / (32 * nr));
-    static int resident[2][2] = {{0, 0}, {0, 0}};  // [nr == 8][act == 0]
-    int& res = resident[nr == 8][act == 0];
-    if (res == 0) {
-        void (*k)(const T*, int, const T*, int, int, const float*, const float*, const float*, const float*, int, T*,
-                  float*, float*, XAcc, XAcc, int);
-        bn_bwd_fused_kernel_ptr<T>(nr, act, k);
-        int dev = 0, cus = 0, occ = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void*>(k), kThreads, 0) !=
-            hipSuccess)
-            occ = 0;
-        res = std::max(cus * occ, -1);
-        if (res == 0) res = -1;
-    }
-    if (res < 0 || G > res) return false;
+    // at most HALF the device's resident capacity: the other half stays free for the grids that co-run on the
+    // weight-gradient stream and, under data parallelism, RCCL's kernels on the comm stream, so the count's blocks
+    // never wait for CUs those grids hold (the B = 256 layers: G = 256 against 2 blocks per CU x 256 CUs)
+    const int res = bn_fused_resident(nr, act, std::is_same<T, bf16>::value);
+    if (res < 0 || 2 * G > res || !dev_status_word()) return false;
     grid = (unsigned)G;
     return true;
 }
 template <typename T>
-static hipError_t bn_fused_launch(hipStream_t s, int nr, int act, unsigned g, const T* da, int lda, const T* y, int R,
+static void bn_fused_launch(hipStream_t s, int nr, int act, unsigned g, const T* da, int lda, const T* y, int R,
                                   int C, const float* mean, const float* invstd, const float* gamma, const float* beta,
                                   T* dy, float* dgamma, float* dbeta, XAcc mom, XAcc bias_acc, int nslab) {
     void (*k)(const T*, int, const T*, int, int, const float*, const float*, const float*, const float*, int, T*, float*,
-              float*, XAcc, XAcc, int);
+              float*, XAcc, XAcc, int, int, unsigned*);
     bn_bwd_fused_kernel_ptr<T>(nr, act, k);
-    k<<<g, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, dy, dgamma, dbeta, mom, bias_acc, nslab);
-    return hipSuccess;
+    k<<<g, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, dy, dgamma, dbeta, mom, bias_acc, nslab,
+                             g_bn_spin_max.load(std::memory_order_relaxed), dev_status_word());
 }
 
 template <typename T>

@@ -264,8 +264,10 @@ class Trainer:
             _allreduce_sum(self.gflat[lo:hi], self.grad_dtype, self.process_group)
 
     def loss_tuple(self, sums, batch=None):
-        """Host floats (total, l_audio, l_text, kld) from device sums (synchronises)."""
+        """Host floats (total, l_audio, l_text, kld) from device sums (synchronises; raises HLMCError when a kernel
+        of the step reported a fault through the library's device status word)."""
         s = sums.cpu().tolist()
+        L.check_device("Trainer.step")
         if self.kind == "simple":
             na, _, nl = self._cache[batch or next(iter(self._cache))]["n"]
             la, kl = s[0] / na, -0.5 * s[2] / nl

@@ -24,12 +24,21 @@ enum hlmc_status {
     HLMC_EINVAL = -1, /* bad shape / pointer / argument */
     HLMC_EHIP = -2,   /* HIP runtime error */
     HLMC_EUNSUP = -3, /* configuration not supported */
+    HLMC_EDEVICE = -4, /* a kernel reported a fault through the device status word (hlmc_device_status) */
 };
 
 enum hlmc_dtype { HLMC_F32 = 0, HLMC_BF16 = 1 };
 
 int hlmc_version(void);
 const char* hlmc_last_error(void);
+/* Device status word: bits a kernel raised instead of hanging or returning silently wrong values (bit 0: the one-launch
+ * BatchNorm backward's grid-wide arrival count timed out, its outputs are NaN).  No synchronisation: kernels write it
+ * with system-scope stores into pinned host memory, so a launch's bit is visible once the launch has completed.  While a
+ * bit is raised, hlmc_net_backward / hlmc_op_bn_bwd return HLMC_EDEVICE.  clear != 0 resets the word.  Returns the bits. */
+int hlmc_device_status(int clear);
+/* test hook: largest R * C taking the one-launch BatchNorm backward (-1: the default 2^22; 0: two passes everywhere)
+ * and the arrival spin's poll bound (-1: the default).  Not for production use. */
+int hlmc_test_bn_fused(int64_t max_elems, int spin_max);
 
 /* ============================================================== features
  * Replaces librosa.feature.melspectrogram + librosa.power_to_db at

@@ -18,6 +18,9 @@ Tolerances:
   * the whole oracle chain (oracle mel -> oracle f64 scaler -> oracle model) vs the HIP chain: the inputs
     differ by the mel tolerance, so ELBO / mu are compared at 1e-3 (fp32 engine).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -107,13 +110,19 @@ def test_bench_train_step_fp32_matches_oracle(cuda, workload):
     shapes and GEMM plans, fp32 engine: one fused Trainer.step vs the oracle (src/Convolutional_VAE.py:224-240,
     src/Conditional_VAE.py:321-331)."""
     h = _hip_chain("fp32", workload)
-    eps = h["eps"]
     ora = _oracle_model(workload)
     for p, q in zip(ora.parameters(), h["init"]):
         assert torch.equal(p.detach(), q)
-    ora64, ora64f = oracle64_with_kink_envelope(_case(workload), ora, _ins(h, workload), eps, None)
+    ora64, ora64f = oracle64_with_kink_envelope(_case(workload), ora, _ins(h, workload), h["eps"], None)
     out, lo = _oracle_step(ora, h, workload)
-    print(f"{workload} B={B} fp32: rel mu {rel(h['mu'], out[2].detach()):.2e}, rel logvar "
+    _check_fp32_step(workload, h, ora, ora64, ora64f, out, lo)
+
+
+def _check_fp32_step(label, h, ora, ora64, ora64f, out, lo):
+    """fp32 engine step vs the oracle step from the same weights / inputs / eps: outputs and ELBO terms at the 1e-4
+    contract, gradients by the f64-yardstick + kink-envelope rule (BN-fed conv / linear biases absolutely), Adam exact
+    vs torch.optim.Adam on the engine's own gradient, BatchNorm running statistics <= 1e-4."""
+    print(f"{label} B={B} fp32: rel mu {rel(h['mu'], out[2].detach()):.2e}, rel logvar "
           f"{rel(h['logvar'], out[3].detach()):.2e}, ELBO {h['loss'][0]:.6e} vs {float(lo[0]):.6e}")
     assert rel(h["mu"], out[2].detach()) < 1e-4 and rel(h["logvar"], out[3].detach()) < 1e-4
     assert rel(h["recon"], out[0].detach()) < 1e-4
@@ -138,7 +147,7 @@ def test_bench_train_step_fp32_matches_oracle(cuda, workload):
         e_ref, e_ours, e_kink = rel(p.grad, g64), rel(g, g64), rel(o64f[name].grad, g64)
         worst = max(worst, e_ours)
         assert e_ours <= max(1e-3, 8 * e_ref) + 1.5 * e_kink, f"grad {name}: {e_ours:.3e} vs {e_ref:.3e} / {e_kink:.3e}"
-    print(f"{workload} B={B} fp32: worst per-tensor gradient error vs float64 {worst:.2e}")
+    print(f"{label} B={B} fp32: worst per-tensor gradient error vs float64 {worst:.2e}")
     # Adam: exact torch.optim.Adam on the engine's own gradient
     ps = [q.clone().requires_grad_(True) for q in h["init"]]
     off = 0
@@ -171,11 +180,45 @@ BF16_TOL = {"audio": (3.5e-2, 5e-4, 5e-2), "hybrid": (3.5e-2, 5e-4, 5e-2), "cvae
 BF16_BN_TOL = {"audio": (1e-2, 1.5e-2), "hybrid": (2e-2, 1.5e-2), "cvae": (1e-2, 1e-2)}
 
 
+# Per-tensor bf16 gradient errors vs the fp32 oracle, measured on MI355X for every workload and committed as a fixture
+# (tests/golden/bf16_tensor_err.json, written by a run with HLMC_RECORD_BF16=<path>): each tensor must stay within
+# 3x its own measured error + 0.01.  The shallow conv layers and BN parameters reach ~0.36 (B = 256 BatchNorm reductions
+# of bf16 activations), the deep layers are at 1e-2 or below, so a wrong tile in one small layer (relative L2 ~1) is
+# caught there instead of hiding under a blanket 0.6.
+TENSOR_ERR_FIXTURE = os.path.join(os.path.dirname(__file__), "golden", "bf16_tensor_err.json")
+
+
+def _tensor_bounds(label):
+    try:
+        with open(TENSOR_ERR_FIXTURE) as f:
+            meas = json.load(f)[label]
+    except (OSError, KeyError):
+        return None
+    return {n: 3.0 * e + 0.01 for n, e in meas.items()}
+
+
+def _record_tensor_errors(label, per):
+    path = os.environ.get("HLMC_RECORD_BF16")
+    if not path:
+        return
+    d = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            d = json.load(f)
+    d[label] = {n: round(e, 6) for n, e in per.items()}
+    with open(path, "w") as f:
+        json.dump(d, f, indent=1, sort_keys=True)
+
+
 @pytest.mark.parametrize("workload", ["audio", "hybrid", "cvae"])
 def test_bench_train_step_bf16_tracks_oracle(cuda, workload):
     h = _hip_chain("bf16", workload)
     ora = _oracle_model(workload)
     out, lo = _oracle_step(ora, h, workload)
+    _check_bf16_step(workload, h, ora, out, lo, BF16_TOL[workload], BF16_BN_TOL[workload])
+
+
+def _check_bf16_step(label, h, ora, out, lo, tol, bn_tol):
     go = torch.cat([p.grad.reshape(-1) for p in ora.parameters()])
     e_mu, e_elbo, e_g = rel(h["mu"], out[2].detach()), abs(h["loss"][0] - float(lo[0])) / abs(float(lo[0])), rel(h["grad"], go)
     # per-tensor gradient errors (BN-fed conv biases excluded: zero true gradient)
@@ -186,14 +229,16 @@ def test_bench_train_step_bf16_tracks_oracle(cuda, workload):
         off += p.numel()
         if not _bias_feeds_bn(ora, name):
             per[name] = rel(g, p.grad)
+    _record_tensor_errors(label, per)
     worst = sorted(per.items(), key=lambda kv: -kv[1])[:4]
-    print(f"{workload} B={B} bf16: rel mu {e_mu:.2e}, rel ELBO {e_elbo:.2e}, global grad rel L2 {e_g:.2e}; "
+    print(f"{label} B={B} bf16: rel mu {e_mu:.2e}, rel ELBO {e_elbo:.2e}, global grad rel L2 {e_g:.2e}; "
           f"worst tensors {[(n, round(e, 4)) for n, e in worst]}")
-    t_mu, t_elbo, t_g = BF16_TOL[workload]
+    t_mu, t_elbo, t_g = tol
     assert e_mu < t_mu and e_elbo < t_elbo and e_g < t_g
-    # no tensor's gradient is garbage (a wrong tile / layout of one layer: relative L2 ~1.4)
-    bad = {n: e for n, e in per.items() if e > 0.6}
-    assert not bad, bad
+    # every tensor within 3x its measured error (+0.01); no tensor's gradient garbage in any case
+    bounds = _tensor_bounds(label)
+    bad = {n: e for n, e in per.items() if e > 0.6 or (bounds is not None and e > bounds[n])}
+    assert not bad, {n: (e, None if bounds is None else bounds[n]) for n, e in bad.items()}
     # every BatchNorm running buffer after the step vs the oracle's (src/Convolutional_VAE.py:80-100, 124-139):
     # from the zero / one initialisation, running_mean = 0.1 * batch mean and running_var = 0.9 + 0.1 * unbiased
     # batch variance, so the error is reported in the batch statistics' own units -- the mean error in batch standard
@@ -214,10 +259,70 @@ def test_bench_train_step_bf16_tracks_oracle(cuda, workload):
             var = (bo.double() - 0.9) / 0.1
             e = float(((bm.double() - bo.double()).abs() / (0.1 * var.clamp_min(1e-12))).max())
             worst_v = max(worst_v, (e, n))
-    print(f"{workload} B={B} bf16 BN buffers: worst mean error {worst_m[0]:.2e} sd ({worst_m[1]}), worst variance "
+    print(f"{label} B={B} bf16 BN buffers: worst mean error {worst_m[0]:.2e} sd ({worst_m[1]}), worst variance "
           f"error {worst_v[0]:.2e} rel ({worst_v[1]})")
-    t_m, t_v = BF16_BN_TOL[workload]
+    t_m, t_v = bn_tol
     assert worst_m[0] < t_m and worst_v[0] < t_v, (worst_m, worst_v)
+
+
+# ---- BASELINE configs[4]'s training shape: HybridVAE 128 x 1024 with 768-d lyrics at B = 256, the model, trainer and
+# GEMM plans pipeline.run_pipeline times in bench.py's config[4] extra (split-K factors, halo / sub-pixel tiles chosen
+# by M = 256 * H * W at 8x the 128 x 128 pixel count).  Input: the pipeline's own chain on 256 synthetic 30 s clips
+# (HIP mel-dB with 1024 kept frames -> per-pixel StandardScaler), lyrics ~ N(0, 1/768), eps ~ Generator(1).  The oracle
+# step (fp32 + the float64 yardstick and its kink envelope) runs once for both dtypes.  Reference:
+# src/Convolutional_VAE.py:207-240 at its native 128 x 1024 (src/1_preprocessing_advanced.py:34, fixed_time_steps=1024).
+C4_TOL = (3.5e-2, 5e-4, 5e-2)
+C4_BN_TOL = (2e-2, 1.5e-2)
+
+
+@pytest.fixture(scope="module")
+def config4_case(cuda):
+    from hlmc_amd import pipeline as P
+    dev = torch.device("cuda", 0)
+    pcm = P.synthetic_clips(B, P.CLIP_SAMPLES, seed=4242, device=dev)
+    mel = hlmc_amd.extract_mel_spectrogram(pcm, fixed_time_steps=P.KEEP_FRAMES)
+    del pcm
+    x = hlmc_amd.StandardScaler().fit(mel.reshape(B, -1)).transform(mel.reshape(B, -1)).reshape(B, 1, 128, 1024)
+    g = torch.Generator().manual_seed(17)
+    text = torch.randn(B, 768, generator=g) / 768 ** 0.5
+    eps = torch.randn(B, 128, generator=torch.Generator().manual_seed(1))
+    x = x.cpu()
+    torch.manual_seed(42)
+    ora = OM.HybridVAE(128, 768, (128, 1024))
+    ora64, ora64f = oracle64_with_kink_envelope({"kind": "hybrid"}, ora, [x, text], eps, None)
+    out = ora(x, text, eps=eps)
+    lo = OM.loss_function(out[0], x, out[1], text, out[2], out[3])
+    lo[0].backward()
+    return dict(x=x, text=text, eps=eps, ora=ora, ora64=ora64, ora64f=ora64f, out=out, lo=lo)
+
+
+def _config4_engine(c, dtype):
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(42)
+    model = hlmc_amd.HybridVAE(128, 768, (128, 1024), compute_dtype=dtype).to(dev)
+    trainer = hlmc_amd.Trainer(model, lr=1e-4)
+    init = [p.detach().cpu().clone() for p in model.parameters()]
+    for p, q in zip(c["ora"].parameters(), init):
+        assert torch.equal(p.detach(), q)
+    sums = trainer.step(c["x"].to(dev), c["text"].to(dev), eps=c["eps"].to(dev))
+    out = trainer._cache[B]["out"]
+    torch.cuda.synchronize()
+    h = dict(loss=trainer.loss_tuple(sums), mu=out["mu"].cpu(), logvar=out["logvar"].cpu(), recon=out["recon"].cpu(),
+             recon_text=out["recon_text"].cpu(), grad=trainer.gflat.detach().cpu().clone(), init=init, model=model)
+    trainer.release()
+    return h
+
+
+def test_config4_train_step_fp32_matches_oracle(config4_case):
+    c = config4_case
+    h = _config4_engine(c, "fp32")
+    _check_fp32_step("config4 128x1024 td768", h, c["ora"], c["ora64"], c["ora64f"], c["out"], c["lo"])
+
+
+def test_config4_train_step_bf16_tracks_oracle(config4_case):
+    c = config4_case
+    h = _config4_engine(c, "bf16")
+    _check_bf16_step("config4", h, c["ora"], c["out"], c["lo"], C4_TOL, C4_BN_TOL)
 
 
 def test_bench_whole_oracle_chain(cuda):

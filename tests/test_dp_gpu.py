@@ -21,6 +21,11 @@ or 0.15, whichever is larger; ranks bit-identical; parameters = torch Adam on th
 Every worker also checks the checkpoint noise contract: Trainer.state_dict() stores the un-keyed Philox seed (equal on
 every rank), and loading rank 0's checkpoint on every rank restores each rank's own keyed stream (ranks keep drawing
 different eps after a resume).
+The three model families of BASELINE configs[1]-[3] run this chain: the audio-only ConvVAE (fp32 wire, bf16 wire,
+bf16 compute), the hybrid ConvVAE with 384-d lyrics (config[2], "DDP 8x": its text encoder's BatchNorm1d buffers ride the
+same broadcast and its text decoder heads the first bucket, engine.cpp HybridNet bucket_starts) and the genre-conditioned
+ConditionalVAE (config[3], "DDP 8x": latent 64, 768-d lyrics, one-hot genres); reference models
+src/Convolutional_VAE.py:75-194 and src/Conditional_VAE.py:109-246.
 RCCL itself is covered by the 1-rank NCCL test in test_trainer_gpu.py."""
 import os
 import tempfile
@@ -36,12 +41,36 @@ B = 4
 STEPS = 3
 
 
-def _batch(rank, step=0):
+# model family -> (engine constructor, oracle constructor, latent dim, lyric dim or None, genre classes or None)
+MODELS = {
+    "audio": (lambda h, c: h.HybridVAE(128, 768, (128, 128), audio_only=True, compute_dtype=c),
+              lambda OM: OM.HybridVAE(128, 768, (128, 128), audio_only=True), 128, None, None),
+    "hybrid384": (lambda h, c: h.HybridVAE(128, 384, (128, 128), compute_dtype=c),
+                  lambda OM: OM.HybridVAE(128, 384, (128, 128)), 128, 384, None),
+    "cvae": (lambda h, c: h.ConditionalVAE(64, 768, 10, (128, 128), compute_dtype=c),
+             lambda OM: OM.ConditionalVAE(64, 768, 10, (128, 128)), 64, 768, 10),
+}
+
+
+def _batch(kind, rank, step=0):
+    """(audio, text or None, one-hot genres or None, eps) of one rank's shard at one step."""
+    _, _, lat, td, nc = MODELS[kind]
     g = torch.Generator().manual_seed(100 + rank + 10 * step)
-    return torch.randn(B, 1, 128, 128, generator=g), torch.randn(B, 128, generator=g)
+    audio = torch.randn(B, 1, 128, 128, generator=g)
+    eps = torch.randn(B, lat, generator=g)
+    text = torch.randn(B, td, generator=g) / td ** 0.5 if td else None
+    cond = torch.nn.functional.one_hot(torch.randint(0, nc, (B,), generator=g), nc).float() if nc else None
+    return audio, text, cond, eps
 
 
-def _worker(rank, port, outdir, grad_dtype, compute="fp32"):
+def _oracle_loss(kind, out, audio, text):
+    from oracle import models_oracle as OM
+    if kind == "cvae":
+        return OM.cvae_loss_function(out[0], audio, out[1], text, out[2], out[3], beta=4.0)
+    return OM.loss_function(out[0], audio, out[1], text, out[2], out[3])
+
+
+def _worker(rank, port, outdir, grad_dtype, compute="fp32", kind="audio"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
@@ -50,13 +79,14 @@ def _worker(rank, port, outdir, grad_dtype, compute="fp32"):
     import hlmc_amd
     torch.cuda.set_device(0)
     torch.manual_seed(42)
-    m = hlmc_amd.HybridVAE(128, 768, (128, 128), audio_only=True, compute_dtype=compute).cuda()
+    m = MODELS[kind][0](hlmc_amd, compute).cuda()
     tr = hlmc_amd.Trainer(m, lr=1e-4, distributed=True, grad_dtype=grad_dtype)
     assert tr._comm is not None and len(tr.buckets) == 4 and tr.broadcast_buffers
     steps = []
     for k in range(STEPS):
-        audio, eps = _batch(rank, k)
-        tr.step(audio.cuda(), None, eps=eps.cuda())
+        audio, text, cond, eps = _batch(kind, rank, k)
+        tr.step(audio.cuda(), None if text is None else text.cuda(), None if cond is None else cond.cuda(),
+                eps=eps.cuda())
         torch.cuda.synchronize()
         steps.append({"grad": tr.gflat.detach().cpu().clone(),
                       "params": {n: p.detach().cpu().clone() for n, p in m.named_parameters()},
@@ -80,7 +110,7 @@ def _worker(rank, port, outdir, grad_dtype, compute="fp32"):
     dist.destroy_process_group()
 
 
-def _oracle_shards(params, buffers, step):
+def _oracle_shards(kind, params, buffers, step):
     """Per-shard gradients of the oracle model at the given parameters / BN buffers (every rank's forward starts from
     the same broadcast statistics), their sum, the float64 sum and its kink-flipped twin (the yardstick of
     test_models_gpu.compare_step), and rank 0's BN statistics after its forward."""
@@ -89,20 +119,21 @@ def _oracle_shards(params, buffers, step):
     total, buf0, t64, t64f = None, None, None, None
     for rank in range(WORLD):
         torch.manual_seed(42)
-        ora = OM.HybridVAE(128, 768, (128, 128), audio_only=True)
+        ora = MODELS[kind][1](OM)
         with torch.no_grad():
             for n, p in ora.named_parameters():
                 p.copy_(params[n])
             for n, b in ora.named_buffers():
                 b.copy_(buffers[n])
-        audio, eps = _batch(rank, step)
-        m64, m64f = oracle64_with_kink_envelope({"kind": "hybrid"}, ora, [audio, None], eps, None)
+        audio, text, cond, eps = _batch(kind, rank, step)
+        ins = [audio, text, cond] if kind == "cvae" else [audio, text]
+        m64, m64f = oracle64_with_kink_envelope({"kind": "cvae" if kind == "cvae" else "hybrid"}, ora, ins, eps, None)
         g64 = torch.cat([p.grad.reshape(-1) for p in m64.parameters()])
         g64f = torch.cat([p.grad.reshape(-1) for p in m64f.parameters()])
         t64 = g64 if t64 is None else t64 + g64
         t64f = g64f if t64f is None else t64f + g64f
-        out = ora(audio, None, eps=eps)
-        OM.loss_function(out[0], audio, None, None, out[2], out[3])[0].backward()
+        out = ora(*ins, eps=eps)
+        _oracle_loss(kind, out, audio, text)[0].backward()
         g = torch.cat([p.grad.reshape(-1) for p in ora.parameters()])
         total = g if total is None else total + g
         if rank == 0:
@@ -110,23 +141,17 @@ def _oracle_shards(params, buffers, step):
     return total, buf0, t64, t64f
 
 
-def _bn_fed_bias(name):
-    # audio_encoder.{0,3,...}.bias / audio_decoder.{1,4,...,13}.bias: conv biases directly followed by a BatchNorm
-    parts = name.split(".")
-    if parts[-1] != "bias" or parts[0] not in ("audio_encoder", "audio_decoder"):
-        return False
-    i = int(parts[1])
-    return (i % 3 == 0) if parts[0] == "audio_encoder" else (i % 3 == 1 and i < 16)
+CASES = {"fp32_wire": (torch.float32, "fp32", "audio"), "bf16_wire": (torch.bfloat16, "fp32", "audio"),
+         "bf16_compute": (torch.float32, "bf16", "audio"), "hybrid384_fp32_wire": (torch.float32, "fp32", "hybrid384"),
+         "cvae_fp32_wire": (torch.float32, "fp32", "cvae")}
 
 
-@pytest.mark.parametrize("grad_dtype,compute", [(torch.float32, "fp32"), (torch.bfloat16, "fp32"),
-                                                (torch.float32, "bf16")],
-                         ids=["fp32_wire", "bf16_wire", "bf16_compute"])
-def test_dp_two_ranks_match_oracle(cuda, grad_dtype, compute):
+@pytest.mark.parametrize("case", list(CASES))
+def test_dp_two_ranks_match_oracle(cuda, case):
+    grad_dtype, compute, kind = CASES[case]
     with tempfile.TemporaryDirectory() as outdir:
-        port = 29700 + (os.getpid() % 300) + {"fp32_wire": 0, "bf16_wire": 300, "bf16_compute": 600}[
-            ("bf16_compute" if compute == "bf16" else "fp32_wire" if grad_dtype == torch.float32 else "bf16_wire")]
-        mp.spawn(_worker, args=(port, outdir, grad_dtype, compute), nprocs=WORLD, join=True)
+        port = 29700 + (os.getpid() % 300) + 300 * list(CASES).index(case)
+        mp.spawn(_worker, args=(port, outdir, grad_dtype, compute, kind), nprocs=WORLD, join=True)
         res = [torch.load(os.path.join(outdir, f"rank{r}.pt"), weights_only=True) for r in range(WORLD)]
     # the checkpoint noise contract: un-keyed base seed on every rank, each rank's own keyed stream after the resume
     rngs = [r[-1]["rng"] for r in res]
@@ -135,8 +160,9 @@ def test_dp_two_ranks_match_oracle(cuda, grad_dtype, compute):
         assert tuple(r["resumed"]) == tuple(r["expect"]) == tuple(r["live"]), r
     assert rngs[0]["resumed"][0] != rngs[1]["resumed"][0]
     from oracle import models_oracle as OM
+    from tests.test_models_gpu import _bias_feeds_bn
     torch.manual_seed(42)
-    chain = OM.HybridVAE(128, 768, (128, 128), audio_only=True)
+    chain = MODELS[kind][1](OM)
     names = [n for n, _ in chain.named_parameters()]
     shapes = [p.shape for p in chain.parameters()]
     offs, o = [], 0
@@ -155,11 +181,11 @@ def test_dp_two_ranks_match_oracle(cuda, grad_dtype, compute):
         for n in r0["buffers"]:
             assert torch.equal(r0["buffers"][n], r1["buffers"][n]), f"step {k}: BN buffer {n} differs across ranks"
         # reduced gradient = oracle per-shard SUM at the chain's parameters and broadcast statistics
-        ref, buf0, ref64, ref64f = _oracle_shards({n: p.detach() for n, p in zip(names, ps)}, bufs, k)
+        ref, buf0, ref64, ref64f = _oracle_shards(kind, {n: p.detach() for n, p in zip(names, ps)}, bufs, k)
         got = r0["grad"]
         keep = torch.ones_like(ref, dtype=torch.bool)
         for name, (a, b) in zip(names, offs):
-            if _bn_fed_bias(name):
+            if _bias_feeds_bn(chain, name):
                 keep[a:b] = False
                 wa, wb = offs[names.index(name[:-4] + "weight")]
                 btol_b = 2e-2 if compute == "bf16" else 1e-3

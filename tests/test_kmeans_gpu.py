@@ -214,3 +214,79 @@ def test_km_assign_matches_sklearn_estep(cuda, n, d, k):
     lab = torch.empty(n, dtype=torch.int32, device="cuda")
     L.check(L.lib().hlmc_km_assign(L.stream(), Xd.data_ptr(), n, d, Cd.data_ptr(), k, lab.data_ptr(), None, None))
     np.testing.assert_array_equal(lab.cpu().numpy(), ref)
+
+
+def test_kmeans_pp_search_bracket_flags_exact_prefixes(cuda):
+    """hlmc_km_pp_search (include/hlmc.h): a draw lying exactly on a float64 cumsum prefix -- here also inside a run of
+    zero distances from duplicate rows, where several prefixes are equal -- cannot be decided by the device's error
+    bracket and must be flagged (amb = 1) for the numpy redo; every draw it does decide equals np.searchsorted of
+    numpy's own float64 cumsum (sklearn _kmeans_plusplus)."""
+    import ctypes as C
+    import torch
+    from hlmc_amd import _lib as L
+    n = 5000
+    g = np.random.default_rng(3)
+    d = g.random(n).astype(np.float32)
+    d[1000:1040] = 0.0                          # duplicate rows of an already-chosen centre: zero distance
+    cs = np.cumsum(d, dtype=np.float64)
+    exact = [cs[10], cs[1000], cs[1020], cs[2500], cs[n - 1]]
+    between = [0.5 * (cs[99] + cs[100]), 0.5 * (cs[3999] + cs[4000]), 0.25 * cs[0]]
+    rv = np.array(exact + between, dtype=np.float64)
+    T = len(rv)
+    prev = torch.from_numpy(d).reshape(1, 1, n).cuda()
+    best = np.zeros(1, dtype=np.int32)
+    cand = torch.empty(T, dtype=torch.int64, device="cuda")
+    amb = torch.empty(T, dtype=torch.int32, device="cuda")
+    L.check(L.lib().hlmc_km_pp_search(L.stream(), n, 1, T, prev.data_ptr(), 1, best.ctypes.data_as(C.POINTER(C.c_int32)),
+                                      rv.ctypes.data_as(C.POINTER(C.c_double)), cand.data_ptr(), amb.data_ptr()))
+    torch.cuda.synchronize()
+    cand, amb = cand.cpu().numpy(), amb.cpu().numpy()
+    ref = np.minimum(np.searchsorted(cs, rv), n - 1)
+    print(f"amb flags {amb.tolist()}, candidates {cand.tolist()} vs numpy {ref.tolist()}")
+    assert amb[:len(exact)].all(), amb
+    assert not amb[len(exact):].any(), amb
+    decided = amb == 0
+    np.testing.assert_array_equal(cand[decided], ref[decided])
+
+
+def test_kmeans_pp_numpy_redo_matches_oracle(cuda, monkeypatch):
+    """The k-means++ fallback where the device bracket cannot decide (KMeans._kmeans_plusplus_batch): with every draw
+    forced ambiguous, each restart's candidates come from numpy's cumsum / searchsorted, the distances are recomputed
+    and written back into the device buffer and the pinned host image -- the chosen centres must still equal the
+    oracle's sklearn _kmeans_plusplus (oracle/kmeans_oracle.kmeans_plusplus) restart by restart, on data with duplicate
+    rows (zero distances)."""
+    import ctypes as C
+    import torch
+    from hlmc_amd import _lib as L
+    from oracle import kmeans_oracle as KO
+    X = FX.blobs(3000, 16, 6, seed=12)
+    X = np.concatenate([X, np.repeat(X[:50], 4, axis=0)]).astype(np.float32)
+    k, n_init = 8, 4
+    km = hlmc_amd.KMeans(n_clusters=k, random_state=7, n_init=n_init)
+    Xd = torch.as_tensor(X, device="cuda")
+    _, _, Xc = km._center(Xd)
+    lib = L.lib()
+    orig = lib.hlmc_km_pp_search
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemsetAsync.argtypes = [C.c_void_p, C.c_int, C.c_size_t, C.c_void_p]
+    forced = []
+
+    def always_ambiguous(stream, n, R, T, prev, prevT, best, rvals, cand, amb):
+        st = orig(stream, n, R, T, prev, prevT, best, rvals, cand, amb)
+        assert hip.hipMemsetAsync(amb, 1, 4 * R * T, stream) == 0
+        forced.append(R * T)
+        return st
+
+    rs = np.random.RandomState(7)
+    seeds, trials = km._draw_seeds(rs, X.shape[0], n_init, set(range(n_init)))
+    monkeypatch.setattr(lib, "hlmc_km_pp_search", always_ambiguous)
+    _, idx = km._kmeans_plusplus_batch(Xc, [seeds[i] for i in range(n_init)], trials)
+    monkeypatch.setattr(lib, "hlmc_km_pp_search", orig)
+    assert len(forced) == k - 1
+    _, idx_dev = km._kmeans_plusplus_batch(Xc, [seeds[i] for i in range(n_init)], trials)
+    Xh = Xc.cpu().numpy()
+    rs = np.random.RandomState(7)
+    for i in range(n_init):
+        _, ref = KO.kmeans_plusplus(Xh, k, rs)
+        np.testing.assert_array_equal(idx[i], ref, err_msg=f"restart {i} (numpy redo)")
+        np.testing.assert_array_equal(idx_dev[i], ref, err_msg=f"restart {i} (device draws)")

@@ -234,6 +234,27 @@ def test_edge_convs(cuda, ws, dt, shape):
     assert rel(dW, refw) < 1e-5
 
 
+@pytest.mark.parametrize("shape", [(1, 7, 64), (3, 11, 64), (1, 5, 64), (2, 9, 24)])
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_wgrad_c1_odd_heights(cuda, ws, dt, shape):
+    """hlmc_op_wgrad_c1 at odd low-res heights and B = 1 (Xh is [B][2 Hl][2 Wl] f32, include/hlmc.h): the row-streamed
+    kernel of the 64-wide layers (wgrad_c1_rows_kernel: high-res width 2 Wl = 128 and height 2 Hl) and the generic one
+    (Wl = 24) against the float64 formula."""
+    code, tdt, _ = DT[dt]
+    B, Hl, Wl = shape
+    g = torch.Generator().manual_seed(Hl * 31 + B)
+    img = torch.randn(B, 2 * Hl, 2 * Wl, generator=g)
+    dy = torch.randn(B, Hl, Wl, 32, generator=g)
+    refw = torch.nn.grad.conv2d_weight(img.double()[:, None], (32, 1, 3, 3), q(dy, tdt).permute(0, 3, 1, 2),
+                                       stride=2, padding=1)
+    dW = torch.empty(32, 1, 3, 3, device=cuda)
+    imgd, dyd = img.to(cuda), dy.to(cuda, tdt).contiguous()
+    L.check(L.lib().hlmc_op_wgrad_c1(L.stream(), code, dyd.data_ptr(), B, Hl, Wl, 32, imgd.data_ptr(), dW.data_ptr(),
+                                     ws.data_ptr(), WS_BYTES))
+    torch.cuda.synchronize()
+    assert rel(dW, refw) < 1e-5
+
+
 @pytest.mark.parametrize("nt", [0, 4 * 384])
 def test_loss_sums_backward_fused_equals_separate(cuda, nt):
     """hlmc_loss_sums_backward (one pass) == hlmc_loss_sums + hlmc_loss_backward, bit for bit (same grid, same
@@ -543,7 +564,8 @@ def test_bn_bwd_fused_repeatable(cuda, R, C):
     arrival count, then the apply on the rows held in registers).  Its statistics are exact integer sums, so every
     block that folds them after the count must see every block's adds: 24 repeats give bit-identical dgamma / dbeta /
     dy / dbias (a fold that ran ahead of an add would change them), and they agree with the two-pass form
-    (HLMC_BN_FUSED=0; its per-thread float32 partials cover other rows, so the totals differ in the last bits)."""
+    (hlmc_test_bn_fused(0, -1); its per-thread float32 partials cover other rows, so the totals differ in the last
+    bits)."""
     g = torch.Generator().manual_seed(R + C)
     y = (torch.randn(R, C, generator=g) * 1.3 - 0.2).to(cuda, torch.bfloat16)
     da = torch.randn(R, C, generator=g).to(cuda, torch.bfloat16)
@@ -568,18 +590,71 @@ def test_bn_bwd_fused_repeatable(cuda, R, C):
     for o in outs:
         for a, b in zip(first, o):
             assert torch.equal(a, b)
-    old = os.environ.get("HLMC_BN_FUSED")
-    os.environ["HLMC_BN_FUSED"] = "0"
+    L.check(L.lib().hlmc_test_bn_fused(0, -1))
     try:
         two = run()
         torch.cuda.synchronize()
     finally:
-        if old is None:
-            del os.environ["HLMC_BN_FUSED"]
-        else:
-            os.environ["HLMC_BN_FUSED"] = old
+        L.check(L.lib().hlmc_test_bn_fused(-1, -1))
     assert rel(first[1], two[1]) < 1e-5 and rel(first[2], two[2]) < 1e-5
     assert rel(first[0], two[0]) < 1e-2
+    assert L.lib().hlmc_device_status(0) == 0
+
+
+@pytest.mark.parametrize("R,C", [(256 * 8 * 8, 256), (256 * 4 * 4, 512)])
+def test_bn_bwd_fused_timeout_is_loud(cuda, R, C):
+    """bn_bwd_fused_kernel's grid-wide arrival spin is bounded; a block whose spin runs out must not fold partial
+    totals into finite values.  With the test hook's spin bound 0 every block but the last to arrive gives up at once:
+    those blocks' dgamma / dbeta / dy come out NaN, the device status word's bit 0 is raised, the next C-ABI backward
+    call returns HLMC_EDEVICE (checked through Trainer-free hlmc_op_bn_bwd), and clearing the word restores service
+    with the default bound (bit-identical to a fresh run)."""
+    g = torch.Generator().manual_seed(R - C)
+    y = torch.randn(R, C, generator=g).to(cuda, torch.bfloat16)
+    da = torch.randn(R, C, generator=g).to(cuda, torch.bfloat16)
+    mean = y.float().mean(0)
+    invstd = 1.0 / torch.sqrt(y.float().var(0, unbiased=False) + 1e-5)
+    gamma, beta = torch.ones(C, device=cuda), torch.zeros(C, device=cuda)
+    wsb = int(L.lib().hlmc_op_bn_bwd_workspace(C))
+    ws = torch.empty(wsb, dtype=torch.uint8, device=cuda)
+    P = L.ptr
+
+    def launch():
+        dy = torch.empty(R, C, dtype=torch.bfloat16, device=cuda)
+        dg, db, dbias = (torch.empty(C, device=cuda) for _ in range(3))
+        st = L.lib().hlmc_op_bn_bwd(L.stream(), L.HLMC_BF16, P(da), P(y), R, C, P(mean), P(invstd), P(gamma), P(beta),
+                                    P(dy), P(dg), P(db), P(dbias), P(ws), wsb)
+        return st, dy, dg, db
+
+    assert L.lib().hlmc_device_status(1) == 0
+    ok = launch()
+    torch.cuda.synchronize()
+    L.check(L.lib().hlmc_test_bn_fused(-1, 0))
+    try:
+        st, dy, dg, db = launch()
+        torch.cuda.synchronize()
+    finally:
+        L.check(L.lib().hlmc_test_bn_fused(-1, -1))
+    assert st == 0
+    assert L.lib().hlmc_device_status(0) & 1
+    nan_rows = (~torch.isfinite(dy.float())).any(1)
+    print(f"spin bound 0: {int(nan_rows.sum())} of {R} dy rows NaN, dgamma finite {bool(torch.isfinite(dg).all())}")
+    assert int(nan_rows.sum()) > 0
+    # every row is either exact (its block saw the full count) or NaN: no finite partial totals
+    fin = ~nan_rows
+    assert torch.equal(dy[fin], ok[1][fin])
+    assert bool(torch.isfinite(dg).all()) == torch.equal(dg, ok[2])
+    # the next backward call reports the fault instead of computing
+    st2, _, _, _ = launch()
+    assert st2 == -4, st2
+    assert "BatchNorm backward" in L.lib().hlmc_last_error().decode()
+    with pytest.raises(L.HLMCError):
+        L.check_device("test")
+    assert L.lib().hlmc_device_status(1) & 1 and L.lib().hlmc_device_status(0) == 0
+    again = launch()
+    torch.cuda.synchronize()
+    assert again[0] == 0
+    for a, b in zip(ok[1:], again[1:]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("R,C", [(256 * 8 * 8, 256), (256 * 4 * 4, 512)])

@@ -153,8 +153,8 @@ def _kmeans_data(n=100000, d=128, k=10, spread=0.3, seed=5):
 
 def time_kmeans(device, dist, world, rank, cpu_leg=True):
     """KMeans(10, random_state=42, n_init=10).fit on 100 000 x 128 latents (src/Convolutional_VAE.py:317-319 at
-    BASELINE config[4]'s clustering scale): the HIP E/M-step kernels + the host k-means++ (restarts sharded over
-    ranks), against sklearn's fit on the host cores (rank 0, N = 1)."""
+    BASELINE config[4]'s clustering scale): the HIP k-means++ draws / distances and Lloyd E/M-step kernels, the
+    n_init restarts in lockstep (sharded over ranks), against sklearn's fit on the host cores (rank 0, N = 1)."""
     X = _kmeans_data()
     Xd = torch.from_numpy(X).to(device)
     group = dist.group.WORLD if dist else None
@@ -392,7 +392,8 @@ def main():
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="fp32",
                     help="gradient all-reduce wire for N > 1 (default fp32, the reference's numerics; bf16 halves the "
                          "xGMI bytes and is reported as the labelled `headline_bf16_wire` extra, DESIGN.md §7)")
-    ap.add_argument("--e2e-clips", type=int, default=20000, help="clips of the config[4] end-to-end extra line")
+    ap.add_argument("--e2e-clips", type=int, default=100000,
+                    help="clips of the config[4] end-to-end extra line (BASELINE configs[4]: 100k synthetic clips)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (N = 1 only; measured 12%% slower on ROCm 7: the graph "
                          "executor serialises the weight-gradient stream's branch, see DESIGN.md)")
@@ -527,7 +528,7 @@ def main():
                                                               steps=args.steps, warmup=args.warmup,
                                                               grad_dtype=torch.bfloat16), grad_wire="bf16")
         extras["kmeans_n100k_k10"] = time_kmeans(device, dist, world, rank)
-        extras["config4_e2e_n20k"] = time_e2e(device, dist, world, args.e2e_clips, grad_dtype)
+        extras[f"config4_e2e_n{args.e2e_clips // 1000}k"] = time_e2e(device, dist, world, args.e2e_clips, grad_dtype)
 
     if rank == 0:
         n_params = params_of_headline

@@ -118,9 +118,6 @@ _SIGS = {
     "hlmc_op_halo_workspace": (c_i64, [c_int, c_int]),
     "hlmc_op_halo_fwd": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp,
                                  c_vp, c_vp, c_vp, c_vp, c_f32, c_f32, c_vp, c_vp, c_vp, c_vp, c_i64]),
-    "hlmc_op_halo_bwd_workspace": (c_i64, [c_int]),
-    "hlmc_op_halo_bwd": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp,
-                                 c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64]),
 }
 
 _lib = None

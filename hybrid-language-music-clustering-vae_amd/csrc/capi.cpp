@@ -574,38 +574,5 @@ int hlmc_op_halo_fwd(void* stream, int kind, const void* x, int B, int Hi, int W
     HLMC_CHECK_ARG(st.done, "hlmc_op_halo_fwd: statistics not delivered by the halo kernel");
     return ops::colsum_to_f64(s, aout, 2 * Co, out_sums);
 }
-int64_t hlmc_op_halo_bwd_workspace(int Ci) {
-    return (int64_t)(((ops::bn_acc_bytes(Ci) + 255) & ~(size_t)255) + ops::bias_acc_bytes(Ci));
-}
-int hlmc_op_halo_bwd(void* stream, int kind, const void* y, const void* da, int B, int Hi, int Wi, int Ci,
-                     const void* wp, int Co, void* out, const float* mean, const float* invstd, const float* gamma,
-                     const float* beta, void* dy, float* dgamma, float* dbeta, float* dbias, void* ws, int64_t ws_bytes) {
-    HLMC_CHECK_ARG(kind == 0 || kind == 1, "hlmc_op_halo_bwd: kind 0 (conv_s2) or 1 (subpixel)");
-    HLMC_CHECK_ARG(y && da && wp && out && mean && invstd && gamma && beta && dy && dgamma && dbeta && ws &&
-                       ws_bytes >= hlmc_op_halo_bwd_workspace(Ci),
-                   "hlmc_op_halo_bwd: arguments / workspace");
-    HLMC_CHECK_ARG(kind == 0 ? ops::conv_s2_takes_input_bn<bf16>(B, Hi, Wi, Ci, Co)
-                             : ops::subpixel_takes_input_bn<bf16>(B, Hi, Wi, Ci, Co),
-                   "hlmc_op_halo_bwd: not an LDS halo-tile shape");
-    HLMC_TRY(device_status_ok());
-    hipStream_t s = S(stream);
-    unsigned char* w = static_cast<unsigned char*>(ws);
-    const size_t o1 = (ops::bn_acc_bytes(Ci) + 255) & ~(size_t)255;
-    XAcc mom{reinterpret_cast<unsigned long long*>(w), xacc_shards(Ci), 2 * Ci};
-    XAcc bacc{reinterpret_cast<unsigned long long*>(w + o1), xacc_shards(Ci), Ci};
-    HLMC_HIP(hipMemsetAsync(ws, 0, (size_t)hlmc_op_halo_bwd_workspace(Ci), s));
-    const int64_t R = (int64_t)B * Hi * Wi;
-    HLMC_TRY(ops::bn_bwd_moments<bf16>(s, (const bf16*)da, Ci, (const bf16*)y, R, Ci, mean, invstd, gamma, beta, 0, mom));
-    ops::BnBwdInput xb{da, mom, R, mean, invstd, gamma, beta, dgamma, dbeta, dbias ? bacc : XAcc{}, dy};
-    Ws none{nullptr, 0};
-    if (kind == 0)
-        HLMC_TRY(ops::conv_s2<bf16>(s, (const bf16*)y, B, Hi, Wi, Ci, (const bf16*)wp, nullptr, Co, (bf16*)out, none,
-                                    nullptr, nullptr, &xb));
-    else
-        HLMC_TRY(ops::subpixel<bf16>(s, (const bf16*)y, B, Hi, Wi, Ci, (const bf16*)wp, nullptr, Co, (bf16*)out, none,
-                                     nullptr, nullptr, &xb));
-    if (dbias) return ops::colsum_finalize(s, bacc, Ci, dbias);
-    return HLMC_OK;
-}
 
 }  // extern "C"

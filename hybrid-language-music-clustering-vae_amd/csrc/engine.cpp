@@ -453,36 +453,6 @@ class NetT : public NetBase {
         }, side_batch());
     }
     ops::BnBwdFuse fuse4{};  // the decoder's last BN layer: moments from the output convT's data gradient
-    size_t chainB = 0;       // second data-gradient chain buffer (the halo kernels that apply a BN backward while
-                             // staging read da from one buffer and write their output into the other)
-    // BatchNorm backward applied inside the next data-gradient halo kernel (XIN 2) for these layers (A/B knob, bit
-    // 0: decoder layer 4, 1: decoder layer 3, 2: encoder layer 1, 3: encoder layer 2)
-    static int bwd_fold_mask() {
-        static const int v = [] {
-            const char* e = std::getenv("HLMC_BWD_FOLD");
-            return e ? std::atoi(e) : 0;
-        }();
-        return v;
-    }
-    // moments (unless the producer of da delivered them), then the data-gradient halo kernel that applies the rest of
-    // the BatchNorm backward while staging: dy (for the weight gradient), dgamma / dbeta, the conv bias sums
-    ops::BnBwdInput bwd_fold_input(hipStream_t s, const T* da, const T* y, int64_t R, int C, const BnBufs& bb, int g,
-                                   int beta, int bias, T* dy, const ops::BnBwdFuse* fused, int& st) {
-        st = HLMC_OK;
-        if (!(fused && fused->done))
-            st = ops::bn_bwd_moments<T>(s, da, C, y, R, C, AF(bb.mean), AF(bb.inv), P[g], P[beta], 0, acc_mom(bb));
-        return ops::BnBwdInput{da, acc_mom(bb), R, AF(bb.mean), AF(bb.inv), P[g], P[beta], G[g], G[beta],
-                               bias >= 0 ? acc_bias(bb) : XAcc{}, dy};
-    }
-    // the conv bias gradient of a folded layer: reduced by its weight gradient's reduce launch (side stream) or here
-    int bwd_fold_bias(hipStream_t s, const BnBufs& bb, int C, int bias) {
-        if (bias < 0) return HLMC_OK;
-        if (use_side) {
-            pend_bias = PendingBias{acc_bias(bb), C, G[bias]};
-            return HLMC_OK;
-        }
-        return ops::colsum_finalize(s, acc_bias(bb), C, G[bias]);
-    }
 
     // ---------------------------------------------------------------- conv encoder (6 x conv-BN-LReLU)
     struct Enc {
@@ -572,35 +542,11 @@ class NetT : public NetBase {
         hs[0] = enc.H;
         ws_[0] = enc.W;
         for (int l = 0; l < 6; ++l) { hs[l + 1] = hs[l] / 2; ws_[l + 1] = ws_[l] / 2; }
-        T* alt = AT(chainB);
         for (int l = 5; l >= 0; --l) {
             const int ci = ENC_CH[l], co = ENC_CH[l + 1];
             const int ho = hs[l + 1], wo = ws_[l + 1];
             const int64_t R = (int64_t)B * ho * wo;
             T* dy = AT(enc.dy[l]);
-            // layers 1 and 2: the BatchNorm backward applied by the sub-pixel data-gradient halo kernel (bf16)
-            const bool fold = l >= 1 && chainB && (bwd_fold_mask() >> (l + 1) & 1) &&
-                              ops::subpixel_takes_input_bn<T>(B, ho, wo, co, ci);
-            if (fold) {
-                int st = HLMC_OK;
-                const ops::BnBwdInput xb = bwd_fold_input(s, gA, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l],
-                                                          enc.b[l], dy, nullptr, st);
-                HLMC_TRY(st);
-                HLMC_TRY(ops::subpixel<T>(s, AT(enc.y[l]), B, ho, wo, co, P1(enc.w[l]), nullptr, ci, alt, scratch,
-                                          nullptr, nullptr, &xb));
-                HLMC_TRY(bwd_fold_bias(s, enc.bb[l], co, enc.b[l]));
-                const T* xin = AT(enc.a[l - 1]);
-                float* gw = G[enc.w[l]];
-                const PendingBias pb = take_bias();  // written by the weight gradient's reduce launch
-                HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) {
-                    return ops::wgrad_s2<T>(q, dy, B, ho, wo, co, xin, ci, gw, sc, pb.acc, pb.gb);
-                }));
-                if (l == 1) HLMC_TRY(flush_side(s));
-                std::swap(gA, alt);
-                if (l == 3 && bucket_hi >= 0) HLMC_TRY(mark(s, bucket_hi));
-                if (l == 2) HLMC_TRY(prelate(s));
-                continue;
-            }
             HLMC_TRY(bn_bwd(s, gA, co, AT(enc.y[l]), R, co, enc.bb[l], enc.g[l], enc.beta[l], 0, nullptr, 1.f, dy, enc.b[l],
                             nullptr, true, true));
             float* gw = G[enc.w[l]];
@@ -728,33 +674,11 @@ class NetT : public NetBase {
                                         &fuse4));
         }
         ops::BnBwdFuse fuse = fuse4;
-        T* alt = AT(chainB);
         for (int l = 4; l >= 0; --l) {
             const int ci = DEC_CH[l], co = DEC_CH[l + 1];
             const int hl = hs[l], wl = ws_[l];
             const int64_t R = (int64_t)B * 4 * hl * wl;
             T* dy = AT(dec.dy[l]);
-            // layers 4 and 3: the BatchNorm backward applied by the conv data-gradient halo kernel (bf16)
-            const bool fold = chainB && (l == 4 || l == 3) && (bwd_fold_mask() >> (4 - l) & 1) &&
-                              ops::conv_s2_takes_input_bn<T>(B, 2 * hl, 2 * wl, co, ci);
-            if (fold) {
-                int st = HLMC_OK;
-                const ops::BnBwdInput xb = bwd_fold_input(s, gA, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l],
-                                                          dec.b[l], dy, &fuse, st);
-                HLMC_TRY(st);
-                HLMC_TRY(ops::conv_s2<T>(s, AT(dec.y[l]), B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, alt, scratch,
-                                         nullptr, nullptr, &xb));
-                HLMC_TRY(bwd_fold_bias(s, dec.bb[l], co, dec.b[l]));
-                const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
-                float* gw = G[dec.w[l]];
-                const PendingBias pb = take_bias();
-                HLMC_TRY(side_bias(s, [=](hipStream_t q, Ws sc) {
-                    return ops::wgrad_s2<T>(q, xin, B, hl, wl, ci, dy, co, gw, sc, pb.acc, pb.gb);
-                }));
-                std::swap(gA, alt);
-                fuse = ops::BnBwdFuse{};
-                continue;
-            }
             HLMC_TRY(bn_bwd(s, gA, co, AT(dec.y[l]), R, co, dec.bb[l], dec.g[l], dec.beta[l], 0, nullptr, 1.f, dy, dec.b[l],
                             &fuse, true, true));
             const T* xin = l == 0 ? u : AT(dec.a[l - 1]);
@@ -766,7 +690,7 @@ class NetT : public NetBase {
             HLMC_TRY(ops::conv_s2<T>(s, dy, B, 2 * hl, 2 * wl, co, P0(dec.w[l]), nullptr, ci, gA, scratch));
             fuse = ops::BnBwdFuse{};  // the stride-2 conv data gradients carry no moments: a separate pass
         }
-        *out = gA;  // (the chain buffer the last data gradient wrote)
+        *out = gA;
         return HLMC_OK;
     }
 };
@@ -892,7 +816,6 @@ class HybridNet : public NetT<T> {
         }
         const size_t gmax = std::max(this->enc_max_elems(B), this->dec_max_elems(B));
         gA_ = A.take(gmax * t);
-        this->chainB = A.take(gmax * t);
         gflat_ = A.take(B * ldF * t);
         gfuse_ = A.take(B * ldFU * t);
         gh_ = A.take(B * 512 * t);
@@ -1091,7 +1014,6 @@ class CvaeNet : public NetT<T> {
         td_bb = this->bn_plan(A, 512);
         const size_t gmax = std::max(this->enc_max_elems(B), this->dec_max_elems(B));
         gA_ = A.take(gmax * t);
-        this->chainB = A.take(gmax * t);
         grt_ = A.take(B * ldT * t);
         gtd_ = A.take(B * 512 * t);
         gt2_ = A.take(B * 512 * t);

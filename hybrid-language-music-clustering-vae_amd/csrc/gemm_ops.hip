@@ -430,108 +430,6 @@ __device__ __forceinline__ uint4 bn_in_apply(uint4 v, const float (&pr)[4][8]) {
     return o;
 }
 
-// ---- train-mode BatchNorm + LeakyReLU(0.01) BACKWARD applied while a data-gradient halo kernel stages its input
-// (XIN 2): the kernel's input pointer is the layer's pre-BN map y and da the gradient of its activation; the block folds
-// the layer's backward moments (sum dz | sum dz x-hat, delivered complete by bn_bwd_moments or the producer of da) in
-// its prologue (block 0 stores dgamma / dbeta, bn_bwd_apply's consumer-side finalize), forms
-// dy = gamma invstd (dz - sum dz / R - x-hat sum(dz x-hat) / R) of each staged 16-byte chunk in registers (the arithmetic
-// of bn_bwd_apply_kernel), writes dy of the rows its tile owns (every row once over the grid: the layer's weight
-// gradient reads it) and adds those rows' stored (bf16-rounded) dy to the conv bias accumulator.  The separate apply
-// pass, its second read of y and da and its launch are gone.  Rows outside the image stay zero (padding).
-struct BnBwdIn {
-    const bf16* da;                 // the activation gradient, same NHWC layout as y
-    XAcc mom;                       // 2C columns: sum dz | sum dz * x-hat (complete)
-    int64_t R;
-    const float *mean, *invstd, *gamma, *beta;
-    float *dgamma, *dbeta;          // block 0 stores them
-    XAcc bias_acc;                  // C columns (off: no conv bias gradient)
-    bf16* dy_out;
-};
-template <int CI>
-struct BnBwdLds {  // prologue scratch (red is reused for the closing bias-sum reduction) + per-channel parameters
-    double tot[2 * CI];
-    long long red[3 * 256];
-    float prm[6 * CI];  // mean | invstd | gamma | beta | sum dz / R | sum dz x-hat / R
-};
-template <int CI>
-__device__ __forceinline__ void bn_bwd_in_prologue(const BnBwdIn& f, BnBwdLds<CI>& L) {
-    xacc_fold(f.mom, L.tot, L.red);
-    const float invR = 1.f / (float)f.R;
-    for (int c = threadIdx.x; c < CI; c += 256) {
-        const float s0 = (float)L.tot[c], sx = (float)L.tot[CI + c];
-        L.prm[c] = f.mean[c];
-        L.prm[CI + c] = f.invstd[c];
-        L.prm[2 * CI + c] = f.gamma[c];
-        L.prm[3 * CI + c] = f.beta[c];
-        L.prm[4 * CI + c] = s0 * invR;
-        L.prm[5 * CI + c] = sx * invR;
-        if (blockIdx.x == 0) {
-            f.dbeta[c] = s0;
-            f.dgamma[c] = sx;
-        }
-    }
-    __syncthreads();
-}
-// dy of 8 bf16 channels from y (v) and da (g); bs += the stored (rounded) dy where `own`
-__device__ __forceinline__ uint4 bn_bwd_in_apply(uint4 v, uint4 g, const float (&pr)[6][8], bool own, float (&bs)[8]) {
-    float x[8], d[8];
-    cvt16_f32<bf16>(v, x);
-    cvt16_f32<bf16>(g, d);
-    uint4 o;
-    unsigned* w = reinterpret_cast<unsigned*>(&o);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        bf16 h2[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int k = 2 * i + e;
-            const float xh = (x[k] - pr[0][k]) * pr[1][k];
-            const float z = xh * pr[2][k] + pr[3][k];
-            const float dz = d[k] * (z > 0.f ? 1.f : 0.01f);
-            h2[e] = __float2bfloat16(pr[2][k] * pr[1][k] * (dz - pr[4][k] - xh * pr[5][k]));
-            bs[k] += own ? __bfloat162float(h2[e]) : 0.f;
-        }
-        w[i] = (unsigned)(*reinterpret_cast<unsigned short*>(&h2[0])) |
-               ((unsigned)(*reinterpret_cast<unsigned short*>(&h2[1])) << 16);
-    }
-    return o;
-}
-// the same with the parameters read from the LDS table (prm [6][CI]) at each call: c0 is made opaque so that the compiler
-// cannot keep the 48 values live across the tile loop (the sub-pixel kernel's register budget)
-template <int CI>
-__device__ __forceinline__ uint4 bn_bwd_in_apply_lds(uint4 v, uint4 g, const float* prm, int c0, bool own,
-                                                     float (&bs)[8]) {
-    asm volatile("" : "+v"(c0));
-    float pr[6][8];
-#pragma unroll
-    for (int q = 0; q < 6; ++q)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pr[q][k] = prm[q * CI + c0 + k];
-    return bn_bwd_in_apply(v, g, pr, own, bs);
-}
-// the block's per-thread bias sums (thread t: channels (t % CPP) * 8 ..) -> the exact accumulator, fixed order: xor
-// tree over the wave's lanes sharing the channel group, then the 4 waves in LDS (scratch: >= 4 CI doubles)
-template <int CI>
-__device__ __forceinline__ void bn_bwd_in_bias(const BnBwdIn& f, float (&bs)[8], double* scratch) {
-    constexpr int CPP = CI / 8;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    double a[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] = bs[k];
-#pragma unroll
-    for (int o = CPP; o < 64; o <<= 1)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) a[k] += __shfl_xor(a[k], o, 64);
-    if (lane < CPP)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) scratch[wave * CI + lane * 8 + k] = a[k];
-    __syncthreads();
-    if (tid < CI) {
-        const double v = (scratch[tid] + scratch[CI + tid]) + (scratch[2 * CI + tid] + scratch[3 * CI + tid]);
-        xacc_add(f.bias_acc, tid, v);
-    }
-}
-
 // ---- stride-2 3x3 conv over LDS halo tiles: Ci = 32, Wo = 32, bf16, Co = CO.
 // Measured (scripts/bench_gemm.py): the 64x64x32 -> 64 conv and the matching decoder data gradient 46.3 / 44.1 ->
 // 36.7 / 34.2 us; bench A/B 106.4k vs 105.0k clips/s (3 alternating rounds).
@@ -542,11 +440,9 @@ __device__ __forceinline__ void bn_bwd_in_bias(const BnBwdIn& f, float (&bs)[8],
 // Template: CI input channels, COB output channels per block (NSPL blocks share a tile's Co = NSPL * COB), WO
 // output width, ROWS output rows per tile (TP = ROWS * WO pixels), DB: double-buffered halo (else one buffer and
 // an extra barrier).  Shapes: 2 WO * CI / 8 == 256 (one 16-byte chunk per thread per input row).
-// XIN: 0 plain input, 1 forward BatchNorm + LeakyReLU of the input (BnIn), 2 BatchNorm backward (BnBwdIn)
-template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP, bool TR = true, int XIN = 0, int WPE = 1>
+template <int CI, int COB, int NSPL, int WO, int ROWS, bool DB, class EP, bool TR = true, bool XIN = false, int WPE = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void conv_s2_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
-                                                           const bf16* __restrict__ wp, EP ep, int M, BnIn xin,
-                                                           BnBwdIn xb) {
+                                                           const bf16* __restrict__ wp, EP ep, int M, BnIn xin) {
     constexpr int WI = 2 * WO, HR = 2 * ROWS + 1, HC = WI + 1, PS = CI + 8;  // halo rows / cols / pixel pitch
     constexpr int TP = ROWS * WO, CPP = CI / 8;                             // tile pixels, chunks per pixel
     static_assert(WI * CPP == 256 && (COB == 64 || COB == 32), "halo chunk map / wave tiling");
@@ -579,7 +475,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         *reinterpret_cast<uint4*>(&Hs[(bufr / HR) * HS + ((bufr % HR) * HC) * PS + q * 8]) = make_uint4(0, 0, 0, 0);
     }
     uint4 hr[HR];  // HR rows x 256 chunks / 256 threads
-    uint4 hg[XIN == 2 ? HR : 1];  // XIN 2: the same rows of da
     auto row_off = [&](int b, int ih) { return (((int64_t)b * Hi + ih) * WI + tid / CPP) * CI + (tid % CPP) * 8; };
     // unconditional loads (row -1 clamped to row 0; zeroed when staged): a branch per row made the compiler wait
     // for the loads right after issuing them
@@ -589,30 +484,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         for (int u = 0; u < HR; ++u) {
             const int ih = 2 * oh0 - 1 + u;
             h[u] = *reinterpret_cast<const uint4*>(x + row_off(b, ih < 0 ? 0 : ih));
-            if constexpr (XIN == 2) hg[u] = *reinterpret_cast<const uint4*>(xb.da + row_off(b, ih < 0 ? 0 : ih));
         }
     };
-    float pr[XIN == 1 ? 4 : XIN == 2 ? 6 : 1][8];  // XIN: this thread's 8 channels' BatchNorm parameters
-    float bsum[XIN == 2 ? 8 : 1];                   // XIN 2: the bias sums of this thread's stored dy
-#pragma unroll
-    for (int k = 0; k < (XIN == 2 ? 8 : 1); ++k) bsum[k] = 0.f;
-    // XIN: the rows of tile t become activations (1) / dy (2) (in range: all but row -1); rows 2 oh0 .. are this
-    // tile's to write
+    float pr[XIN ? 4 : 1][8];  // XIN: this thread's 8 channels' BatchNorm parameters
+    // XIN: the rows of tile t become activations (in range: all but row -1); rows 2 oh0 .. are this tile's to write
     auto xform_rows = [&](uint4* h, int t) {
-        if constexpr (XIN != 0) {
+        if constexpr (XIN) {
             const int b = t / tpi, oh0 = (t - b * tpi) * ROWS;
 #pragma unroll
             for (int u = 0; u < HR; ++u) {
                 const int ih = 2 * oh0 - 1 + u;
                 if (ih < 0) continue;
-                const bool own = u > 0 && nh == 0;
-                if constexpr (XIN == 1) {
-                    h[u] = bn_in_apply(h[u], pr);
-                    if (own) *reinterpret_cast<uint4*>(xin.a_out + row_off(b, ih)) = h[u];
-                } else {
-                    h[u] = bn_bwd_in_apply(h[u], hg[u], pr, own, bsum);
-                    if (own) *reinterpret_cast<uint4*>(xb.dy_out + row_off(b, ih)) = h[u];
-                }
+                h[u] = bn_in_apply(h[u], pr);
+                if (u > 0 && nh == 0) *reinterpret_cast<uint4*>(xin.a_out + row_off(b, ih)) = h[u];
             }
         }
     };
@@ -625,7 +509,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     };
     int t = blockIdx.x / NSPL, buf = 0;
     if (t < ntiles) load_rows(hr, t);  // in flight during the statistics prologue
-    if constexpr (XIN == 1) {
+    if constexpr (XIN) {
         __shared__ BnInLds<CI> bl;
         bn_in_prologue<CI>(xin, bl);
         const int c0 = (tid % CPP) * 8;
@@ -636,15 +520,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             pr[2][k] = bl.prm[2 * CI + c0 + k];
             pr[3][k] = bl.prm[3 * CI + c0 + k];
         }
-    }
-    if constexpr (XIN == 2) {
-        __shared__ BnBwdLds<CI> bbl;
-        bn_bwd_in_prologue<CI>(xb, bbl);
-        const int c0 = (tid % CPP) * 8;
-#pragma unroll
-        for (int q = 0; q < 6; ++q)
-#pragma unroll
-            for (int k = 0; k < 8; ++k) pr[q][k] = bbl.prm[q * CI + c0 + k];
     }
     if (t < ntiles) {
         xform_rows(hr, t);
@@ -741,12 +616,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             xacc_add_shard(ep.acc, shard, CO + n0 + tid, q);
         }
     }
-    if constexpr (XIN == 2) {
-        if (xb.bias_acc.on()) {
-            __syncthreads();  // the halo buffer is free: scratch for the closing reduction
-            bn_bwd_in_bias<CI>(xb, bsum, reinterpret_cast<double*>(Hs));
-        }
-    }
 }
 
 // ---- sub-pixel (stride-2 transposed 3x3) conv over LDS halo tiles: Ci = 64,
@@ -757,10 +626,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // Template: CI input channels, COB output channels per block (NSPL blocks per tile), WI low-res width, ROWS
 // low-res rows per tile (TP = ROWS * WI = 128 pixels), DB: double-buffered halo.  WI * CI / 8 == 256.
 // WPE: waves per SIMD the register allocation targets (2: two blocks per CU, with DB = false to fit the LDS)
-template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP, bool TR = true, int XIN = 0, int WPE = 1>
+template <int CI, int COB, int NSPL, int WI, int ROWS, bool DB, class EP, bool TR = true, bool XIN = false, int WPE = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void subpixel_halo_kernel(const bf16* __restrict__ x, int Hi, int ntiles,
-                                                            const bf16* __restrict__ wp, EP ep, int M, BnIn xin,
-                                                            BnBwdIn xb) {
+                                                            const bf16* __restrict__ wp, EP ep, int M, BnIn xin) {
     constexpr int HR = ROWS + 1, HC = WI + 1, PS = CI + 8, CPP = CI / 8, TP = ROWS * WI;
     static_assert(WI * CPP == 256 && TP == 128 && (COB == 32 || COB == 16), "halo chunk map / wave tiling");
     constexpr int KP = 9 * CI + 8;                        // weight row: fragment rows on distinct 16-byte slots
@@ -785,7 +653,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         *reinterpret_cast<uint4*>(&Hs[(bufr / HR) * HS + ((bufr % HR) * HC + WI) * PS + q * 8]) = make_uint4(0, 0, 0, 0);
     }
     uint4 hr[HR];  // HR rows x 256 chunks / 256 threads
-    uint4 hg[XIN == 2 ? HR : 1];  // XIN 2: the same rows of da
     auto row_off = [&](int b, int ih) { return (((int64_t)b * Hi + ih) * WI + tid / CPP) * CI + (tid % CPP) * 8; };
     auto load_rows = [&](uint4* h, int t) {
         const int b = t / tpi, r0 = (t - b * tpi) * ROWS;
@@ -793,31 +660,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         for (int u = 0; u < HR; ++u) {
             const int ih = r0 + u;
             h[u] = *reinterpret_cast<const uint4*>(x + row_off(b, ih < Hi ? ih : Hi - 1));  // zeroed when staged
-            if constexpr (XIN == 2) hg[u] = *reinterpret_cast<const uint4*>(xb.da + row_off(b, ih < Hi ? ih : Hi - 1));
         }
     };
-    float pr[XIN == 1 ? 4 : 1][8];  // XIN 1: this thread's 8 channels' BatchNorm parameters (XIN 2: from LDS)
-    float bsum[XIN == 2 ? 8 : 1];    // XIN 2: the bias sums of this thread's stored dy
-    __shared__ std::conditional_t<XIN == 2, BnBwdLds<CI>, char> bbl;
-#pragma unroll
-    for (int k = 0; k < (XIN == 2 ? 8 : 1); ++k) bsum[k] = 0.f;
-    // XIN: the rows of tile t inside the image become activations (1) / dy (2); rows r0 .. r0 + ROWS - 1 are this
-    // tile's to write
+    float pr[XIN ? 4 : 1][8];  // XIN: this thread's 8 channels' BatchNorm parameters
+    // XIN: the rows of tile t inside the image become activations; rows r0 .. r0 + ROWS - 1 are this tile's to write
     auto xform_rows = [&](uint4* h, int t) {
-        if constexpr (XIN != 0) {
+        if constexpr (XIN) {
             const int b = t / tpi, r0 = (t - b * tpi) * ROWS;
 #pragma unroll
             for (int u = 0; u < HR; ++u) {
                 const int ih = r0 + u;
                 if (ih >= Hi) continue;
-                const bool own = u < ROWS && nh == 0;
-                if constexpr (XIN == 1) {
-                    h[u] = bn_in_apply(h[u], pr);
-                    if (own) *reinterpret_cast<uint4*>(xin.a_out + row_off(b, ih)) = h[u];
-                } else {
-                    h[u] = bn_bwd_in_apply_lds<CI>(h[u], hg[u], bbl.prm, (tid % CPP) * 8, own, bsum);
-                    if (own) *reinterpret_cast<uint4*>(xb.dy_out + row_off(b, ih)) = h[u];
-                }
+                h[u] = bn_in_apply(h[u], pr);
+                if (u < ROWS && nh == 0) *reinterpret_cast<uint4*>(xin.a_out + row_off(b, ih)) = h[u];
             }
         }
     };
@@ -830,7 +685,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     };
     int t = blockIdx.x / NSPL, buf = 0;
     if (t < ntiles) load_rows(hr, t);  // in flight during the statistics prologue
-    if constexpr (XIN == 1) {
+    if constexpr (XIN) {
         __shared__ BnInLds<CI> bl;
         bn_in_prologue<CI>(xin, bl);
         const int c0 = (tid % CPP) * 8;
@@ -842,7 +697,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             pr[3][k] = bl.prm[3 * CI + c0 + k];
         }
     }
-    if constexpr (XIN == 2) bn_bwd_in_prologue<CI>(xb, bbl);
     if (t < ntiles) {
         xform_rows(hr, t);
         store_rows(hr, 0, t);
@@ -944,12 +798,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             xacc_add_shard(ep.acc, shard, CO + n0 + tid, q);
         }
     }
-    if constexpr (XIN == 2) {
-        if (xb.bias_acc.on()) {
-            __syncthreads();  // the halo buffer is free: scratch for the closing reduction
-            bn_bwd_in_bias<CI>(xb, bsum, reinterpret_cast<double*>(Hs));
-        }
-    }
 }
 
 
@@ -963,14 +811,6 @@ static BnIn bn_in_of(const BnInput* xi) {
     b.acc = xi->acc; b.R = xi->R; b.mean = xi->mean; b.invstd = xi->invstd; b.rmean = xi->rmean; b.rvar = xi->rvar;
     b.nbt = xi->nbt; b.momentum = xi->momentum; b.eps = xi->eps; b.gamma = xi->gamma; b.beta = xi->beta;
     b.a_out = static_cast<bf16*>(xi->a_out);
-    return b;
-}
-static BnBwdIn bn_bwd_in_of(const BnBwdInput* xb) {
-    BnBwdIn b{};
-    if (!xb) return b;
-    b.da = static_cast<const bf16*>(xb->da); b.mom = xb->mom; b.R = xb->R; b.mean = xb->mean; b.invstd = xb->invstd;
-    b.gamma = xb->gamma; b.beta = xb->beta; b.dgamma = xb->dgamma; b.dbeta = xb->dbeta; b.bias_acc = xb->bias_acc;
-    b.dy_out = static_cast<bf16*>(xb->dy_out);
     return b;
 }
 static bool conv_halo_shape(int Ci, int Co, int Wi, int Hi, int& which) {
@@ -996,12 +836,8 @@ bool subpixel_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co) {
 
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-            ColStats* st, const BnInput* xin, const BnBwdInput* xb) {
+            ColStats* st, const BnInput* xin) {
     HLMC_CHECK_ARG(!xin || conv_s2_takes_input_bn<T>(B, Hi, Wi, Ci, Co), "conv_s2: input BatchNorm needs a halo shape");
-    HLMC_CHECK_ARG(!xb || (conv_s2_takes_input_bn<T>(B, Hi, Wi, Ci, Co) && !xin && !(st && st->acc.on()) && xb->da &&
-                           xb->dy_out && xb->mom.p && xb->mom.ncols == 2 * Ci && (!xb->bias_acc.on() ||
-                           xb->bias_acc.ncols == Ci)),
-                   "conv_s2: input BatchNorm backward arguments / halo shape");
     if (xin) HLMC_CHECK_ARG(xin->acc.p && xin->acc.ncols == 2 * Ci && xin->a_out && st && st->acc.on(),
                             "conv_s2: input BatchNorm arguments");
     constexpr int V = Vec16<T>::N;
@@ -1018,8 +854,7 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
         conv_halo_shape(Ci, Co, Wi, Hi, which);
         // (CI, Co, Wi): (32, 64, 64) below; (64, 128, 32) two 64-channel halves per 64-pixel tile, one halo buffer
         // (the weights take half the LDS)
-        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, auto kern_xb, int tp, int nspl,
-                       int cap = 256) -> int {
+        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int tp, int nspl, int cap = 256) -> int {
             const int ntiles = M / tp;  // whole output rows: tiles stay inside an image
             const int grid = std::min(ntiles * nspl, cap);
             HLMC_PROBE_BEGIN(s);
@@ -1027,13 +862,12 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
                 WithStats<StoreRM<T>> eps;
                 static_cast<StoreRM<T>&>(eps) = ep;
                 eps.acc = st->acc;
-                if (xin) kern_xin<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, bn_in_of(xin), BnBwdIn{});
-                else kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, BnIn{}, BnBwdIn{});
+                if (xin) kern_xin<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, bn_in_of(xin));
+                else kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, BnIn{});
                 st->done = true;
             } else {
                 if (st) st->done = false;
-                if (xb) kern_xb<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{}, bn_bwd_in_of(xb));
-                else kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{}, BnBwdIn{});
+                kern_plain<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{});
             }
             HLMC_PROBE_END(s);
             HLMC_LAUNCHED();
@@ -1046,15 +880,13 @@ int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* w
         // block per CU before); the same with 4-row tiles and two 32-channel blocks per tile (the halo read twice)
         // lost (50 -> 55 us)
         if (which == 1)
-            return run(conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StoreRM<T>, false, 0, 2>,
-                       conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StRM, false, 0, 2>,
-                       conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StRM, false, 1, 2>,
-                       conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StoreRM<T>, false, 2, 2>, 64, 1, 512);
+            return run(conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StoreRM<T>, false, false, 2>,
+                       conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StRM, false, false, 2>,
+                       conv_s2_halo_kernel<32, 64, 1, 32, 2, false, StRM, false, true, 2>, 64, 1, 512);
         if (which == 2)
             return run(conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, false>,
                        conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false>,
-                       conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false, 1>,
-                       conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StoreRM<T>, false, 2>, 64, 2);
+                       conv_s2_halo_kernel<64, 64, 2, 16, 4, false, StRM, false, true>, 64, 2);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, K, 1, ws, st);
 }
@@ -1066,12 +898,8 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co) {
 
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-             ColStats* st, const BnInput* xin, const BnBwdInput* xb) {
+             ColStats* st, const BnInput* xin) {
     HLMC_CHECK_ARG(!xin || subpixel_takes_input_bn<T>(B, Hi, Wi, Ci, Co), "subpixel: input BatchNorm needs a halo shape");
-    HLMC_CHECK_ARG(!xb || (subpixel_takes_input_bn<T>(B, Hi, Wi, Ci, Co) && !xin && !(st && st->acc.on()) && xb->da &&
-                           xb->dy_out && xb->mom.p && xb->mom.ncols == 2 * Ci && (!xb->bias_acc.on() ||
-                           xb->bias_acc.ncols == Ci)),
-                   "subpixel: input BatchNorm backward arguments / halo shape");
     if (xin) HLMC_CHECK_ARG(xin->acc.p && xin->acc.ncols == 2 * Ci && xin->a_out && st && st->acc.on(),
                             "subpixel: input BatchNorm arguments");
     constexpr int V = Vec16<T>::N;
@@ -1089,8 +917,7 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
         subpixel_halo_shape(Ci, Co, Wi, Hi, which);
         // (nspl, cap): channel splits and grid cap of the statistics / input-BN launches; (nspl_p, cap_p): of the
         // plain launch
-        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, auto kern_xb, int nspl, int cap, int nspl_p,
-                       int cap_p) -> int {
+        auto run = [&](auto kern_plain, auto kern_stats, auto kern_xin, int nspl, int cap, int nspl_p, int cap_p) -> int {
             const int ntiles = M / 128;  // 128 low-res pixels (whole rows) per tile, inside one image
             HLMC_PROBE_BEGIN(s);
             if (st && st->acc.on()) {
@@ -1098,17 +925,12 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
                 WithStats<StoreSubpixel<T>> eps;
                 static_cast<StoreSubpixel<T>&>(eps) = ep;
                 eps.acc = st->acc;
-                if (xin) kern_xin<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, bn_in_of(xin), BnBwdIn{});
-                else kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, BnIn{}, BnBwdIn{});
+                if (xin) kern_xin<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, bn_in_of(xin));
+                else kern_stats<<<grid, 256, 0, s>>>(x, Hi, ntiles, wp, eps, M, BnIn{});
                 st->done = true;
             } else {
                 if (st) st->done = false;
-                if (xb)
-                    kern_xb<<<std::min(ntiles * nspl_p, cap_p), 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{},
-                                                                             bn_bwd_in_of(xb));
-                else
-                    kern_plain<<<std::min(ntiles * nspl_p, cap_p), 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{},
-                                                                                BnBwdIn{});
+                kern_plain<<<std::min(ntiles * nspl_p, cap_p), 256, 0, s>>>(x, Hi, ntiles, wp, ep, M, BnIn{});
             }
             HLMC_PROBE_END(s);
             HLMC_LAUNCHED();
@@ -1123,15 +945,13 @@ int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* 
         // input-BN forms need 90 KB (one block per CU) and lost 48 -> 68 us; the Ci 32 -> Co 64 conv with two
         // 32-channel blocks per tile (the halo read twice) lost 50 -> 55 / 32 -> 36 us
         if (which == 1)
-            return run(subpixel_halo_kernel<64, 32, 1, 32, 4, false, StoreSubpixel<T>, false, 0, 2>,
-                       subpixel_halo_kernel<64, 32, 1, 32, 4, false, StSP, false, 0, 2>,
-                       subpixel_halo_kernel<64, 32, 1, 32, 4, false, StSP, false, 1, 2>,
-                       subpixel_halo_kernel<64, 32, 1, 32, 4, false, StoreSubpixel<T>, false, 2, 2>, 1, 512, 1, 512);
+            return run(subpixel_halo_kernel<64, 32, 1, 32, 4, false, StoreSubpixel<T>, false, false, 2>,
+                       subpixel_halo_kernel<64, 32, 1, 32, 4, false, StSP, false, false, 2>,
+                       subpixel_halo_kernel<64, 32, 1, 32, 4, false, StSP, false, true, 2>, 1, 512, 1, 512);
         if (which == 2)
-            return run(subpixel_halo_kernel<128, 16, 4, 16, 8, false, StoreSubpixel<T>, false, 0, 2>,
+            return run(subpixel_halo_kernel<128, 16, 4, 16, 8, false, StoreSubpixel<T>, false, false, 2>,
                        subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false>,
-                       subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, 1>,
-                       subpixel_halo_kernel<128, 16, 4, 16, 8, false, StoreSubpixel<T>, false, 2, 1>, 2, 256, 4, 512);
+                       subpixel_halo_kernel<128, 32, 2, 16, 8, false, StSP, false, true>, 2, 256, 4, 512);
     }
     return dispatch_nt<T>(s, al, bl, ep, M, Co, 4 * Ci, 4, ws, st);
 }
@@ -1219,12 +1039,12 @@ size_t linear_wgrad_ws(int Mb, int N, int K) {  // with or without the bias colu
 
 #define INST(T)                                                                                                     \
     template int conv_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,         \
-                            ColStats*, const BnInput*, const BnBwdInput*);                               \
+                            ColStats*, const BnInput*);                                                  \
     template bool conv_s2_takes_input_bn<T>(int, int, int, int, int);                                              \
     template bool subpixel_takes_input_bn<T>(int, int, int, int, int);                                             \
     template size_t conv_s2_ws<T>(int, int, int, int, int);                                                        \
     template int subpixel<T>(hipStream_t, const T*, int, int, int, int, const T*, const float*, int, T*, Ws,        \
-                             ColStats*, const BnInput*, const BnBwdInput*);                                                          \
+                             ColStats*, const BnInput*);                                                                             \
     template size_t subpixel_ws<T>(int, int, int, int, int);                                                       \
     template int wgrad_s2<T>(hipStream_t, const T*, int, int, int, int, const T*, int, float*, Ws, XAcc, float*);  \
     template size_t wgrad_s2_ws<T>(int, int, int, int, int);                                                       \

@@ -1863,20 +1863,6 @@ int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C
     if (dbias) return colsum_finalize(s, bias_acc, C, dbias);
     return HLMC_OK;
 }
-template <typename T>
-int bn_bwd_moments(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean,
-                   const float* invstd, const float* gamma, const float* beta, int act, XAcc mom) {
-    HLMC_TRY(check_bn_shape<T>(C));
-    HLMC_TRY(check_acc(mom, 2 * C));
-    HLMC_CHECK_ARG(lda % Vec16<T>::N == 0, "bn_bwd_moments: grad row stride must be a multiple of 16 bytes");
-    const int nblk = bn_blocks(R, C);
-    const int64_t rpb = bn_rows_per_blk(R, C);
-    auto k = act == 0 ? bn_bwd_moments_kernel<T, false, 0> : bn_bwd_moments_kernel<T, false>;
-    HLMC_BN_PROBED(s, 2.0 * sizeof(T) * R * C,
-                   (k<<<nblk, kThreads, 0, s>>>(da, lda, y, R, C, mean, invstd, gamma, beta, act, nullptr, 1.f, rpb, mom)));
-    HLMC_LAUNCHED();
-    return HLMC_OK;
-}
 int colsum_to_f64(hipStream_t s, XAcc acc, int C, double* out) {
     HLMC_CHECK_ARG(out && C > 0, "colsum_to_f64: bad arguments");
     HLMC_TRY(check_acc(acc, C));
@@ -2231,8 +2217,6 @@ int pack(hipStream_t s, const AdamJob* jobs_dev, int njobs, int total_tiles) {
     template int bn_act_bwd<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,          \
                                const float*, const float*, int, const uint8_t*, float, T*, float*, float*, XAcc,      \
                                const BnBwdFuse*, XAcc, float*, float*);                                              \
-    template int bn_bwd_moments<T>(hipStream_t, const T*, int, const T*, int64_t, int, const float*, const float*,      \
-                                   const float*, const float*, int, XAcc);                                            \
     template int conv_c1_s2<T>(hipStream_t, const float*, int, int, int, const float*, const float*, int, T*,        \
                                ColStats*, BnBwdFuse*);                                                               \
     template int convT_c1<T>(hipStream_t, const T*, int, int, int, int, const float*, const float*, float*);         \

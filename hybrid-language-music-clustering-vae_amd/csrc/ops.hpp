@@ -47,25 +47,10 @@ template <typename T>
 bool conv_s2_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co);
 template <typename T>
 bool subpixel_takes_input_bn(int B, int Hi, int Wi, int Ci, int Co);
-// Train-mode BatchNorm + LeakyReLU(0.01) BACKWARD of a data-gradient conv's input applied while an LDS halo-tile kernel
-// stages it (bf16 halo shapes, no statistics output): x is then the BN layer's pre-BN map y, da its activation gradient
-// (x's layout), mom its backward moments (2 Ci columns, complete); the kernel writes dgamma / dbeta like
-// bn_bwd_apply, dy_out (x's layout, for the layer's weight gradient) and the conv bias sums of the stored dy into
-// bias_acc (may be off).  The separate apply pass is not run.
-struct BnBwdInput {
-    const void* da;
-    XAcc mom;
-    int64_t R;
-    const float *mean, *invstd, *gamma, *beta;
-    float *dgamma, *dbeta;
-    XAcc bias_acc;
-    void* dy_out;
-};
 // xin (nullable): BnInput (train-mode BatchNorm of the input applied while staging; needs st)
-// xb (nullable): BnBwdInput (only where *_takes_input_bn says so; no st)
 template <typename T>
 int conv_s2(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-            ColStats* st = nullptr, const BnInput* xin = nullptr, const BnBwdInput* xb = nullptr);
+            ColStats* st = nullptr, const BnInput* xin = nullptr);
 template <typename T>
 size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -73,7 +58,7 @@ size_t conv_s2_ws(int B, int Hi, int Wi, int Ci, int Co);
 // (also the data gradient of a stride-2 conv with the conv weight re-packed [Ci_conv][3][3][Co_conv])
 template <typename T>
 int subpixel(hipStream_t s, const T* x, int B, int Hi, int Wi, int Ci, const T* wp, const float* bias, int Co, T* y, Ws ws,
-             ColStats* st = nullptr, const BnInput* xin = nullptr, const BnBwdInput* xb = nullptr);
+             ColStats* st = nullptr, const BnInput* xin = nullptr);
 template <typename T>
 size_t subpixel_ws(int B, int Hi, int Wi, int Ci, int Co);
 
@@ -150,11 +135,6 @@ template <typename T>
 int bn_act_bwd(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean, const float* invstd,
                const float* gamma, const float* beta, int act, const uint8_t* mask, float mscale, T* dy, float* dgamma,
                float* dbeta, XAcc mom, const BnBwdFuse* fused, XAcc bias_acc, float* dbias, float* sums);
-// The backward moments pass alone (sum dz | sum dz * x-hat of act+BN into the zeroed accumulator mom, 2C columns): the
-// first half of bn_act_bwd, for a consumer that applies the rest while staging dy (BnBwdInput)
-template <typename T>
-int bn_bwd_moments(hipStream_t s, const T* da, int lda, const T* y, int64_t R, int C, const float* mean,
-                   const float* invstd, const float* gamma, const float* beta, int act, XAcc mom);
 // out[c] = total of column c of acc (C columns)
 int colsum_finalize(hipStream_t s, XAcc acc, int C, float* out);
 // out[c] (f64) = column c of an exact accumulator (the op-level statistics entry)

@@ -368,17 +368,6 @@ int hlmc_op_halo_fwd(void* stream, int kind, const void* x, int B, int Hi, int W
                      const float* bias, int Co, void* y, double* out_sums, const float* gamma, const float* beta,
                      float* running_mean, float* running_var, int64_t* num_batches_tracked, float momentum, float eps,
                      float* mean_out, float* invstd_out, void* a_out, void* ws, int64_t ws_bytes);
-/* The BatchNorm + LeakyReLU(0.01) BACKWARD of the same shapes' data-gradient kernels, applied while they stage their
- * input (bf16; the engine's fused backward of the 64 x 64 / 32 x 32 decoder and 32 x 32 / 16 x 16 encoder layers, the
- * backward of src/Convolutional_VAE.py:80-100, 124-139): the backward moments pass over (y, da), then ONE halo launch
- * that forms dy = BN-backward(da) per staged chunk, writes dy [B, Hi, Wi, Ci] (every row once), dgamma / dbeta and (dbias
- * nullable) the column sums of the stored dy, and computes out = kind 0: conv_s2(dy) [B, Hi/2, Wi/2, Co] / kind 1:
- * subpixel(dy) [B, 2Hi, 2Wi, Co] with the packed weight wp and no bias.  Equals hlmc_op_bn_bwd followed by
- * hlmc_op_conv_s2 / hlmc_op_subpixel on its dy.  ws: hlmc_op_halo_bwd_workspace(Ci) bytes (zeroed here). */
-int64_t hlmc_op_halo_bwd_workspace(int Ci);
-int hlmc_op_halo_bwd(void* stream, int kind, const void* y, const void* da, int B, int Hi, int Wi, int Ci,
-                     const void* wp, int Co, void* out, const float* mean, const float* invstd, const float* gamma,
-                     const float* beta, void* dy, float* dgamma, float* dbeta, float* dbias, void* ws, int64_t ws_bytes);
 
 #ifdef __cplusplus
 }

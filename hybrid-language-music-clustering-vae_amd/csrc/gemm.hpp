@@ -1049,9 +1049,12 @@ struct KRowDense {
     // K loop made the compiler wait for every outstanding load at its join: the loads issued one at a time.)
     __host__ bool vec_ok() const { return vec && Md % Vec16<T>::N == 0; }
     __device__ uint4 vload(int k, const Col& cl) const {
-        const void* a = (k < Kd && cl.m < Md) ? static_cast<const void*>(p + (int64_t)k * ld + cl.m)
-                        : (k < Kd && ones && cl.m == Md) ? static_cast<const void*>(&g_one16<T>)
-                                                         : static_cast<const void*>(&g_zero16);
+        // every candidate address formed, then selected (a conditional expression over them compiled to divergent
+        // branches around the index math)
+        const bool in = k < Kd && cl.m < Md, one = k < Kd && ones && cl.m == Md;
+        const uintptr_t pa = reinterpret_cast<uintptr_t>(p + (int64_t)k * ld + cl.m);
+        const uintptr_t po = reinterpret_cast<uintptr_t>(&g_one16<T>), pz = reinterpret_cast<uintptr_t>(&g_zero16);
+        const uintptr_t a = in ? pa : (one ? po : pz);
         return *reinterpret_cast<const uint4*>(a);
     }
     __device__ uint4 load(int k, const Col& cl) const {
@@ -1086,15 +1089,18 @@ struct KRowConvS2 {
         const int kh = tap / 3, kw = tap - kh * 3;
         return Col{(kh * 2 * Wl + kw) * C + ci, kh, kw, true};
     }
+    // branch-free: every term computed for every lane and the zero chunk chosen by a select (early returns compiled
+    // to divergent branches around the index math, and the joins cost the weight-gradient loop its exact wait counts:
+    // it waited for every outstanding load at the LDS store of the oldest)
     __device__ const void* addr(int k, const Col& cl) const {
-        if (k >= Kd || !cl.ok) return &g_zero16;
         const uint32_t t = dW.div((uint32_t)k);
         const int c = k - (int)t * Wl;
         const uint32_t b = dH.div(t);
         const int r = (int)t - (int)b * Hl;
-        if ((r == 0 && cl.kh == 0) || (c == 0 && cl.kw == 0)) return &g_zero16;
+        const bool zero = k >= Kd || !cl.ok || (r == 0 && cl.kh == 0) || (c == 0 && cl.kw == 0);
         const int64_t pix = ((int64_t)b * 2 * Hl + 2 * r - 1) * (2 * Wl) + 2 * c - 1;
-        return x + pix * C + cl.off;
+        const uintptr_t a = reinterpret_cast<uintptr_t>(x + pix * C + cl.off);
+        return reinterpret_cast<const void*>(zero ? reinterpret_cast<uintptr_t>(&g_zero16) : a);
     }
     __host__ bool vec_ok() const { return true; }
     __device__ uint4 vload(int k, const Col& cl) const { return *reinterpret_cast<const uint4*>(addr(k, cl)); }
@@ -1110,6 +1116,62 @@ struct KRowConvS2 {
     }
 };
 
+// Buffer-descriptor forms of the two weight-gradient loaders for power-of-two sizes (every layer of the model: image
+// sides, channel counts and row strides are powers of two) and operands under 2 GB: one 32-bit byte offset per 16-byte
+// chunk from shifts and adds, loaded with raw_buffer_load_b128 through a range-checked descriptor, so every zero chunk
+// (padding taps, rows past K, columns past N) is an offset past the descriptor's end that the hardware returns as zeros
+// -- no select between addresses, no 64-bit products.  The general loaders above spent ~1,700 VALU cycles per K-step
+// and wave on their index math (28 v_mul_lo_u32 / 16 v_mad_u64_u32 / 8 v_mul_hi_u32 among 243 vector instructions, the
+// quarter-rate ones 16 cycles each) against 512 cycles of MFMA, with one wave per SIMD to issue both.
+constexpr int kBufOut = 0x7FFFFFF0;  // a byte offset past every descriptor's end: the load returns zeros
+template <typename T>
+struct KRowDenseP2 {  // X[k * 2^lld + m], k < Kd, m < Md (Md % V == 0)
+    const T* p;
+    int lld, Kd, Md;
+    uint32_t bytes;   // Kd << lld elements, in bytes
+    struct Col {
+        int m;
+    };
+    __device__ Col prep(int m) const { return Col{m}; }
+    __host__ bool vec_ok() const { return true; }
+    __device__ uint4 vload(int k, const Col& cl) const {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(p), (short)0, (int)bytes, 0x00020000);
+        const int off = (k < Kd && cl.m < Md) ? ((k << lld) + cl.m) * (int)sizeof(T) : kBufOut;
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+    __device__ uint4 load(int k, const Col& cl) const { return vload(k, cl); }
+};
+template <typename T>
+struct KRowConvS2P2 {  // KRowConvS2 with Hl = 2^lh, Wl = 2^lw, C = 2^lc
+    const T* x;
+    int lh, lw, lc, Kd;
+    uint32_t bytes;   // the high-res map [B, 2Hl, 2Wl, C] in bytes
+    struct Col {
+        int off;  // (kh * 2Wl + kw) * C + ci relative to pixel (2r-1, 2c-1)
+        int kh, kw;
+        bool ok;
+    };
+    __device__ Col prep(int n) const {
+        const int C = 1 << lc;
+        if (n >= 9 * C) return Col{0, 0, 0, false};
+        const int tap = n >> lc, ci = n & (C - 1);
+        const int kh = tap / 3, kw = tap - kh * 3;
+        return Col{((kh << (lw + 1)) + kw) * C + ci, kh, kw, true};
+    }
+    __host__ bool vec_ok() const { return true; }
+    __device__ uint4 vload(int k, const Col& cl) const {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(x), (short)0, (int)bytes, 0x00020000);
+        const int c = k & ((1 << lw) - 1), t = k >> lw;
+        const int r = t & ((1 << lh) - 1), b = t >> lh;
+        const bool zero = k >= Kd || !cl.ok || (r == 0 && cl.kh == 0) || (c == 0 && cl.kw == 0);
+        // pixel (2r - 1, 2c - 1) of image b in the [2Hl][2Wl] map, then the tap / channel offset
+        const int pix = ((((b << lh) + r) * 2 - 1) << (lw + 1)) + 2 * c - 1;
+        const int off = zero ? kBufOut : ((pix << lc) + cl.off) * (int)sizeof(T);
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
+    __device__ uint4 load(int k, const Col& cl) const { return vload(k, cl); }
+};
+
 // ============================================================================ TN main loop
 // XOR swizzle of the 16-byte chunks of a bf16 k-row (CPR chunks per row, 8 or 16) for the ds_read_b64_tr_b16
 // fragment reads: the 8 k-rows one 32-lane half reads (q = 0..3, g = 0..1) land on disjoint bank groups.
@@ -1120,7 +1182,9 @@ __device__ __forceinline__ int tn_swz(int row) {
 }
 
 // Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_grouped_kernel).
-// One K-step of global loads in flight in one register set, double-buffered LDS images.
+// One K-step of global loads in flight in one register set, double-buffered LDS images.  (Two to four register sets
+// in flight at one block per CU measured no faster, round 6: the loop is bound by its issue -- MFMA, LDS and the
+// loaders' index math -- not by load latency.)
 template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, bool VEC = false>
 __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len,
                                                       int remap) {
@@ -1174,19 +1238,21 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) rg.a[i] = VEC ? ll.vload(k0 + c / ACPR, acol[i]) : ll.load(k0 + c / ACPR, acol[i]);
+            if (ACH % 256 == 0 || c < ACH)  // (a provable guard: a runtime one put every load in a branch)
+                rg.a[i] = VEC ? ll.vload(k0 + c / ACPR, acol[i]) : ll.load(k0 + c / ACPR, acol[i]);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) rg.b[i] = VEC ? hl.vload(k0 + c / BCPR, bcol[i]) : hl.load(k0 + c / BCPR, bcol[i]);
+            if (BCH % 256 == 0 || c < BCH)
+                rg.b[i] = VEC ? hl.vload(k0 + c / BCPR, bcol[i]) : hl.load(k0 + c / BCPR, bcol[i]);
         }
     };
     auto lstore = [&](const Regs& rg, int buf) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
             int c = tid + i * 256;
-            if (c < ACH) {
+            if (ACH % 256 == 0 || c < ACH) {
                 const int row = c / ACPR, cc = c % ACPR;
                 const int pc = SWA ? (cc ^ tn_swz<ACPR>(row)) : cc;
                 *reinterpret_cast<uint4*>(&Lbuf(buf)[row * LDA + pc * V]) = rg.a[i];
@@ -1195,7 +1261,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
             int c = tid + i * 256;
-            if (c < BCH) {
+            if (BCH % 256 == 0 || c < BCH) {
                 const int row = c / BCPR, cc = c % BCPR;
                 const int pc = SWB ? (cc ^ tn_swz<BCPR>(row)) : cc;
                 *reinterpret_cast<uint4*>(&Hbuf(buf)[row * LDB + pc * V]) = rg.b[i];

@@ -967,11 +967,20 @@ int wgrad_s2(hipStream_t s, const T* L, int B, int Hl, int Wl, int M, const T* X
     HLMC_CHECK_ARG(!dbias || bias_acc.on(), "wgrad_s2: a bias gradient needs its accumulator");
     HLMC_CHECK_ARG(M % V == 0 && C % V == 0, "wgrad_s2: channel counts must be multiples of the vector width");
     const int K = B * Hl * Wl, N = 9 * C;
-    KRowDense<T> ll{L, M, K, M, aligned16(L)};
-    KRowConvS2<T> hl{Xh, Hl, Wl, C, K, FastDiv((uint32_t)Wl), FastDiv((uint32_t)Hl)};
     StoreWgradConv ep{dW, C, bias_acc, dbias};
     probe::site(probe::kWgradS2, 2.0 * M * N * K,
                 (double)sizeof(T) * ((double)K * M + 4.0 * K * C) + 4.0 * M * N);
+    // power-of-two sides / channels and operands under 2 GB (every layer of the model): the buffer-descriptor loaders
+    const double lbytes = (double)K * M * sizeof(T), xbytes = 4.0 * K * C * sizeof(T);
+    const int lh = log2_exact(Hl), lw = log2_exact(Wl), lc = log2_exact(C), lm = log2_exact(M);
+    if (lh >= 0 && lw >= 0 && lc >= 0 && lm >= 0 && lbytes < 2147483000.0 && xbytes < 2147483000.0 && aligned16(L) &&
+        aligned16(Xh)) {
+        KRowDenseP2<T> ll{L, lm, K, M, (uint32_t)lbytes};
+        KRowConvS2P2<T> hl{Xh, lh, lw, lc, K, (uint32_t)xbytes};
+        return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
+    }
+    KRowDense<T> ll{L, M, K, M, aligned16(L)};
+    KRowConvS2<T> hl{Xh, Hl, Wl, C, K, FastDiv((uint32_t)Wl), FastDiv((uint32_t)Hl)};
     return dispatch_tn<T>(s, ll, hl, ep, M, N, K, ws);
 }
 template <typename T>

@@ -1068,7 +1068,15 @@ struct KRowDense {
         for (int i = 0; i < V; ++i)
             x.e[i] = (m + i < Md) ? r[m + i] : from_f32<T>((ones && m + i == Md) ? 1.f : 0.f);
         return x.u;
-    }
+    }    // stepped form (gemm_tn_kernel): the chunk's row j of the K-step and its column, the step's first row k0
+    struct Pre {
+        Col cl;
+        int j;
+    };
+    __device__ Pre pre(int j, int m) const { return Pre{prep(m), j}; }
+    __device__ int step(int k0) const { return k0; }
+    template <bool VEC>
+    __device__ uint4 sload(int k0, const Pre& p) const { return VEC ? vload(k0 + p.j, p.cl) : load(k0 + p.j, p.cl); }
 };
 
 // H loader for stride-2 conv / transposed conv weight gradient: k = (b, r, c) over the LOW-res grid,
@@ -1113,7 +1121,15 @@ struct KRowConvS2 {
         if ((r == 0 && cl.kh == 0) || (c == 0 && cl.kw == 0)) return make_uint4(0, 0, 0, 0);
         const int64_t pix = ((int64_t)b * 2 * Hl + 2 * r - 1) * (2 * Wl) + 2 * c - 1;
         return *reinterpret_cast<const uint4*>(x + pix * C + cl.off);
-    }
+    }    // stepped form (gemm_tn_kernel): the chunk's row j of the K-step and its column, the step's first row k0
+    struct Pre {
+        Col cl;
+        int j;
+    };
+    __device__ Pre pre(int j, int m) const { return Pre{prep(m), j}; }
+    __device__ int step(int k0) const { return k0; }
+    template <bool VEC>
+    __device__ uint4 sload(int k0, const Pre& p) const { return VEC ? vload(k0 + p.j, p.cl) : load(k0 + p.j, p.cl); }
 };
 
 // Buffer-descriptor forms of the two weight-gradient loaders for power-of-two sizes (every layer of the model: image
@@ -1140,6 +1156,18 @@ struct KRowDenseP2 {  // X[k * 2^lld + m], k < Kd, m < Md (Md % V == 0)
         return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
     __device__ uint4 load(int k, const Col& cl) const { return vload(k, cl); }
+    // stepped form: byte offset of (row j, column m) -- kBufOut past the columns -- plus the step's k0 rows; rows
+    // past Kd land past the descriptor's end (Kd << lld elements) and read as zeros with no test
+    struct Pre {
+        uint32_t v;
+    };
+    __device__ Pre pre(int j, int m) const { return Pre{m < Md ? (uint32_t)(((j << lld) + m) * (int)sizeof(T)) : (uint32_t)kBufOut}; }
+    __device__ uint32_t step(int k0) const { return (uint32_t)(k0 << lld) * (uint32_t)sizeof(T); }
+    template <bool VEC>
+    __device__ uint4 sload(uint32_t s, const Pre& pr) const {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(p), (short)0, (int)bytes, 0x00020000);
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(pr.v + s), 0, 0));
+    }
 };
 template <typename T>
 struct KRowConvS2P2 {  // KRowConvS2 with Hl = 2^lh, Wl = 2^lw, C = 2^lc
@@ -1170,6 +1198,38 @@ struct KRowConvS2P2 {  // KRowConvS2 with Hl = 2^lh, Wl = 2^lw, C = 2^lc
         return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
     }
     __device__ uint4 load(int k, const Col& cl) const { return vload(k, cl); }
+    // stepped form.  With k0 % 64 == 0, j < 64 and power-of-two sides, k0 + j splits into (b, r, c) without carries:
+    // c = c0 + cj, r = r0 + rj, b = b0 + bj, each first term from k0 alone (wave-uniform), each second from j alone
+    // (fixed per chunk), so the pixel offset is a per-step scalar plus a per-chunk constant and the padding tests
+    // (r == 0 with kh == 0, c == 0 with kw == 0) are a uniform flag AND a per-chunk flag.  Rows past Kd (b >= B)
+    // land past the descriptor's end.
+    struct Pre {
+        int v;       // byte offset of the chunk at k0 = 0: pixel (2rj - 1 + kh, 2cj - 1 + kw) of image bj, its channels
+        bool zr, zc;  // rj == 0 and kh == 0 / cj == 0 and kw == 0
+    };
+    struct Step {
+        uint32_t s;  // byte offset of the step's (b0, r0, c0) pixel block
+        bool r0, c0;  // r0 == 0 / c0 == 0
+    };
+    __device__ Pre pre(int j, int n) const {
+        const Col cl = prep(n);
+        const int cj = j & ((1 << lw) - 1), tj = j >> lw, rj = tj & ((1 << lh) - 1), bj = tj >> lh;
+        const int pix = ((((bj << lh) + rj) * 2 - 1) << (lw + 1)) + 2 * cj - 1;
+        if (!cl.ok) return Pre{kBufOut, false, false};  // a column past N: kBufOut + any step offset is past the end
+        return Pre{((pix << lc) + cl.off) * (int)sizeof(T), rj == 0 && cl.kh == 0, cj == 0 && cl.kw == 0};
+    }
+    __device__ Step step(int k0) const {
+        const int c0 = k0 & ((1 << lw) - 1), t0 = k0 >> lw, r0 = t0 & ((1 << lh) - 1), b0 = t0 >> lh;
+        const uint32_t pix = ((uint32_t)((b0 << lh) + r0) << (lw + 2)) + 2u * (uint32_t)c0;
+        return Step{(pix << lc) * (uint32_t)sizeof(T), r0 == 0, c0 == 0};
+    }
+    template <bool VEC>
+    __device__ uint4 sload(const Step& st, const Pre& pr) const {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(x), (short)0, (int)bytes, 0x00020000);
+        const bool zero = (st.r0 && pr.zr) || (st.c0 && pr.zc);
+        const int off = zero ? kBufOut : (int)((uint32_t)pr.v + st.s);
+        return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    }
 };
 
 // ============================================================================ TN main loop
@@ -1186,7 +1246,7 @@ __device__ __forceinline__ int tn_swz(int row) {
 // in flight at one block per CU measured no faster, round 6: the loop is bound by its issue -- MFMA, LDS and the
 // loaders' index math -- not by load latency.)
 template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, bool VEC = false>
-__global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len,
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len,
                                                       int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;            // k rows per tile (KCH 16-byte chunks of one column)
@@ -1198,10 +1258,11 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
     constexpr int LDA = SWA ? BM : BM + V;  // LDS row (elements)
     constexpr int LDB = SWB ? BN : BN + V;
     constexpr int WAVES_N = BN / WN;
-    static_assert((BM / WM) * WAVES_N == 4, "4 waves per block");
+    constexpr int NTH = 64 * (BM / WM) * WAVES_N;  // 4 or 8 waves
+    static_assert(NTH == 256 || NTH == 512, "4 or 8 waves per block");
     constexpr int TM = WM / 16, TN = WN / 16;
     constexpr int ACH = BK * BM / V, BCH = BK * BN / V;
-    constexpr int AR = (ACH + 255) / 256, BR = (BCH + 255) / 256;
+    constexpr int AR = (ACH + NTH - 1) / NTH, BR = (BCH + NTH - 1) / NTH;
     constexpr int LSZ = BK * LDA, HSZ = BK * LDB;
     __shared__ __attribute__((aligned(16))) T tn_sm[2 * (LSZ + HSZ)];
 
@@ -1228,31 +1289,40 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
     struct Regs {
         uint4 a[AR], b[BR];
     };
-    typename LL::Col acol[AR];
-    typename HL::Col bcol[BR];
+    // each chunk's K-step row and column are fixed for the whole kernel: the loaders' per-chunk constants once
+    // (pre), the per-K-step part once per step (step: wave-uniform), one select / add per chunk and step (sload)
+    typename LL::Pre apre[AR];
+    typename HL::Pre bpre[BR];
 #pragma unroll
-    for (int i = 0; i < AR; ++i) acol[i] = ll.prep(m0 + ((tid + i * 256) % ACPR) * V);
+    for (int i = 0; i < AR; ++i) {
+        const int c = tid + i * NTH;
+        apre[i] = ll.pre(c / ACPR, m0 + (c % ACPR) * V);
+    }
 #pragma unroll
-    for (int i = 0; i < BR; ++i) bcol[i] = hl.prep(n0 + ((tid + i * 256) % BCPR) * V);
+    for (int i = 0; i < BR; ++i) {
+        const int c = tid + i * NTH;
+        bpre[i] = hl.pre(c / BCPR, n0 + (c % BCPR) * V);
+    }
     auto gload = [&](Regs& rg, int k0) {
+        const auto sa = ll.step(k0);
+        const auto sb = hl.step(k0);
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
-            int c = tid + i * 256;
-            if (ACH % 256 == 0 || c < ACH)  // (a provable guard: a runtime one put every load in a branch)
-                rg.a[i] = VEC ? ll.vload(k0 + c / ACPR, acol[i]) : ll.load(k0 + c / ACPR, acol[i]);
+            int c = tid + i * NTH;
+            if (ACH % NTH == 0 || c < ACH)  // (a provable guard: a runtime one put every load in a branch)
+                rg.a[i] = ll.template sload<VEC>(sa, apre[i]);
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
-            int c = tid + i * 256;
-            if (BCH % 256 == 0 || c < BCH)
-                rg.b[i] = VEC ? hl.vload(k0 + c / BCPR, bcol[i]) : hl.load(k0 + c / BCPR, bcol[i]);
+            int c = tid + i * NTH;
+            if (BCH % NTH == 0 || c < BCH) rg.b[i] = hl.template sload<VEC>(sb, bpre[i]);
         }
     };
     auto lstore = [&](const Regs& rg, int buf) {
 #pragma unroll
         for (int i = 0; i < AR; ++i) {
-            int c = tid + i * 256;
-            if (ACH % 256 == 0 || c < ACH) {
+            int c = tid + i * NTH;
+            if (ACH % NTH == 0 || c < ACH) {
                 const int row = c / ACPR, cc = c % ACPR;
                 const int pc = SWA ? (cc ^ tn_swz<ACPR>(row)) : cc;
                 *reinterpret_cast<uint4*>(&Lbuf(buf)[row * LDA + pc * V]) = rg.a[i];
@@ -1260,8 +1330,8 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
         }
 #pragma unroll
         for (int i = 0; i < BR; ++i) {
-            int c = tid + i * 256;
-            if (BCH % 256 == 0 || c < BCH) {
+            int c = tid + i * NTH;
+            if (BCH % NTH == 0 || c < BCH) {
                 const int row = c / BCPR, cc = c % BCPR;
                 const int pc = SWB ? (cc ^ tn_swz<BCPR>(row)) : cc;
                 *reinterpret_cast<uint4*>(&Hbuf(buf)[row * LDB + pc * V]) = rg.b[i];
@@ -1331,6 +1401,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(LL ll, HL hl, float* ws, i
         gload(r0, kb);
         lstore(r0, 0);
         __syncthreads();
+        // unrolled by the two LDS images, so that every LDS address is a per-thread base plus an immediate offset
         for (int st = 0; st < nsteps; ++st) {
             const int cur = st & 1;
             const bool more = st + 1 < nsteps;

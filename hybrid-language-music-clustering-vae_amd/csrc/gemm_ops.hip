@@ -296,12 +296,13 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
     // the 64-deep K-step for splits of >= 1024 rows (measured: 490.9 vs 450.9 us for the 9 conv layers when
     // every split took it), the 32-deep one below; branch-free 16-byte loads where both operands allow them
     const bool vec = ll.vec_ok() && hl.vec_ok();
+    constexpr int NTH = 64 * (BM / WM) * (BN / WN);
     if (pl.ksl >= kTnKch8Min) {
-        if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, true><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-        else gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, true><<<grid, NTH, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        else gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, NTH, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
     } else {
-        if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, true><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-        else gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, 256, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, true><<<grid, NTH, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+        else gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, NTH, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
     }
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();

@@ -1401,7 +1401,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL 
         gload(r0, kb);
         lstore(r0, 0);
         __syncthreads();
-        // unrolled by the two LDS images, so that every LDS address is a per-thread base plus an immediate offset
         for (int st = 0; st < nsteps; ++st) {
             const int cur = st & 1;
             const bool more = st + 1 < nsteps;

@@ -1232,6 +1232,17 @@ struct KRowConvS2P2 {  // KRowConvS2 with Hl = 2^lh, Wl = 2^lw, C = 2^lc
     }
 };
 
+#ifdef HLMC_TN_TS  // diagnostic build only: per-block phase timestamps of gemm_tn_kernel (100 MHz wall clock)
+__device__ unsigned long long g_tn_ts[8192][4];
+#define TN_TS(i)                                                                                   \
+    do {                                                                                           \
+        const unsigned b_ = blockIdx.x + gridDim.x * blockIdx.z;                                    \
+        if (threadIdx.x == 0 && b_ < 8192u) g_tn_ts[b_][i] = wall_clock64();                        \
+    } while (0)
+#else
+#define TN_TS(i)
+#endif
+
 // ============================================================================ TN main loop
 // XOR swizzle of the 16-byte chunks of a bf16 k-row (CPR chunks per row, 8 or 16) for the ds_read_b64_tr_b16
 // fragment reads: the 8 k-rows one 32-lane half reads (q = 0..3, g = 0..1) land on disjoint bank groups.
@@ -1266,6 +1277,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL 
     constexpr int LSZ = BK * LDA, HSZ = BK * LDB;
     __shared__ __attribute__((aligned(16))) T tn_sm[2 * (LSZ + HSZ)];
 
+    TN_TS(0);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     T* const Lg = tn_sm;  // L0 H0 L1 H1
     auto Lbuf = [&](int buf) { return Lg + buf * (LSZ + HSZ); };
@@ -1401,6 +1413,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL 
         gload(r0, kb);
         lstore(r0, 0);
         __syncthreads();
+        TN_TS(1);
         for (int st = 0; st < nsteps; ++st) {
             const int cur = st & 1;
             const bool more = st + 1 < nsteps;
@@ -1410,6 +1423,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL 
             __syncthreads();
         }
     }
+    TN_TS(2);
     float* slab = ws + (int64_t)bz * M * N;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1421,6 +1435,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL 
                 int n = n0 + wn0 + j * 16 + (lane & 15);
                 if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
             }
+    TN_TS(3);
 }
 
 // Split-K reduction parallel over the splits as well as the outputs: a block holds 256 / G outputs x G split

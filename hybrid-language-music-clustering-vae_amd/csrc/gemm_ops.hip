@@ -1072,3 +1072,8 @@ template int linear<bf16, float>(hipStream_t, const bf16*, int, int, int, const 
 
 }  // namespace ops
 }  // namespace hlmc
+#ifdef HLMC_TN_TS
+extern "C" int hlmc_debug_tn_ts(void* host, int nblocks) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(hlmc::g_tn_ts), (size_t)nblocks * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -955,6 +955,38 @@ __global__ void splitk_reduce_kernel(const float* ws, EP ep, int M, int N, int S
     }
 }
 
+// The same with one float4 of outputs per thread (N % 4 == 0, phases * S * M * N < 2^31, 16-byte aligned slabs):
+// 16-byte slab loads and 32-bit index math (the 64-bit divisions above cost more than the loads); each output's
+// additions in the same order as above (the same bits)
+template <class EP>
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(const float* __restrict__ ws, EP ep, int M, int N, int S,
+                                                             int phases, FastDiv dN, FastDiv dM) {
+    const uint32_t e = (blockIdx.x * 256u + threadIdx.x) * 4u;
+    if (e >= (uint32_t)phases * (uint32_t)M * (uint32_t)N) return;
+    const uint32_t t = dN.div(e), n = e - t * (uint32_t)N;
+    const uint32_t ph = dM.div(t), m = t - ph * (uint32_t)M;
+    const uint32_t st = (uint32_t)M * (uint32_t)N;
+    const float* p = ws + ((ph * (uint32_t)S) * (uint32_t)M + m) * (uint32_t)N + n;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto add = [](float4& x, const float4& y) { x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w; };
+    int k = 0;
+    for (; k + 4 <= S; k += 4) {
+        const float4 a0 = *reinterpret_cast<const float4*>(p + k * st);
+        const float4 a1 = *reinterpret_cast<const float4*>(p + (k + 1) * st);
+        const float4 a2 = *reinterpret_cast<const float4*>(p + (k + 2) * st);
+        const float4 a3 = *reinterpret_cast<const float4*>(p + (k + 3) * st);
+        add(a, a0); add(a, a1); add(a, a2); add(a, a3);
+    }
+    for (; k < S; ++k) add(a, *reinterpret_cast<const float4*>(p + k * st));
+    EP o = ep;
+    o.set_phase((int)ph);
+    const auto rw = o.row((int)m);
+    o.store(rw, (int)n, a.x);
+    o.store(rw, (int)n + 1, a.y);
+    o.store(rw, (int)n + 2, a.z);
+    o.store(rw, (int)n + 3, a.w);
+}
+
 // The same reduction for a launch whose output feeds a train-mode BatchNorm: block = a tile of 4 * RU output rows
 // (phase-major) x 64 columns; it also delivers the column sums / sums of squares of the values it stored to `acc`
 // (2N columns, common.hpp XAcc) -- no separate moments pass over the output.  Thread (column tid % 64, row group
@@ -1481,6 +1513,50 @@ __global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(const float*
         EP e = ep;
         e.set_phase(0);
         e.store(e.row(m), n, acc);
+    }
+}
+// The same with 4 consecutive outputs per thread (N % 4 == 0, 16-byte aligned slabs): 16-byte slab loads, 4x the
+// bytes in flight per thread; each output's additions in the same order as above (the same bits)
+template <int G, class EP>
+__global__ __launch_bounds__(256) void splitk_reduce_grouped4_kernel(const float* __restrict__ ws, EP ep, int M, int N,
+                                                                     int S) {
+    ep_extra(ep, 0);
+    constexpr int OPB = 256 / G;  // float4 outputs per block
+    __shared__ float4 part[G][OPB];
+    const int o = threadIdx.x % OPB, g = threadIdx.x / OPB;
+    const int64_t idx = ((int64_t)blockIdx.x * OPB + o) * 4;
+    const int64_t total = (int64_t)M * N;
+    const int64_t st = total;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto add = [](float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; };
+    if (idx < total) {
+        const float* p = ws + idx;
+        int k = g;
+        for (; k + 3 * G < S; k += 4 * G) {
+            const float4 a0 = *reinterpret_cast<const float4*>(p + k * st);
+            const float4 a1 = *reinterpret_cast<const float4*>(p + (k + G) * st);
+            const float4 a2 = *reinterpret_cast<const float4*>(p + (k + 2 * G) * st);
+            const float4 a3 = *reinterpret_cast<const float4*>(p + (k + 3 * G) * st);
+            add(acc, a0); add(acc, a1); add(acc, a2); add(acc, a3);
+        }
+        for (; k < S; k += G) add(acc, *reinterpret_cast<const float4*>(p + k * st));
+    }
+    if constexpr (G > 1) {
+        part[g][o] = acc;
+        __syncthreads();
+        if (g != 0) return;
+#pragma unroll
+        for (int j = 1; j < G; ++j) add(acc, part[j][o]);
+    }
+    if (idx < total) {
+        const int m = (int)(idx / N), n = (int)(idx - (int64_t)m * N);  // N % 4 == 0: the 4 outputs share row m
+        EP e = ep;
+        e.set_phase(0);
+        const auto rw = e.row(m);
+        e.store(rw, n, acc.x);
+        e.store(rw, n + 1, acc.y);
+        e.store(rw, n + 2, acc.z);
+        e.store(rw, n + 3, acc.w);
     }
 }
 

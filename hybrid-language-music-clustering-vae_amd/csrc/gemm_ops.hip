@@ -144,6 +144,12 @@ int launch_nt(hipStream_t s, const AL& al, const BL& bl, const EP& ep, int M, in
         return HLMC_OK;
     }
     int64_t total = (int64_t)phases * M * N;
+    if (N % 4 == 0 && (double)phases * pl.S * M * N < 2147483648.0 && ((uintptr_t)ws.p & 15) == 0) {
+        const unsigned nb = (unsigned)((total / 4 + 255) / 256);
+        splitk_reduce4_kernel<EP><<<nb, 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases, FastDiv((uint32_t)N), FastDiv((uint32_t)M));
+        HLMC_LAUNCHED();
+        return HLMC_OK;
+    }
     int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
     splitk_reduce_kernel<EP><<<blocks, 256, 0, s>>>(ws.p, ep, M, N, pl.S, phases);
     HLMC_LAUNCHED();
@@ -262,20 +268,62 @@ __global__ __launch_bounds__(288) void splitk_reduce_wgrad_conv_kernel(const flo
     ep.dW[(int64_t)m * N + (int64_t)ci0 * 9 + t] = tile[t];
 }
 
+// The same for C % 128 == 0 with 16-byte slab loads: a 288-thread block per (row m, 128 input channels), each thread
+// summing 4 consecutive channels of one tap in split order (the same order, so the same bits, as the kernel above),
+// the block's 1,152 consecutive dW floats written as float4 through LDS.  (Four-byte loads left too few bytes in
+// flight: 2.6-3.5 TB/s on the 2- and 4-split layers.)
+__global__ __launch_bounds__(288) void splitk_reduce_wgrad_conv4_kernel(const float* __restrict__ ws, StoreWgradConv ep,
+                                                                        int M, int C, int S) {
+    ep_extra(ep, 0);
+    __shared__ __attribute__((aligned(16))) float tile[128 * 9];
+    const int cb = C / 128;
+    const int m = blockIdx.x / cb, ci0 = (blockIdx.x - m * cb) * 128;
+    const int t = threadIdx.x, tap = t >> 5, cl = t & 31;
+    const int64_t N = 9LL * C, st = (int64_t)M * N;
+    const float* p = ws + (int64_t)m * N + tap * C + ci0 + 4 * cl;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int k = 0;
+    for (; k + 3 < S; k += 4) {
+        const float4 a0 = *reinterpret_cast<const float4*>(p + k * st), a1 = *reinterpret_cast<const float4*>(p + (k + 1) * st);
+        const float4 a2 = *reinterpret_cast<const float4*>(p + (k + 2) * st), a3 = *reinterpret_cast<const float4*>(p + (k + 3) * st);
+        acc.x += a0.x; acc.y += a0.y; acc.z += a0.z; acc.w += a0.w;
+        acc.x += a1.x; acc.y += a1.y; acc.z += a1.z; acc.w += a1.w;
+        acc.x += a2.x; acc.y += a2.y; acc.z += a2.z; acc.w += a2.w;
+        acc.x += a3.x; acc.y += a3.y; acc.z += a3.z; acc.w += a3.w;
+    }
+    for (; k < S; ++k) {
+        const float4 a = *reinterpret_cast<const float4*>(p + k * st);
+        acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+    }
+    tile[(4 * cl + 0) * 9 + tap] = acc.x;
+    tile[(4 * cl + 1) * 9 + tap] = acc.y;
+    tile[(4 * cl + 2) * 9 + tap] = acc.z;
+    tile[(4 * cl + 3) * 9 + tap] = acc.w;
+    __syncthreads();
+    *reinterpret_cast<float4*>(ep.dW + (int64_t)m * N + (int64_t)ci0 * 9 + 4 * t) = *reinterpret_cast<const float4*>(&tile[4 * t]);
+}
+
 // S-way split-K reduction with the splits spread over G thread groups (splitk_reduce_grouped_kernel)
 template <class EP>
 void reduce_splits(hipStream_t s, const float* ws, const EP& ep, int M, int N, int S) {
     if constexpr (std::is_same<EP, StoreWgradConv>::value) {
+        if (S <= 4 && ep.C % 128 == 0 && (((uintptr_t)ws | (uintptr_t)ep.dW) & 15) == 0) {
+            splitk_reduce_wgrad_conv4_kernel<<<(unsigned)(M * (ep.C / 128)), 288, 0, s>>>(ws, ep, M, ep.C, S);
+            return;
+        }
         if (S <= 4 && ep.C % 32 == 0) {
             splitk_reduce_wgrad_conv_kernel<<<(unsigned)(M * (ep.C / 32)), 288, 0, s>>>(ws, ep, M, ep.C, S);
             return;
         }
     }
     const int64_t total = (int64_t)M * N;
+    const bool v4 = N % 4 == 0 && ((uintptr_t)ws & 15) == 0;
     auto go = [&](auto gtag) {
         constexpr int G = decltype(gtag)::value;
-        const int64_t blocks = (total + 256 / G - 1) / (256 / G);
-        splitk_reduce_grouped_kernel<G, EP><<<(unsigned)blocks, 256, 0, s>>>(ws, ep, M, N, S);
+        const int64_t per = v4 ? 4 * (256 / G) : 256 / G;  // outputs per block
+        const int64_t blocks = (total + per - 1) / per;
+        if (v4) splitk_reduce_grouped4_kernel<G, EP><<<(unsigned)blocks, 256, 0, s>>>(ws, ep, M, N, S);
+        else splitk_reduce_grouped_kernel<G, EP><<<(unsigned)blocks, 256, 0, s>>>(ws, ep, M, N, S);
     };
     if (S >= 32) go(std::integral_constant<int, 8>{});
     else if (S >= 8) go(std::integral_constant<int, 4>{});

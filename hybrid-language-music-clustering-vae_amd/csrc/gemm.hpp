@@ -236,6 +236,7 @@ __device__ __forceinline__ void store4_round(OutT* p, float (&v)[4]) {
 template <typename OutT>
 struct StoreRM {
     static constexpr int kStatMode = 0;
+    static constexpr bool kDirectTn = true;  // gemm_tn_kernel may store through it directly (TnDirect)
     OutT* out;
     const float* bias;
     int ld, act, accumulate;
@@ -1284,13 +1285,33 @@ __device__ __forceinline__ int tn_swz(int row) {
     else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
 }
 
-// Writes partial slabs ws[(split * M + m) * N + n] (always split-K; reduced by splitk_reduce_grouped_kernel).
-// One K-step of global loads in flight in one register set, double-buffered LDS images.  (Two to four register sets
-// in flight at one block per CU measured no faster, round 6: the loop is bound by its issue -- MFMA, LDS and the
-// loaders' index math -- not by load latency.)
-template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, bool VEC = false>
-__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL ll, HL hl, float* ws, int M, int N, int K, int ksplit_len,
-                                                      int remap) {
+// Output of gemm_tn_kernel: the split's fp32 slab ws[(split * M + m) * N + n], reduced by a split-K reduce launch
+struct TnSlab {
+    float* ws;
+    __device__ void put(int bz, int m, int n, int M, int N, float v) const { ws[((int64_t)bz * M + m) * N + n] = v; }
+};
+// ... or, when the grid has one split, the final epilogue itself (no slab, no reduce launch): epilogues that flag
+// kDirectTn (a store(row(m), n, v) with no once-per-launch side task)
+template <class EP>
+struct TnDirect {
+    EP ep;
+    __device__ void put(int, int m, int n, int, int, float v) const {
+        EP e = ep;
+        e.set_phase(0);
+        e.store(e.row(m), n, v);
+    }
+};
+template <class E, class = void>
+struct tn_direct : std::false_type {};
+template <class E>
+struct tn_direct<E, std::void_t<decltype(E::kDirectTn)>> : std::bool_constant<E::kDirectTn> {};
+
+// One K-step of global loads in flight in one register set, double-buffered LDS images.  (Two register sets -- loads
+// two K-steps ahead -- measured no faster, round 6, nor did 8-wave blocks or 256-wide tiles: per-block timestamps
+// put the K loop at ~0.86 us per 64-deep K-step on the deep layers, bound by the per-CU load throughput.)
+template <typename T, int BM, int BN, int WM, int WN, int KCH, class LL, class HL, bool VEC = false, class OUT = TnSlab>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL ll, HL hl, OUT out, int M, int N, int K,
+                                                                             int ksplit_len, int remap) {
     constexpr int V = Vec16<T>::N;
     constexpr int BK = KCH * V;            // k rows per tile (KCH 16-byte chunks of one column)
     constexpr int ACPR = BM / V, BCPR = BN / V;  // chunks per k-row
@@ -1456,7 +1477,6 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL 
         }
     }
     TN_TS(2);
-    float* slab = ws + (int64_t)bz * M * N;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1465,7 +1485,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void gemm_tn_kernel(LL 
             for (int r = 0; r < 4; ++r) {
                 int m = m0 + wm0 + i * 16 + (lane >> 4) * 4 + r;
                 int n = n0 + wn0 + j * 16 + (lane & 15);
-                if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
+                if (m < M && n < N) out.put(bz, m, n, M, N, acc[i][j][r]);
             }
     TN_TS(3);
 }

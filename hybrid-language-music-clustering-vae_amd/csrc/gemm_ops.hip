@@ -345,13 +345,25 @@ int launch_tn(hipStream_t s, const LL& ll, const HL& hl, const EP& ep, int M, in
     // every split took it), the 32-deep one below; branch-free 16-byte loads where both operands allow them
     const bool vec = ll.vec_ok() && hl.vec_ok();
     constexpr int NTH = 64 * (BM / WM) * (BN / WN);
-    if (pl.ksl >= kTnKch8Min) {
-        if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, true><<<grid, NTH, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-        else gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL><<<grid, NTH, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-    } else {
-        if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, true><<<grid, NTH, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
-        else gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL><<<grid, NTH, 0, s>>>(ll, hl, ws.p, M, N, K, pl.ksl, rm);
+    auto go = [&](auto out) {
+        using OUT = decltype(out);
+        if (pl.ksl >= kTnKch8Min) {
+            if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, true, OUT><<<grid, NTH, 0, s>>>(ll, hl, out, M, N, K, pl.ksl, rm);
+            else gemm_tn_kernel<T, BM, BN, WM, WN, 8, LL, HL, false, OUT><<<grid, NTH, 0, s>>>(ll, hl, out, M, N, K, pl.ksl, rm);
+        } else {
+            if (vec) gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, true, OUT><<<grid, NTH, 0, s>>>(ll, hl, out, M, N, K, pl.ksl, rm);
+            else gemm_tn_kernel<T, BM, BN, WM, WN, 4, LL, HL, false, OUT><<<grid, NTH, 0, s>>>(ll, hl, out, M, N, K, pl.ksl, rm);
+        }
+    };
+    if constexpr (tn_direct<EP>::value) {
+        if (pl.S == 1) {  // one split (the dense layers' batch-long reductions): the epilogue stores from registers
+            go(TnDirect<EP>{ep});
+            HLMC_PROBE_END(s);
+            HLMC_LAUNCHED();
+            return HLMC_OK;
+        }
     }
+    go(TnSlab{ws.p});
     HLMC_PROBE_END(s);
     HLMC_LAUNCHED();
     reduce_splits(s, ws.p, ep, M, N, pl.S);
@@ -1064,6 +1076,7 @@ size_t linear_ws(int M, int K, int N) {
 // Final epilogue of a dense weight gradient whose H operand carries the ones column: C[n][k < K] -> dW[n][k],
 // C[n][K] -> db[n] (the bias gradient, a column sum of dy, from the same GEMM and split-K reduction).
 struct StoreWgradBias {
+    static constexpr bool kDirectTn = true;  // gemm_tn_kernel may store through it directly (TnDirect)
     float* dW;
     float* db;
     int K;

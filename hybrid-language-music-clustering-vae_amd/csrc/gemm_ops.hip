@@ -13,7 +13,7 @@ namespace {
 // linears) 512: 101.8k vs 101.2k at 256 (round 2, after the small split-K grids moved to the LDS-DMA ring;
 // round 1 measured 256 ahead of 512 and 128); TN (weight gradients) 512: 93.2k vs 92.8k at 1024, 90.7k at 2048
 constexpr int kNtTargetBlocks = 512;
-constexpr int kTnTargetBlocks = 256;
+constexpr int kTnTargetBlocks = 192;
 constexpr int kTnLongK = 131072;
 constexpr int kTnKch8Min = 1024;
 // XCD-aware block order (gemm.hpp xcd_logical_block) for these op kinds: measured per layer (scripts/bench_gemm.py),
@@ -44,7 +44,9 @@ inline Plan plan_tn(int tiles, int K, int BK) {
     // bench_gemm.py) 47 vs 60 us at 512, while every shorter layer is fastest at 512 (1024: +10-20 %).
     // Round 4 (with the NT GEMMs at two blocks per CU beside them): one 256-block target for every layer measured
     // 134.1k vs 132.9k clips/s at 512 / 1024 (128: 129.6k, 192: 133.6k, 320: 133.6k, 384: 132.1k, 768: 130.8k);
-    // the long layers at 512 then 134.5k vs 134.0k (1024: 134.1k).
+    // the long layers at 512 then 134.5k vs 134.0k (1024: 134.1k).  Round 6, with the cheap power-of-two loaders: 192
+    // 142.5k vs 141.8k at 256, 384 139.2k vs 141.9k (3 pairs each; 384 is 7 % faster standalone: the side-stream grids
+    // take CUs from the main stream).
     const int target = K >= kTnLongK ? 2 * kTnTargetBlocks : kTnTargetBlocks;
     int S = cdiv(target, tiles);
     S = std::max(1, std::min(S, K / (4 * BK)));
